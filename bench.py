@@ -1,0 +1,207 @@
+"""Benchmark: train positives/s of BPR-MF on the ml-20m-shape workload (C2).
+
+BASELINE.json metric: "train positives/sec (+neg) per node; full-sort eval
+users/sec". Workload: 138,493 users x 26,744 items (+PAD),
+~20 M synthetic interactions (item popularity Zipf(1.0), user activity
+log-normal(sigma=1) rescaled to mean 144.4, min 20), RO_RS 0.8/0.1/0.1 split,
+embedding_size 128, 4 uniform negatives per positive, train_batch_size 2,048
+rows -> 512 positives per step, Adam lr 1e-3 — built and trained through the
+product path (Dataset -> data_preparation -> BPR -> FusedBPRTrainStep).
+
+A step = one batch: K4 sampler walk -> K3 fused BPR fwd/bwd -> K2 grouping ->
+K5 dense Adam over every row of both tables -> loss bookkeeping. Inputs are
+resident in HBM before the timed region.
+
+Prints ONE JSON line (rank 0). With --gpus N>1 (torchrun) each rank trains an
+independent replica on its own GPU ("replicas only" in round 1: the table
+sharding with an RCCL exchange is the next step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
+    """Synthetic ml-20m-shape interactions (ids 1..n, 0 = PAD)."""
+    rng = np.random.default_rng(seed)
+    act = rng.lognormal(0.0, 1.0, n_users)
+    p = 1.0 / np.arange(1, n_items + 1)
+    cdf = np.cumsum(p / p.sum())
+    scale = 144.4
+    for _ in range(3):                                 # dedupe shrinks heavy users: rescale
+        a = np.maximum(np.round(act / act.mean() * scale), 20).astype(np.int64)
+        a = np.minimum(a, n_items // 2)
+        u = np.repeat(np.arange(1, n_users + 1, dtype=np.int64), a)
+        i = np.searchsorted(cdf, rng.random(len(u))).astype(np.int64) + 1
+        key = np.unique(u * (n_items + 1) + i)
+        if abs(len(key) - target) / target < 0.02:
+            break
+        scale *= target / len(key)
+    u, i = key // (n_items + 1), key % (n_items + 1)
+    order = rng.permutation(len(u))                    # file order: not grouped by user
+    return u[order], i[order], n_users + 1, n_items + 1
+
+
+def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020):
+    from recbole_amd.config import Config
+    from recbole_amd.data import data_preparation
+    from recbole_amd.data.dataset import Dataset
+    from recbole_amd.model.general_recommender import BPR
+    from recbole_amd.trainer.fused import FusedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    from recbole_amd.utils import init_seed
+    config = Config(model='BPR', dataset='synthetic-ml20m', config_dict={
+        'data_path': ROOT, 'embedding_size': d, 'training_neg_sample_num': neg,
+        'train_batch_size': batch_rows, 'eval_setting': 'RO_RS,full', 'use_gpu': True,
+        'state': 'ERROR'})
+    config['device'] = dev
+    init_seed(config['seed'], config['reproducibility'])
+    u, i, nU, nI = make_c2(seed)
+    ds = Dataset.from_interactions(config, u, i, nU, nI)
+    train, valid, test = data_preparation(config, ds)
+    model = BPR(config, train).to(dev)
+    opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+    return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train)
+
+
+def cpu_baseline(train, step_obj, d, neg, steps):
+    from oracle import cpu_baseline as cb
+    users = train.dataset.inter_feat['user_id'].cpu().numpy()
+    items = train.dataset.inter_feat['item_id'].cpu().numpy()
+    ptr, cols = train.sampler.used_csr['train']
+    threads = min(16, os.cpu_count() or 1)
+    pps, dt, used = cb.time_bpr_steps(users, items, ptr, cols, train.sampler.random_list,
+                                      step_obj.nU, step_obj.nI, d, step_obj.B, neg, steps=steps,
+                                      warmup=2, threads=threads)
+    return {'value': round(pps, 1), 'unit': 'positives/s', 'cores': used, 'kind': 'port',
+            'sample': f'{steps} C2 steps ({steps * step_obj.B} positives x {neg} negatives) of '
+                      f'the oracle restatement: Python rejection sampler + torch-CPU '
+                      f'nn.Embedding/BPRLoss/dense Adam, {dt:.1f} s'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--cpu-steps', type=int, default=20)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-eval', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    d, neg = 128, 4
+    t_setup = time.time()
+    config, train, test, model, opt, step = build_workload(dev, d=d, neg=neg)
+    setup_s = time.time() - t_setup
+    nb = step.begin_epoch()
+    K, W = args.steps, args.warmup
+    if W + 2 * K > nb:
+        raise SystemExit(f'steps+warmup exceed one epoch ({nb} batches)')
+    for b in range(W):
+        step.launch_batch(b)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step.kernel_events = []
+    for b in range(W, W + K):
+        step.launch_batch(b)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    events = step.kernel_events
+    step.kernel_events = None
+    if dist:
+        t = torch.tensor([elapsed], device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = step.end_epoch(W + K)
+    assert all(np.isfinite(losses)), 'non-finite loss'
+
+    # K5 (dense Adam, the dominant kernel): HIP events around each launch
+    tU = np.mean([e[0].elapsed_time(e[1]) for e in events]) * 1e-3
+    tI = np.mean([e[1].elapsed_time(e[2]) for e in events]) * 1e-3
+    bytesU = 6 * step.nU * d * 4
+    bytesI = 6 * step.nI * d * 4
+    adam_gbs = (bytesU + bytesI) / (tU + tI) / 1e9
+
+    positives = K * step.B * world
+    result = {
+        'metric': 'train positives/sec (+neg) per node',
+        'value': round(positives / elapsed, 1),
+        'unit': 'positives/s',
+        'n_gpus': world,
+        'steps': K,
+        'warmup': W,
+        'ms_per_step': round(elapsed / K * 1e3, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'fp32',
+        'data': 'synthetic (ml-20m-shape, seeded), random xavier-normal init',
+        'config': {'workload': 'C2 BPR-MF ml-20m-shape: 138,494 users x 26,745 items (incl. '
+                               'PAD), ~20M interactions RO_RS 0.8/0.1/0.1, embedding 128, '
+                               '4 uniform negatives, 512 positives (2,048 rows) per step, '
+                               'dense Adam',
+                   'global_batch': step.B * world, 'train_interactions': int(
+                       train.dataset.inter_num), 'parallelism': 'single' if world == 1
+                   else f'replicas{world}'},
+        'roofline': {'kernel': 'K5 adam_sparse_grad (dense Adam over both tables)',
+                     'bound': 'hbm', 'achieved': round(adam_gbs, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(adam_gbs / HBM_PEAK_GBS, 4),
+                     'traffic': None,
+                     'bytes_per_launch': {'user_table': bytesU, 'item_table': bytesI},
+                     'avg_launch_us': {'user_table': round(tU * 1e6, 2),
+                                       'item_table': round(tI * 1e6, 2)}},
+        'setup_s': round(setup_s, 1),
+    }
+    if not args.no_eval and rank == 0:
+        from recbole_amd.trainer.fused import fused_full_sort_eval
+        from recbole_amd.evaluator import TopKEvaluator
+        ev = TopKEvaluator(config, ['recall', 'mrr', 'ndcg', 'hit', 'precision'])
+        fused_full_sort_eval(model, test, ev, user_batch=8192)   # warm
+        torch.cuda.synchronize()
+        e0 = time.perf_counter()
+        fused_full_sort_eval(model, test, ev, user_batch=8192)
+        torch.cuda.synchronize()
+        e_dt = time.perf_counter() - e0
+        n_users = len(test.uid_list)
+        result['eval'] = {'metric': 'full-sort eval users/sec', 'value': round(n_users / e_dt, 1),
+                          'users': n_users, 'seconds': round(e_dt, 4),
+                          'flops_per_user': 2 * step.nI * d}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline(train, step, d, neg, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

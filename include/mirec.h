@@ -1,0 +1,191 @@
+/*
+ * mirec.h — C-ABI of libmirec.so, the MI355X (gfx950) native hot path behind
+ * recbole_amd (a drop-in for ghazalehnt/RecBole's embedding-lookup +
+ * negative-sampling train loop and full-sort evaluator).
+ *
+ * Conventions:
+ *   - every tensor argument is a DEVICE pointer owned by the caller (the PyTorch
+ *     caching allocator); the library never allocates or frees caller memory;
+ *   - scratch comes from a caller buffer sized by the matching *_workspace_size();
+ *   - every call is stream-ordered on `stream` (a hipStream_t passed as void*),
+ *     re-entrant, and does not synchronise the host (graph-capturable);
+ *   - return 0 on success, <0 on error (argument error = -1, HIP error = -(1000+hipError_t));
+ *     mirec_last_error() gives a thread-local message.
+ *
+ * The reference is pure Python/PyTorch: there is no FFI in it. Each entry
+ * below cites the reference function whose arithmetic it replaces; the host
+ * binding (ctypes) lives in recbole_amd/_native.py.
+ */
+#ifndef MIREC_H
+#define MIREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIREC_ABI_VERSION 1
+
+int mirec_abi_version(void);
+const char* mirec_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * K4  Negative sampler: cyclic walk over a pre-shuffled list + rejection.
+ * Replaces AbstractSampler.random_num / sample_by_key_ids
+ *   (recbole/sampler/sampler.py:82-101, 103-154) as driven by
+ *   Sampler.sample_by_user_ids (:246-265) and RepeatableSampler (:341-420).
+ * Bit-exact: out[j*Kb + k] is the j-th negative of key k of a batch of Kb keys;
+ * round 0 takes random_list[(pr + t) mod L] for slot t, and every slot whose
+ * value is in used[key] is refilled IN ASCENDING SLOT ORDER from the
+ * continuing walk until none is left. *pr_dev is advanced (kept mod L) and
+ * persists across calls exactly like `random_pr`.
+ *
+ * Processes n_batches consecutive batches in ONE launch: batch b uses keys
+ * keys[b*batch_keys .. min((b+1)*batch_keys, n_keys)) and writes
+ * out + b*batch_keys*num.  used_ptr[n_key_space+1]/used_cols is a CSR of the
+ * phase's used item ids per key, each row sorted ascending; reject==0 skips
+ * the rejection (RepeatableSampler).  Returns -2 if a key is out of range
+ * (the reference raises ValueError in sample_by_user_ids).
+ * ------------------------------------------------------------------------- */
+size_t mirec_sample_walk_workspace_size(int64_t batch_keys, int64_t num);
+int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t* pr_dev,
+                      const int64_t* keys, int64_t n_keys, int64_t batch_keys,
+                      int64_t n_batches, int64_t num,
+                      const int64_t* used_ptr, const int32_t* used_cols,
+                      int64_t n_key_space, int reject,
+                      int64_t* out, int32_t* status_dev,
+                      void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K1  Row gather (any row width, 16-B vectorised when aligned).
+ * Replaces nn.Embedding forward / index_select (bpr.py:58-72 via
+ *   torch.nn.functional.embedding) and the column gathers of Interaction
+ *   slicing / shuffle (interaction.py:260-276).
+ * out[i, :] = table[idx[i], :];  idx must lie in [0, n_rows).
+ * ------------------------------------------------------------------------- */
+int mirec_gather_rows(const void* table, int64_t n_rows, int64_t row_bytes,
+                      const int64_t* idx, int64_t n, void* out, void* stream);
+int mirec_gather_rows_i32idx(const void* table, int64_t n_rows, int64_t row_bytes,
+                             const int32_t* idx, int64_t n, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K3  Fused BPR forward + backward.
+ * Replaces BPR.calculate_loss (recbole/model/general_recommender/bpr.py:74-83),
+ *   BPRLoss.forward (recbole/model/loss.py:47-49) and their autograd backward.
+ * Pairwise layout of GeneralNegSampleDataLoader (general_dataloader.py:235-241):
+ *   row r = j*B + k pairs (user[k], pos[k], neg[j*B+k]) for j < times.
+ * Per row: x = <u,p> - <u,n>;  loss_r = -log(gamma + sigmoid(x));
+ *   dloss/dx_r = grad_scale * (-(s*(1-s)) / (gamma + s)),  s = sigmoid(x)
+ *   (grad_scale = 1/(B*times) reproduces .mean()).
+ * Outputs (any may be NULL):
+ *   loss_k[B]          = sum_j loss_{j*B+k}       (fixed j order)
+ *   pos_score[B], neg_score[times*B]
+ *   gU[B,d]            = sum_j dx_jk * (p_k - n_jk)      (d loss / d u_k)
+ *   gI[(1+times)*B,d]  rows 0..B-1: (sum_j dx_jk) * u_k  (d loss / d p_k)
+ *                      rows B+r   : -dx_r * u_k          (d loss / d n_r)
+ * d in {32, 64, 128, 256}.
+ * ------------------------------------------------------------------------- */
+int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                          int32_t d, const int64_t* user, const int64_t* pos,
+                          const int64_t* neg, int64_t B, int32_t times,
+                          float gamma, float grad_scale,
+                          float* loss_k, float* pos_score, float* neg_score,
+                          float* gU, float* gI, void* stream);
+
+/* score[r] = <EU[u[r]], EI[i[r]]>  — BPR.predict (bpr.py:85-89), used by the
+ * sampled-evaluation loaders (trainer.py:400-406). d in {32,64,128,256}. */
+int mirec_dot_rows_f32(const float* EU, int64_t nU, const float* EI, int64_t nI, int32_t d,
+                       const int64_t* u, const int64_t* i, int64_t n, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Deterministic reductions used by the trainer loop (trainer.py:157-174).
+ * out[0] = sum(x[0..n)) in a fixed tree order (launch-shape independent).
+ * ------------------------------------------------------------------------- */
+int mirec_sum_f32(const float* x, int64_t n, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K2  Segment sort: group contribution rows by table row id, deterministic.
+ * Replaces the index_add in torch's embedding_dense_backward for
+ *   nn.Embedding(sparse=False) (bpr.py:40-41; trainer.py:170).
+ * Stable sort of (keys[c], c): perm[i] = c sorted by (key, c);
+ *   uniq[u] = distinct keys ascending, seg[u]..seg[u+1] their slice of perm,
+ *   *n_uniq_dev = number of distinct keys. Keys must lie in [0, key_space).
+ * ------------------------------------------------------------------------- */
+size_t mirec_segment_sort_workspace_size(int64_t n, int64_t key_space);
+int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
+                       int32_t* perm, int32_t* uniq, int32_t* seg,
+                       int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
+
+/* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :]  (fixed order)
+ * — the dense-gradient form used by the autograd-compatible path. */
+int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
+                                  const int32_t* uniq, const int32_t* seg,
+                                  const int32_t* n_uniq_dev, int64_t n_max_uniq,
+                                  float* dense, int64_t n_rows, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K5  Dense Adam over every row, with the gradient supplied in compact form.
+ * Replaces optim.Adam.step (trainer.py:109-130, 173; torch optim/adam.py
+ *   _single_tensor_adam) for a table whose dense gradient would be zero
+ *   except on the rows in `uniq` — i.e. exactly the dense Adam the reference
+ *   runs over nn.Embedding(sparse=False) weights, in ONE streaming pass over
+ *   p, m, v (no dense gradient buffer).
+ * g[row] = sum_{i in seg[u]..seg[u+1]} rows[perm[i]]  if row == uniq[u], else 0
+ * (+ dense_grad[row] when dense_grad != NULL; the grouped part may be omitted
+ * with n_uniq_dev == NULL) (+ wd*p).  d in {4,16,32,64,128,256} floats per row
+ * (any tensor whose numel % 4 == 0 can be viewed as [numel/4, 4]).
+ * Per element (torch order):
+ *   m = m + (1-b1)*(g-m);  v = v*b2 + (1-b2)*g*g;
+ *   p = p - step_size * m / (sqrt(v)/bc2_sqrt + eps)
+ * step_consts_dev[2*step_idx_dev[0] + {0,1}] = {step_size, bc2_sqrt} (float),
+ * precomputed on the host in double like torch does; step_idx_dev is a device
+ * counter (advanced by mirec_step_finish) so that a captured graph replays
+ * successive optimizer steps.
+ * ------------------------------------------------------------------------- */
+int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
+                               const float* rows, const int32_t* perm,
+                               const int32_t* uniq, const int32_t* seg,
+                               const int32_t* n_uniq_dev, int64_t n_max_uniq,
+                               const float* dense_grad,
+                               const float* step_consts_dev, const int32_t* step_idx_dev,
+                               double beta1, double beta2, double eps, double weight_decay,
+                               void* stream);
+
+/* End-of-step bookkeeping of Trainer._train_epoch (trainer.py:161-169):
+ * loss_hist[step] = (sum of loss_k[0..n), fixed order) / denom, then
+ * step_idx_dev[0] += 1.  Keeps the per-batch `losses.item()` on the device
+ * (read once per epoch) instead of a host sync per batch. */
+int mirec_step_finish(const float* loss_k, int64_t n, float denom, float* loss_hist,
+                      int32_t* step_idx_dev, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K6  Full-sort scorer + mask + top-K + positive flags, fused (no [n,I] matrix).
+ * Replaces BPR.full_sort_predict (bpr.py:91-96) + Trainer._full_sort_batch_eval
+ *   (trainer.py:328-353: pad column and history set to -inf, positives swapped
+ *   to the front) + TopKEvaluator.collect (evaluators.py:53-76: flip + topk) +
+ *   the pos_idx test of TopKEvaluator._calculate_metrics (:134).
+ * For query q with user vector Uq[q,:]: score(i) = <Uq[q], EI[i]> for
+ *   i in [1, I) not in hist[q]; top_ids[q, 0..K) = the K best items ordered by
+ *   (score desc, item asc); pos_flags[q, r] = top_ids[q, r] in pos[q].
+ *   Slots beyond the number of unmasked items get id -1, score -inf, flag 0.
+ * hist/pos: CSR over queries, column ids sorted ascending per query.
+ * FP32 MFMA (v_mfma_f32_32x32x2_f32), exact f32 products.
+ * d in {32, 64, 128, 256};  1 <= K <= 50.
+ * ------------------------------------------------------------------------- */
+int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,
+                            int32_t d, const int64_t* hist_ptr, const int32_t* hist_cols,
+                            const int64_t* pos_ptr, const int32_t* pos_cols, int32_t K,
+                            float* top_scores, int32_t* top_ids, uint8_t* pos_flags,
+                            void* stream);
+
+/* Plain score matrix S[q, i] = <Uq[q], EI[i]> (FP32 MFMA) for the
+ * full_sort_predict API contract (flat [nq*I] scores, bpr.py:91-96). */
+int mirec_score_matrix_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,
+                           int32_t d, float* S, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIREC_H */

@@ -1,0 +1,93 @@
+"""ctypes binding of libmirec.so (the C-ABI declared in include/mirec.h).
+
+The library is loaded AFTER ``import torch`` so that its NEEDED
+``libamdhip64.so.7`` resolves to the HIP runtime torch already mapped (same
+soname): one HIP runtime per process, and ``torch.cuda.current_stream().cuda_stream``
+is a valid ``hipStream_t`` for every entry point.
+
+There is no fallback: if the shared library is missing the import of any op
+raises, so a GPU run can never silently take a CPU / PyTorch path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p, c_char_p
+
+import torch  # noqa: F401  (must be imported before the library is dlopen'ed)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MIREC_LIB", os.path.join(_HERE, "_lib", "libmirec.so"))
+
+# Every symbol include/mirec.h declares: name -> (restype, argtypes)
+_P = c_void_p
+SIGNATURES = {
+    "mirec_abi_version": (c_int, []),
+    "mirec_last_error": (c_char_p, []),
+    "mirec_sample_walk_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "mirec_sample_walk": (c_int, [_P, c_int64, _P, _P, c_int64, c_int64, c_int64, c_int64,
+                                  _P, _P, c_int64, c_int, _P, _P, _P, c_size_t, _P]),
+    "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
+    "mirec_gather_rows_i32idx": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
+    "mirec_bpr_fwd_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
+                                      c_int32, c_float, c_float, _P, _P, _P, _P, _P, _P]),
+    "mirec_dot_rows_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, c_int64, _P, _P]),
+    "mirec_sum_f32": (c_int, [_P, c_int64, _P, _P]),
+    "mirec_segment_sort_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "mirec_segment_sort": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
+                                              c_int64, _P]),
+    "mirec_adam_sparse_grad_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, _P, _P,
+                                           c_int64, _P, _P, _P, c_double, c_double, c_double,
+                                           c_double, _P]),
+    "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
+    "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
+                                        c_int32, _P, _P, _P, _P]),
+    "mirec_score_matrix_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P]),
+}
+
+ABI_VERSION = 1
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Return the loaded library (loads it on first use); raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"libmirec.so not found at {LIB_PATH}: build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+    handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if handle.mirec_abi_version() != ABI_VERSION:
+        raise NativeError("libmirec.so ABI version mismatch; rebuild it")
+    _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().mirec_last_error()
+        raise NativeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

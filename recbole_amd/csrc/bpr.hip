@@ -1,0 +1,220 @@
+// K3 — fused BPR forward + backward, one wavefront per positive.
+//
+// Restates BPR.calculate_loss (recbole/model/general_recommender/bpr.py:74-83)
+// and BPRLoss (recbole/model/loss.py:43-49) plus the autograd backward torch
+// runs for them, on the pairwise layout of GeneralNegSampleDataLoader
+// (general_dataloader.py:235-241, Interaction.repeat interaction.py:189-217):
+// row r = j*B + k carries (user[k], pos[k], neg[r]).  All `times` rows of one
+// positive share u_k and p_k, so a wave loads them ONCE and streams only the
+// negatives: (2 + times) rows per positive instead of 3*times.
+//
+// Backward follows torch's op order: mean -> neg -> log -> add -> sigmoid:
+//   g = -(1/R) / (gamma + s);  dx = g * (1 - s) * s;  d pos = dx, d neg = -dx
+//   du = dx*p - dx*n, dp = dx*u, dn = -dx*u   (summed over the rows of a key
+//   by the segment reduction, K2/K5).
+#include "common.h"
+
+namespace mirec {
+
+template <int D>
+struct RowVec {
+  static constexpr int E = D >= 64 ? D / 64 : 1;   // floats per lane
+  static constexpr int ACT = D >= 64 ? 64 : D;     // active lanes
+  float x[E];
+};
+
+template <int D>
+__device__ __forceinline__ void load_row(const float* __restrict__ base, int lane, RowVec<D>& r) {
+  constexpr int E = RowVec<D>::E;
+  const float* p = base + lane * E;
+  if constexpr (E == 4) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    r.x[0] = v.x; r.x[1] = v.y; r.x[2] = v.z; r.x[3] = v.w;
+  } else if constexpr (E == 2) {
+    float2 v = *reinterpret_cast<const float2*>(p);
+    r.x[0] = v.x; r.x[1] = v.y;
+  } else {
+    r.x[0] = p[0];
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void store_row(float* __restrict__ base, int lane, const float* x) {
+  constexpr int E = RowVec<D>::E;
+  float* p = base + lane * E;
+  if constexpr (E == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  } else if constexpr (E == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
+  } else {
+    p[0] = x[0];
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
+    const float* __restrict__ EU, int64_t nU, const float* __restrict__ EI, int64_t nI,
+    const int64_t* __restrict__ user, const int64_t* __restrict__ pos,
+    const int64_t* __restrict__ neg, int64_t B, int times, float gamma, float grad_scale,
+    float* __restrict__ loss_k, float* __restrict__ pos_score, float* __restrict__ neg_score,
+    float* __restrict__ gU, float* __restrict__ gI) {
+  constexpr int E = RowVec<D>::E;
+  constexpr int ACT = RowVec<D>::ACT;
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (k >= B) return;  // whole wave exits together
+  const bool act = lane < ACT;
+
+  int64_t uid = user[k], pid = pos[k];
+  uid = uid < 0 ? 0 : (uid >= nU ? nU - 1 : uid);
+  pid = pid < 0 ? 0 : (pid >= nI ? nI - 1 : pid);
+  RowVec<D> u, p;
+  if (act) {
+    load_row<D>(EU + uid * D, lane, u);
+    load_row<D>(EI + pid * D, lane, p);
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) { u.x[e] = 0.f; p.x[e] = 0.f; }
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) part += u.x[e] * p.x[e];
+  const float sp = wave_sum(part);
+
+  float gu[E], gp[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { gu[e] = 0.f; gp[e] = 0.f; }
+  float lsum = 0.f;
+  const float ng = -grad_scale;
+
+  // software-pipeline the negative rows: load row j+1 while reducing row j
+  RowVec<D> n_cur, n_nxt;
+  auto load_neg = [&](int j, RowVec<D>& dst) {
+    int64_t nid = neg[(int64_t)j * B + k];
+    nid = nid < 0 ? 0 : (nid >= nI ? nI - 1 : nid);
+    if (act) load_row<D>(EI + nid * D, lane, dst);
+    else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) dst.x[e] = 0.f;
+    }
+  };
+  if (times > 0) load_neg(0, n_cur);
+  for (int j = 0; j < times; ++j) {
+    if (j + 1 < times) load_neg(j + 1, n_nxt);
+    float pn = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) pn += u.x[e] * n_cur.x[e];
+    const float sn = wave_sum(pn);
+    const float x = sp - sn;
+    const float s = 1.f / (1.f + expf(-x));
+    const float gs = gamma + s;
+    lsum += -logf(gs);
+    const float g = ng / gs;
+    const float dx = (g * (1.f - s)) * s;
+    float gn[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      gu[e] += dx * p.x[e] - dx * n_cur.x[e];
+      gp[e] += dx * u.x[e];
+      gn[e] = -dx * u.x[e];
+    }
+    const int64_t r = (int64_t)j * B + k;
+    if (gI && act) store_row<D>(gI + (B + r) * D, lane, gn);
+    if (neg_score && lane == 0) neg_score[r] = sn;
+    n_cur = n_nxt;
+  }
+  if (act) {
+    if (gU) store_row<D>(gU + k * D, lane, gu);
+    if (gI) store_row<D>(gI + k * D, lane, gp);
+  }
+  if (lane == 0) {
+    if (loss_k) loss_k[k] = lsum;
+    if (pos_score) pos_score[k] = sp;
+  }
+}
+
+// score[r] = <EU[u[r]], EI[i[r]]> — BPR.predict (bpr.py:85-89) and the
+// sampled-evaluation scorer; one wave per row.
+template <int D>
+__global__ __launch_bounds__(256) void dot_rows_kernel(const float* __restrict__ EU, int64_t nU,
+                                                       const float* __restrict__ EI, int64_t nI,
+                                                       const int64_t* __restrict__ u,
+                                                       const int64_t* __restrict__ it, int64_t n,
+                                                       float* __restrict__ out) {
+  constexpr int E = RowVec<D>::E;
+  constexpr int ACT = RowVec<D>::ACT;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  int64_t a = u[r], b = it[r];
+  a = a < 0 ? 0 : (a >= nU ? nU - 1 : a);
+  b = b < 0 ? 0 : (b >= nI ? nI - 1 : b);
+  float part = 0.f;
+  if (lane < ACT) {
+    RowVec<D> x, y;
+    load_row<D>(EU + a * D, lane, x);
+    load_row<D>(EI + b * D, lane, y);
+#pragma unroll
+    for (int e = 0; e < E; ++e) part += x.x[e] * y.x[e];
+  }
+  const float s = wave_sum(part);
+  if (lane == 0) out[r] = s;
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_dot_rows_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                                  int32_t d, const int64_t* u, const int64_t* i, int64_t n,
+                                  float* out, void* stream) {
+  if (n == 0) return 0;
+  if (!EU || !EI || !u || !i || !out || n < 0) {
+    set_error("mirec_dot_rows_f32: bad arguments");
+    return -1;
+  }
+  const dim3 grd((unsigned)((n + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  switch (d) {
+    case 32: hipLaunchKernelGGL(dot_rows_kernel<32>, grd, dim3(256), 0, st, EU, nU, EI, nI, u, i, n, out); break;
+    case 64: hipLaunchKernelGGL(dot_rows_kernel<64>, grd, dim3(256), 0, st, EU, nU, EI, nI, u, i, n, out); break;
+    case 128: hipLaunchKernelGGL(dot_rows_kernel<128>, grd, dim3(256), 0, st, EU, nU, EI, nI, u, i, n, out); break;
+    case 256: hipLaunchKernelGGL(dot_rows_kernel<256>, grd, dim3(256), 0, st, EU, nU, EI, nI, u, i, n, out); break;
+    default:
+      set_error("mirec_dot_rows_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+  return launch_status("mirec_dot_rows_f32");
+}
+
+extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                                     int32_t d, const int64_t* user, const int64_t* pos,
+                                     const int64_t* neg, int64_t B, int32_t times, float gamma,
+                                     float grad_scale, float* loss_k, float* pos_score,
+                                     float* neg_score, float* gU, float* gI, void* stream) {
+  if (B == 0) return 0;
+  if (!EU || !EI || !user || !pos || (times > 0 && !neg) || B < 0 || times < 0 || nU <= 0 ||
+      nI <= 0) {
+    set_error("mirec_bpr_fwd_bwd_f32: bad arguments");
+    return -1;
+  }
+  const dim3 blk(256);
+  const dim3 grd((unsigned)((B + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_BPR_CASE(DD)                                                                    \
+  case DD:                                                                                    \
+    hipLaunchKernelGGL(bpr_fwd_bwd_kernel<DD>, grd, blk, 0, st, EU, nU, EI, nI, user, pos,    \
+                       neg, B, times, gamma, grad_scale, loss_k, pos_score, neg_score, gU, gI); \
+    break;
+  switch (d) {
+    MIREC_BPR_CASE(32)
+    MIREC_BPR_CASE(64)
+    MIREC_BPR_CASE(128)
+    MIREC_BPR_CASE(256)
+    default:
+      set_error("mirec_bpr_fwd_bwd_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_BPR_CASE
+  return launch_status("mirec_bpr_fwd_bwd_f32");
+}

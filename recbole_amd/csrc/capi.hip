@@ -1,0 +1,73 @@
+// Error state, version and the small reduction kernels of the trainer loop.
+#include <stdarg.h>
+#include "common.h"
+
+namespace mirec {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// Fixed-order sum: 1024 threads, thread t sums x[t], x[t+1024], ... in order,
+// then a fixed binary tree over the 1024 partials. Independent of timing.
+__device__ __forceinline__ float block_fixed_sum(const float* __restrict__ x, int64_t n,
+                                                 float* lds /*1024*/) {
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) acc += x[i];
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) lds[threadIdx.x] += lds[threadIdx.x + s];
+    __syncthreads();
+  }
+  return lds[0];
+}
+
+__global__ __launch_bounds__(1024) void sum_kernel(const float* __restrict__ x, int64_t n,
+                                                   float* __restrict__ out) {
+  __shared__ float lds[1024];
+  float s = block_fixed_sum(x, n, lds);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+__global__ __launch_bounds__(1024) void step_finish_kernel(const float* __restrict__ loss_k,
+                                                           int64_t n, float denom,
+                                                           float* __restrict__ loss_hist,
+                                                           int32_t* __restrict__ step_idx) {
+  __shared__ float lds[1024];
+  float s = block_fixed_sum(loss_k, n, lds);
+  if (threadIdx.x == 0) {
+    int32_t st = step_idx[0];
+    if (loss_hist) loss_hist[st] = s / denom;
+    step_idx[0] = st + 1;
+  }
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_abi_version(void) { return MIREC_ABI_VERSION; }
+extern "C" const char* mirec_last_error(void) { return mirec::g_err; }
+
+extern "C" int mirec_sum_f32(const float* x, int64_t n, float* out, void* stream) {
+  if (!out || n < 0 || (n > 0 && !x)) { set_error("mirec_sum_f32: bad arguments"); return -1; }
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, n, out);
+  return launch_status("mirec_sum_f32");
+}
+
+extern "C" int mirec_step_finish(const float* loss_k, int64_t n, float denom, float* loss_hist,
+                                 int32_t* step_idx_dev, void* stream) {
+  if (!step_idx_dev || n < 0 || (n > 0 && !loss_k)) {
+    set_error("mirec_step_finish: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, loss_k, n,
+                     denom, loss_hist, step_idx_dev);
+  return launch_status("mirec_step_finish");
+}

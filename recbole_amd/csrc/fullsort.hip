@@ -1,0 +1,277 @@
+// K6 — full-sort evaluator: user x all-items scores on FP32 MFMA, fused with
+// the pad/history mask, a per-user top-K and the positive test, so the
+// [users x items] score matrix never exists in HBM.
+//
+// Restates, for one batch of users:
+//   BPR.full_sort_predict          scores = U[u] @ E_I^T       (bpr.py:91-96)
+//   Trainer._full_sort_batch_eval  [:,0] = -inf; [history] = -inf;
+//                                  positives swapped into columns [0,pos_len)
+//                                                              (trainer.py:328-353)
+//   TopKEvaluator.collect          flip(-1) + topk(max(topk))  (evaluators.py:53-76)
+//   _calculate_metrics             pos_idx = topk_idx >= I - pos_len (:134)
+// The swap + flip only relabel columns so that "index >= I - pos_len" means
+// "is a positive": per item the (score, is_positive) pair is unchanged, so the
+// result is the K best unmasked items and, per rank, whether it is a positive.
+// Ties are broken by (score desc, item id asc); torch.topk leaves tie order
+// unspecified, so tied scores are the one place results may legitimately differ.
+//
+// Tiling (gfx950, wave64): a workgroup = 4 waves = 128 users. Each wave keeps
+// its 32 users' embedding in registers as the MFMA B operand
+// (v_mfma_f32_32x32x2_f32: lane l holds B[k][j = l&31]) and sweeps all items in
+// tiles of 32 staged once per workgroup in LDS (rows padded to D+2 floats so the
+// ds_read_b64 A-fragment reads are conflict-free). The 32x32 accumulator puts one
+// USER per lane column and 16 ITEMS per lane, so each lane keeps a private
+// register top-K for its user over its half of the items (no cross-lane traffic in
+// the sweep); the two halves merge at the end. The k order inside the dot product
+// is permuted (k = 4*(s>>1) + 2h + (s&1)) so both operands load as float2; the
+// MFMA result is an exact-f32 fma chain in that order.
+#include "common.h"
+
+namespace mirec {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kFsThreads = 256;
+
+template <int KC>
+__device__ __forceinline__ void topk_insert(float (&ts)[KC], int (&ti)[KC], float v, int id) {
+  // "better" = (score desc, id asc); ts/ti sorted best-first
+#pragma unroll
+  for (int t = KC - 1; t > 0; --t) {
+    const bool up = (v > ts[t - 1]) || (v == ts[t - 1] && id < ti[t - 1]);
+    const bool here = (v > ts[t]) || (v == ts[t] && id < ti[t]);
+    const float ns = up ? ts[t - 1] : (here ? v : ts[t]);
+    const int ni = up ? ti[t - 1] : (here ? id : ti[t]);
+    ts[t] = ns;
+    ti[t] = ni;
+  }
+  const bool h0 = (v > ts[0]) || (v == ts[0] && id < ti[0]);
+  ts[0] = h0 ? v : ts[0];
+  ti[0] = h0 ? id : ti[0];
+}
+
+// Stage items [base, base+32) of EI into LDS rows of LDR floats (zero past I).
+template <int D>
+__device__ __forceinline__ void stage_tile(const float* __restrict__ EI, int64_t I, int64_t base,
+                                           float* __restrict__ tile) {
+  constexpr int LDR = D + 2;
+  constexpr int V4 = D / 4;
+  const float4* __restrict__ E4 = reinterpret_cast<const float4*>(EI);
+#pragma unroll
+  for (int f = threadIdx.x; f < 32 * V4; f += kFsThreads) {
+    const int row = f / V4;
+    const int c4 = f - row * V4;
+    const int64_t item = base + row;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (item < I) x = E4[item * V4 + c4];
+    float2* dst = reinterpret_cast<float2*>(tile + row * LDR + 4 * c4);
+    dst[0] = make_float2(x.x, x.y);
+    dst[1] = make_float2(x.z, x.w);
+  }
+}
+
+// lane (j = l&31, h = l>>5) holds user row q's elements in the permuted k order
+template <int D>
+__device__ __forceinline__ void load_user_operand(const float* __restrict__ Uq, int64_t q, bool qv,
+                                                  int h, float (&ub)[D / 2]) {
+#pragma unroll
+  for (int s2 = 0; s2 < D / 4; ++s2) {
+    float2 x = make_float2(0.f, 0.f);
+    if (qv) x = *reinterpret_cast<const float2*>(Uq + q * D + 4 * s2 + 2 * h);
+    ub[2 * s2] = x.x;
+    ub[2 * s2 + 1] = x.y;
+  }
+}
+
+template <int D, int KC>
+__global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
+    const float* __restrict__ Uq, int64_t nq, const float* __restrict__ EI, int64_t I,
+    const int64_t* __restrict__ hist_ptr, const int32_t* __restrict__ hist_cols,
+    const int64_t* __restrict__ pos_ptr, const int32_t* __restrict__ pos_cols, int K,
+    float* __restrict__ top_scores, int32_t* __restrict__ top_ids,
+    uint8_t* __restrict__ pos_flags) {
+  constexpr int LDR = D + 2;
+  __shared__ __attribute__((aligned(16))) float tile[32 * LDR];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int j = lane & 31;
+  const int h = lane >> 5;
+  const int64_t q = ((int64_t)blockIdx.x * 4 + w) * 32 + j;
+  const bool qv = q < nq;
+
+  float ub[D / 2];
+  load_user_operand<D>(Uq, q, qv, h, ub);
+
+  float ts[KC];
+  int ti[KC];
+#pragma unroll
+  for (int t = 0; t < KC; ++t) { ts[t] = -INFINITY; ti[t] = -1; }
+  float thr = -INFINITY;
+  int64_t hcur = 0, hend = 0;
+  if (qv && hist_ptr) { hcur = hist_ptr[q]; hend = hist_ptr[q + 1]; }
+
+  const int64_t ntile = (I + 31) / 32;
+  for (int64_t t = 0; t < ntile; ++t) {
+    const int64_t base = t * 32;
+    __syncthreads();
+    stage_tile<D>(EI, I, base, tile);
+    __syncthreads();
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float* arow = tile + j * LDR + 2 * h;
+#pragma unroll
+    for (int s2 = 0; s2 < D / 4; ++s2) {
+      const float2 a = *reinterpret_cast<const float2*>(arow + 4 * s2);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, ub[2 * s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, ub[2 * s2 + 1], acc, 0, 0, 0);
+    }
+    // C[item row][user col]: rows (r&3) + 8*(r>>2) + 4h, increasing in r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t item = base + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float sc = acc[r];
+      const bool cand = qv && item < I && item != 0 && sc > thr;
+      if (cand) {
+        while (hcur < hend && (int64_t)hist_cols[hcur] < item) ++hcur;
+        const bool masked = hcur < hend && (int64_t)hist_cols[hcur] == item;
+        if (!masked) {
+          topk_insert<KC>(ts, ti, sc, (int)item);
+          thr = ts[KC - 1];
+        }
+      }
+    }
+  }
+
+  // merge the two item halves of each user: lane j takes lane j+32's list
+#pragma unroll
+  for (int t = 0; t < KC; ++t) {
+    const float os = __shfl(ts[t], j + 32, 64);
+    const int oi = __shfl(ti[t], j + 32, 64);
+    if (h == 0) topk_insert<KC>(ts, ti, os, oi);
+  }
+  if (h == 0 && qv) {
+    const int64_t p0 = pos_ptr ? pos_ptr[q] : 0;
+    const int64_t p1 = pos_ptr ? pos_ptr[q + 1] : 0;
+#pragma unroll
+    for (int t = 0; t < KC; ++t) {
+      if (t < K) {
+        const int64_t o = q * K + t;
+        if (top_scores) top_scores[o] = ts[t];
+        if (top_ids) top_ids[o] = ti[t];
+        if (pos_flags)
+          pos_flags[o] = (ti[t] >= 0 && sorted_contains(pos_cols, p0, p1, ti[t])) ? 1 : 0;
+      }
+    }
+  }
+}
+
+// Plain score matrix S[q, i] (compat path for full_sort_predict): A = users in
+// registers, B = item tile from LDS, so the accumulator has the ITEM on the lane
+// and each store instruction writes 128 contiguous bytes of a score row.
+template <int D>
+__global__ __launch_bounds__(kFsThreads) void score_matrix_kernel(const float* __restrict__ Uq,
+                                                                  int64_t nq,
+                                                                  const float* __restrict__ EI,
+                                                                  int64_t I, float* __restrict__ S) {
+  constexpr int LDR = D + 2;
+  __shared__ __attribute__((aligned(16))) float tile[32 * LDR];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int j = lane & 31;
+  const int h = lane >> 5;
+  const int64_t qb = ((int64_t)blockIdx.x * 4 + w) * 32;
+  const int64_t q = qb + j;
+  float ub[D / 2];
+  load_user_operand<D>(Uq, q, q < nq, h, ub);
+  const int64_t ntile = (I + 31) / 32;
+  for (int64_t t = 0; t < ntile; ++t) {
+    const int64_t base = t * 32;
+    __syncthreads();
+    stage_tile<D>(EI, I, base, tile);
+    __syncthreads();
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float* brow = tile + j * LDR + 2 * h;
+#pragma unroll
+    for (int s2 = 0; s2 < D / 4; ++s2) {
+      const float2 b = *reinterpret_cast<const float2*>(brow + 4 * s2);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ub[2 * s2], b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ub[2 * s2 + 1], b.y, acc, 0, 0, 0);
+    }
+    const int64_t item = base + j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t uq = qb + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (uq < nq && item < I) S[uq * I + item] = acc[r];
+    }
+  }
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,
+                                       int32_t d, const int64_t* hist_ptr,
+                                       const int32_t* hist_cols, const int64_t* pos_ptr,
+                                       const int32_t* pos_cols, int32_t K, float* top_scores,
+                                       int32_t* top_ids, uint8_t* pos_flags, void* stream) {
+  if (nq == 0) return 0;
+  if (!Uq || !EI || nq < 0 || I <= 0 || K < 1 || (hist_ptr && !hist_cols) ||
+      (pos_ptr && !pos_cols) || (pos_flags && !pos_ptr)) {
+    set_error("mirec_fullsort_topk_f32: bad arguments");
+    return -1;
+  }
+  if (I > INT32_MAX) {
+    set_error("mirec_fullsort_topk_f32: item count exceeds int32");
+    return -1;
+  }
+  const dim3 grd((unsigned)((nq + 127) / 128));
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_FS(DD, KK)                                                                      \
+  hipLaunchKernelGGL((fullsort_topk_kernel<DD, KK>), grd, dim3(kFsThreads), 0, st, Uq, nq, EI, \
+                     I, hist_ptr, hist_cols, pos_ptr, pos_cols, K, top_scores, top_ids,        \
+                     pos_flags)
+#define MIREC_FS_D(DD)                                 \
+  case DD:                                             \
+    if (K <= 10) MIREC_FS(DD, 10);                     \
+    else if (K <= 20) MIREC_FS(DD, 20);                \
+    else if (K <= 50) MIREC_FS(DD, 50);                \
+    else { set_error("mirec_fullsort_topk_f32: K=%d > 50", K); return -1; } \
+    break;
+  switch (d) {
+    MIREC_FS_D(32)
+    MIREC_FS_D(64)
+    MIREC_FS_D(128)
+    MIREC_FS_D(256)
+    default:
+      set_error("mirec_fullsort_topk_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_FS_D
+#undef MIREC_FS
+  return launch_status("mirec_fullsort_topk_f32");
+}
+
+extern "C" int mirec_score_matrix_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,
+                                      int32_t d, float* S, void* stream) {
+  if (nq == 0) return 0;
+  if (!Uq || !EI || !S || nq < 0 || I <= 0) {
+    set_error("mirec_score_matrix_f32: bad arguments");
+    return -1;
+  }
+  const dim3 grd((unsigned)((nq + 127) / 128));
+  hipStream_t st = (hipStream_t)stream;
+  switch (d) {
+    case 32: hipLaunchKernelGGL(score_matrix_kernel<32>, grd, dim3(kFsThreads), 0, st, Uq, nq, EI, I, S); break;
+    case 64: hipLaunchKernelGGL(score_matrix_kernel<64>, grd, dim3(kFsThreads), 0, st, Uq, nq, EI, I, S); break;
+    case 128: hipLaunchKernelGGL(score_matrix_kernel<128>, grd, dim3(kFsThreads), 0, st, Uq, nq, EI, I, S); break;
+    case 256: hipLaunchKernelGGL(score_matrix_kernel<256>, grd, dim3(kFsThreads), 0, st, Uq, nq, EI, I, S); break;
+    default:
+      set_error("mirec_score_matrix_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+  return launch_status("mirec_score_matrix_f32");
+}

@@ -1,0 +1,80 @@
+// K1 — row gather out[i,:] = table[idx[i],:] for any row width.
+// Replaces nn.Embedding forward (torch embedding = index_select of rows,
+// bpr.py:58-72) and the column gathers of Interaction slicing / shuffle
+// (recbole/data/interaction.py:260-276). Vectorised to 16 B per lane whenever
+// the row width and both base pointers allow it, so one wave moves 1 KiB per
+// instruction; consecutive lanes walk one row, so each row is read as whole
+// 64-B segments.
+#include "common.h"
+
+namespace mirec {
+
+template <typename V, typename I>
+__global__ __launch_bounds__(256) void gather_kernel(const V* __restrict__ table, int64_t n_rows,
+                                                     int64_t vpr, const I* __restrict__ idx,
+                                                     int64_t n, V* __restrict__ out) {
+  const int64_t total = n * vpr;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / vpr;
+    const int64_t c = e - i * vpr;
+    int64_t r = (int64_t)idx[i];
+    // out-of-range ids are a caller bug; clamp so the kernel never faults
+    r = r < 0 ? 0 : (r >= n_rows ? n_rows - 1 : r);
+    out[e] = table[r * vpr + c];
+  }
+}
+
+template <typename I>
+static int gather_impl(const void* table, int64_t n_rows, int64_t row_bytes, const I* idx,
+                       int64_t n, void* out, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!table || !idx || !out || n < 0 || row_bytes <= 0 || n_rows <= 0) {
+    set_error("mirec_gather_rows: bad arguments");
+    return -1;
+  }
+  const uintptr_t al = (uintptr_t)table | (uintptr_t)out | (uintptr_t)row_bytes;
+  int64_t total;
+  auto grid = [&](int64_t tot) {
+    int64_t g = (tot + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g < 1) g = 1;
+    return dim3((unsigned)g);
+  };
+  if ((al & 15) == 0) {
+    const int64_t vpr = row_bytes / 16;
+    total = n * vpr;
+    hipLaunchKernelGGL((gather_kernel<int4, I>), grid(total), dim3(256), 0, st,
+                       (const int4*)table, n_rows, vpr, idx, n, (int4*)out);
+  } else if ((al & 7) == 0) {
+    const int64_t vpr = row_bytes / 8;
+    total = n * vpr;
+    hipLaunchKernelGGL((gather_kernel<int2, I>), grid(total), dim3(256), 0, st,
+                       (const int2*)table, n_rows, vpr, idx, n, (int2*)out);
+  } else if ((al & 3) == 0) {
+    const int64_t vpr = row_bytes / 4;
+    total = n * vpr;
+    hipLaunchKernelGGL((gather_kernel<int, I>), grid(total), dim3(256), 0, st,
+                       (const int*)table, n_rows, vpr, idx, n, (int*)out);
+  } else {
+    const int64_t vpr = row_bytes;
+    total = n * vpr;
+    hipLaunchKernelGGL((gather_kernel<char, I>), grid(total), dim3(256), 0, st,
+                       (const char*)table, n_rows, vpr, idx, n, (char*)out);
+  }
+  return launch_status("mirec_gather_rows");
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_gather_rows(const void* table, int64_t n_rows, int64_t row_bytes,
+                                 const int64_t* idx, int64_t n, void* out, void* stream) {
+  return gather_impl<int64_t>(table, n_rows, row_bytes, idx, n, out, (hipStream_t)stream);
+}
+
+extern "C" int mirec_gather_rows_i32idx(const void* table, int64_t n_rows, int64_t row_bytes,
+                                        const int32_t* idx, int64_t n, void* out, void* stream) {
+  return gather_impl<int32_t>(table, n_rows, row_bytes, idx, n, out, (hipStream_t)stream);
+}

@@ -1,0 +1,220 @@
+// K2 — deterministic grouping of gradient contributions by table row.
+//
+// torch's nn.Embedding(sparse=False) backward (bpr.py:40-41) zero-fills a dense
+// [n_rows, d] gradient and index_adds every looked-up row into it.  Here the
+// contributions are grouped instead: a stable LSD radix sort of (row id,
+// contribution index) gives, per distinct row, the ordered list of its
+// contributions, which K5 (adam.hip) or the dense scatter below sums in that
+// fixed order — bitwise reproducible, no float atomics.
+//
+// The sort runs in ONE workgroup (1024 lanes): n is a training batch's
+// contribution count (C2: 512 user keys, 2,560 item keys), far too small to
+// fill the chip, and the sort depends only on ids, so the trainer runs it
+// ahead of the model step on a side stream.  Up to kLdsMax keys the whole
+// sort lives in LDS (1-bit stable splits, one block scan per bit); larger n
+// uses the same algorithm over global ping-pong buffers.
+#include "common.h"
+
+namespace mirec {
+
+constexpr int kSortThreads = 1024;
+constexpr int kLdsMax = 8192;
+constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
+
+__device__ __forceinline__ int nbits_for(int64_t key_space) {
+  int b = 0;
+  while (b < 31 && ((int64_t)1 << b) < key_space) ++b;
+  return b;
+}
+
+// uniq/seg from sorted keys held in `skey` (LDS or global), blocked arrangement
+template <typename KeyPtr>
+__device__ void emit_segments(KeyPtr skey, int n, int32_t* __restrict__ uniq,
+                              int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq,
+                              int* scan_lds) {
+  int base_u = 0;
+  for (int c0 = 0; c0 < n; c0 += kSortThreads) {
+    const int i = c0 + threadIdx.x;
+    int f = 0;
+    int32_t kv = 0;
+    if (i < n) {
+      kv = skey[i];
+      f = (i == 0 || skey[i - 1] != kv) ? 1 : 0;
+    }
+    int tot;
+    const int ex = block_exclusive_scan(f, scan_lds, &tot);
+    if (f) {
+      uniq[base_u + ex] = kv;
+      seg[base_u + ex] = i;
+    }
+    base_u += tot;
+  }
+  if (threadIdx.x == 0) {
+    seg[base_u] = n;
+    n_uniq[0] = base_u;
+  }
+}
+
+__global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
+    const int64_t* __restrict__ keys, int n, int nbits, int32_t* __restrict__ perm,
+    int32_t* __restrict__ uniq, int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq) {
+  __shared__ int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
+  __shared__ int scan_lds[kSortThreads / 64 + 1];
+  for (int i = threadIdx.x; i < n; i += kSortThreads) {
+    kA[i] = (int32_t)keys[i];
+    vA[i] = i;
+  }
+  __syncthreads();
+  int32_t *ks = kA, *vs = vA, *kd = kB, *vd = vB;
+  const int ipt = (n + kSortThreads - 1) / kSortThreads;
+  const int lo = threadIdx.x * ipt;
+  const int hi = min(n, lo + ipt);
+  for (int bit = 0; bit < nbits; ++bit) {
+    int z = 0;
+    for (int i = lo; i < hi; ++i) z += ((ks[i] >> bit) & 1) ? 0 : 1;
+    int Z;
+    const int ez = block_exclusive_scan(z, scan_lds, &Z);
+    int zb = ez;  // zeros before element i
+    for (int i = lo; i < hi; ++i) {
+      const int32_t kv = ks[i];
+      const int one = (kv >> bit) & 1;
+      const int dst = one ? (Z + (i - zb)) : zb;
+      kd[dst] = kv;
+      vd[dst] = vs[i];
+      zb += 1 - one;
+    }
+    __syncthreads();
+    int32_t* t;
+    t = ks; ks = kd; kd = t;
+    t = vs; vs = vd; vd = t;
+  }
+  for (int i = threadIdx.x; i < n; i += kSortThreads) perm[i] = vs[i];
+  emit_segments(ks, n, uniq, seg, n_uniq, scan_lds);
+}
+
+// Same algorithm, global ping-pong buffers, processed in chunks of
+// kSortThreads*kIpt with running offsets (any n up to INT32_MAX).
+__global__ __launch_bounds__(kSortThreads) void segsort_global_kernel(
+    const int64_t* __restrict__ keys, int n, int nbits, int32_t* __restrict__ perm,
+    int32_t* __restrict__ uniq, int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq,
+    int32_t* __restrict__ kA, int32_t* __restrict__ vA, int32_t* __restrict__ kB,
+    int32_t* __restrict__ vB) {
+  __shared__ int scan_lds[kSortThreads / 64 + 1];
+  for (int i = threadIdx.x; i < n; i += kSortThreads) {
+    kA[i] = (int32_t)keys[i];
+    vA[i] = i;
+  }
+  __syncthreads();
+  int32_t *ks = kA, *vs = vA, *kd = kB, *vd = vB;
+  constexpr int CH = kSortThreads * kIpt;
+  for (int bit = 0; bit < nbits; ++bit) {
+    // total zeros
+    int zloc = 0;
+    for (int i = threadIdx.x; i < n; i += kSortThreads) zloc += ((ks[i] >> bit) & 1) ? 0 : 1;
+    int Z;
+    (void)block_exclusive_scan(zloc, scan_lds, &Z);
+    int zrun = 0;  // zeros in earlier chunks
+    for (int c0 = 0; c0 < n; c0 += CH) {
+      const int lo = c0 + threadIdx.x * kIpt;
+      const int hi = min(n, lo + kIpt);
+      int z = 0;
+      for (int i = lo; i < hi; ++i) z += ((ks[i] >> bit) & 1) ? 0 : 1;
+      int zc;
+      const int ez = block_exclusive_scan(z, scan_lds, &zc);
+      int zb = zrun + ez;
+      for (int i = lo; i < hi; ++i) {
+        const int32_t kv = ks[i];
+        const int one = (kv >> bit) & 1;
+        const int dst = one ? (Z + (i - zb)) : zb;
+        kd[dst] = kv;
+        vd[dst] = vs[i];
+        zb += 1 - one;
+      }
+      zrun += zc;
+    }
+    __threadfence_block();
+    __syncthreads();
+    int32_t* t;
+    t = ks; ks = kd; kd = t;
+    t = vs; vs = vd; vd = t;
+  }
+  for (int i = threadIdx.x; i < n; i += kSortThreads) perm[i] = vs[i];
+  __syncthreads();
+  emit_segments(ks, n, uniq, seg, n_uniq, scan_lds);
+}
+
+// Dense scatter of grouped sums (autograd-compatible path): one wave per
+// distinct row, lanes over the row's columns, contributions in fixed order.
+__global__ __launch_bounds__(256) void segment_scatter_add_kernel(
+    const float* __restrict__ rows, int d, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ n_uniq_dev, float* __restrict__ dense, int64_t n_rows) {
+  const int nu = n_uniq_dev[0];
+  const int lane = threadIdx.x & 63;
+  for (int u = blockIdx.x * 4 + (threadIdx.x >> 6); u < nu; u += gridDim.x * 4) {
+    const int64_t row = uniq[u];
+    if (row < 0 || row >= n_rows) continue;
+    const int s0 = seg[u], s1 = seg[u + 1];
+    for (int c = lane; c < d; c += 64) {
+      float acc = 0.f;
+      for (int i = s0; i < s1; ++i) acc += rows[(int64_t)perm[i] * d + c];
+      dense[row * d + c] += acc;
+    }
+  }
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" size_t mirec_segment_sort_workspace_size(int64_t n, int64_t key_space) {
+  (void)key_space;
+  if (n <= kLdsMax) return 256;
+  return (size_t)4 * (size_t)n * sizeof(int32_t) + 256;
+}
+
+extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
+                                  int32_t* perm, int32_t* uniq, int32_t* seg,
+                                  int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || key_space <= 0 || key_space > INT32_MAX || n > INT32_MAX || !seg ||
+      !n_uniq_dev || (n > 0 && (!keys || !perm || !uniq))) {
+    set_error("mirec_segment_sort: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = [&] {
+    int b = 0;
+    while (b < 31 && ((int64_t)1 << b) < key_space) ++b;
+    return b;
+  }();
+  if (n <= kLdsMax) {
+    hipLaunchKernelGGL(segsort_lds_kernel, dim3(1), dim3(kSortThreads), 0, st, keys, (int)n, nb,
+                       perm, uniq, seg, n_uniq_dev);
+  } else {
+    const size_t need = mirec_segment_sort_workspace_size(n, key_space);
+    if (!ws || ws_bytes < need) {
+      set_error("mirec_segment_sort: workspace %zu < %zu", ws_bytes, need);
+      return -1;
+    }
+    int32_t* b = (int32_t*)ws;
+    hipLaunchKernelGGL(segsort_global_kernel, dim3(1), dim3(kSortThreads), 0, st, keys, (int)n,
+                       nb, perm, uniq, seg, n_uniq_dev, b, b + n, b + 2 * n, b + 3 * n);
+  }
+  return launch_status("mirec_segment_sort");
+}
+
+extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
+                                             const int32_t* uniq, const int32_t* seg,
+                                             const int32_t* n_uniq_dev, int64_t n_max_uniq,
+                                             float* dense, int64_t n_rows, void* stream) {
+  if (n_max_uniq == 0) return 0;
+  if (!rows || !perm || !uniq || !seg || !n_uniq_dev || !dense || d <= 0 || n_max_uniq < 0) {
+    set_error("mirec_segment_scatter_add_f32: bad arguments");
+    return -1;
+  }
+  int64_t g = (n_max_uniq + 3) / 4;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(segment_scatter_add_kernel, dim3((unsigned)g), dim3(256), 0,
+                     (hipStream_t)stream, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows);
+  return launch_status("mirec_segment_scatter_add_f32");
+}

@@ -1,0 +1,84 @@
+"""Dataset / loader construction (mirror of recbole/data/utils.py:27-286),
+including the fork's hard-coded switch of a `full` VALIDATION to uni1000
+(data/utils.py:86-88) — only the test phase is ranked against all items."""
+from logging import getLogger
+
+from recbole_amd.config import EvalSetting
+from recbole_amd.data.dataloader import (GeneralDataLoader, GeneralFullDataLoader,
+                                         GeneralNegSampleDataLoader)
+from recbole_amd.data.dataset import Dataset
+from recbole_amd.sampler import RepeatableSampler, Sampler
+from recbole_amd.utils import ModelType
+
+
+def create_dataset(config):
+    model_type = config['MODEL_TYPE']
+    if model_type in (ModelType.GENERAL, ModelType.TRADITIONAL):
+        return Dataset(config)
+    raise NotImplementedError(f'model type {model_type} datasets are not part of this build yet')
+
+
+def get_data_loader(name, config, neg_sample_args):
+    model_type = config['MODEL_TYPE']
+    if model_type not in (ModelType.GENERAL, ModelType.TRADITIONAL):
+        raise NotImplementedError(f'model type {model_type} loaders are not part of this build yet')
+    strategy = neg_sample_args['strategy']
+    if strategy == 'none':
+        return GeneralDataLoader
+    if strategy == 'by':
+        return GeneralNegSampleDataLoader
+    if strategy == 'full':
+        return GeneralFullDataLoader
+    raise NotImplementedError(f'neg_sample strategy [{strategy}] is not implemented')
+
+
+def data_preparation(config, dataset, save=False):
+    model_type = config['MODEL_TYPE']
+    es = EvalSetting(config)
+    built = dataset.build(es)
+    train_dataset, valid_dataset, test_dataset = built
+    phases = ['train', 'valid', 'test']
+    sampler = None
+    logger = getLogger()
+    train_args = config['train_neg_sample_args']
+    eval_args = es.neg_sample_args
+    valid_args = dict(eval_args)
+    if eval_args['strategy'] == 'full' and config['benchmark_filename'] is None:
+        logger.warning('validation strategy switched to uniform 1000 (fork behaviour, '
+                       'data/utils.py:86-88)')
+        valid_args = {'strategy': 'by', 'by': 1000, 'distribution': 'uniform'}
+
+    train_kwargs = {'config': config, 'dataset': train_dataset,
+                    'batch_size': config['train_batch_size'],
+                    'dl_format': config['MODEL_INPUT_TYPE'], 'shuffle': True}
+    if train_args['strategy'] != 'none':
+        if dataset.label_field in dataset.inter_feat and not config['train_use_bothway_sampler']:
+            raise ValueError(f'`training_neg_sample_num` should be 0 '
+                             f'if inter_feat have label_field [{dataset.label_field}].')
+        if model_type != ModelType.SEQUENTIAL:
+            sampler = Sampler(phases, built, train_args['distribution'])
+        else:
+            sampler = RepeatableSampler(phases, dataset, train_args['distribution'])
+        train_kwargs['sampler'] = sampler.set_phase('train')
+        train_kwargs['neg_sample_args'] = train_args
+    train_data = get_data_loader('train', config, train_args)(**train_kwargs)
+
+    eval_kwargs = {'config': config, 'batch_size': config['eval_batch_size'],
+                   'dl_format': config['MODEL_INPUT_TYPE'].__class__.POINTWISE, 'shuffle': False}
+    valid_kwargs = dict(eval_kwargs, dataset=valid_dataset)
+    test_kwargs = dict(eval_kwargs, dataset=test_dataset)
+    if eval_args['strategy'] != 'none':
+        if sampler is None:
+            if model_type != ModelType.SEQUENTIAL:
+                sampler = Sampler(phases, built, eval_args['distribution'])
+            else:
+                sampler = RepeatableSampler(phases, dataset, eval_args['distribution'])
+        else:
+            sampler.set_distribution(eval_args['distribution'])
+        test_kwargs['neg_sample_args'] = eval_args
+        valid_kwargs['neg_sample_args'] = valid_args
+        valid_kwargs['sampler'] = sampler.set_phase('valid')
+        test_kwargs['sampler'] = sampler.set_phase('test')
+    valid_data = get_data_loader('evaluation', config, valid_args)(**valid_kwargs)
+    test_data = get_data_loader('evaluation', config, eval_args)(**test_kwargs)
+    return train_data, valid_data, test_data

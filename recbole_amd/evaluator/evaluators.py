@@ -1,0 +1,103 @@
+"""Evaluators (mirror of recbole/evaluator/evaluators.py:37-370,
+abstract_evaluator.py:18-120). TopKEvaluator.collect keeps the reference's
+score-matrix contract for models without a fused scorer; the fused full-sort
+path feeds `evaluate_pos_idx` with the K6 kernel's positive flags directly."""
+from collections import ChainMap
+
+import numpy as np
+import torch
+from torch.nn.utils.rnn import pad_sequence
+
+from recbole_amd.evaluator.metrics import metrics_dict
+
+topk_metrics = {m.lower(): m for m in ['Hit', 'Recall', 'MRR', 'Precision', 'NDCG', 'MAP']}
+loss_metrics = {m.lower(): m for m in ['AUC', 'RMSE', 'MAE', 'LOGLOSS']}
+rank_metrics = {m.lower(): m for m in ['GAUC']}
+group_metrics = ChainMap(topk_metrics, rank_metrics)
+individual_metrics = ChainMap(loss_metrics)
+
+
+class BaseEvaluator(object):
+
+    def __init__(self, config, metrics):
+        self.metrics = metrics
+        self.full = ('full' in config['eval_setting'])
+        self.precision = config['metric_decimal_place']
+
+
+class TopKEvaluator(BaseEvaluator):
+
+    def __init__(self, config, metrics):
+        super().__init__(config, metrics)
+        self.topk = config['topk']
+        self._check_args()
+
+    def _check_args(self):
+        if isinstance(self.topk, (int, list)):
+            if isinstance(self.topk, int):
+                self.topk = [self.topk]
+            for k in self.topk:
+                if k <= 0:
+                    raise ValueError(f'topk must be a positive integer or a list of positive '
+                                     f'integers, but get `{k}`')
+        else:
+            raise TypeError('The topk must be a integer, list')
+
+    # score-matrix contract (abstract_evaluator.py:65-95, evaluators.py:53-76)
+    def get_score_matrix(self, scores_tensor, user_len_list):
+        if self.full:
+            return scores_tensor.view(len(user_len_list), -1)
+        scores_list = torch.split(scores_tensor, list(user_len_list), dim=0)
+        padding = pad_sequence(scores_list, batch_first=True, padding_value=-np.inf)
+        if padding.shape[1] < max(self.topk):
+            new = torch.full((padding.shape[0], max(self.topk)), -np.inf, device=padding.device)
+            new[:, :padding.shape[1]] = padding
+            padding = new
+        return padding
+
+    def collect(self, interaction, scores_tensor):
+        user_len_list = interaction.user_len_list
+        scores = torch.flip(self.get_score_matrix(scores_tensor, user_len_list), dims=[-1])
+        shape = torch.full((len(user_len_list), 1), scores.shape[1], device=scores.device)
+        _, topk_idx = torch.topk(scores, max(self.topk), dim=-1)
+        return torch.cat((topk_idx, shape), dim=1)
+
+    def evaluate(self, batch_matrix_list, eval_data):
+        pos_len_list = eval_data.get_pos_len_list()
+        res = torch.cat(batch_matrix_list, dim=0).cpu().numpy()
+        topk_idx, shapes = res[:, :-1], res[:, -1]
+        assert len(pos_len_list) == len(topk_idx)
+        pos_idx = topk_idx >= (shapes - pos_len_list).reshape(-1, 1)
+        return self.evaluate_pos_idx(pos_idx, pos_len_list)
+
+    def evaluate_pos_idx(self, pos_idx, pos_len_list):
+        """Metric reduction from the [n_users, max(topk)] positive matrix
+        (evaluators.py:78-141)."""
+        out = {}
+        vals = np.stack([metrics_dict[m.lower()](pos_idx, pos_len_list) for m in self.metrics],
+                        axis=0).mean(axis=1)
+        for m, v in zip(self.metrics, vals):
+            for k in self.topk:
+                out[f'{m}@{k}'] = round(v[k - 1], self.precision)
+        return out
+
+
+class LossEvaluator(BaseEvaluator):
+
+    def __init__(self, config, metrics):
+        super().__init__(config, metrics)
+        self.label_field = config['LABEL_FIELD']
+
+    def collect(self, interaction, pred_scores):
+        trues = interaction[self.label_field].to(pred_scores.device)
+        assert len(trues) == len(pred_scores)
+        return torch.stack((trues.float(), pred_scores.detach().float()), dim=1)
+
+    def evaluate(self, batch_matrix_list, *args):
+        concat = torch.cat(batch_matrix_list, dim=0).cpu().numpy()
+        trues, preds = concat[:, 0], concat[:, 1]
+        return {m: round(metrics_dict[m.lower()](trues, preds), self.precision)
+                for m in self.metrics}
+
+
+metric_eval_bind = [(topk_metrics, TopKEvaluator), (loss_metrics, LossEvaluator)]

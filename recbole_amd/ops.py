@@ -1,0 +1,253 @@
+"""Thin torch-tensor wrappers over the libmirec.so C-ABI (include/mirec.h).
+
+Every function here launches a hand-written gfx950 kernel on the current HIP
+stream. Inputs must already be device tensors of the stated dtype; nothing is
+copied to the host and nothing falls back to PyTorch or the CPU — a tensor on
+the wrong device or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from recbole_amd._native import NativeError, check, lib, ptr, stream_handle
+
+
+def _dev(t: torch.Tensor, dtype, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise NativeError(f"{name} must live on the GPU (got {t.device}); no CPU fallback exists")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+# ---------------------------------------------------------------- K4 sampler
+def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Tensor, num: int,
+                used_ptr: torch.Tensor | None, used_cols: torch.Tensor | None, n_key_space: int,
+                reject: bool, batch_keys: int | None = None, n_batches: int = 1,
+                out: torch.Tensor | None = None, status: torch.Tensor | None = None,
+                ws: torch.Tensor | None = None) -> torch.Tensor:
+    """Bit-exact cyclic-walk negative sampling (sampler.py:82-154)."""
+    _dev(random_list, torch.int32, "random_list")
+    _dev(pr_dev, torch.int64, "pr_dev")
+    _dev(keys, torch.int64, "keys")
+    n_keys = keys.numel()
+    if batch_keys is None:
+        batch_keys = max(n_keys, 1)
+    if out is None:
+        out = torch.empty(n_keys * num, dtype=torch.int64, device=keys.device)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=keys.device)
+    if reject:
+        _dev(used_ptr, torch.int64, "used_ptr")
+        _dev(used_cols, torch.int32, "used_cols")
+    wsz = lib().mirec_sample_walk_workspace_size(batch_keys, num)
+    if ws is None or ws.numel() < wsz:
+        ws = torch.empty(wsz, dtype=torch.uint8, device=keys.device)
+    rc = lib().mirec_sample_walk(ptr(random_list), random_list.numel(), ptr(pr_dev), ptr(keys),
+                                 n_keys, batch_keys, n_batches, num,
+                                 ptr(used_ptr) if reject else None,
+                                 ptr(used_cols) if reject else None, n_key_space,
+                                 1 if reject else 0, ptr(out), ptr(status), ptr(ws), ws.numel(),
+                                 stream_handle())
+    check(rc, "mirec_sample_walk")
+    return out
+
+
+# ---------------------------------------------------------------- K1 gather
+def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None):
+    if not table.is_cuda or not idx.is_cuda:
+        raise NativeError("gather_rows: tensors must live on the GPU")
+    if not table.is_contiguous():
+        raise ValueError("table must be contiguous")
+    idx = idx.contiguous()
+    row_shape = table.shape[1:]
+    if out is None:
+        out = torch.empty((idx.numel(),) + tuple(row_shape), dtype=table.dtype,
+                          device=table.device)
+    row_bytes = table.element_size() * (table[0].numel() if table.dim() > 1 else 1)
+    if idx.dtype == torch.int64:
+        fn = lib().mirec_gather_rows
+    elif idx.dtype == torch.int32:
+        fn = lib().mirec_gather_rows_i32idx
+    else:
+        raise TypeError("idx must be int32 or int64")
+    rc = fn(ptr(table), table.shape[0], row_bytes, ptr(idx), idx.numel(), ptr(out),
+            stream_handle())
+    check(rc, "mirec_gather_rows")
+    return out
+
+
+# ---------------------------------------------------------------- K3 BPR
+def bpr_fwd_bwd(EU, EI, user, pos, neg, times: int, gamma: float = 1e-10,
+                grad_scale: float | None = None, grads: bool = True, scores: bool = False,
+                out: dict | None = None) -> dict:
+    """Fused BPR forward/backward on the pairwise layout (bpr.py:74-83, loss.py:47-49)."""
+    _dev(EU, torch.float32, "EU")
+    _dev(EI, torch.float32, "EI")
+    for n_, t_ in (("user", user), ("pos", pos), ("neg", neg)):
+        _dev(t_, torch.int64, n_)
+    B = user.numel()
+    d = EU.shape[1]
+    if EI.shape[1] != d or pos.numel() != B or neg.numel() != B * times:
+        raise ValueError("bpr_fwd_bwd: inconsistent shapes")
+    if grad_scale is None:
+        grad_scale = float(torch.tensor(1.0, dtype=torch.float32) /
+                           torch.tensor(float(B * times), dtype=torch.float32))
+    o = {} if out is None else out
+    dev = EU.device
+    if "loss_k" not in o:
+        o["loss_k"] = torch.empty(B, dtype=torch.float32, device=dev)
+    if scores:
+        o.setdefault("pos_score", torch.empty(B, dtype=torch.float32, device=dev))
+        o.setdefault("neg_score", torch.empty(B * times, dtype=torch.float32, device=dev))
+    if grads:
+        o.setdefault("gU", torch.empty(B, d, dtype=torch.float32, device=dev))
+        o.setdefault("gI", torch.empty((1 + times) * B, d, dtype=torch.float32, device=dev))
+    rc = lib().mirec_bpr_fwd_bwd_f32(ptr(EU), EU.shape[0], ptr(EI), EI.shape[0], d, ptr(user),
+                                     ptr(pos), ptr(neg), B, times, gamma, grad_scale,
+                                     ptr(o["loss_k"]), ptr(o.get("pos_score")),
+                                     ptr(o.get("neg_score")), ptr(o.get("gU")),
+                                     ptr(o.get("gI")), stream_handle())
+    check(rc, "mirec_bpr_fwd_bwd_f32")
+    return o
+
+
+def dot_rows(EU, EI, u, i, out=None):
+    """score[r] = <EU[u[r]], EI[i[r]]> (BPR.predict, bpr.py:85-89)."""
+    _dev(EU, torch.float32, "EU")
+    _dev(EI, torch.float32, "EI")
+    u = u.contiguous()
+    i = i.contiguous()
+    _dev(u, torch.int64, "u")
+    _dev(i, torch.int64, "i")
+    if out is None:
+        out = torch.empty(u.numel(), dtype=torch.float32, device=EU.device)
+    rc = lib().mirec_dot_rows_f32(ptr(EU), EU.shape[0], ptr(EI), EI.shape[0], EU.shape[1], ptr(u),
+                                  ptr(i), u.numel(), ptr(out), stream_handle())
+    check(rc, "mirec_dot_rows_f32")
+    return out
+
+
+def fixed_sum(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _dev(x, torch.float32, "x")
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+    check(lib().mirec_sum_f32(ptr(x), x.numel(), ptr(out), stream_handle()), "mirec_sum_f32")
+    return out
+
+
+# ---------------------------------------------------------------- K2 grouping
+class Segments:
+    """Grouping of contribution rows by table row (output of K2)."""
+
+    __slots__ = ("perm", "uniq", "seg", "n_uniq", "n", "ws")
+
+    def __init__(self, n: int, device, ws_bytes: int = 0):
+        cap = max(n, 1)
+        self.n = n
+        self.perm = torch.empty(cap, dtype=torch.int32, device=device)
+        self.uniq = torch.empty(cap, dtype=torch.int32, device=device)
+        self.seg = torch.empty(cap + 1, dtype=torch.int32, device=device)
+        self.n_uniq = torch.zeros(1, dtype=torch.int32, device=device)
+        self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
+
+
+def segment_sort(keys: torch.Tensor, key_space: int, segs: Segments | None = None) -> Segments:
+    _dev(keys, torch.int64, "keys")
+    n = keys.numel()
+    wsz = lib().mirec_segment_sort_workspace_size(n, key_space)
+    if segs is None or segs.n < n or segs.ws.numel() < wsz:
+        segs = Segments(n, keys.device, wsz)
+    rc = lib().mirec_segment_sort(ptr(keys), n, key_space, ptr(segs.perm), ptr(segs.uniq),
+                                  ptr(segs.seg), ptr(segs.n_uniq), ptr(segs.ws), segs.ws.numel(),
+                                  stream_handle())
+    check(rc, "mirec_segment_sort")
+    return segs
+
+
+def segment_scatter_add(rows: torch.Tensor, segs: Segments, dense: torch.Tensor) -> torch.Tensor:
+    _dev(rows, torch.float32, "rows")
+    _dev(dense, torch.float32, "dense")
+    rc = lib().mirec_segment_scatter_add_f32(ptr(rows), rows.shape[1], ptr(segs.perm),
+                                             ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq),
+                                             segs.n, ptr(dense), dense.shape[0], stream_handle())
+    check(rc, "mirec_segment_scatter_add_f32")
+    return dense
+
+
+# ---------------------------------------------------------------- K5 Adam
+def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None = None,
+              dense_grad=None, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+    """One dense Adam step over every row of p (K5); the gradient is the grouped
+    compact rows (rows + segs) and/or a dense gradient tensor."""
+    for n_, t_ in (("p", p), ("m", m), ("v", v)):
+        _dev(t_, torch.float32, n_)
+    _dev(step_consts, torch.float32, "step_consts")
+    _dev(step_idx, torch.int32, "step_idx")
+    if p.dim() == 2 and p.shape[1] in (16, 32, 64, 128, 256):
+        n_rows, d = p.shape
+    elif p.numel() % 4 == 0:
+        n_rows, d = p.numel() // 4, 4
+        if segs is not None:
+            raise ValueError("grouped gradients need a 2-D table")
+    else:
+        raise NotImplementedError(f"adam_step: parameter of shape {tuple(p.shape)} "
+                                  f"(numel % 4 != 0) is not supported by the fused kernel")
+    if dense_grad is not None:
+        _dev(dense_grad, torch.float32, "dense_grad")
+    rc = lib().mirec_adam_sparse_grad_f32(
+        ptr(p), ptr(m), ptr(v), n_rows, d, ptr(rows),
+        ptr(segs.perm) if segs else None, ptr(segs.uniq) if segs else None,
+        ptr(segs.seg) if segs else None, ptr(segs.n_uniq) if segs else None,
+        segs.n if segs else 0, ptr(dense_grad), ptr(step_consts), ptr(step_idx), beta1, beta2,
+        eps, weight_decay, stream_handle())
+    check(rc, "mirec_adam_sparse_grad_f32")
+
+
+def step_finish(loss_k, denom: float, loss_hist, step_idx):
+    _dev(loss_k, torch.float32, "loss_k")
+    _dev(step_idx, torch.int32, "step_idx")
+    rc = lib().mirec_step_finish(ptr(loss_k), loss_k.numel(), float(denom), ptr(loss_hist),
+                                 ptr(step_idx), stream_handle())
+    check(rc, "mirec_step_finish")
+
+
+# ---------------------------------------------------------------- K6 full sort
+def fullsort_topk(Uq, EI, K: int, hist_ptr=None, hist_cols=None, pos_ptr=None, pos_cols=None,
+                  out: dict | None = None) -> dict:
+    _dev(Uq, torch.float32, "Uq")
+    _dev(EI, torch.float32, "EI")
+    nq, d = Uq.shape
+    if EI.shape[1] != d:
+        raise ValueError("fullsort_topk: embedding sizes differ")
+    for n_, t_, dt in (("hist_ptr", hist_ptr, torch.int64), ("hist_cols", hist_cols, torch.int32),
+                       ("pos_ptr", pos_ptr, torch.int64), ("pos_cols", pos_cols, torch.int32)):
+        if t_ is not None:
+            _dev(t_, dt, n_)
+    o = {} if out is None else out
+    dev = Uq.device
+    o.setdefault("scores", torch.empty(nq, K, dtype=torch.float32, device=dev))
+    o.setdefault("ids", torch.empty(nq, K, dtype=torch.int32, device=dev))
+    if pos_ptr is not None:
+        o.setdefault("pos_flags", torch.empty(nq, K, dtype=torch.uint8, device=dev))
+    rc = lib().mirec_fullsort_topk_f32(ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr),
+                                       ptr(hist_cols), ptr(pos_ptr), ptr(pos_cols), K,
+                                       ptr(o["scores"]), ptr(o["ids"]), ptr(o.get("pos_flags")),
+                                       stream_handle())
+    check(rc, "mirec_fullsort_topk_f32")
+    return o
+
+
+def score_matrix(Uq, EI, out=None):
+    _dev(Uq, torch.float32, "Uq")
+    _dev(EI, torch.float32, "EI")
+    if out is None:
+        out = torch.empty(Uq.shape[0], EI.shape[0], dtype=torch.float32, device=Uq.device)
+    rc = lib().mirec_score_matrix_f32(ptr(Uq), Uq.shape[0], ptr(EI), EI.shape[0], Uq.shape[1],
+                                      ptr(out), stream_handle())
+    check(rc, "mirec_score_matrix_f32")
+    return out

@@ -1,0 +1,269 @@
+"""Negative samplers (mirror of recbole/sampler/sampler.py:22-265, 341-420).
+
+Same public API — Sampler(phases, datasets, distribution), set_phase(),
+set_distribution(), sample_by_user_ids(user_ids, num), RepeatableSampler —
+and the same bit-exact output, but the walk runs on the GPU (K4,
+recbole_amd/csrc/sampler.hip):
+
+* random_list: built and shuffled on the host with the GLOBAL numpy RNG exactly
+  as the reference (sampler.py:45-57: first numpy draw after init_seed), then
+  kept resident in HBM as int32;
+* random_pr: one int64 in HBM per phase copy (set_phase returns a shallow copy
+  with its own pointer, like the reference's copy.copy of an int attribute);
+* used_ids: per phase a CSR (row_ptr int64[U+1], sorted int32 cols) built with
+  vectorised numpy instead of the reference's per-interaction Python
+  set.add loop (sampler.py:206-227); the `used_ids` attribute is still
+  available as an array of Python sets, built lazily, for API compatibility.
+
+Differences, documented: sample_by_user_ids returns a tensor on the sampler's
+device (the reference returns a CPU tensor), and an out-of-range user id
+raises ValueError before the walk advances (the reference advances
+random_pr by one round first; ids < 0 wrap around there).
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+
+from recbole_amd import ops
+
+
+class AbstractSampler(object):
+
+    def __init__(self, distribution):
+        self.distribution = ''
+        self.random_list = np.zeros(0, dtype=np.int64)
+        self.random_list_length = 0
+        self.device = None
+        self._rl_dev = None
+        self._pr_dev = None
+        self._pr_host = 0
+        self.set_distribution(distribution)
+        self.used_csr = self.get_used_csr()
+
+    # ------------------------------------------------------------ distribution
+    def set_distribution(self, distribution):
+        """sampler.py:45-57."""
+        if self.distribution == distribution:
+            return
+        self.distribution = distribution
+        rl = np.asarray(self.get_random_list())
+        np.random.shuffle(rl)
+        self.random_list = rl
+        self.random_list_length = len(rl)
+        self._rl_dev = None
+        self._pr_dev = None
+        self._pr_host = 0
+
+    def get_random_list(self):
+        raise NotImplementedError('method [get_random_list] should be implemented')
+
+    def get_used_csr(self):
+        raise NotImplementedError('method [get_used_csr] should be implemented')
+
+    # ------------------------------------------------------------ device state
+    def to_device(self, device):
+        device = torch.device(device)
+        if device.type != 'cuda':
+            raise RuntimeError('recbole_amd samplers run on the GPU only (no CPU fallback)')
+        if self.device != device or self._rl_dev is None:
+            self.device = device
+            self._rl_dev = torch.as_tensor(self.random_list.astype(np.int32), device=device)
+            self._pr_dev = torch.tensor([self._pr_host], dtype=torch.int64, device=device)
+            self._status = torch.zeros(1, dtype=torch.int32, device=device)
+            self._ws = None
+        return self
+
+    @property
+    def random_pr(self):
+        if self._pr_dev is not None:
+            return int(self._pr_dev.item())
+        return self._pr_host
+
+    @random_pr.setter
+    def random_pr(self, value):
+        self._pr_host = int(value)
+        if self._pr_dev is not None:
+            self._pr_dev.fill_(int(value))
+
+    def _used_dev(self):
+        return None, None
+
+    def _default_device(self):
+        if self.device is not None:
+            return self.device
+        if not torch.cuda.is_available():
+            raise RuntimeError('recbole_amd samplers run on the GPU only (no CPU fallback)')
+        return torch.device('cuda', torch.cuda.current_device())
+
+    # ------------------------------------------------------------ sampling
+    def sample_by_key_ids(self, key_ids, num):
+        """sampler.py:103-154 (both branches), on the device."""
+        if self.random_list_length == 0:
+            raise ValueError('the random list is empty; nothing to sample from')
+        if self._rl_dev is None:
+            self.to_device(self._default_device())
+        keys = torch.as_tensor(key_ids)
+        if keys.dim() == 0:
+            keys = keys.view(1)
+        keys = keys.to(device=self.device, dtype=torch.int64).contiguous()
+        up, uc = self._used_dev()
+        reject = up is not None
+        return ops.sample_walk(self._rl_dev, self._pr_dev, keys, int(num), up, uc,
+                               self.n_users, reject, status=self._status)
+
+    def launch_batches(self, keys_dev, batch_keys, n_batches, num, out):
+        """Walk `n_batches` consecutive batches in ONE kernel launch (the trainer's
+        ahead-of-time path); keys_dev are device user ids, out[b*batch_keys*num:]
+        receives batch b in the j*Kb + k layout."""
+        if self._rl_dev is None:
+            self.to_device(keys_dev.device)
+        up, uc = self._used_dev()
+        return ops.sample_walk(self._rl_dev, self._pr_dev, keys_dev, int(num), up, uc,
+                               self.n_users, up is not None, batch_keys=batch_keys,
+                               n_batches=n_batches, out=out, status=self._status)
+
+    def sample_by_user_ids(self, user_ids, num):
+        """sampler.py:246-265: empty input returns None (the reference's IndexError
+        path); ids outside [0, n_users) raise ValueError."""
+        ids = torch.as_tensor(user_ids)
+        if ids.numel() == 0:
+            return None
+        mn, mx = int(ids.min()), int(ids.max())
+        if mn < 0 or mx >= self.n_users:
+            bad = mn if mn < 0 else mx
+            raise ValueError(f'user_id [{bad}] not exist.')
+        return self.sample_by_key_ids(ids, num)
+
+
+def _csr_from_pairs(n_keys, keys, values):
+    keys = np.asarray(keys, dtype=np.int64)
+    values = np.asarray(values, dtype=np.int64)
+    order = np.lexsort((values, keys))
+    k, v = keys[order], values[order]
+    if len(k):
+        keep = np.ones(len(k), dtype=bool)
+        keep[1:] = (k[1:] != k[:-1]) | (v[1:] != v[:-1])
+        k, v = k[keep], v[keep]
+    ptr = np.zeros(n_keys + 1, dtype=np.int64)
+    np.add.at(ptr, k + 1, 1)
+    return np.cumsum(ptr), v.astype(np.int32)
+
+
+class Sampler(AbstractSampler):
+    """sampler.py:157-265: per-phase used sets are cumulative (train ⊂ valid ⊂ test)."""
+
+    def __init__(self, phases, datasets, distribution='uniform'):
+        if not isinstance(phases, list):
+            phases = [phases]
+        if not isinstance(datasets, list):
+            datasets = [datasets]
+        if len(phases) != len(datasets):
+            raise ValueError(f'Phases {phases} and datasets {datasets} should have the same length.')
+        self.phases = phases
+        self.datasets = datasets
+        self.uid_field = datasets[0].uid_field
+        self.iid_field = datasets[0].iid_field
+        self.n_users = datasets[0].user_num
+        self.n_items = datasets[0].item_num
+        self.phase = None
+        self._used_dev_cache = {}
+        super().__init__(distribution=distribution)
+
+    def get_random_list(self):
+        if self.distribution == 'uniform':
+            return np.arange(1, self.n_items)
+        if self.distribution == 'popularity':
+            return np.concatenate([d.inter_feat[self.iid_field].numpy() for d in self.datasets])
+        raise NotImplementedError(f'Distribution [{self.distribution}] has not been implemented.')
+
+    def get_used_csr(self):
+        """Cumulative per-phase used item sets as CSR (sampler.py:206-227)."""
+        out = {}
+        ks, vs = [], []
+        for phase, ds in zip(self.phases, self.datasets):
+            ks.append(ds.inter_feat[self.uid_field].numpy())
+            vs.append(ds.inter_feat[self.iid_field].numpy())
+            out[phase] = _csr_from_pairs(self.n_users, np.concatenate(ks), np.concatenate(vs))
+        last_ptr = out[self.phases[-1]][0]
+        if (np.diff(last_ptr) + 1 == self.n_items).any():
+            raise ValueError('Some users have interacted with all items, '
+                             'which we can not sample negative items for them. '
+                             'Please set `max_user_inter_num` to filter those users.')
+        return out
+
+    def set_phase(self, phase):
+        if phase not in self.phases:
+            raise ValueError(f'Phase [{phase}] not exist.')
+        new = copy.copy(self)
+        new.phase = phase
+        new._used_dev_cache = self._used_dev_cache
+        new._pr_host = self.random_pr
+        if self._pr_dev is not None:
+            new._pr_dev = self._pr_dev.clone()
+        return new
+
+    def _used_dev(self):
+        if self.phase is None:
+            raise ValueError('call set_phase() before sampling')
+        key = (self.phase, self.device)
+        if key not in self._used_dev_cache:
+            ptr, cols = self.used_csr[self.phase]
+            self._used_dev_cache[key] = (
+                torch.as_tensor(ptr, device=self.device),
+                torch.as_tensor(cols if len(cols) else np.zeros(1, np.int32), device=self.device))
+        return self._used_dev_cache[key]
+
+    @property
+    def used_ids(self):
+        """The reference's array of Python sets for the current phase (slow; API only)."""
+        src = self.used_csr[self.phase] if self.phase is not None else None
+        if src is None:
+            return {p: _sets(*self.used_csr[p]) for p in self.phases}
+        return _sets(*src)
+
+
+def _sets(ptr, cols):
+    return np.array([set(cols[ptr[u]:ptr[u + 1]].tolist()) for u in range(len(ptr) - 1)],
+                    dtype=object)
+
+
+class RepeatableSampler(AbstractSampler):
+    """sampler.py:341-420: no rejection (used sets are empty)."""
+
+    def __init__(self, phases, dataset, distribution='uniform'):
+        if not isinstance(phases, list):
+            phases = [phases]
+        self.phases = phases
+        self.dataset = dataset
+        self.iid_field = dataset.iid_field
+        self.n_users = dataset.user_num
+        self.n_items = dataset.item_num
+        self.phase = None
+        super().__init__(distribution=distribution)
+
+    def get_random_list(self):
+        if self.distribution == 'uniform':
+            return np.arange(1, self.n_items)
+        if self.distribution == 'popularity':
+            return self.dataset.inter_feat[self.iid_field].numpy()
+        raise NotImplementedError(f'Distribution [{self.distribution}] has not been implemented.')
+
+    def get_used_csr(self):
+        return None
+
+    @property
+    def used_ids(self):
+        return np.array([set() for _ in range(self.n_users)], dtype=object)
+
+    def set_phase(self, phase):
+        if phase not in self.phases:
+            raise ValueError(f'Phase [{phase}] not exist.')
+        new = copy.copy(self)
+        new.phase = phase
+        new._pr_host = self.random_pr
+        if self._pr_dev is not None:
+            new._pr_dev = self._pr_dev.clone()
+        return new

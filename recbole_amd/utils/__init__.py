@@ -1,0 +1,10 @@
+from recbole_amd.utils.enum_type import (DataLoaderType, EvaluatorType, FeatureSource,
+                                         FeatureType, InputType, ModelType)
+from recbole_amd.utils.logger import init_logger
+from recbole_amd.utils.utils import (calculate_valid_score, dict2str, early_stopping, ensure_dir,
+                                     get_local_time, get_model, get_trainer, init_seed, set_color)
+
+__all__ = ['ModelType', 'DataLoaderType', 'EvaluatorType', 'InputType', 'FeatureType',
+           'FeatureSource', 'init_logger', 'get_local_time', 'ensure_dir', 'get_model',
+           'get_trainer', 'early_stopping', 'calculate_valid_score', 'dict2str', 'init_seed',
+           'set_color']

@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
+
+
+@pytest.fixture(scope='session')
+def dev():
+    import torch
+    assert torch.cuda.is_available(), 'gpu tests need a GPU'
+    return torch.device('cuda', 0)

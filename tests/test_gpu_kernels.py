@@ -1,0 +1,366 @@
+"""Parity of every HIP kernel against the oracle (CPU restatement of the
+reference) on seeded inputs, through the C-ABI. Bit-exact for integer / index
+work; float kernels within the stated tolerance (north_star: 1e-4 fp32)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+# fp32 tolerance for losses / scores / gradients (north_star: "within 1e-4 fp32")
+RTOL, ATOL = 1e-4, 1e-6
+
+
+def _walk_dev(rl, ptr, cols, dev):
+    return (torch.as_tensor(np.asarray(rl, np.int32), device=dev),
+            torch.as_tensor(np.asarray(ptr, np.int64), device=dev),
+            torch.as_tensor(np.asarray(cols if len(cols) else [0], np.int32), device=dev))
+
+
+# ---------------------------------------------------------------- K4 sampler
+def test_sampler_golden_vectors(dev):
+    from recbole_amd import ops
+    for c in json.load(open(os.path.join(GOLDEN, 'sampler_walk.json'))):
+        rl, up, uc = _walk_dev(c['random_list'], c['used_ptr'], c['used_cols'], dev)
+        pr = torch.zeros(1, dtype=torch.int64, device=dev)
+        for b in c['batches']:
+            keys = torch.as_tensor(b['keys'], dtype=torch.int64, device=dev)
+            out = ops.sample_walk(rl, pr, keys, b['num'], up, uc, c['n_users'], True)
+            assert out.cpu().tolist() == b['out']
+            assert int(pr.item()) == b['pr']
+
+
+@pytest.mark.parametrize('n_items,n_users,K,num', [(1683, 944, 2048, 1), (26745, 3000, 512, 4),
+                                                   (50, 20, 3000, 7), (7, 3, 5, 9)])
+def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num):
+    from recbole_amd import ops
+    rng = np.random.default_rng(n_items + K)
+    deg = np.minimum(rng.integers(0, max(2, n_items // 2), n_users), n_items // 2)
+    u = np.repeat(np.arange(n_users), deg)
+    i = rng.integers(1, n_items, len(u))
+    ptr, cols = cpu_ref.used_csr(n_users, u, i)
+    rl = rng.permutation(np.arange(1, n_items))
+    drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
+    pr_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    pr = 0
+    for b in range(5):
+        keys = rng.integers(0, n_users, K)
+        if b == 3:
+            keys[:] = keys[0]                       # single-key branch
+        exp, pr = cpu_ref.c_sample_walk(rl, pr, keys, num, ptr, cols, n_users, True)
+        got = ops.sample_walk(drl, pr_d, torch.as_tensor(keys, device=dev), num, dup, duc,
+                              n_users, True)
+        assert np.array_equal(got.cpu().numpy(), exp)
+        assert int(pr_d.item()) == pr
+
+
+def test_sampler_multi_batch_launch_equals_sequential(dev):
+    from recbole_amd import ops
+    rng = np.random.default_rng(11)
+    n_users, n_items, B, T, nb = 500, 3000, 256, 4, 7
+    u = rng.integers(0, n_users, 40000)
+    i = rng.integers(1, n_items, 40000)
+    ptr, cols = cpu_ref.used_csr(n_users, u, i)
+    rl = rng.permutation(np.arange(1, n_items))
+    keys = rng.integers(0, n_users, B * nb - 100)          # last batch ragged
+    exp, pr = [], 0
+    for b in range(nb):
+        kb = keys[b * B:(b + 1) * B]
+        o, pr = cpu_ref.c_sample_walk(rl, pr, kb, T, ptr, cols, n_users, True)
+        exp.append(o)
+    drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
+    pr_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    out = torch.empty(len(keys) * T, dtype=torch.int64, device=dev)
+    ops.sample_walk(drl, pr_d, torch.as_tensor(keys, device=dev), T, dup, duc, n_users, True,
+                    batch_keys=B, n_batches=nb, out=out)
+    assert np.array_equal(out.cpu().numpy(), np.concatenate(exp))
+    assert int(pr_d.item()) == pr
+
+
+def test_repeatable_sampler_no_rejection(dev):
+    from recbole_amd import ops
+    rng = np.random.default_rng(5)
+    rl = rng.permutation(np.arange(1, 1000))
+    keys = rng.integers(0, 50, 333)
+    exp, pr = cpu_ref.c_sample_walk(rl, 990, keys, 100, None, None, 50, False)
+    drl = torch.as_tensor(rl.astype(np.int32), device=dev)
+    pr_d = torch.tensor([990], dtype=torch.int64, device=dev)
+    got = ops.sample_walk(drl, pr_d, torch.as_tensor(keys, device=dev), 100, None, None, 50, False)
+    assert np.array_equal(got.cpu().numpy(), exp) and int(pr_d.item()) == pr
+
+
+def test_sampler_livelock_reports_status(dev):
+    from recbole_amd import ops
+    rl = np.array([1, 2, 3, 4])
+    ptr, cols = cpu_ref.used_csr(2, np.array([0, 0, 0, 1, 1, 1]), np.array([1, 3, 4, 2, 3, 4]))
+    drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.sample_walk(drl, torch.zeros(1, dtype=torch.int64, device=dev),
+                    torch.tensor([0, 1], device=dev), 1, dup, duc, 2, True, status=status)
+    assert int(status.item()) == -3
+
+
+def test_sampler_api_mirror(dev):
+    """Sampler(phases, datasets) / set_phase / sample_by_user_ids like the reference."""
+    from recbole_amd.sampler import Sampler
+
+    class _DS:
+        uid_field, iid_field = 'user_id', 'item_id'
+
+        def __init__(self, u, i, nu, ni):
+            from recbole_amd.data.interaction import Interaction
+            self.inter_feat = Interaction({'user_id': torch.as_tensor(u),
+                                           'item_id': torch.as_tensor(i)})
+            self.user_num, self.item_num = nu, ni
+
+    rng = np.random.default_rng(9)
+    nu, ni = 40, 300
+    parts = [(rng.integers(0, nu, n), rng.integers(1, ni, n)) for n in (800, 100, 100)]
+    np.random.seed(2020)
+    s = Sampler(['train', 'valid', 'test'], [_DS(u, i, nu, ni) for u, i in parts])
+    np.random.seed(2020)
+    rl = cpu_ref.random_list_uniform(ni)
+    assert s.random_list.tolist() == rl.tolist()
+    tr = s.set_phase('train')
+    ptr, cols = cpu_ref.used_csr(nu, parts[0][0], parts[0][1])
+    pr = 0
+    for _ in range(3):
+        keys = rng.integers(0, nu, 64)
+        exp, pr = cpu_ref.c_sample_walk(rl, pr, keys, 2, ptr, cols, nu, True)
+        got = tr.sample_by_user_ids(torch.as_tensor(keys), 2)
+        assert np.array_equal(got.cpu().numpy(), exp)
+    assert tr.random_pr == pr
+    assert s.set_phase('test').random_pr == 0          # independent pointer per phase copy
+    assert tr.sample_by_user_ids([], 3) is None
+    with pytest.raises(ValueError):
+        tr.sample_by_user_ids([0, nu], 1)
+
+
+# ---------------------------------------------------------------- K1 gather / dot
+@pytest.mark.parametrize('shape,dtype', [((1000, 64), torch.float32), ((777,), torch.int64),
+                                         ((50, 3), torch.float32), ((300, 7), torch.int8)])
+def test_gather_rows_exact(dev, shape, dtype):
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(0)
+    t = (torch.randn(shape, generator=g) * 100).to(dtype)
+    idx = torch.randint(0, shape[0], (4097,), generator=g)
+    got = ops.gather_rows(t.to(dev), idx.to(dev))
+    assert torch.equal(got.cpu(), t[idx])
+    got32 = ops.gather_rows(t.to(dev), idx.to(torch.int32).to(dev))
+    assert torch.equal(got32.cpu(), t[idx])
+
+
+@pytest.mark.parametrize('d', [32, 64, 128, 256])
+def test_dot_rows(dev, d):
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(d)
+    EU, EI = torch.randn(300, d, generator=g), torch.randn(500, d, generator=g)
+    u, i = torch.randint(0, 300, (1001,), generator=g), torch.randint(0, 500, (1001,), generator=g)
+    got = ops.dot_rows(EU.to(dev), EI.to(dev), u.to(dev), i.to(dev)).cpu()
+    exp = (EU[u].double() * EI[i].double()).sum(1).float()
+    torch.testing.assert_close(got, exp, rtol=RTOL, atol=1e-5)
+
+
+# ---------------------------------------------------------------- K3 BPR
+@pytest.mark.parametrize('d,times,B', [(64, 1, 2048), (128, 4, 512), (32, 3, 100),
+                                       (256, 2, 333), (128, 1, 1)])
+def test_bpr_fwd_bwd_vs_torch_autograd(dev, d, times, B):
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(d * 7 + times)
+    nU, nI = 400, 900
+    EU = torch.randn(nU, d, generator=g) * 0.1
+    EI = torch.randn(nI, d, generator=g) * 0.1
+    user = torch.randint(0, nU, (B,), generator=g)
+    pos = torch.randint(1, nI, (B,), generator=g)
+    neg = torch.randint(1, nI, (B * times,), generator=g)
+    # reference: rows r = j*B + k, torch CPU autograd (bpr.py:74-83, loss.py:47-49)
+    m = cpu_ref.BPRCPU(nU, nI, d, init=False)
+    m.user_embedding.weight.data.copy_(EU)
+    m.item_embedding.weight.data.copy_(EI)
+    ur, pr_, nr = cpu_ref.pairwise_rows(user, pos, neg, times)
+    loss = m.calculate_loss(ur, pr_, nr)
+    loss.backward()
+    o = ops.bpr_fwd_bwd(EU.to(dev), EI.to(dev), user.to(dev), pos.to(dev), neg.to(dev), times,
+                        grads=True, scores=True)
+    got_loss = o['loss_k'].sum().item() / (B * times)
+    assert got_loss == pytest.approx(loss.item(), rel=RTOL)
+    ps = (EU[user] * EI[pos]).sum(1)
+    torch.testing.assert_close(o['pos_score'].cpu(), ps, rtol=RTOL, atol=ATOL)
+    # group row gradients into dense table gradients with K2 + scatter
+    dEU = torch.zeros(nU, d, device=dev)
+    dEI = torch.zeros(nI, d, device=dev)
+    ops.segment_scatter_add(o['gU'], ops.segment_sort(user.to(dev), nU), dEU)
+    ops.segment_scatter_add(o['gI'], ops.segment_sort(torch.cat([pos, neg]).to(dev), nI), dEI)
+    torch.testing.assert_close(dEU.cpu(), m.user_embedding.weight.grad, rtol=RTOL, atol=ATOL)
+    torch.testing.assert_close(dEI.cpu(), m.item_embedding.weight.grad, rtol=RTOL, atol=ATOL)
+
+
+def test_bpr_extreme_scores_no_nan(dev):
+    from recbole_amd import ops
+    d = 64
+    EU = torch.full((2, d), 3.0)
+    EI = torch.zeros(3, d)
+    EI[1] = -3.0          # pos score -576 -> sigmoid underflows; loss = -log(1e-10)
+    EI[2] = 3.0
+    o = ops.bpr_fwd_bwd(EU.to(dev), EI.to(dev), torch.tensor([0], device=dev),
+                        torch.tensor([1], device=dev), torch.tensor([2], device=dev), 1)
+    assert o['loss_k'].item() == pytest.approx(-np.log(1e-10), rel=1e-5)
+    assert torch.isfinite(o['gU']).all() and torch.isfinite(o['gI']).all()
+
+
+# ---------------------------------------------------------------- K2 segment sort
+@pytest.mark.parametrize('n,key_space', [(0, 10), (1, 1), (100, 7), (2560, 26745),
+                                         (8192, 138494), (20000, 5000), (513, 2 ** 22)])
+def test_segment_sort_exact(dev, n, key_space):
+    from recbole_amd import ops
+    rng = np.random.default_rng(n + key_space)
+    keys = rng.integers(0, key_space, n).astype(np.int64)
+    segs = ops.segment_sort(torch.as_tensor(keys, device=dev), key_space)
+    nu = int(segs.n_uniq.item())
+    perm = np.argsort(keys, kind='stable')
+    uniq, starts = np.unique(keys[perm], return_index=True)
+    assert nu == len(uniq)
+    assert np.array_equal(segs.perm[:n].cpu().numpy(), perm)
+    assert np.array_equal(segs.uniq[:nu].cpu().numpy(), uniq)
+    assert np.array_equal(segs.seg[:nu + 1].cpu().numpy(), np.r_[starts, n])
+
+
+# ---------------------------------------------------------------- K5 Adam
+@pytest.mark.parametrize('d,wd', [(64, 0.0), (128, 0.0), (32, 0.01)])
+def test_adam_compact_vs_torch_dense_adam(dev, d, wd):
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(d)
+    n, R = 700, 300
+    p0 = torch.randn(n, d, generator=g) * 0.1
+    ref = torch.nn.Parameter(p0.clone())
+    topt = torch.optim.Adam([ref], lr=1e-3, weight_decay=wd)
+    mine = torch.nn.Parameter(p0.clone().to(dev))
+    fopt = FusedAdam([mine], lr=1e-3, weight_decay=wd)
+    consts, idx = fopt.prepare_window(6, dev)
+    for step in range(6):
+        keys = torch.randint(0, n, (R,), generator=g)
+        rows = torch.randn(R, d, generator=g) * 0.01
+        dense = torch.zeros(n, d).index_add_(0, keys, rows)
+        ref.grad = dense
+        topt.step()
+        segs = ops.segment_sort(keys.to(dev), n)
+        fopt.step_compact(mine, rows.to(dev), segs, consts, idx)
+        idx += 1                                       # step_finish's job in the trainer
+    fopt.advance(6)
+    torch.testing.assert_close(mine.detach().cpu(), ref.detach(), rtol=RTOL, atol=1e-6)
+    st = fopt.state_dict()['state'][0]
+    torch.testing.assert_close(st['exp_avg'].cpu(), topt.state[ref]['exp_avg'], rtol=RTOL,
+                               atol=1e-8)
+    torch.testing.assert_close(st['exp_avg_sq'].cpu(), topt.state[ref]['exp_avg_sq'],
+                               rtol=RTOL, atol=1e-10)
+    assert float(st['step']) == float(topt.state[ref]['step'])
+
+
+def test_fused_adam_dense_step_matches_torch(dev):
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(3)
+    shapes = [(50, 64), (13, 4), (7,)]          # 2-D table, flat view, odd 1-D (numel%4!=0)
+    ps = [torch.randn(s, generator=g) for s in shapes[:2]]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    mine = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+    topt = torch.optim.Adam(ref, lr=1e-2)
+    fopt = FusedAdam(mine, lr=1e-2)
+    for _ in range(4):
+        gr = [torch.randn(p.shape, generator=g) for p in ps]
+        for r, m, x in zip(ref, mine, gr):
+            r.grad, m.grad = x.clone(), x.clone().to(dev)
+        topt.step()
+        fopt.step()
+    for r, m in zip(ref, mine):
+        torch.testing.assert_close(m.detach().cpu(), r.detach(), rtol=RTOL, atol=1e-6)
+
+
+# ---------------------------------------------------------------- K6 full sort
+def _fullsort_case(rng, nq, I, d, K, max_hist=30, max_pos=8):
+    U = rng.standard_normal((nq, d)).astype(np.float32)
+    E = rng.standard_normal((I, d)).astype(np.float32)
+    hist, pos = [], []
+    for q in range(nq):
+        perm = rng.permutation(np.arange(1, I))
+        npos = int(rng.integers(1, min(max_pos, I - 2) + 1))
+        nh = int(rng.integers(0, min(max_hist, I - 1 - npos) + 1))
+        pos.append(sorted(perm[:npos].tolist()))
+        hist.append(sorted(perm[npos:npos + nh].tolist()))
+    return U, E, hist, pos
+
+
+def _csr(lists):
+    ptr = np.r_[0, np.cumsum([len(x) for x in lists])].astype(np.int64)
+    cols = np.concatenate([np.asarray(x, np.int32) for x in lists]) if ptr[-1] else \
+        np.zeros(1, np.int32)
+    return ptr, cols
+
+
+def _check_topk(U, E, hist, pos, K, got_ids, got_flags, got_scores):
+    """Exact ids unless two scores tie within fp32 rounding (then either order)."""
+    scores = torch.as_tensor(U) @ torch.as_tensor(E).T
+    exp_flags, exp_ids = cpu_ref.full_sort_pos_idx(scores, hist, pos, K)
+    s64 = U.astype(np.float64) @ E.astype(np.float64).T
+    for q in range(len(U)):
+        for r in range(K):
+            if got_ids[q, r] == exp_ids[q, r]:
+                assert bool(got_flags[q, r]) == bool(exp_flags[q, r])
+                continue
+            a, b = got_ids[q, r], exp_ids[q, r]
+            assert a >= 0 and abs(s64[q, a] - s64[q, b]) <= 1e-4 * max(1.0, abs(s64[q, b])), \
+                (q, r, a, b)
+        valid = got_ids[q] >= 0
+        np.testing.assert_allclose(got_scores[q][valid], s64[q, got_ids[q][valid]],
+                                   rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('nq,I,d,K', [(300, 1682, 64, 10), (129, 2000, 128, 20),
+                                      (64, 517, 256, 10), (40, 300, 32, 50), (5, 33, 64, 1)])
+def test_fullsort_topk_vs_oracle(dev, nq, I, d, K):
+    from recbole_amd import ops
+    rng = np.random.default_rng(nq * I + d)
+    U, E, hist, pos = _fullsort_case(rng, nq, I, d, K)
+    hp, hc = _csr(hist)
+    pp, pc = _csr(pos)
+    T = lambda x: torch.as_tensor(x, device=dev)
+    o = ops.fullsort_topk(T(U), T(E), K, hist_ptr=T(hp), hist_cols=T(hc), pos_ptr=T(pp),
+                          pos_cols=T(pc))
+    _check_topk(U, E, hist, pos, K, o['ids'].cpu().numpy(), o['pos_flags'].cpu().numpy(),
+                o['scores'].cpu().numpy())
+
+
+def test_fullsort_fewer_items_than_k(dev):
+    from recbole_amd import ops
+    rng = np.random.default_rng(1)
+    U = rng.standard_normal((3, 64)).astype(np.float32)
+    E = rng.standard_normal((9, 64)).astype(np.float32)
+    hist = [[1, 2, 3, 4, 5, 6], [], [2, 4, 6, 8]]
+    pos = [[7], [1, 2], [3]]
+    hp, hc = _csr(hist)
+    pp, pc = _csr(pos)
+    T = lambda x: torch.as_tensor(x, device=dev)
+    o = ops.fullsort_topk(T(U), T(E), 10, hist_ptr=T(hp), hist_cols=T(hc), pos_ptr=T(pp),
+                          pos_cols=T(pc))
+    ids = o['ids'].cpu().numpy()
+    assert sorted(ids[0][ids[0] >= 0].tolist()) == [7, 8]           # items 1..8 minus history
+    assert (ids[0][2:] == -1).all() and np.isneginf(o['scores'].cpu().numpy()[0][2:]).all()
+    assert sorted(ids[1][ids[1] >= 0].tolist()) == list(range(1, 9))
+    assert o['pos_flags'].cpu().numpy()[0][ids[0] == 7].all()
+
+
+@pytest.mark.parametrize('nq,I,d', [(130, 1000, 64), (33, 70, 128), (1, 5, 32), (200, 257, 256)])
+def test_score_matrix(dev, nq, I, d):
+    from recbole_amd import ops
+    rng = np.random.default_rng(I)
+    U = rng.standard_normal((nq, d)).astype(np.float32)
+    E = rng.standard_normal((I, d)).astype(np.float32)
+    got = ops.score_matrix(torch.as_tensor(U, device=dev), torch.as_tensor(E, device=dev)).cpu()
+    exp = torch.as_tensor(U.astype(np.float64) @ E.astype(np.float64).T).float()
+    torch.testing.assert_close(got, exp, rtol=RTOL, atol=1e-4)
