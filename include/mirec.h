@@ -43,8 +43,10 @@ const char* mirec_last_error(void);
  * persists across calls exactly like `random_pr`.
  *
  * Processes n_batches consecutive batches in ONE launch: batch b uses keys
- * keys[b*batch_keys .. min((b+1)*batch_keys, n_keys)) and writes
- * out + b*batch_keys*num.  used_ptr[n_key_space+1]/used_cols is a CSR of the
+ * keys[b*batch_keys .. min((b+1)*batch_keys, n_keys)) and writes its
+ * Kb*num values at out + b*out_stride (out_stride 0 = batch_keys*num), so the
+ * trainer can sample a chunk of future batches straight into their
+ * [pos | neg] key rows.  used_ptr[n_key_space+1]/used_cols is a CSR of the
  * phase's used item ids per key, each row sorted ascending; reject==0 skips
  * the rejection (RepeatableSampler).  Returns -2 if a key is out of range
  * (the reference raises ValueError in sample_by_user_ids).
@@ -55,7 +57,7 @@ int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t* pr_dev,
                       int64_t n_batches, int64_t num,
                       const int64_t* used_ptr, const int32_t* used_cols,
                       int64_t n_key_space, int reject,
-                      int64_t* out, int32_t* status_dev,
+                      int64_t* out, int64_t out_stride, int32_t* status_dev,
                       void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
@@ -118,6 +120,14 @@ int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
                        int32_t* perm, int32_t* uniq, int32_t* seg,
                        int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
 
+/* Batched form: batch b groups keys[b*batch_n, min((b+1)*batch_n, n)) into
+ * perm/uniq + b*batch_n, seg + b*(batch_n+1), n_uniq_dev[b]; one workgroup per
+ * batch, so a whole chunk of future training batches is grouped in one launch.
+ * Workspace: mirec_segment_sort_workspace_size(n_batches*batch_n, key_space). */
+int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
+                               int64_t key_space, int32_t* perm, int32_t* uniq, int32_t* seg,
+                               int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
+
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :]  (fixed order)
  * — the dense-gradient form used by the autograd-compatible path. */
 int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
@@ -152,6 +162,27 @@ int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows, int
                                const float* step_consts_dev, const int32_t* step_idx_dev,
                                double beta1, double beta2, double eps, double weight_decay,
                                void* stream);
+
+/* Several tables in ONE launch (e.g. the user and the item embedding of BPR),
+ * same arithmetic per table. `tables` is a HOST array of n_tables <= 4
+ * descriptors; every pointer inside is a device pointer. */
+typedef struct mirec_adam_table {
+  float* p;
+  float* m;
+  float* v;
+  int64_t n_rows;
+  const float* rows;        /* grouped gradient rows (or NULL)             */
+  const int32_t* perm;      /* K2 grouping of `rows` by table row          */
+  const int32_t* uniq;
+  const int32_t* seg;
+  const int32_t* n_uniq;    /* device counter; NULL = no grouped gradient  */
+  const float* dense_grad;  /* optional dense gradient [n_rows, d] or NULL */
+} mirec_adam_table;
+
+int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                         const float* step_consts_dev, const int32_t* step_idx_dev,
+                         double beta1, double beta2, double eps, double weight_decay,
+                         void* stream);
 
 /* End-of-step bookkeeping of Trainer._train_epoch (trainer.py:161-169):
  * loss_hist[step] = (sum of loss_k[0..n), fixed order) / denom, then

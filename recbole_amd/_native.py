@@ -19,14 +19,22 @@ import torch  # noqa: F401  (must be imported before the library is dlopen'ed)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIREC_LIB", os.path.join(_HERE, "_lib", "libmirec.so"))
 
-# Every symbol include/mirec.h declares: name -> (restype, argtypes)
 _P = c_void_p
+
+
+class AdamTable(ctypes.Structure):
+    """struct mirec_adam_table (include/mirec.h)."""
+    _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
+                ('perm', _P), ('uniq', _P), ('seg', _P), ('n_uniq', _P), ('dense_grad', _P)]
+
+
+# Every symbol include/mirec.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "mirec_abi_version": (c_int, []),
     "mirec_last_error": (c_char_p, []),
     "mirec_sample_walk_workspace_size": (c_size_t, [c_int64, c_int64]),
     "mirec_sample_walk": (c_int, [_P, c_int64, _P, _P, c_int64, c_int64, c_int64, c_int64,
-                                  _P, _P, c_int64, c_int, _P, _P, _P, c_size_t, _P]),
+                                  _P, _P, c_int64, c_int, _P, c_int64, _P, _P, c_size_t, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_gather_rows_i32idx": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
@@ -35,11 +43,15 @@ SIGNATURES = {
     "mirec_sum_f32": (c_int, [_P, c_int64, _P, _P]),
     "mirec_segment_sort_workspace_size": (c_size_t, [c_int64, c_int64]),
     "mirec_segment_sort": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "mirec_segment_sort_batched": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
+                                           c_size_t, _P]),
     "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
                                               c_int64, _P]),
     "mirec_adam_sparse_grad_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, _P, _P,
                                            c_int64, _P, _P, _P, c_double, c_double, c_double,
                                            c_double, _P]),
+    "mirec_adam_multi_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
+                                     c_double, c_double, c_double, c_double, _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
                                         c_int32, _P, _P, _P, _P]),

@@ -23,29 +23,49 @@ namespace mirec {
 
 constexpr int kAdamThreads = 256;
 constexpr int kAdamRows = 64;  // table rows per block
+constexpr int kMaxTables = 4;
 
 struct AdamConsts {
   float omb1, b2, omb2, eps, wd;
 };
 
+// Up to kMaxTables tables in one launch; blocks [block_start[t], block_start[t+1])
+// belong to table t (one grid over e.g. the user AND item tables, so the
+// smaller table does not run as its own under-filled launch).
+struct AdamTables {
+  mirec_adam_table t[kMaxTables];
+  int64_t block_start[kMaxTables + 1];
+  int n;
+};
+
 template <int D>
-__global__ __launch_bounds__(kAdamThreads) void adam_sparse_grad_kernel(
-    float* __restrict__ P, float* __restrict__ M, float* __restrict__ V, int64_t n_rows,
-    const float* __restrict__ rows, const int32_t* __restrict__ perm,
-    const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
-    const int32_t* __restrict__ n_uniq_dev, const float* __restrict__ dense_grad,
-    const float* __restrict__ step_consts, const int32_t* __restrict__ step_idx, AdamConsts k) {
+__global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
+    const AdamTables tabs, const float* __restrict__ step_consts,
+    const int32_t* __restrict__ step_idx, AdamConsts k) {
   constexpr int VPR = D / 4;                        // float4 per row
   constexpr int RPP = kAdamThreads / VPR;           // rows per pass
   static_assert(kAdamThreads % VPR == 0, "row width");
   __shared__ int32_t slot[kAdamRows];
   __shared__ int32_t s_range[2];
 
-  const int64_t lo = (int64_t)blockIdx.x * kAdamRows;
-  const int64_t hi = min(n_rows, lo + kAdamRows);
+  int ti = 0;
+#pragma unroll
+  for (int q = 1; q < kMaxTables; ++q)
+    if (q < tabs.n && (int64_t)blockIdx.x >= tabs.block_start[q]) ti = q;
+  const mirec_adam_table& T = tabs.t[ti];
+  float* __restrict__ P = T.p;
+  float* __restrict__ M = T.m;
+  float* __restrict__ V = T.v;
+  const int32_t* __restrict__ uniq = T.uniq;
+  const int32_t* __restrict__ seg = T.seg;
+  const int32_t* __restrict__ perm = T.perm;
+  const float* __restrict__ dense_grad = T.dense_grad;
+
+  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[ti]) * kAdamRows;
+  const int64_t hi = min(T.n_rows, lo + kAdamRows);
   if (threadIdx.x < kAdamRows) slot[threadIdx.x] = -1;
   if (threadIdx.x == 0) {
-    const int nu = n_uniq_dev ? n_uniq_dev[0] : 0;
+    const int nu = T.n_uniq ? T.n_uniq[0] : 0;
     // lower_bound(uniq, lo), lower_bound(uniq, hi)
     int a = 0, b = nu;
     while (a < b) { int mid = (a + b) >> 1; if (uniq[mid] < lo) a = mid + 1; else b = mid; }
@@ -62,7 +82,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_sparse_grad_kernel(
   const int st = step_idx[0];
   const float step_size = step_consts[2 * st];
   const float bc2s = step_consts[2 * st + 1];
-  const float4* __restrict__ R4 = reinterpret_cast<const float4*>(rows);
+  const float4* __restrict__ R4 = reinterpret_cast<const float4*>(T.rows);
 
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
@@ -104,6 +124,60 @@ __global__ __launch_bounds__(kAdamThreads) void adam_sparse_grad_kernel(
 
 using namespace mirec;
 
+extern "C" int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                                    const float* step_consts_dev, const int32_t* step_idx_dev,
+                                    double beta1, double beta2, double eps, double weight_decay,
+                                    void* stream) {
+  if (n_tables < 1 || n_tables > kMaxTables || !tables || !step_consts_dev || !step_idx_dev) {
+    set_error("mirec_adam_multi_f32: bad arguments (n_tables=%d)", n_tables);
+    return -1;
+  }
+  AdamTables tabs;
+  memset(&tabs, 0, sizeof(tabs));
+  tabs.n = n_tables;
+  int64_t blocks = 0;
+  for (int q = 0; q < n_tables; ++q) {
+    const mirec_adam_table& t = tables[q];
+    if (!t.p || !t.m || !t.v || t.n_rows < 0 ||
+        (t.n_uniq && (!t.uniq || !t.seg || !t.perm || !t.rows))) {
+      set_error("mirec_adam_multi_f32: bad table %d", q);
+      return -1;
+    }
+    tabs.t[q] = t;
+    tabs.block_start[q] = blocks;
+    blocks += (t.n_rows + kAdamRows - 1) / kAdamRows;
+  }
+  tabs.block_start[n_tables] = blocks;
+  for (int q = n_tables + 1; q <= kMaxTables; ++q) tabs.block_start[q] = blocks;
+  if (blocks == 0) return 0;
+  AdamConsts k;
+  k.omb1 = (float)(1.0 - beta1);
+  k.b2 = (float)beta2;
+  k.omb2 = (float)(1.0 - beta2);
+  k.eps = (float)eps;
+  k.wd = (float)weight_decay;
+  const dim3 grd((unsigned)blocks);
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_ADAM_CASE(DD)                                                                  \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, dim3(kAdamThreads), 0, st, tabs,          \
+                       step_consts_dev, step_idx_dev, k);                                    \
+    break;
+  switch (d) {
+    MIREC_ADAM_CASE(4)
+    MIREC_ADAM_CASE(16)
+    MIREC_ADAM_CASE(32)
+    MIREC_ADAM_CASE(64)
+    MIREC_ADAM_CASE(128)
+    MIREC_ADAM_CASE(256)
+    default:
+      set_error("mirec_adam_multi_f32: row width %d not in {4,16,32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_ADAM_CASE
+  return launch_status("mirec_adam_multi_f32");
+}
+
 extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows,
                                           int32_t d, const float* rows, const int32_t* perm,
                                           const int32_t* uniq, const int32_t* seg,
@@ -114,36 +188,10 @@ extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t 
                                           void* stream) {
   (void)n_max_uniq;
   if (n_rows == 0) return 0;
-  if (!p || !m || !v || !step_consts_dev || !step_idx_dev || n_rows < 0 ||
-      (n_uniq_dev && (!uniq || !seg || !perm || !rows))) {
-    set_error("mirec_adam_sparse_grad_f32: bad arguments");
-    return -1;
-  }
-  AdamConsts k;
-  k.omb1 = (float)(1.0 - beta1);
-  k.b2 = (float)beta2;
-  k.omb2 = (float)(1.0 - beta2);
-  k.eps = (float)eps;
-  k.wd = (float)weight_decay;
-  const dim3 grd((unsigned)((n_rows + kAdamRows - 1) / kAdamRows));
-  hipStream_t st = (hipStream_t)stream;
-#define MIREC_ADAM_CASE(DD)                                                                  \
-  case DD:                                                                                   \
-    hipLaunchKernelGGL(adam_sparse_grad_kernel<DD>, grd, dim3(kAdamThreads), 0, st, p, m, v, \
-                       n_rows, rows, perm, uniq, seg, n_uniq_dev, dense_grad, step_consts_dev,\
-                       step_idx_dev, k);                                                     \
-    break;
-  switch (d) {
-    MIREC_ADAM_CASE(4)
-    MIREC_ADAM_CASE(16)
-    MIREC_ADAM_CASE(32)
-    MIREC_ADAM_CASE(64)
-    MIREC_ADAM_CASE(128)
-    MIREC_ADAM_CASE(256)
-    default:
-      set_error("mirec_adam_sparse_grad_f32: row width %d not in {4,16,32,64,128,256}", d);
-      return -1;
-  }
-#undef MIREC_ADAM_CASE
-  return launch_status("mirec_adam_sparse_grad_f32");
+  mirec_adam_table t;
+  t.p = p; t.m = m; t.v = v; t.n_rows = n_rows;
+  t.rows = rows; t.perm = perm; t.uniq = uniq; t.seg = seg; t.n_uniq = n_uniq_dev;
+  t.dense_grad = dense_grad;
+  return mirec_adam_multi_f32(&t, 1, d, step_consts_dev, step_idx_dev, beta1, beta2, eps,
+                              weight_decay, stream);
 }

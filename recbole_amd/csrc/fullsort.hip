@@ -33,19 +33,40 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kFsThreads = 256;
 
+// Sorted insert into a best-first register list, branch-free (v_cndmask only;
+// bitwise |/& on the predicates so clang emits no exec-mask branches).
+// Scan form: strict '>' — each lane visits its items in increasing id order,
+// so an equal score arriving later (higher id) correctly ranks after.
 template <int KC>
 __device__ __forceinline__ void topk_insert(float (&ts)[KC], int (&ti)[KC], float v, int id) {
-  // "better" = (score desc, id asc); ts/ti sorted best-first
 #pragma unroll
   for (int t = KC - 1; t > 0; --t) {
-    const bool up = (v > ts[t - 1]) || (v == ts[t - 1] && id < ti[t - 1]);
-    const bool here = (v > ts[t]) || (v == ts[t] && id < ti[t]);
+    const bool up = v > ts[t - 1];
+    const bool here = v > ts[t];
     const float ns = up ? ts[t - 1] : (here ? v : ts[t]);
     const int ni = up ? ti[t - 1] : (here ? id : ti[t]);
     ts[t] = ns;
     ti[t] = ni;
   }
-  const bool h0 = (v > ts[0]) || (v == ts[0] && id < ti[0]);
+  const bool h0 = v > ts[0];
+  ts[0] = h0 ? v : ts[0];
+  ti[0] = h0 ? id : ti[0];
+}
+
+// Merge form: full order (score desc, id asc) for combining two lanes' lists.
+template <int KC>
+__device__ __forceinline__ void topk_merge_insert(float (&ts)[KC], int (&ti)[KC], float v,
+                                                  int id) {
+#pragma unroll
+  for (int t = KC - 1; t > 0; --t) {
+    const bool up = (v > ts[t - 1]) | ((v == ts[t - 1]) & (id < ti[t - 1]));
+    const bool here = (v > ts[t]) | ((v == ts[t]) & (id < ti[t]));
+    const float ns = up ? ts[t - 1] : (here ? v : ts[t]);
+    const int ni = up ? ti[t - 1] : (here ? id : ti[t]);
+    ts[t] = ns;
+    ti[t] = ni;
+  }
+  const bool h0 = (v > ts[0]) | ((v == ts[0]) & (id < ti[0]));
   ts[0] = h0 ? v : ts[0];
   ti[0] = h0 ? id : ti[0];
 }
@@ -91,7 +112,10 @@ __global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
     float* __restrict__ top_scores, int32_t* __restrict__ top_ids,
     uint8_t* __restrict__ pos_flags) {
   constexpr int LDR = D + 2;
-  __shared__ __attribute__((aligned(16))) float tile[32 * LDR];
+  constexpr int V4 = D / 4;
+  constexpr int NPF = (32 * V4 + kFsThreads - 1) / kFsThreads;   // float4 per thread per tile
+  __shared__ __attribute__((aligned(16))) float tile[2][32 * LDR];
+  __shared__ uint32_t hmask[2][128];   // history bits of the WG's 128 users over one tile
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int j = lane & 31;
@@ -107,40 +131,111 @@ __global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
 #pragma unroll
   for (int t = 0; t < KC; ++t) { ts[t] = -INFINITY; ti[t] = -1; }
   float thr = -INFINITY;
+
+  // History cursor, one per user, owned by thread u < 128 of the workgroup:
+  // `hnext` is the user's next history item >= the current tile; a tile's mask
+  // only loads when it actually consumes an entry (~deg/ntile per tile).
+  const int64_t qu = (int64_t)blockIdx.x * 128 + threadIdx.x;
   int64_t hcur = 0, hend = 0;
-  if (qv && hist_ptr) { hcur = hist_ptr[q]; hend = hist_ptr[q + 1]; }
+  int64_t hnext = INT64_MAX;
+  if (threadIdx.x < 128 && qu < nq && hist_ptr) {
+    hcur = hist_ptr[qu];
+    hend = hist_ptr[qu + 1];
+    if (hcur < hend) hnext = hist_cols[hcur];
+  }
+  auto build_mask = [&](int64_t base, uint32_t* dst) {
+    if (threadIdx.x < 128) {
+      uint32_t msk = 0;
+      while (hnext < base + 32) {
+        msk |= 1u << (uint32_t)(hnext - base);
+        ++hcur;
+        hnext = hcur < hend ? (int64_t)hist_cols[hcur] : INT64_MAX;
+      }
+      dst[threadIdx.x] = msk;
+    }
+  };
+
+  const float4* __restrict__ E4 = reinterpret_cast<const float4*>(EI);
+  float4 pf[NPF];
+  auto load_tile = [&](int64_t base) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int f = threadIdx.x + k * kFsThreads;
+      const int row = f / V4;
+      const int c4 = f - row * V4;
+      const int64_t item = base + row;
+      pf[k] = (f < 32 * V4 && item < I) ? E4[item * V4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_tile = [&](float* dst) {
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int f = threadIdx.x + k * kFsThreads;
+      if (f < 32 * V4) {
+        const int row = f / V4;
+        const int c4 = f - row * V4;
+        float2* p = reinterpret_cast<float2*>(dst + row * LDR + 4 * c4);
+        p[0] = make_float2(pf[k].x, pf[k].y);
+        p[1] = make_float2(pf[k].z, pf[k].w);
+      }
+    }
+  };
 
   const int64_t ntile = (I + 31) / 32;
+  load_tile(0);
+  store_tile(tile[0]);
+  build_mask(0, hmask[0]);
+  __syncthreads();
+  int cur = 0;
+  const int ul = w * 32 + j;   // this lane's user within the workgroup
   for (int64_t t = 0; t < ntile; ++t) {
     const int64_t base = t * 32;
-    __syncthreads();
-    stage_tile<D>(EI, I, base, tile);
-    __syncthreads();
+    const bool more = t + 1 < ntile;
+    if (more) load_tile(base + 32);          // global loads in flight under the MFMAs
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const float* arow = tile + j * LDR + 2 * h;
+    const float* arow = tile[cur] + j * LDR + 2 * h;
 #pragma unroll
     for (int s2 = 0; s2 < D / 4; ++s2) {
       const float2 a = *reinterpret_cast<const float2*>(arow + 4 * s2);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, ub[2 * s2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, ub[2 * s2 + 1], acc, 0, 0, 0);
     }
-    // C[item row][user col]: rows (r&3) + 8*(r>>2) + 4h, increasing in r
+    // Rows of this lane that can enter its list: valid item, not pad, not history.
+    // C[item row][user col]: rows (r&3) + 8*(r>>2) + 4h
+    const uint32_t hm = hmask[cur][ul];
+    uint32_t ok = 0;
+    float best = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t item = base + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float sc = acc[r];
-      const bool cand = qv && item < I && item != 0 && sc > thr;
-      if (cand) {
-        while (hcur < hend && (int64_t)hist_cols[hcur] < item) ++hcur;
-        const bool masked = hcur < hend && (int64_t)hist_cols[hcur] == item;
-        if (!masked) {
-          topk_insert<KC>(ts, ti, sc, (int)item);
-          thr = ts[KC - 1];
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t item = base + row;
+      const bool valid = qv & (item < I) & (item != 0) & !((hm >> row) & 1u);
+      ok |= (valid ? 1u : 0u) << r;
+      best = fmaxf(best, valid ? acc[r] : -INFINITY);
+    }
+    // The two lanes of a user scan disjoint item halves; an item below the
+    // partner's K-th best already has K better items, so it can never reach the
+    // final (merged) top-K: filter with the stronger of the two thresholds.
+    thr = fmaxf(thr, __shfl_xor(thr, 32, 64));
+    if (__any(best > thr)) {             // wave-uniform: rare once the lists fill up
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float sc = acc[r];
+        if (((ok >> r) & 1u) && sc > thr) {
+          topk_insert<KC>(ts, ti, sc, (int)(base + row));
+          thr = fmaxf(thr, ts[KC - 1]);
         }
       }
     }
+    if (more) {
+      build_mask(base + 32, hmask[cur ^ 1]);
+      store_tile(tile[cur ^ 1]);
+    }
+    __syncthreads();
+    cur ^= 1;
   }
 
   // merge the two item halves of each user: lane j takes lane j+32's list
@@ -148,7 +243,7 @@ __global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
   for (int t = 0; t < KC; ++t) {
     const float os = __shfl(ts[t], j + 32, 64);
     const int oi = __shfl(ti[t], j + 32, 64);
-    if (h == 0) topk_insert<KC>(ts, ti, os, oi);
+    if (h == 0) topk_merge_insert<KC>(ts, ti, os, oi);
   }
   if (h == 0 && qv) {
     const int64_t p0 = pos_ptr ? pos_ptr[q] : 0;

@@ -23,7 +23,8 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
     const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
     int64_t num, const int64_t* __restrict__ used_ptr, const int32_t* __restrict__ used_cols,
-    int64_t key_space, int reject, int64_t* __restrict__ out, int32_t* __restrict__ status,
+    int64_t key_space, int reject, int64_t* __restrict__ out, int64_t out_stride,
+    int32_t* __restrict__ status,
     int32_t* __restrict__ rejA, int32_t* __restrict__ rejB) {
   __shared__ int scan_lds[kSampThreads / 64 + 1];
   int64_t pr = pr_dev[0] % L;
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     if (Kb <= 0) break;
     const int64_t total = Kb * num;
     const int64_t* __restrict__ bkeys = keys + k0;
-    int64_t* __restrict__ bout = out + k0 * num;
+    int64_t* __restrict__ bout = out + b * out_stride;
 
     // ---- round 0: fill every slot, collect rejected slots in ascending order
     int32_t nrej = 0;
@@ -120,7 +121,8 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
                                  const int64_t* keys, int64_t n_keys, int64_t batch_keys,
                                  int64_t n_batches, int64_t num, const int64_t* used_ptr,
                                  const int32_t* used_cols, int64_t n_key_space, int reject,
-                                 int64_t* out, int32_t* status_dev, void* ws, size_t ws_bytes,
+                                 int64_t* out, int64_t out_stride, int32_t* status_dev, void* ws,
+                                 size_t ws_bytes,
                                  void* stream) {
   if (L <= 0 || !random_list || !pr_dev || !out || !status_dev || n_keys < 0 || num < 0 ||
       batch_keys <= 0 || n_batches < 0) {
@@ -141,10 +143,11 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
     set_error("mirec_sample_walk: workspace %zu < %zu", ws_bytes, need);
     return -1;
   }
+  if (out_stride == 0) out_stride = batch_keys * num;
   int32_t* rejA = (int32_t*)ws;
   int32_t* rejB = rejA + batch_keys * num;
   hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, (hipStream_t)stream,
                      random_list, L, pr_dev, keys, n_keys, batch_keys, n_batches, num, used_ptr,
-                     used_cols, n_key_space, reject, out, status_dev, rejA, rejB);
+                     used_cols, n_key_space, reject, out, out_stride, status_dev, rejA, rejB);
   return launch_status("mirec_sample_walk");
 }

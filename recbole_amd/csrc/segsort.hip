@@ -55,11 +55,21 @@ __device__ void emit_segments(KeyPtr skey, int n, int32_t* __restrict__ uniq,
   }
 }
 
+// One workgroup per batch: batch b sorts keys[b*batch_n, min((b+1)*batch_n, n_total))
+// and writes perm/uniq at b*batch_n, seg at b*(batch_n+1), n_uniq[b].
 __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
-    const int64_t* __restrict__ keys, int n, int nbits, int32_t* __restrict__ perm,
-    int32_t* __restrict__ uniq, int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq) {
+    const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n, int nbits,
+    int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all) {
   __shared__ int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
   __shared__ int scan_lds[kSortThreads / 64 + 1];
+  const int64_t b = blockIdx.x;
+  const int n = (int)min((int64_t)batch_n, n_total - b * batch_n);
+  const int64_t* __restrict__ keys = keys_all + b * batch_n;
+  int32_t* __restrict__ perm = perm_all + b * batch_n;
+  int32_t* __restrict__ uniq = uniq_all + b * batch_n;
+  int32_t* __restrict__ seg = seg_all + b * (batch_n + 1);
+  int32_t* __restrict__ n_uniq = n_uniq_all + b;
   for (int i = threadIdx.x; i < n; i += kSortThreads) {
     kA[i] = (int32_t)keys[i];
     vA[i] = i;
@@ -95,11 +105,21 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
 // Same algorithm, global ping-pong buffers, processed in chunks of
 // kSortThreads*kIpt with running offsets (any n up to INT32_MAX).
 __global__ __launch_bounds__(kSortThreads) void segsort_global_kernel(
-    const int64_t* __restrict__ keys, int n, int nbits, int32_t* __restrict__ perm,
-    int32_t* __restrict__ uniq, int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq,
-    int32_t* __restrict__ kA, int32_t* __restrict__ vA, int32_t* __restrict__ kB,
-    int32_t* __restrict__ vB) {
+    const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n, int nbits,
+    int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all, int32_t* __restrict__ ws) {
   __shared__ int scan_lds[kSortThreads / 64 + 1];
+  const int64_t b = blockIdx.x;
+  const int n = (int)min((int64_t)batch_n, n_total - b * batch_n);
+  const int64_t* __restrict__ keys = keys_all + b * batch_n;
+  int32_t* __restrict__ perm = perm_all + b * batch_n;
+  int32_t* __restrict__ uniq = uniq_all + b * batch_n;
+  int32_t* __restrict__ seg = seg_all + b * (batch_n + 1);
+  int32_t* __restrict__ n_uniq = n_uniq_all + b;
+  int32_t* kA = ws + b * 4 * (int64_t)batch_n;
+  int32_t* vA = kA + batch_n;
+  int32_t* kB = vA + batch_n;
+  int32_t* vB = kB + batch_n;
   for (int i = threadIdx.x; i < n; i += kSortThreads) {
     kA[i] = (int32_t)keys[i];
     vA[i] = i;
@@ -173,34 +193,45 @@ extern "C" size_t mirec_segment_sort_workspace_size(int64_t n, int64_t key_space
   return (size_t)4 * (size_t)n * sizeof(int32_t) + 256;
 }
 
-extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
-                                  int32_t* perm, int32_t* uniq, int32_t* seg,
-                                  int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream) {
-  if (n < 0 || key_space <= 0 || key_space > INT32_MAX || n > INT32_MAX || !seg ||
-      !n_uniq_dev || (n > 0 && (!keys || !perm || !uniq))) {
+extern "C" int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
+                                          int64_t key_space, int32_t* perm, int32_t* uniq,
+                                          int32_t* seg, int32_t* n_uniq_dev, void* ws,
+                                          size_t ws_bytes, void* stream) {
+  if (n < 0 || key_space <= 0 || key_space > INT32_MAX || n > INT32_MAX || batch_n < 0 ||
+      !seg || !n_uniq_dev || (n > 0 && (!keys || !perm || !uniq || batch_n == 0))) {
     set_error("mirec_segment_sort: bad arguments");
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
-  const int nb = [&] {
-    int b = 0;
-    while (b < 31 && ((int64_t)1 << b) < key_space) ++b;
-    return b;
-  }();
-  if (n <= kLdsMax) {
-    hipLaunchKernelGGL(segsort_lds_kernel, dim3(1), dim3(kSortThreads), 0, st, keys, (int)n, nb,
-                       perm, uniq, seg, n_uniq_dev);
+  int nb = 0;
+  while (nb < 31 && ((int64_t)1 << nb) < key_space) ++nb;
+  if (n == 0) {  // one empty batch: seg[0] = 0, n_uniq = 0
+    hipLaunchKernelGGL(segsort_lds_kernel, dim3(1), dim3(kSortThreads), 0, st, keys, (int64_t)0,
+                       1, nb, perm, uniq, seg, n_uniq_dev);
+    return launch_status("mirec_segment_sort");
+  }
+  const int64_t n_batches = (n + batch_n - 1) / batch_n;
+  if (batch_n <= kLdsMax) {
+    hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)n_batches), dim3(kSortThreads), 0, st,
+                       keys, n, (int)batch_n, nb, perm, uniq, seg, n_uniq_dev);
   } else {
-    const size_t need = mirec_segment_sort_workspace_size(n, key_space);
+    const size_t need = (size_t)4 * (size_t)(n_batches * batch_n) * sizeof(int32_t);
     if (!ws || ws_bytes < need) {
       set_error("mirec_segment_sort: workspace %zu < %zu", ws_bytes, need);
       return -1;
     }
-    int32_t* b = (int32_t*)ws;
-    hipLaunchKernelGGL(segsort_global_kernel, dim3(1), dim3(kSortThreads), 0, st, keys, (int)n,
-                       nb, perm, uniq, seg, n_uniq_dev, b, b + n, b + 2 * n, b + 3 * n);
+    hipLaunchKernelGGL(segsort_global_kernel, dim3((unsigned)n_batches), dim3(kSortThreads), 0,
+                       st, keys, n, (int)batch_n, nb, perm, uniq, seg, n_uniq_dev,
+                       (int32_t*)ws);
   }
   return launch_status("mirec_segment_sort");
+}
+
+extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
+                                  int32_t* perm, int32_t* uniq, int32_t* seg,
+                                  int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream) {
+  return mirec_segment_sort_batched(keys, n, n > 0 ? n : 1, key_space, perm, uniq, seg,
+                                    n_uniq_dev, ws, ws_bytes, stream);
 }
 
 extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,

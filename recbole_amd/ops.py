@@ -29,7 +29,7 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
                 used_ptr: torch.Tensor | None, used_cols: torch.Tensor | None, n_key_space: int,
                 reject: bool, batch_keys: int | None = None, n_batches: int = 1,
                 out: torch.Tensor | None = None, status: torch.Tensor | None = None,
-                ws: torch.Tensor | None = None) -> torch.Tensor:
+                ws: torch.Tensor | None = None, out_stride: int = 0) -> torch.Tensor:
     """Bit-exact cyclic-walk negative sampling (sampler.py:82-154)."""
     _dev(random_list, torch.int32, "random_list")
     _dev(pr_dev, torch.int64, "pr_dev")
@@ -51,7 +51,8 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
                                  n_keys, batch_keys, n_batches, num,
                                  ptr(used_ptr) if reject else None,
                                  ptr(used_cols) if reject else None, n_key_space,
-                                 1 if reject else 0, ptr(out), ptr(status), ptr(ws), ws.numel(),
+                                 1 if reject else 0, ptr(out), out_stride, ptr(status), ptr(ws),
+                                 ws.numel(),
                                  stream_handle())
     check(rc, "mirec_sample_walk")
     return out
@@ -167,6 +168,22 @@ def segment_sort(keys: torch.Tensor, key_space: int, segs: Segments | None = Non
                                   stream_handle())
     check(rc, "mirec_segment_sort")
     return segs
+
+
+def segment_sort_batched(keys: torch.Tensor, batch_n: int, key_space: int, perm, uniq, seg,
+                         n_uniq, ws=None):
+    """K2 over consecutive batches of `batch_n` keys, one workgroup per batch."""
+    _dev(keys, torch.int64, "keys")
+    n = keys.numel()
+    nb = max(1, -(-n // max(batch_n, 1)))
+    wsz = lib().mirec_segment_sort_workspace_size(nb * batch_n, key_space)
+    if ws is None or ws.numel() < wsz:
+        ws = torch.empty(wsz, dtype=torch.uint8, device=keys.device)
+    rc = lib().mirec_segment_sort_batched(ptr(keys), n, batch_n, key_space, ptr(perm), ptr(uniq),
+                                          ptr(seg), ptr(n_uniq), ptr(ws), ws.numel(),
+                                          stream_handle())
+    check(rc, "mirec_segment_sort_batched")
+    return ws
 
 
 def segment_scatter_add(rows: torch.Tensor, segs: Segments, dense: torch.Tensor) -> torch.Tensor:

@@ -114,16 +114,17 @@ class AbstractSampler(object):
         return ops.sample_walk(self._rl_dev, self._pr_dev, keys, int(num), up, uc,
                                self.n_users, reject, status=self._status)
 
-    def launch_batches(self, keys_dev, batch_keys, n_batches, num, out):
+    def launch_batches(self, keys_dev, batch_keys, n_batches, num, out, out_stride=0, ws=None):
         """Walk `n_batches` consecutive batches in ONE kernel launch (the trainer's
-        ahead-of-time path); keys_dev are device user ids, out[b*batch_keys*num:]
-        receives batch b in the j*Kb + k layout."""
+        ahead-of-time path); keys_dev are device user ids, batch b's values land at
+        out[b*out_stride:] (default stride batch_keys*num) in the j*Kb + k layout."""
         if self._rl_dev is None:
             self.to_device(keys_dev.device)
         up, uc = self._used_dev()
         return ops.sample_walk(self._rl_dev, self._pr_dev, keys_dev, int(num), up, uc,
                                self.n_users, up is not None, batch_keys=batch_keys,
-                               n_batches=n_batches, out=out, status=self._status)
+                               n_batches=n_batches, out=out, status=self._status, ws=ws,
+                               out_stride=out_stride)
 
     def sample_by_user_ids(self, user_ids, num):
         """sampler.py:246-265: empty input returns None (the reference's IndexError

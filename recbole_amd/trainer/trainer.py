@@ -124,8 +124,10 @@ class Trainer(AbstractTrainer):
         self.model.train()
         if loss_func is None and self._fused_applicable(train_data):
             if self._fused_step is None or self._fused_step.data is not train_data:
-                self._fused_step = FusedBPRTrainStep(self.model, self.optimizer, train_data)
-            losses = self._fused_step.run_epoch(use_graph=bool(self.config['train_graph']))
+                self._fused_step = FusedBPRTrainStep(
+                    self.model, self.optimizer, train_data,
+                    use_graph=self.config['train_graph'] is not False)
+            losses = self._fused_step.run_epoch()
             total = None
             for v in losses:
                 total = v if total is None else total + v

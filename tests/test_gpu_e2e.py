@@ -50,11 +50,13 @@ def _pipeline(tmp_path, **over):
 
 def _oracle_train(init_u, init_i, users0, items0, rng_state, rl, used_ptr, used_cols, n_users,
                   B, T, epochs, lr):
-    torch.set_rng_state(rng_state)
+    # nn.Embedding's constructor draws from the CPU generator: build first, then
+    # restore the generator so the epoch permutations line up with the product's
     m = cpu_ref.BPRCPU(init_u.shape[0], init_i.shape[0], init_u.shape[1], init=False)
     m.user_embedding.weight.data.copy_(init_u)
     m.item_embedding.weight.data.copy_(init_i)
     opt = torch.optim.Adam(m.parameters(), lr=lr)
+    torch.set_rng_state(rng_state)
     users, items = users0.clone(), items0.clone()
     pr = 0
     epoch_losses = []
