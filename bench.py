@@ -54,7 +54,7 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
     return u[order], i[order], n_users + 1, n_items + 1
 
 
-def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020):
+def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred'):
     from recbole_amd.config import Config
     from recbole_amd.data import data_preparation
     from recbole_amd.data.dataset import Dataset
@@ -73,7 +73,50 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020):
     train, valid, test = data_preparation(config, ds)
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
-    return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train)
+    return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train,
+                                                              adam_mode=adam_mode)
+
+
+def roofline(step, events, uniq, d):
+    """Roofline of the dominant model-side kernel from the per-launch HIP events.
+
+    Algorithmic bytes per launch (fp32 rows of d floats, R = d*4 bytes):
+      adam/streamed  6 * (n_users + n_items) * R          (read+write p, m, v of every row)
+      adam/deferred  sum over tables of 6*u*R + c*R + 20*u + 4*c
+                     (touched rows u: p, m, v r+w, last r+w, uniq, seg; contributions
+                     c: grouped gradient rows + perm)
+      bpr            (B + (1+T)B) * R (embedding rows) + (B + (1+T)B) * R (gradients)
+                     + (B + (1+T)B) * 8 (ids) + B * 4 (losses)
+    """
+    per = {}
+    for name, a, b in events:
+        per.setdefault(name, []).append(a.elapsed_time(b) * 1e-3)
+    kernels_us = {k: round(float(np.mean(v)) * 1e6, 2) for k, v in per.items()}
+    R, B, T = d * 4, step.B, step.times
+    rowsI = (1 + T) * B
+    if step.adam_mode == 'streamed':
+        adam_bytes = 6 * (step.nU + step.nI) * R
+        adam_formula = '6 * (n_users + n_items) * d * 4 (read+write p, m, v of every row)'
+        adam_name = f'K5 adam_multi_kernel<{d}> (streamed dense Adam, user+item tables)'
+    else:
+        u = torch.stack(uniq).double().mean(0).cpu().numpy()
+        adam_bytes = float(6 * (u[0] + u[1]) * R + (B + rowsI) * R + 20 * (u[0] + u[1])
+                           + 4 * (B + rowsI))
+        adam_formula = (f'6*u*d*4 + c*d*4 + 20*u + 4*c summed over tables; mean touched rows '
+                        f'u = {u[0]:.1f} users + {u[1]:.1f} items, c = {B} + {rowsI}')
+        adam_name = f'K5 adam_deferred_kernel<{d}> (deferred dense Adam, user+item tables)'
+    bpr_bytes = 2 * (B + rowsI) * R + (B + rowsI) * 8 + B * 4
+    cands = {'adam': (adam_name, adam_bytes, adam_formula),
+             'bpr': (f'K3 bpr_fwd_bwd<{d}>', bpr_bytes,
+                     '2*(B+(1+T)B)*d*4 + 8*(B+(1+T)B) + 4*B')}
+    top = max(cands, key=lambda k: kernels_us.get(k, 0.0))
+    name, nbytes, formula = cands[top]
+    t = kernels_us[top] * 1e-6
+    gbs = nbytes / t / 1e9
+    return ({'kernel': name, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
+             'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+             'bytes_per_launch': round(nbytes), 'avg_launch_us': kernels_us[top],
+             'bytes_formula': formula}, kernels_us)
 
 
 def cpu_baseline(train, step_obj, d, neg, steps):
@@ -99,6 +142,7 @@ def main():
     ap.add_argument('--cpu-steps', type=int, default=20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-eval', action='store_true')
+    ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -114,7 +158,8 @@ def main():
 
     d, neg = 128, 4
     t_setup = time.time()
-    config, train, test, model, opt, step = build_workload(dev, d=d, neg=neg)
+    config, train, test, model, opt, step = build_workload(dev, d=d, neg=neg,
+                                                           adam_mode=args.adam_mode)
     setup_s = time.time() - t_setup
     nb = step.begin_epoch()
     K, W, M = args.steps, args.warmup, 32
@@ -127,6 +172,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     step.run_batches(W, W + K)
+    step.sync_params()          # deferred schedule: every row complete inside the timed region
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -137,22 +183,18 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # K5 (dense Adam over both tables in one launch, the dominant kernel): HIP
-    # events around each launch, on the stream it runs on, over M further steps
-    # launched eagerly behind a spin kernel so the events bracket kernel time
-    # only (not host enqueue gaps).
+    # Per-kernel HIP events around each model-side launch, on the stream it runs
+    # on, over M further steps launched eagerly behind a spin kernel so the
+    # events bracket kernel time only (not host enqueue gaps).
     torch.cuda._sleep(int(5e6))
-    step.kernel_events = []
+    step.kernel_events, step.kernel_uniq = [], []
     step.run_batches(W + K, W + K + M)
     torch.cuda.synchronize()
-    events = step.kernel_events
+    events, uniq = step.kernel_events, step.kernel_uniq
     step.kernel_events = None
     losses = step.end_epoch(W + K + M)
     assert all(np.isfinite(losses)), 'non-finite loss'
-    t_adam = float(np.mean([a.elapsed_time(b) for a, b in events])) * 1e-3
-    adam_bytes = 6 * (step.nU + step.nI) * d * 4
-    adam_gbs = adam_bytes / t_adam / 1e9
-
+    roof, kernels_us = roofline(step, events, uniq, d)
     positives = K * step.B * world
     result = {
         'metric': 'train positives/sec (+neg) per node',
@@ -174,12 +216,9 @@ def main():
                    'global_batch': step.B * world, 'train_interactions': int(
                        train.dataset.inter_num), 'parallelism': 'single' if world == 1
                    else f'replicas{world}'},
-        'roofline': {'kernel': 'K5 adam_multi_kernel<128> (dense Adam, user+item tables)',
-                     'bound': 'hbm', 'achieved': round(adam_gbs, 1), 'peak': HBM_PEAK_GBS,
-                     'unit': 'GB/s', 'frac': round(adam_gbs / HBM_PEAK_GBS, 4),
-                     'traffic': None, 'bytes_per_launch': adam_bytes,
-                     'avg_launch_us': round(t_adam * 1e6, 2),
-                     'bytes_formula': '6 * (n_users + n_items) * d * 4 (read+write p, m, v)'},
+        'roofline': roof,
+        'kernels_us': kernels_us,
+        'adam_mode': step.adam_mode,
         'setup_s': round(setup_s, 1),
     }
     if not args.no_eval and rank == 0:

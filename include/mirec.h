@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 1
+#define MIREC_ABI_VERSION 2
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -177,12 +177,41 @@ typedef struct mirec_adam_table {
   const int32_t* seg;
   const int32_t* n_uniq;    /* device counter; NULL = no grouped gradient  */
   const float* dense_grad;  /* optional dense gradient [n_rows, d] or NULL */
+  int32_t* last;            /* deferred schedule: steps applied per row    */
+  const int32_t* ahead_uniq;   /* deferred: rows the next batch reads, sorted */
+  const int32_t* ahead_n_uniq; /* device count of ahead_uniq (NULL = none)    */
 } mirec_adam_table;
 
+/* Streamed schedule: every row of every table, step index
+ * s = step_base_dev[0] + step_off (consts at 2s, 2s+1). `last` is ignored. */
 int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
-                         const float* step_consts_dev, const int32_t* step_idx_dev,
-                         double beta1, double beta2, double eps, double weight_decay,
-                         void* stream);
+                         const float* step_consts_dev, const int32_t* step_base_dev,
+                         int32_t step_off, double beta1, double beta2, double eps,
+                         double weight_decay, void* stream);
+
+/* Deferred schedule — bit-identical to the streamed one. Only the rows in each
+ * table's `uniq` are touched at step s = step_base_dev[0] + step_off: row r
+ * first replays steps last[r]..s-1 with a zero gradient (exactly the updates
+ * the streamed kernel would have applied), then applies step s with its
+ * gradient; last[r] = s + 1. Look-ahead: rows in ahead_uniq (the rows the
+ * next batch's forward pass reads) and not in uniq replay steps last[r]..s with
+ * a zero gradient; last[r] = s + 1 — so the next forward reads complete rows.
+ * n_max_uniq[q] (host array) bounds table q's n_uniq and ahead count (grid
+ * size). dense_grad must be NULL. Rows never touched lag until
+ * mirec_adam_flush_f32. */
+int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n_tables,
+                            const int64_t* n_max_uniq, int32_t d,
+                            const float* step_consts_dev, const int32_t* step_base_dev,
+                            int32_t step_off, double beta1, double beta2, double eps,
+                            double weight_decay, void* stream);
+
+/* Flush of the deferred schedule: every row r of every table with
+ * last[r] < t = step_base_dev[0] + step_off replays steps last[r]..t-1 with a
+ * zero gradient; last[r] = t. After it, p, m, v equal the streamed result. */
+int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                         const float* step_consts_dev, const int32_t* step_base_dev,
+                         int32_t step_off, double beta1, double beta2, double eps,
+                         double weight_decay, void* stream);
 
 /* End-of-step bookkeeping of Trainer._train_epoch (trainer.py:161-169):
  * loss_hist[step] = (sum of loss_k[0..n), fixed order) / denom, then
@@ -190,6 +219,12 @@ int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32
  * (read once per epoch) instead of a host sync per batch. */
 int mirec_step_finish(const float* loss_k, int64_t n, float denom, float* loss_hist,
                       int32_t* step_idx_dev, void* stream);
+
+/* The same for n_steps consecutive steps whose losses sit at
+ * loss_k[c*stride .. c*stride+n): loss_hist[step_base + c] (same reduction
+ * order as mirec_step_finish), then step_base_dev[0] += n_steps. */
+int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride, int32_t n_steps,
+                       float denom, float* loss_hist, int32_t* step_base_dev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K6  Full-sort scorer + mask + top-K + positive flags, fused (no [n,I] matrix).

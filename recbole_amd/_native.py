@@ -25,7 +25,8 @@ _P = c_void_p
 class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
-                ('perm', _P), ('uniq', _P), ('seg', _P), ('n_uniq', _P), ('dense_grad', _P)]
+                ('perm', _P), ('uniq', _P), ('seg', _P), ('n_uniq', _P), ('dense_grad', _P),
+                ('last', _P), ('ahead_uniq', _P), ('ahead_n_uniq', _P)]
 
 
 # Every symbol include/mirec.h declares: name -> (restype, argtypes)
@@ -51,14 +52,20 @@ SIGNATURES = {
                                            c_int64, _P, _P, _P, c_double, c_double, c_double,
                                            c_double, _P]),
     "mirec_adam_multi_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
-                                     c_double, c_double, c_double, c_double, _P]),
+                                     c_int32, c_double, c_double, c_double, c_double, _P]),
+    "mirec_adam_deferred_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, _P, c_int32, _P,
+                                        _P, c_int32, c_double, c_double, c_double, c_double,
+                                        _P]),
+    "mirec_adam_flush_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
+                                     c_int32, c_double, c_double, c_double, c_double, _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
+    "mirec_chunk_finish": (c_int, [_P, c_int64, c_int64, c_int32, c_float, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
                                         c_int32, _P, _P, _P, _P]),
     "mirec_score_matrix_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class NativeError(RuntimeError):

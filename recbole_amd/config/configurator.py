@@ -8,7 +8,9 @@ reference's float resolver) and command-line strings are parsed with
 ast.literal_eval instead of eval() — same results for literal values.
 
 New keys (MI355X build): ``n_gpus``, ``fused_train`` (use the fused HIP train
-step, default True), ``train_graph`` (capture steps in a HIP graph).
+step, default True), ``train_graph`` (capture steps in a HIP graph),
+``adam_mode`` ('deferred' | 'streamed': two bit-identical schedules of the dense
+Adam, see trainer/fused.py).
 """
 from __future__ import annotations
 

@@ -20,6 +20,7 @@ OVERALL = dict(
     metric_decimal_place=4,
     # MI355X build extensions
     n_gpus=1, fused_train=True, fused_eval=True, train_graph=True, profile=False,
+    adam_mode='deferred',
 )
 
 SAMPLE = dict(

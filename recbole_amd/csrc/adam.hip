@@ -1,75 +1,135 @@
-// K5 — dense Adam over every row of an embedding table in ONE streaming pass,
-// with the gradient supplied in grouped (compact) form.
+// K5 — dense Adam over every row of the embedding tables, with the gradient
+// supplied in grouped (compact) form. Two schedules, bit-identical results:
+//
+//  * streamed (adam_multi_kernel): one pass over p, m, v of EVERY row each step
+//    (6 * n_rows * d * 4 bytes per step, the HBM roofline of the step);
+//  * deferred (adam_deferred_kernel + adam_flush_kernel): a row whose gradient is
+//    zero at step s is advanced by exactly the same per-element operations as
+//    the streamed kernel would apply — but only when the row is next touched,
+//    or at a flush. `last[row]` counts the steps already applied to the row. A
+//    touch at step s replays steps last..s-1 with g = 0 and then applies step s;
+//    a flush replays every row up to the global step count. Same FLOPs, same
+//    bits, but each step only moves the rows it touches.
 //
 // Restates optim.Adam.step as the reference runs it (trainer.py:109-130, 173;
 // torch optim/adam.py _single_tensor_adam, CPU, foreach=False) on
 // nn.Embedding(sparse=False) weights: every row moves every step (rows with a
-// zero gradient still decay m and v and move p).  The dense gradient buffer
-// and its zero-fill are never materialised: the kernel reads p, m, v once and
-// writes them once (6 * n_rows * d * 4 bytes per step — the HBM roofline of
-// the whole training step at C2), and for the few rows present in `uniq` it
-// sums their contributions (grouped by K2) in a fixed order on the fly.
-//
-// Per element, in torch's order:
-//   g  = g + wd * p                       (grad.add(param, alpha=wd))
-//   m  = m + (1-b1) * (g - m)             (exp_avg.lerp_(grad, 1-b1), weight < .5)
-//   v  = v * b2 + ((1-b2) * g) * g        (mul_(b2).addcmul_(g, g, value=1-b2))
-//   p  = p + (-step_size) * (m / (sqrt(v) / bc2_sqrt + eps))   (addcdiv_)
-// step_size = lr / (1 - b1^t) and bc2_sqrt = sqrt(1 - b2^t) come from a host
-// table computed in double, indexed by the device step counter.
+// zero gradient still decay m and v and move p). Per element, torch's order and
+// rounding (fma where ATen's vectorised CPU kernels fuse):
+//   g  = fma(p, wd, g)                    (grad.add(param, alpha=wd))
+//   m  = fma(1-b1, g - m, m)              (exp_avg.lerp_(grad, 1-b1), weight < .5)
+//   v  = fma((1-b2) * g, g, v * b2)       (mul_(b2).addcmul_(g, g, value=1-b2))
+//   p  = p + ((-step_size) * m) / (sqrt(v) / bc2_sqrt + eps)   (addcdiv_)
+// This reproduces torch CPU's m, v and p bit-for-bit given the same sqrt; torch
+// CPU takes sqrt from the vendor vector math library (not always correctly
+// rounded), so p and v agree to an ulp there, exactly elsewhere.
+// step_size = lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t): a host table computed
+// in double, consts[2s], consts[2s+1] for the 0-based step index s.
 #include "common.h"
+
+// No FMA contraction: every op rounds on its own, as in torch's op-by-op
+// _single_tensor_adam, and the streamed / deferred schedules stay bit-identical
+// whatever the compiler could fuse in either context.
+#pragma clang fp contract(off)
 
 namespace mirec {
 
 constexpr int kAdamThreads = 256;
-constexpr int kAdamRows = 64;  // table rows per block
+constexpr int kAdamRows = 64;  // table rows per block (streamed / flush)
 constexpr int kMaxTables = 4;
 
 struct AdamConsts {
-  float omb1, b2, omb2, eps, wd;
+  float omb1, omb1m1, b2, omb2, eps, wd;
+  int lerp_small;  // 1 - beta1 < 0.5: lerp from m (torch's is_lerp_weight_small)
 };
 
-// Up to kMaxTables tables in one launch; blocks [block_start[t], block_start[t+1])
-// belong to table t (one grid over e.g. the user AND item tables, so the
-// smaller table does not run as its own under-filled launch).
+// Launch = a list of segments, each a contiguous block range over one table.
+// Streamed / flush: segment q = table q. Deferred: segment 2q = table q's
+// touched rows, 2q+1 = its look-ahead rows.
 struct AdamTables {
   mirec_adam_table t[kMaxTables];
-  int64_t block_start[kMaxTables + 1];
-  int n;
+  int64_t block_start[2 * kMaxTables + 1];
+  int n_seg;
 };
 
+// One Adam step of one element. Shared by every schedule so the arithmetic is
+// the same instruction sequence wherever a step is applied.
+// The fused multiply-adds are where torch's vectorised CPU kernels fuse
+// (add with alpha, lerp, addcmul); every other op rounds on its own.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float step_size,
+                                          float bc2s, const AdamConsts& k) {
+  if (k.wd != 0.f) g = fmaf(p, k.wd, g);
+  const float dlt = g - m;
+  const float me = k.lerp_small ? fmaf(k.omb1, dlt, m) : fmaf(k.omb1m1, dlt, g);
+  const float ve = fmaf(k.omb2 * g, g, v * k.b2);
+  const float den = sqrtf(ve) / bc2s + k.eps;
+  p = p + ((-step_size) * me) / den;
+  m = me;
+  v = ve;
+}
+
+__device__ __forceinline__ void adam_vec(float4& p, float4& m, float4& v, const float4& g,
+                                         float ss, float bc2s, const AdamConsts& k) {
+  adam_elem(p.x, m.x, v.x, g.x, ss, bc2s, k);
+  adam_elem(p.y, m.y, v.y, g.y, ss, bc2s, k);
+  adam_elem(p.z, m.z, v.z, g.z, ss, bc2s, k);
+  adam_elem(p.w, m.w, v.w, g.w, ss, bc2s, k);
+}
+
+// Replay steps [s0, s1) with a zero gradient (the exact per-step sequence).
+__device__ __forceinline__ void adam_replay(float4& p, float4& m, float4& v, int s0, int s1,
+                                            const float* __restrict__ consts,
+                                            const AdamConsts& k) {
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = s0; s < s1; ++s) adam_vec(p, m, v, z, consts[2 * s], consts[2 * s + 1], k);
+}
+
+__device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
+  int si = 0;
+#pragma unroll
+  for (int q = 1; q < 2 * kMaxTables; ++q)
+    if (q < tabs.n_seg && b >= tabs.block_start[q]) si = q;
+  return si;
+}
+
+// Sum of the grouped contributions of row slot s for float4 column c.
+__device__ __forceinline__ float4 grouped_grad(const mirec_adam_table& T, int s, int VPR, int c) {
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* __restrict__ R4 = reinterpret_cast<const float4*>(T.rows);
+  const int i1 = T.seg[s + 1];
+  for (int i = T.seg[s]; i < i1; ++i) {
+    const float4 x = R4[(int64_t)T.perm[i] * VPR + c];
+    g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+  }
+  return g;
+}
+
+// ---------------------------------------------------------------- streamed
 template <int D>
 __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
-    const AdamTables tabs, const float* __restrict__ step_consts,
-    const int32_t* __restrict__ step_idx, AdamConsts k) {
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k) {
   constexpr int VPR = D / 4;                        // float4 per row
   constexpr int RPP = kAdamThreads / VPR;           // rows per pass
   static_assert(kAdamThreads % VPR == 0, "row width");
   __shared__ int32_t slot[kAdamRows];
   __shared__ int32_t s_range[2];
 
-  int ti = 0;
-#pragma unroll
-  for (int q = 1; q < kMaxTables; ++q)
-    if (q < tabs.n && (int64_t)blockIdx.x >= tabs.block_start[q]) ti = q;
-  const mirec_adam_table& T = tabs.t[ti];
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si];
   float* __restrict__ P = T.p;
   float* __restrict__ M = T.m;
   float* __restrict__ V = T.v;
   const int32_t* __restrict__ uniq = T.uniq;
-  const int32_t* __restrict__ seg = T.seg;
-  const int32_t* __restrict__ perm = T.perm;
-  const float* __restrict__ dense_grad = T.dense_grad;
 
-  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[ti]) * kAdamRows;
+  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[si]) * kAdamRows;
   const int64_t hi = min(T.n_rows, lo + kAdamRows);
   if (threadIdx.x < kAdamRows) slot[threadIdx.x] = -1;
   if (threadIdx.x == 0) {
     const int nu = T.n_uniq ? T.n_uniq[0] : 0;
-    // lower_bound(uniq, lo), lower_bound(uniq, hi)
-    int a = 0, b = nu;
+    int a = 0, b = nu;                       // lower_bound(uniq, lo)
     while (a < b) { int mid = (a + b) >> 1; if (uniq[mid] < lo) a = mid + 1; else b = mid; }
-    int c = a, e = nu;
+    int c = a, e = nu;                       // lower_bound(uniq, hi)
     while (c < e) { int mid = (c + e) >> 1; if (uniq[mid] < hi) c = mid + 1; else e = mid; }
     s_range[0] = a;
     s_range[1] = c;
@@ -79,11 +139,9 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
     slot[uniq[u] - lo] = u;
   __syncthreads();
 
-  const int st = step_idx[0];
-  const float step_size = step_consts[2 * st];
-  const float bc2s = step_consts[2 * st + 1];
-  const float4* __restrict__ R4 = reinterpret_cast<const float4*>(T.rows);
-
+  const int st = step_base[0] + step_off;
+  const float ss = consts[2 * st];
+  const float bc2s = consts[2 * st + 1];
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
 #pragma unroll 2
@@ -93,30 +151,95 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
     float4 m = reinterpret_cast<const float4*>(M)[off];
     float4 v = reinterpret_cast<const float4*>(V)[off];
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (dense_grad) g = reinterpret_cast<const float4*>(dense_grad)[off];
+    if (T.dense_grad) g = reinterpret_cast<const float4*>(T.dense_grad)[off];
     const int s = slot[r - lo];
     if (s >= 0) {
-      const int i1 = seg[s + 1];
-      for (int i = seg[s]; i < i1; ++i) {
-        const float4 x = R4[(int64_t)perm[i] * VPR + c];
-        g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-      }
+      const float4 x = grouped_grad(T, s, VPR, c);
+      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
     }
-    float* pp = &p.x; float* mm = &m.x; float* vv = &v.x; float* gg = &g.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float ge = gg[e];
-      if (k.wd != 0.f) ge = ge + k.wd * pp[e];
-      const float me = mm[e] + k.omb1 * (ge - mm[e]);
-      const float ve = vv[e] * k.b2 + (k.omb2 * ge) * ge;
-      const float den = sqrtf(ve) / bc2s + k.eps;
-      pp[e] = pp[e] + (-step_size) * (me / den);
-      mm[e] = me;
-      vv[e] = ve;
-    }
+    adam_vec(p, m, v, g, ss, bc2s, k);
     reinterpret_cast<float4*>(P)[off] = p;
     reinterpret_cast<float4*>(M)[off] = m;
     reinterpret_cast<float4*>(V)[off] = v;
+  }
+}
+
+// ---------------------------------------------------------------- deferred
+// One thread per (row, float4 column); RPB rows per block.
+//  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
+//               zero gradient, applies step s with its gradient; last = s+1.
+//  segment 2q+1 (look-ahead): row = ahead_uniq[u], the rows the NEXT batch reads,
+//               unless also touched now (binary search in the sorted uniq).
+//               Replays last..s (zero gradient); last = s+1 — so the next
+//               forward pass reads rows that are complete through step s.
+// The two lists of a table are disjoint after the membership test: no row is
+// written by two threads.
+template <int D>
+__global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
+    const AdamTables tabs, const float* __restrict__ consts,
+    const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
+  constexpr int VPR = D / 4;
+  constexpr int RPB = kAdamThreads / VPR;           // rows per block
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si >> 1];
+  const bool ahead = si & 1;
+  const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
+  const int c = threadIdx.x % VPR;
+  const int nu = T.n_uniq[0];
+  int64_t row;
+  if (!ahead) {
+    if (u >= nu) return;
+    row = T.uniq[u];
+  } else {
+    if (u >= T.ahead_n_uniq[0]) return;
+    row = T.ahead_uniq[u];
+    int a = 0, b = nu;                              // lower_bound(uniq, row)
+    while (a < b) { const int mid = (a + b) >> 1; if (T.uniq[mid] < row) a = mid + 1; else b = mid; }
+    if (a < nu && T.uniq[a] == row) return;         // the touched segment owns it
+  }
+  const int st = step_base[0] + step_off;
+  const int last = T.last[row];
+  const int64_t off = row * VPR + c;
+  float4 p = reinterpret_cast<const float4*>(T.p)[off];
+  float4 m = reinterpret_cast<const float4*>(T.m)[off];
+  float4 v = reinterpret_cast<const float4*>(T.v)[off];
+  adam_replay(p, m, v, last, st, consts, k);       // the zero-gradient steps it skipped
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!ahead) g = grouped_grad(T, u, VPR, c);
+  adam_vec(p, m, v, g, consts[2 * st], consts[2 * st + 1], k);
+  reinterpret_cast<float4*>(T.p)[off] = p;
+  reinterpret_cast<float4*>(T.m)[off] = m;
+  reinterpret_cast<float4*>(T.v)[off] = v;
+  // every lane of this row read `last` above (same wave: VPR divides 64)
+  if (c == 0) T.last[row] = st + 1;
+}
+
+// Bring every row up to `n_steps` applied steps (zero-gradient replays).
+template <int D>
+__global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k) {
+  constexpr int VPR = D / 4;
+  constexpr int RPP = kAdamThreads / VPR;
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si];
+  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[si]) * kAdamRows;
+  const int64_t hi = min(T.n_rows, lo + kAdamRows);
+  const int target = step_base[0] + step_off;
+  const int rsub = threadIdx.x / VPR;
+  const int c = threadIdx.x % VPR;
+  for (int64_t r = lo + rsub; r < hi; r += RPP) {
+    const int last = T.last[r];
+    if (last >= target) continue;
+    const int64_t off = r * VPR + c;
+    float4 p = reinterpret_cast<const float4*>(T.p)[off];
+    float4 m = reinterpret_cast<const float4*>(T.m)[off];
+    float4 v = reinterpret_cast<const float4*>(T.v)[off];
+    adam_replay(p, m, v, last, target, consts, k);
+    reinterpret_cast<float4*>(T.p)[off] = p;
+    reinterpret_cast<float4*>(T.m)[off] = m;
+    reinterpret_cast<float4*>(T.v)[off] = v;
+    if (c == 0) T.last[r] = target;
   }
 }
 
@@ -124,58 +247,117 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 
 using namespace mirec;
 
-extern "C" int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
-                                    const float* step_consts_dev, const int32_t* step_idx_dev,
-                                    double beta1, double beta2, double eps, double weight_decay,
-                                    void* stream) {
-  if (n_tables < 1 || n_tables > kMaxTables || !tables || !step_consts_dev || !step_idx_dev) {
-    set_error("mirec_adam_multi_f32: bad arguments (n_tables=%d)", n_tables);
+namespace {
+
+enum class Sched { kStreamed, kDeferred, kFlush };
+
+int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
+                const int64_t* n_max_uniq, int32_t d, const float* consts,
+                const int32_t* step_base, int32_t step_off, double beta1, double beta2,
+                double eps, double weight_decay, void* stream, const char* what) {
+  if (n_tables < 1 || n_tables > kMaxTables || !tables || !consts || !step_base) {
+    set_error("%s: bad arguments (n_tables=%d)", what, n_tables);
     return -1;
   }
+  if (d != 4 && d != 16 && d != 32 && d != 64 && d != 128 && d != 256) {
+    set_error("%s: row width %d not in {4,16,32,64,128,256}", what, d);
+    return -1;
+  }
+  const int VPR = d / 4;
   AdamTables tabs;
   memset(&tabs, 0, sizeof(tabs));
-  tabs.n = n_tables;
+  const bool deferred = sched == Sched::kDeferred;
+  tabs.n_seg = deferred ? 2 * n_tables : n_tables;
   int64_t blocks = 0;
   for (int q = 0; q < n_tables; ++q) {
     const mirec_adam_table& t = tables[q];
+    const bool grouped = t.n_uniq != nullptr;
     if (!t.p || !t.m || !t.v || t.n_rows < 0 ||
-        (t.n_uniq && (!t.uniq || !t.seg || !t.perm || !t.rows))) {
-      set_error("mirec_adam_multi_f32: bad table %d", q);
+        (grouped && (!t.uniq || !t.seg || !t.perm || !t.rows)) ||
+        (sched != Sched::kStreamed && !t.last) ||
+        (deferred && (!grouped || t.dense_grad || !n_max_uniq || n_max_uniq[q] < 0)) ||
+        (deferred && (t.ahead_uniq == nullptr) != (t.ahead_n_uniq == nullptr))) {
+      set_error("%s: bad table %d", what, q);
       return -1;
     }
     tabs.t[q] = t;
-    tabs.block_start[q] = blocks;
-    blocks += (t.n_rows + kAdamRows - 1) / kAdamRows;
+    if (deferred) {
+      const int rpb = kAdamThreads / VPR;
+      const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
+      tabs.block_start[2 * q] = blocks;
+      blocks += nb;
+      tabs.block_start[2 * q + 1] = blocks;
+      if (t.ahead_uniq) blocks += nb;
+    } else {
+      tabs.block_start[q] = blocks;
+      blocks += (t.n_rows + kAdamRows - 1) / kAdamRows;
+    }
   }
-  tabs.block_start[n_tables] = blocks;
-  for (int q = n_tables + 1; q <= kMaxTables; ++q) tabs.block_start[q] = blocks;
+  for (int q = tabs.n_seg; q <= 2 * kMaxTables; ++q) tabs.block_start[q] = blocks;
   if (blocks == 0) return 0;
   AdamConsts k;
   k.omb1 = (float)(1.0 - beta1);
+  k.omb1m1 = k.omb1 - 1.0f;
+  k.lerp_small = fabsf(k.omb1) < 0.5f;
   k.b2 = (float)beta2;
   k.omb2 = (float)(1.0 - beta2);
   k.eps = (float)eps;
   k.wd = (float)weight_decay;
-  const dim3 grd((unsigned)blocks);
+  const dim3 grd((unsigned)blocks), blk(kAdamThreads);
   hipStream_t st = (hipStream_t)stream;
-#define MIREC_ADAM_CASE(DD)                                                                  \
+#define MIREC_ADAM_SCHED(DD)                                                                 \
   case DD:                                                                                   \
-    hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, dim3(kAdamThreads), 0, st, tabs,          \
-                       step_consts_dev, step_idx_dev, k);                                    \
+    if (sched == Sched::kStreamed)                                                           \
+      hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
+                         step_off, k);                                                       \
+    else if (sched == Sched::kDeferred)                                                      \
+      hipLaunchKernelGGL(adam_deferred_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base, \
+                         step_off, k);                                                       \
+    else                                                                                     \
+      hipLaunchKernelGGL(adam_flush_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
+                         step_off, k);                                                       \
     break;
   switch (d) {
-    MIREC_ADAM_CASE(4)
-    MIREC_ADAM_CASE(16)
-    MIREC_ADAM_CASE(32)
-    MIREC_ADAM_CASE(64)
-    MIREC_ADAM_CASE(128)
-    MIREC_ADAM_CASE(256)
-    default:
-      set_error("mirec_adam_multi_f32: row width %d not in {4,16,32,64,128,256}", d);
-      return -1;
+    MIREC_ADAM_SCHED(4)
+    MIREC_ADAM_SCHED(16)
+    MIREC_ADAM_SCHED(32)
+    MIREC_ADAM_SCHED(64)
+    MIREC_ADAM_SCHED(128)
+    MIREC_ADAM_SCHED(256)
   }
-#undef MIREC_ADAM_CASE
-  return launch_status("mirec_adam_multi_f32");
+#undef MIREC_ADAM_SCHED
+  return launch_status(what);
+}
+
+}  // namespace
+
+extern "C" int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                                    const float* step_consts_dev, const int32_t* step_base_dev,
+                                    int32_t step_off, double beta1, double beta2, double eps,
+                                    double weight_decay, void* stream) {
+  return launch_adam(Sched::kStreamed, tables, n_tables, nullptr, d, step_consts_dev,
+                     step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
+                     "mirec_adam_multi_f32");
+}
+
+extern "C" int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n_tables,
+                                       const int64_t* n_max_uniq, int32_t d,
+                                       const float* step_consts_dev,
+                                       const int32_t* step_base_dev, int32_t step_off,
+                                       double beta1, double beta2, double eps,
+                                       double weight_decay, void* stream) {
+  return launch_adam(Sched::kDeferred, tables, n_tables, n_max_uniq, d, step_consts_dev,
+                     step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
+                     "mirec_adam_deferred_f32");
+}
+
+extern "C" int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                                    const float* step_consts_dev, const int32_t* step_base_dev,
+                                    int32_t step_off, double beta1, double beta2, double eps,
+                                    double weight_decay, void* stream) {
+  return launch_adam(Sched::kFlush, tables, n_tables, nullptr, d, step_consts_dev,
+                     step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
+                     "mirec_adam_flush_f32");
 }
 
 extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows,
@@ -189,9 +371,10 @@ extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t 
   (void)n_max_uniq;
   if (n_rows == 0) return 0;
   mirec_adam_table t;
+  memset(&t, 0, sizeof(t));
   t.p = p; t.m = m; t.v = v; t.n_rows = n_rows;
   t.rows = rows; t.perm = perm; t.uniq = uniq; t.seg = seg; t.n_uniq = n_uniq_dev;
   t.dense_grad = dense_grad;
-  return mirec_adam_multi_f32(&t, 1, d, step_consts_dev, step_idx_dev, beta1, beta2, eps,
+  return mirec_adam_multi_f32(&t, 1, d, step_consts_dev, step_idx_dev, 0, beta1, beta2, eps,
                               weight_decay, stream);
 }

@@ -71,3 +71,34 @@ extern "C" int mirec_step_finish(const float* loss_k, int64_t n, float denom, fl
                      denom, loss_hist, step_idx_dev);
   return launch_status("mirec_step_finish");
 }
+
+// Per-chunk version: n_steps losses at loss_k[c*stride .. +n), each reduced in
+// exactly step_finish's order, written to loss_hist[step_base + c]; then
+// step_base += n_steps (one launch per chunk instead of one per step).
+__global__ __launch_bounds__(1024) void chunk_finish_kernel(const float* __restrict__ loss_k,
+                                                            int64_t n, int64_t stride,
+                                                            int32_t n_steps, float denom,
+                                                            float* __restrict__ loss_hist,
+                                                            int32_t* __restrict__ step_base) {
+  __shared__ float lds[1024];
+  const int32_t st = step_base[0];
+  for (int c = 0; c < n_steps; ++c) {
+    float s = block_fixed_sum(loss_k + (int64_t)c * stride, n, lds);
+    if (threadIdx.x == 0 && loss_hist) loss_hist[st + c] = s / denom;
+    __syncthreads();  // lds reused by the next reduction
+  }
+  if (threadIdx.x == 0) step_base[0] = st + n_steps;
+}
+
+extern "C" int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride,
+                                  int32_t n_steps, float denom, float* loss_hist,
+                                  int32_t* step_base_dev, void* stream) {
+  if (!step_base_dev || n < 0 || n_steps < 0 || stride < n || (n > 0 && n_steps > 0 && !loss_k)) {
+    set_error("mirec_chunk_finish: bad arguments");
+    return -1;
+  }
+  if (n_steps == 0) return 0;
+  hipLaunchKernelGGL(chunk_finish_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, loss_k, n,
+                     stride, n_steps, denom, loss_hist, step_base_dev);
+  return launch_status("mirec_chunk_finish");
+}

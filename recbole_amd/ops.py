@@ -225,6 +225,61 @@ def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None =
     check(rc, "mirec_adam_sparse_grad_f32")
 
 
+def adam_tables(specs):
+    """ctypes array of mirec_adam_table from dicts with keys p, m, v (2-D float32
+    tables of one width) and optional rows + segs (grouped gradient), dense_grad,
+    last (int32 per-row step counts of the deferred schedule), ahead (Segments of
+    the next batch: rows the deferred schedule completes for the next forward)."""
+    from recbole_amd._native import AdamTable
+    arr = (AdamTable * len(specs))()
+    for t, s in zip(arr, specs):
+        for n_ in ("p", "m", "v"):
+            _dev(s[n_], torch.float32, n_)
+        t.p, t.m, t.v, t.n_rows = ptr(s["p"]), ptr(s["m"]), ptr(s["v"]), s["p"].shape[0]
+        segs = s.get("segs")
+        if segs is not None:
+            _dev(s["rows"], torch.float32, "rows")
+            t.rows, t.perm, t.uniq = ptr(s["rows"]), ptr(segs.perm), ptr(segs.uniq)
+            t.seg, t.n_uniq = ptr(segs.seg), ptr(segs.n_uniq)
+        if s.get("dense_grad") is not None:
+            t.dense_grad = ptr(_dev(s["dense_grad"], torch.float32, "dense_grad"))
+        if s.get("last") is not None:
+            t.last = ptr(_dev(s["last"], torch.int32, "last"))
+        if s.get("ahead") is not None:
+            t.ahead_uniq, t.ahead_n_uniq = ptr(s["ahead"].uniq), ptr(s["ahead"].n_uniq)
+    return arr
+
+
+def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
+               schedule: str = "streamed", n_max_uniq=None, beta1=0.9, beta2=0.999, eps=1e-8,
+               weight_decay=0.0):
+    """K5 over several tables in one launch: schedule 'streamed' (every row),
+    'deferred' (touched rows, replaying skipped zero-gradient steps) or 'flush'."""
+    import ctypes
+    _dev(step_consts, torch.float32, "step_consts")
+    _dev(step_base, torch.int32, "step_base")
+    args = (ptr(step_consts), ptr(step_base), step_off, beta1, beta2, eps, weight_decay,
+            stream_handle())
+    if schedule == "streamed":
+        rc = lib().mirec_adam_multi_f32(tables, len(tables), d, *args)
+    elif schedule == "deferred":
+        nm = (ctypes.c_int64 * len(tables))(*n_max_uniq)
+        rc = lib().mirec_adam_deferred_f32(tables, len(tables), nm, d, *args)
+    elif schedule == "flush":
+        rc = lib().mirec_adam_flush_f32(tables, len(tables), d, *args)
+    else:
+        raise ValueError(f"unknown schedule {schedule!r}")
+    check(rc, f"adam_multi[{schedule}]")
+
+
+def chunk_finish(loss_k, n: int, stride: int, n_steps: int, denom: float, loss_hist, step_base):
+    _dev(loss_k, torch.float32, "loss_k")
+    _dev(step_base, torch.int32, "step_base")
+    rc = lib().mirec_chunk_finish(ptr(loss_k), n, stride, n_steps, float(denom), ptr(loss_hist),
+                                  ptr(step_base), stream_handle())
+    check(rc, "mirec_chunk_finish")
+
+
 def step_finish(loss_k, denom: float, loss_hist, step_idx):
     _dev(loss_k, torch.float32, "loss_k")
     _dev(step_idx, torch.int32, "step_idx")

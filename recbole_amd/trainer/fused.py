@@ -10,9 +10,11 @@ data side (depends only on ids; runs AHEAD on a side stream, CHUNK batches per l
   K2 segment sort  (embedding backward)   rows grouped by table row, one workgroup/batch
 model side (main stream, per batch)
   K3 fused BPR     (bpr.py:74-83)         loss rows + per-row gradients
-  K5 dense Adam    (optim.Adam.step)      every row of BOTH tables in one launch,
-                                           grouped gradients summed on the fly
-  step_finish                             per-step mean loss kept on the device
+  K5 dense Adam    (optim.Adam.step)      both tables in one launch, grouped gradients
+                                           summed on the fly; schedule 'deferred' (default)
+                                           or 'streamed', bit-identical (see adam.hip)
+  chunk_finish                            per-step mean losses kept on the device
+  K5 flush         ('deferred' only)      once per chunk: every row caught up
 
 The batch is a contiguous slice of the train table resident in HBM, shuffled
 once per epoch with torch.randperm on the CPU generator (interaction.py:272-276)
@@ -25,9 +27,18 @@ chunk is relative to its slot, and the Adam constants / loss history / step
 counter live in persistent device buffers, so the CHUNK steps of a slot are
 captured ONCE into a HIP graph and replayed for every chunk that lands in it
 (one host launch per CHUNK steps instead of three per step).
+
+Deferred Adam: the reference's dense Adam moves every row every step, but a row
+with a zero gradient moves as a function of its own (p, m, v) and the step
+constants only. The deferred schedule applies those zero-gradient steps when the
+row is next touched (or at the per-chunk flush), with the same per-element
+arithmetic, so the parameters after a flush are bit-identical to the streamed
+schedule's while a step moves only the rows its batch touches. Parameters are
+complete after end_epoch() / sync_params().
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -35,6 +46,8 @@ import torch
 
 from recbole_amd import ops
 from recbole_amd._native import AdamTable, check, lib
+
+ADAM_MODES = ('deferred', 'streamed')
 
 
 class _Slot(object):
@@ -64,7 +77,10 @@ class FusedBPRTrainStep(object):
 
     CHUNK = 64
 
-    def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True):
+    def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
+                 adam_mode='deferred'):
+        if adam_mode not in ADAM_MODES:
+            raise ValueError(f'adam_mode must be one of {ADAM_MODES}, got {adam_mode!r}')
         self.model = model
         self.opt = optimizer
         self.data = train_data
@@ -76,12 +92,13 @@ class FusedBPRTrainStep(object):
         self.iid_field = train_data.iid_field
         self.C = chunk or self.CHUNK
         self.use_graph = use_graph
+        self.adam_mode = adam_mode
         B, T, d = self.B, self.times, self.pU.shape[1]
         self.d = d
         dev = self.device
         self.gU = torch.empty(B, d, dtype=torch.float32, device=dev)
         self.gI = torch.empty((1 + T) * B, d, dtype=torch.float32, device=dev)
-        self.loss_k = torch.empty(B, dtype=torch.float32, device=dev)
+        self.loss_k = torch.empty(self.C * B, dtype=torch.float32, device=dev)
         self.slots = [_Slot(self.C, B, T, dev), _Slot(self.C, B, T, dev)]
         self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(B, T),
                                    dtype=torch.uint8, device=dev)
@@ -90,12 +107,18 @@ class FusedBPRTrainStep(object):
         self.loss_hist = torch.zeros(1, dtype=torch.float32, device=dev)
         self.consts = torch.zeros(2, dtype=torch.float32, device=dev)
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.kernel_events = None   # list -> HIP events around the K5 launches (bench.py)
+        self.kernel_events = None   # list -> (name, start, end) HIP events (bench.py)
+        self.kernel_uniq = []       # per eager step: [touched users, touched items]
         self.opt._ensure_state(self.pU)
         self.opt._ensure_state(self.pI)
         self._tables = (AdamTable * 2)()
+        if adam_mode == 'deferred':
+            self.lastU = torch.zeros(self.nU, dtype=torch.int32, device=dev)
+            self.lastI = torch.zeros(self.nI, dtype=torch.int32, device=dev)
+            self._n_max = (ctypes.c_int64 * 2)(B, (1 + T) * B)
         g = self.opt.param_groups[0]
         self._adam_args = (g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'])
+        self._fill_tables()
 
     # ------------------------------------------------------------------ data side
     def _chunks(self):
@@ -131,48 +154,101 @@ class FusedBPRTrainStep(object):
         slot.chunk = chunk
 
     # ------------------------------------------------------------------ model side
-    def _step(self, slot, c, Bc, stream):
-        """Model-side kernels of batch c of `slot` (batch size Bc); every pointer
-        is relative to the slot or a persistent buffer (graph-capturable)."""
+    def _fill_tables(self):
+        """Per-table pointers that do not depend on the batch."""
+        stU = self.opt.state[self.pU]
+        stI = self.opt.state[self.pI]
+        t = self._tables
+        t[0].p, t[0].m, t[0].v, t[0].n_rows = (self.pU.data_ptr(), stU['exp_avg'].data_ptr(),
+                                               stU['exp_avg_sq'].data_ptr(), self.nU)
+        t[1].p, t[1].m, t[1].v, t[1].n_rows = (self.pI.data_ptr(), stI['exp_avg'].data_ptr(),
+                                               stI['exp_avg_sq'].data_ptr(), self.nI)
+        t[0].rows, t[1].rows = self.gU.data_ptr(), self.gI.data_ptr()
+        t[0].dense_grad = t[1].dense_grad = None
+        if self.adam_mode == 'deferred':
+            t[0].last, t[1].last = self.lastU.data_ptr(), self.lastI.data_ptr()
+        else:
+            t[0].last = t[1].last = None
+
+    def _record(self, name, stream, fn):
+        ev = self.kernel_events
+        if ev is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        ev.append((name, e0, e1))
+
+    def _step(self, slot, c, Bc, stream, step_off, ahead):
+        """Model-side kernels of batch c of `slot` (batch size Bc) as optimizer
+        step step_idx + step_off; every pointer is relative to the slot or a
+        persistent buffer (graph-capturable). `ahead`: batch c+1 of the slot
+        runs next, so the deferred Adam also completes the rows it reads."""
         T = self.times
         KI = (1 + T) * Bc
         user_p = slot.user_keys.data_ptr() + 8 * c * Bc
         keys_p = slot.item_keys.data_ptr() + 8 * c * KI
         L = lib()
         st = stream.cuda_stream
-        rc = L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(), self.nI,
-                                     self.d, user_p, keys_p, keys_p + 8 * Bc, Bc, T, 1e-10,
-                                     self._grad_scale(Bc), self.loss_k.data_ptr(), None, None,
-                                     self.gU.data_ptr(), self.gI.data_ptr(), st)
-        check(rc, 'mirec_bpr_fwd_bwd_f32')
-        stU = self.opt.state[self.pU]
-        stI = self.opt.state[self.pI]
+        loss_p = self.loss_k.data_ptr() + 4 * c * self.B
+
+        def bpr():
+            check(L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
+                                          self.nI, self.d, user_p, keys_p, keys_p + 8 * Bc, Bc,
+                                          T, 1e-10, self._grad_scale(Bc), loss_p, None, None,
+                                          self.gU.data_ptr(), self.gI.data_ptr(), st),
+                  'mirec_bpr_fwd_bwd_f32')
+        self._record('bpr', stream, bpr)
         t = self._tables
-        t[0].p, t[0].m, t[0].v, t[0].n_rows = (self.pU.data_ptr(), stU['exp_avg'].data_ptr(),
-                                               stU['exp_avg_sq'].data_ptr(), self.nU)
-        t[0].rows, t[0].perm = self.gU.data_ptr(), slot.u_perm.data_ptr() + 4 * c * Bc
+        t[0].perm = slot.u_perm.data_ptr() + 4 * c * Bc
         t[0].uniq = slot.u_uniq.data_ptr() + 4 * c * Bc
         t[0].seg = slot.u_seg.data_ptr() + 4 * c * (Bc + 1)
-        t[0].n_uniq, t[0].dense_grad = slot.u_nu.data_ptr() + 4 * c, None
-        t[1].p, t[1].m, t[1].v, t[1].n_rows = (self.pI.data_ptr(), stI['exp_avg'].data_ptr(),
-                                               stI['exp_avg_sq'].data_ptr(), self.nI)
-        t[1].rows, t[1].perm = self.gI.data_ptr(), slot.i_perm.data_ptr() + 4 * c * KI
+        t[0].n_uniq = slot.u_nu.data_ptr() + 4 * c
+        t[1].perm = slot.i_perm.data_ptr() + 4 * c * KI
         t[1].uniq = slot.i_uniq.data_ptr() + 4 * c * KI
         t[1].seg = slot.i_seg.data_ptr() + 4 * c * (KI + 1)
-        t[1].n_uniq, t[1].dense_grad = slot.i_nu.data_ptr() + 4 * c, None
-        ev = self.kernel_events
-        if ev is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        rc = L.mirec_adam_multi_f32(t, 2, self.d, self.consts.data_ptr(),
-                                    self.step_idx.data_ptr(), *self._adam_args, st)
-        check(rc, 'mirec_adam_multi_f32')
-        if ev is not None:
-            e1.record(stream)
-            ev.append((e0, e1))
-        rc = L.mirec_step_finish(self.loss_k.data_ptr(), Bc, float(Bc * T),
-                                 self.loss_hist.data_ptr(), self.step_idx.data_ptr(), st)
-        check(rc, 'mirec_step_finish')
+        t[1].n_uniq = slot.i_nu.data_ptr() + 4 * c
+        if self.adam_mode == 'deferred' and ahead:
+            t[0].ahead_uniq = slot.u_uniq.data_ptr() + 4 * (c + 1) * Bc
+            t[0].ahead_n_uniq = slot.u_nu.data_ptr() + 4 * (c + 1)
+            t[1].ahead_uniq = slot.i_uniq.data_ptr() + 4 * (c + 1) * KI
+            t[1].ahead_n_uniq = slot.i_nu.data_ptr() + 4 * (c + 1)
+        else:
+            t[0].ahead_uniq = t[0].ahead_n_uniq = t[1].ahead_uniq = t[1].ahead_n_uniq = None
+
+        if self.adam_mode == 'deferred':
+            def adam():
+                check(L.mirec_adam_deferred_f32(t, 2, self._n_max, self.d, self.consts.data_ptr(),
+                                                self.step_idx.data_ptr(), step_off,
+                                                *self._adam_args, st), 'mirec_adam_deferred_f32')
+        else:
+            def adam():
+                check(L.mirec_adam_multi_f32(t, 2, self.d, self.consts.data_ptr(),
+                                             self.step_idx.data_ptr(), step_off,
+                                             *self._adam_args, st), 'mirec_adam_multi_f32')
+        self._record('adam', stream, adam)
+        if self.kernel_events is not None:       # rows touched, for the bench's byte count
+            self.kernel_uniq.append(torch.stack([slot.u_nu[c], slot.i_nu[c]]))
+
+    def _finish(self, c0, n_steps, Bc, stream):
+        """Losses of batches c0..c0+n_steps of the slot -> loss_hist; step_idx += n."""
+        rc = lib().mirec_chunk_finish(self.loss_k.data_ptr() + 4 * c0 * self.B, Bc, self.B,
+                                      n_steps, float(Bc * self.times),
+                                      self.loss_hist.data_ptr(), self.step_idx.data_ptr(),
+                                      stream.cuda_stream)
+        check(rc, 'mirec_chunk_finish')
+
+    def _flush(self, stream):
+        """Deferred schedule: bring every row to step_idx applied steps."""
+        if self.adam_mode != 'deferred':
+            return
+
+        def flush():
+            check(lib().mirec_adam_flush_f32(self._tables, 2, self.d, self.consts.data_ptr(),
+                                             self.step_idx.data_ptr(), 0, *self._adam_args,
+                                             stream.cuda_stream), 'mirec_adam_flush_f32')
+        self._record('flush', stream, flush)
 
     def _grad_scale(self, Bc):
         R = Bc * self.times
@@ -188,7 +264,9 @@ class FusedBPRTrainStep(object):
             cap.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=cap):
                 for c in range(self.C):
-                    self._step(slot, c, self.B, cap)
+                    self._step(slot, c, self.B, cap, c, c + 1 < self.C)
+                self._finish(0, self.C, self.B, cap)
+                self._flush(cap)
             torch.cuda.current_stream(self.device).wait_stream(cap)
             slot.graph = g
         return slot.graph
@@ -212,9 +290,17 @@ class FusedBPRTrainStep(object):
             self.loss_hist = torch.zeros(max(nb, 1), dtype=torch.float32, device=self.device)
             for s in self.slots:
                 s.graph = None
+        ptrs = [(t.p, t.m, t.v) for t in self._tables]
+        self._fill_tables()                    # optimizer state may have been reloaded
+        if ptrs != [(t.p, t.m, t.v) for t in self._tables]:
+            for s in self.slots:
+                s.graph = None
         self.consts[:table.size].copy_(torch.from_numpy(table))
         self.loss_hist.zero_()
         self.step_idx.zero_()
+        if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
+            self.lastU.zero_()
+            self.lastI.zero_()
         if self.use_graph and nb >= self.C:
             for s in self.slots:                # capture up front: capture synchronizes
                 self._graph_for(s)
@@ -249,7 +335,8 @@ class FusedBPRTrainStep(object):
 
     def run_batches(self, b_start, b_end):
         """Enqueue batches [b_start, b_end) in order (no host sync). Whole chunks
-        replay their captured graph; partial chunks launch eagerly."""
+        replay their captured graph; partial chunks launch eagerly, one step and
+        one loss bookkeeping launch at a time, flushing when a chunk completes."""
         stream = torch.cuda.current_stream(self.device)
         b = b_start
         while b < b_end:
@@ -263,7 +350,10 @@ class FusedBPRTrainStep(object):
                 self._graph_for(slot).replay()
             else:
                 for c in range(c0, c1):
-                    self._step(slot, c, Bc, stream)
+                    self._step(slot, c, Bc, stream, 0, c + 1 < nb)
+                    self._finish(c, 1, Bc, stream)
+                if c1 == nb:
+                    self._flush(stream)
             b = b0 + c1
 
     def launch_batch(self, b):
@@ -275,11 +365,17 @@ class FusedBPRTrainStep(object):
             return len(self._plan) - 1
         return b // self.C
 
+    def sync_params(self):
+        """Make the parameters current (deferred schedule: flush every row)."""
+        self._flush(torch.cuda.current_stream(self.device))
+
     def end_epoch(self, n_done=None):
-        """Account the optimizer steps and read the per-batch losses back (one sync)."""
+        """Complete the parameters, account the optimizer steps and read the
+        per-batch losses back (one sync)."""
         n_done = self.n_batches if n_done is None else n_done
         stream = torch.cuda.current_stream(self.device)
         stream.wait_stream(self.prep_stream)
+        self.sync_params()
         self.opt.advance(n_done)
         self.data.pr = 0
         return [float(x) for x in self.loss_hist[:n_done].cpu().numpy()]

@@ -126,7 +126,8 @@ class Trainer(AbstractTrainer):
             if self._fused_step is None or self._fused_step.data is not train_data:
                 self._fused_step = FusedBPRTrainStep(
                     self.model, self.optimizer, train_data,
-                    use_graph=self.config['train_graph'] is not False)
+                    use_graph=self.config['train_graph'] is not False,
+                    adam_mode=self.config['adam_mode'] or 'deferred')
             losses = self._fused_step.run_epoch()
             total = None
             for v in losses:

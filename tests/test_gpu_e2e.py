@@ -105,6 +105,31 @@ def test_fit_matches_oracle(tmp_path, fused):
                                m.item_embedding.weight.detach(), rtol=1e-3, atol=2e-5)
 
 
+def test_fused_adam_schedules_bitwise_identical(tmp_path):
+    """Deferred and streamed dense Adam, graph-replayed chunks and eager steps:
+    identical bits in the weights, the optimizer state and the losses."""
+    from recbole_amd.trainer.fused import FusedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    out = {}
+    for mode, graph in (('streamed', True), ('deferred', True), ('deferred', False)):
+        config, train, valid, test, model = _pipeline(tmp_path)
+        opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+        fs = FusedBPRTrainStep(model, opt, train, chunk=8, use_graph=graph, adam_mode=mode)
+        losses = []
+        for _ in range(2):
+            nb = fs.begin_epoch()
+            fs.run_batches(0, 11)                 # a graph chunk, then eager partial chunks
+            fs.run_batches(11, nb)
+            losses += fs.end_epoch()
+        st = [opt.state[p][k].cpu() for p in (fs.pU, fs.pI) for k in ('exp_avg', 'exp_avg_sq')]
+        out[(mode, graph)] = ([fs.pU.detach().cpu(), fs.pI.detach().cpu()] + st, losses)
+    ref_t, ref_l = out[('streamed', True)]
+    for key, (ts, ls) in out.items():
+        assert ls == ref_l, key
+        for a, b in zip(ref_t, ts):
+            assert torch.equal(a, b), key
+
+
 def test_fused_full_sort_eval_matches_generic(tmp_path):
     """The fused K6 evaluator and the reference's full_sort_predict + mask + swap +
     TopKEvaluator.collect sequence give identical metrics."""

@@ -282,6 +282,110 @@ def test_fused_adam_dense_step_matches_torch(dev):
         torch.testing.assert_close(m.detach().cpu(), r.detach(), rtol=RTOL, atol=1e-6)
 
 
+@pytest.mark.parametrize('d,beta1,wd', [(128, 0.9, 0.0), (32, 0.3, 0.01), (64, 0.9, 0.0)])
+def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
+    """The deferred schedule (touch + replay, flushes at irregular steps) leaves
+    p, m, v bit-identical to the streamed dense Adam over every row."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(d)
+    sizes, R, steps = (300, 517), (40, 200), 37
+    init = [torch.randn(n, d, generator=g) * 0.1 for n in sizes]
+    # a hot set touched often plus a cold tail touched rarely, as in a Zipf stream
+    batches = []
+    for s in range(steps):
+        ks = []
+        for n, r in zip(sizes, R):
+            hot = torch.randint(0, n // 10, (r // 2,), generator=g)
+            cold = torch.randint(0, n, (r - r // 2,), generator=g)
+            ks.append(torch.cat([hot, cold]))
+        batches.append([(k, torch.randn(k.numel(), d, generator=g) * 0.05) for k in ks])
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(1))], lr=1e-2, betas=(beta1, 0.999),
+                    weight_decay=wd)
+    consts = torch.from_numpy(opt.step_constants(1, steps).reshape(-1)).to(dev)
+
+    segs = [[ops.segment_sort(k.to(dev), sizes[q]) for q, (k, _) in enumerate(b)]
+            for b in batches]
+    snaps = []
+
+    def run(schedule, flush_at=(), check_ahead=False):
+        P = [x.clone().to(dev) for x in init]
+        M = [torch.zeros_like(x) for x in P]
+        V = [torch.zeros_like(x) for x in P]
+        last = [torch.zeros(x.shape[0], dtype=torch.int32, device=dev) for x in P]
+        base = torch.zeros(1, dtype=torch.int32, device=dev)
+        for s, batch in enumerate(batches):
+            specs = []
+            for q, (k, rows) in enumerate(batch):
+                specs.append(dict(p=P[q], m=M[q], v=V[q], rows=rows.to(dev), segs=segs[s][q],
+                                  last=last[q],
+                                  ahead=segs[s + 1][q] if s + 1 < steps else None))
+            tabs = ops.adam_tables(specs)
+            ops.adam_multi(tabs, d, consts, base, 0, schedule,
+                           n_max_uniq=[b[0].numel() for b in batch], beta1=beta1,
+                           weight_decay=wd)
+            base += 1
+            if s in flush_at:
+                ops.adam_multi(tabs, d, consts, base, 0, 'flush', beta1=beta1, weight_decay=wd)
+            if schedule == 'streamed':
+                snaps.append([x.cpu() for x in P])
+            elif check_ahead and s + 1 < steps:       # next forward reads complete rows
+                for q in range(2):
+                    k = batches[s + 1][q][0]
+                    assert torch.equal(P[q].cpu()[k], snaps[s][q][k]), (s, q)
+        if schedule == 'deferred':
+            ops.adam_multi(tabs, d, consts, base, 0, 'flush', beta1=beta1, weight_decay=wd)
+            assert all(bool((x == steps).all()) for x in last)
+        return [t.cpu() for t in P + M + V]
+
+    ref = run('streamed')
+    for flush_at, chk in (((), True), ((5, 6, 20), False)):
+        got = run('deferred', flush_at, chk)
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b), (a - b).abs().max()
+
+
+def test_adam_matches_torch_cpu_rounding(dev):
+    """m and v agree with torch CPU's Adam to the bit (same fma pattern); p to
+    the ulp the CPU's vector sqrt may differ by."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(7)
+    n, d = 256, 64
+    p0 = torch.randn(n, d, generator=g) * 0.1
+    ref = torch.nn.Parameter(p0.clone())
+    topt = torch.optim.Adam([ref], lr=1e-3, weight_decay=0.01)
+    mine = torch.nn.Parameter(p0.clone().to(dev))
+    fopt = FusedAdam([mine], lr=1e-3, weight_decay=0.01)
+    consts, idx = fopt.prepare_window(1, dev)
+    grad = torch.randn(n, d, generator=g) * 0.01
+    ref.grad = grad
+    topt.step()
+    fopt._ensure_state(mine)
+    st = fopt.state[mine]
+    ops.adam_step(mine.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
+                  dense_grad=grad.to(dev), weight_decay=0.01)
+    assert torch.equal(st['exp_avg'].cpu(), topt.state[ref]['exp_avg'])
+    torch.testing.assert_close(st['exp_avg_sq'].cpu(), topt.state[ref]['exp_avg_sq'],
+                               rtol=0, atol=0)
+    torch.testing.assert_close(mine.detach().cpu(), ref.detach(), rtol=3e-7, atol=1e-9)
+
+
+def test_chunk_finish_matches_step_finish(dev):
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(1)
+    C, B = 5, 300
+    loss = (torch.rand(C * 512, generator=g)).to(dev)
+    h1 = torch.zeros(8, device=dev)
+    h2 = torch.zeros(8, device=dev)
+    i1 = torch.full((1,), 2, dtype=torch.int32, device=dev)
+    i2 = i1.clone()
+    for c in range(C):
+        ops.step_finish(loss[c * 512:c * 512 + B].contiguous(), 1200.0, h1, i1)
+    ops.chunk_finish(loss, B, 512, C, 1200.0, h2, i2)
+    assert torch.equal(h1, h2) and int(i1) == int(i2) == 2 + C
+
+
 # ---------------------------------------------------------------- K6 full sort
 def _fullsort_case(rng, nq, I, d, K, max_hist=30, max_pos=8):
     U = rng.standard_normal((nq, d)).astype(np.float32)
