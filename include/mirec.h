@@ -47,18 +47,29 @@ const char* mirec_last_error(void);
  * Kb*num values at out + b*out_stride (out_stride 0 = batch_keys*num), so the
  * trainer can sample a chunk of future batches straight into their
  * [pos | neg] key rows.  used_ptr[n_key_space+1]/used_cols is a CSR of the
- * phase's used item ids per key, each row sorted ascending; reject==0 skips
- * the rejection (RepeatableSampler).  Returns -2 if a key is out of range
- * (the reference raises ValueError in sample_by_user_ids).
+ * phase's used item ids per key, each row sorted ascending; used_bits (or
+ * NULL) the same sets as a [n_key_space, ceil(n_bits/32)] bitmap built by
+ * mirec_used_bitmap_build — one load per membership test instead of a binary
+ * search; either representation gives identical results. reject==0 skips
+ * the rejection (RepeatableSampler).  Status -2: a key is out of range
+ * (the reference raises ValueError in sample_by_user_ids); -3: the walk did
+ * not terminate within 4*L+1024 refill rounds (the reference loops forever).
  * ------------------------------------------------------------------------- */
 size_t mirec_sample_walk_workspace_size(int64_t batch_keys, int64_t num);
 int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t* pr_dev,
                       const int64_t* keys, int64_t n_keys, int64_t batch_keys,
                       int64_t n_batches, int64_t num,
                       const int64_t* used_ptr, const int32_t* used_cols,
+                      const uint32_t* used_bits, int64_t n_bits,
                       int64_t n_key_space, int reject,
                       int64_t* out, int64_t out_stride, int32_t* status_dev,
                       void* ws, size_t ws_bytes, void* stream);
+
+/* Used-id bitmap of a CSR (sampler.py:206-227 used_ids as bits):
+ * bits[k * ceil(n_bits/32) + v/32] bit v%32 set iff v in used[k], v < n_bits. */
+size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits);
+int mirec_used_bitmap_build(const int64_t* used_ptr, const int32_t* used_cols, int64_t n_keys,
+                            int64_t n_bits, uint32_t* bits, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K1  Row gather (any row width, 16-B vectorised when aligned).

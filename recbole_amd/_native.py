@@ -35,7 +35,10 @@ SIGNATURES = {
     "mirec_last_error": (c_char_p, []),
     "mirec_sample_walk_workspace_size": (c_size_t, [c_int64, c_int64]),
     "mirec_sample_walk": (c_int, [_P, c_int64, _P, _P, c_int64, c_int64, c_int64, c_int64,
-                                  _P, _P, c_int64, c_int, _P, c_int64, _P, _P, c_size_t, _P]),
+                                  _P, _P, _P, c_int64, c_int64, c_int, _P, c_int64, _P, _P,
+                                  c_size_t, _P]),
+    "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
+    "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_gather_rows_i32idx": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,

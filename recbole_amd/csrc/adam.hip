@@ -92,13 +92,29 @@ __device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
   return si;
 }
 
-// Sum of the grouped contributions of row slot s for float4 column c.
+// Sum of the grouped contributions of row slot s for float4 column c, added in
+// perm order. Loads are issued 8 at a time (hot rows of a Zipf stream have
+// tens of contributions; a dependent chain of loads would serialise them);
+// the additions stay in order.
 __device__ __forceinline__ float4 grouped_grad(const mirec_adam_table& T, int s, int VPR, int c) {
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   const float4* __restrict__ R4 = reinterpret_cast<const float4*>(T.rows);
+  const int32_t* __restrict__ perm = T.perm;
+  int i = T.seg[s];
   const int i1 = T.seg[s + 1];
-  for (int i = T.seg[s]; i < i1; ++i) {
-    const float4 x = R4[(int64_t)T.perm[i] * VPR + c];
+  constexpr int U = 8;
+  for (; i + U <= i1; i += U) {
+    int32_t pi[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) pi[j] = perm[i + j];
+    float4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) x[j] = R4[(int64_t)pi[j] * VPR + c];
+#pragma unroll
+    for (int j = 0; j < U; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
+  }
+  for (; i < i1; ++i) {
+    const float4 x = R4[(int64_t)perm[i] * VPR + c];
     g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
   }
   return g;

@@ -9,8 +9,13 @@
 //             value[check] = random_num(len(check))
 // Both branches of sample_by_key_ids (single key / many keys) have exactly this
 // semantics. The walk is inherently sequential in `random_pr`, so one
-// workgroup walks the batches in order; the membership tests of a round run in
-// parallel over 1024 lanes and the refill order is a block prefix sum.
+// workgroup walks the batches in order: round 0 tests kPer consecutive slots
+// per lane (independent loads in flight) and one block scan orders the
+// rejected slots; refill rounds with more than 64 pending slots run over the
+// block, the tail (<= 64 pending, the common case) runs in ONE wave with
+// ballots and no block barrier. Pending lists and the batch's keys live in LDS.
+// Membership: a per-key bitmap (one load per test) when the caller provides
+// one, else binary search in the CSR of used ids.
 // The sampler only depends on the data pipeline (never on model state), so the
 // trainer runs it ahead of the model step on a side stream.
 #include "common.h"
@@ -18,48 +23,121 @@
 namespace mirec {
 
 constexpr int kSampThreads = 1024;
+constexpr int kPer = 4;          // round-0 slots per lane per pass
+constexpr int kListLds = 4096;   // pending-slot lists in LDS up to this many slots
+constexpr int kKeyLds = 4096;    // batch keys cached in LDS up to this many keys
+
+struct UsedSet {
+  const int64_t* ptr;
+  const int32_t* cols;
+  const uint32_t* bits;  // [n_keys, words] bitmap or NULL
+  int64_t words;
+  int64_t nbits;
+};
+
+__device__ __forceinline__ bool is_used(const UsedSet& u, int64_t key, int32_t v) {
+  if (u.bits)
+    return (uint64_t)(uint32_t)v < (uint64_t)u.nbits &&
+           ((u.bits[key * u.words + (v >> 5)] >> (v & 31)) & 1u);
+  return sorted_contains(u.cols, u.ptr[key], u.ptr[key + 1], v);
+}
+
+// Exclusive scan of 0/1 flags over the block with ballots: one barrier.
+// `lds` (blockDim/64 ints) must not be reused before the next block barrier.
+__device__ __forceinline__ int block_flag_scan(int flag, int* lds, int* total) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const uint64_t m = __ballot(flag);
+  const int pre = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) lds[wid] = __popcll(m);
+  __syncthreads();
+  int before = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int c = lds[w];
+    before += (w < wid) ? c : 0;
+    tot += c;
+  }
+  *total = tot;
+  return before + pre;
+}
 
 __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
     const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
-    int64_t num, const int64_t* __restrict__ used_ptr, const int32_t* __restrict__ used_cols,
-    int64_t key_space, int reject, int64_t* __restrict__ out, int64_t out_stride,
-    int32_t* __restrict__ status,
-    int32_t* __restrict__ rejA, int32_t* __restrict__ rejB) {
-  __shared__ int scan_lds[kSampThreads / 64 + 1];
+    int64_t num, UsedSet used, int64_t key_space, int reject, int64_t* __restrict__ out,
+    int64_t out_stride, int32_t* __restrict__ status, int32_t* __restrict__ rejA_g,
+    int32_t* __restrict__ rejB_g) {
+  __shared__ int scan_lds[2][kSampThreads / 64 + 1];
+  __shared__ int32_t listA[kListLds];
+  __shared__ int32_t listB[kListLds];
+  __shared__ int32_t key_lds[kKeyLds];
+  __shared__ int32_t wl[64];
+  __shared__ int64_t pr_lds;
+  const int lane = threadIdx.x & 63;
   int64_t pr = pr_dev[0] % L;
   int bad_key = 0;
+  int livelock = 0;
 
-  for (int64_t b = 0; b < n_batches; ++b) {
+  for (int64_t b = 0; b < n_batches && !livelock; ++b) {
     const int64_t k0 = b * batch_keys;
     const int64_t Kb = min(batch_keys, n_keys - k0);
     if (Kb <= 0) break;
     const int64_t total = Kb * num;
     const int64_t* __restrict__ bkeys = keys + k0;
     int64_t* __restrict__ bout = out + b * out_stride;
+    const bool lds_lists = total <= kListLds;
+    int32_t* cur = lds_lists ? listA : rejA_g;
+    int32_t* nxt = lds_lists ? listB : rejB_g;
+    const bool lds_keys = Kb <= kKeyLds;
+    if (reject && lds_keys) {
+      for (int64_t k = threadIdx.x; k < Kb; k += kSampThreads) {
+        const int64_t key = bkeys[k];
+        key_lds[k] = (key < 0 || key >= key_space) ? -1 : (int32_t)key;
+      }
+      __syncthreads();
+    }
+    // key of slot t (-1 = out of range)
+    auto key_of = [&](int64_t t) -> int64_t {
+      const int64_t k = t % Kb;
+      if (lds_keys) return key_lds[k];
+      const int64_t key = bkeys[k];
+      return (key < 0 || key >= key_space) ? -1 : key;
+    };
 
     // ---- round 0: fill every slot, collect rejected slots in ascending order
     int32_t nrej = 0;
-    for (int64_t base = 0; base < total; base += kSampThreads) {
-      const int64_t t = base + threadIdx.x;
-      int rej = 0;
-      if (t < total) {
-        int64_t pos = pr + t;
+    for (int64_t base = 0; base < total; base += (int64_t)kSampThreads * kPer) {
+      const int64_t t0 = base + (int64_t)threadIdx.x * kPer;
+      int32_t vals[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        int64_t pos = pr + t0 + j;
         if (pos >= L) pos %= L;
-        const int32_t v = rl[pos];
-        bout[t] = v;
-        if (reject) {
-          const int64_t key = bkeys[t % Kb];
-          if (key < 0 || key >= key_space) {
-            bad_key = 1;
-          } else {
-            rej = sorted_contains(used_cols, used_ptr[key], used_ptr[key + 1], v) ? 1 : 0;
+        vals[j] = (t0 + j < total) ? rl[pos] : 0;
+      }
+      int flags = 0, cnt = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int64_t t = t0 + j;
+        if (t < total) {
+          bout[t] = vals[j];
+          if (reject) {
+            const int64_t key = key_of(t);
+            if (key < 0) {
+              bad_key = 1;
+            } else if (is_used(used, key, vals[j])) {
+              flags |= 1 << j;
+              ++cnt;
+            }
           }
         }
       }
       int tot;
-      const int excl = block_exclusive_scan(rej, scan_lds, &tot);
-      if (rej) rejA[nrej + excl] = (int32_t)t;
+      int excl = block_exclusive_scan(cnt, scan_lds[0], &tot);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if ((flags >> j) & 1) cur[nrej + excl++] = (int32_t)(t0 + j);
       nrej += tot;
     }
     pr = (pr + total) % L;
@@ -69,15 +147,11 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     // The reference loops until no slot is rejected; on adversarial inputs
     // (a user whose free items all sit outside the walk positions its slots
     // can reach) that never ends. Give up after a bound and report -3.
-    int32_t* cur = rejA;
-    int32_t* nxt = rejB;
     int64_t rounds = 0;
     const int64_t max_rounds = 4 * L + 1024;
-    while (nrej > 0) {
-      if (++rounds > max_rounds) {
-        if (threadIdx.x == 0) atomicExch(status, -3);
-        break;
-      }
+    int sel = 0;
+    while (nrej > 64) {                       // wide rounds: whole block
+      if (++rounds > max_rounds) { livelock = 1; break; }
       int32_t nnew = 0;
       for (int32_t base = 0; base < nrej; base += kSampThreads) {
         const int32_t i = base + threadIdx.x;
@@ -89,11 +163,11 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
           if (pos >= L) pos %= L;
           const int32_t v = rl[pos];
           bout[t] = v;
-          const int64_t key = bkeys[t % Kb];
-          rej = sorted_contains(used_cols, used_ptr[key], used_ptr[key + 1], v) ? 1 : 0;
+          rej = is_used(used, key_of(t), v) ? 1 : 0;
         }
         int tot;
-        const int excl = block_exclusive_scan(rej, scan_lds, &tot);
+        const int excl = block_flag_scan(rej, scan_lds[sel], &tot);
+        sel ^= 1;
         if (rej) nxt[nnew + excl] = t;
         nnew += tot;
       }
@@ -102,10 +176,58 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
       nrej = nnew;
       __syncthreads();
     }
+    if (nrej > 0 && !livelock) {              // tail: one wave, no block barriers
+      if (threadIdx.x < 64) {
+        int n = nrej;
+        int64_t p = pr;
+        int32_t t = lane < n ? cur[lane] : 0;
+        int ll = 0;
+        while (n > 0) {
+          if (++rounds > max_rounds) { ll = 1; break; }
+          int rej = 0;
+          if (lane < n) {
+            int64_t pos = p + lane;
+            if (pos >= L) pos %= L;
+            const int32_t v = rl[pos];
+            bout[t] = v;
+            rej = is_used(used, key_of(t), v) ? 1 : 0;
+          }
+          const uint64_t m = __ballot(rej);
+          if (rej) wl[__popcll(m & ((1ull << lane) - 1ull))] = t;
+          __builtin_amdgcn_wave_barrier();
+          p = (p + n) % L;
+          n = __popcll(m);
+          t = lane < n ? wl[lane] : 0;
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (lane == 0) { pr_lds = p; scan_lds[1][kSampThreads / 64] = ll; }
+      }
+      __syncthreads();
+      pr = pr_lds;
+      livelock = scan_lds[1][kSampThreads / 64];
+    }
+    __syncthreads();                          // LDS lists / keys reused by the next batch
   }
   if (bad_key) atomicExch(status, -2);
+  if (livelock && threadIdx.x == 0) atomicExch(status, -3);
   __syncthreads();
   if (threadIdx.x == 0) pr_dev[0] = pr;
+}
+
+// bits[key, v>>5] |= 1 << (v & 31) for every used id; one wave per key.
+__global__ __launch_bounds__(256) void used_bitmap_kernel(const int64_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ cols,
+                                                          int64_t n_keys, int64_t words,
+                                                          int64_t nbits,
+                                                          uint32_t* __restrict__ bits) {
+  const int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (key >= n_keys) return;
+  const int64_t j1 = ptr[key + 1];
+  for (int64_t j = ptr[key] + (threadIdx.x & 63); j < j1; j += 64) {
+    const int32_t v = cols[j];
+    if ((uint64_t)(uint32_t)v < (uint64_t)nbits)
+      atomicOr(&bits[key * words + (v >> 5)], 1u << (v & 31));
+  }
 }
 
 }  // namespace mirec
@@ -117,21 +239,47 @@ extern "C" size_t mirec_sample_walk_workspace_size(int64_t batch_keys, int64_t n
   return (size_t)(2 * batch_keys * num) * sizeof(int32_t) + 256;
 }
 
+extern "C" size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits) {
+  if (n_keys <= 0 || n_bits <= 0) return 0;
+  return (size_t)n_keys * (size_t)((n_bits + 31) / 32) * sizeof(uint32_t);
+}
+
+extern "C" int mirec_used_bitmap_build(const int64_t* used_ptr, const int32_t* used_cols,
+                                       int64_t n_keys, int64_t n_bits, uint32_t* bits,
+                                       void* stream) {
+  if (!used_ptr || !used_cols || !bits || n_keys < 0 || n_bits <= 0) {
+    set_error("mirec_used_bitmap_build: bad arguments");
+    return -1;
+  }
+  if (n_keys == 0) return 0;
+  const int64_t words = (n_bits + 31) / 32;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(bits, 0, (size_t)n_keys * words * sizeof(uint32_t), st);
+  if (e != hipSuccess) return hip_status(e, "mirec_used_bitmap_build: memset");
+  hipLaunchKernelGGL(used_bitmap_kernel, dim3((unsigned)((n_keys + 3) / 4)), dim3(256), 0, st,
+                     used_ptr, used_cols, n_keys, words, n_bits, bits);
+  return launch_status("mirec_used_bitmap_build");
+}
+
 extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t* pr_dev,
                                  const int64_t* keys, int64_t n_keys, int64_t batch_keys,
                                  int64_t n_batches, int64_t num, const int64_t* used_ptr,
-                                 const int32_t* used_cols, int64_t n_key_space, int reject,
-                                 int64_t* out, int64_t out_stride, int32_t* status_dev, void* ws,
-                                 size_t ws_bytes,
-                                 void* stream) {
+                                 const int32_t* used_cols, const uint32_t* used_bits,
+                                 int64_t n_bits, int64_t n_key_space, int reject, int64_t* out,
+                                 int64_t out_stride, int32_t* status_dev, void* ws,
+                                 size_t ws_bytes, void* stream) {
   if (L <= 0 || !random_list || !pr_dev || !out || !status_dev || n_keys < 0 || num < 0 ||
       batch_keys <= 0 || n_batches < 0) {
     set_error("mirec_sample_walk: bad arguments (L=%lld)", (long long)L);
     return -1;
   }
   if (n_keys == 0 || num == 0 || n_batches == 0) return 0;
-  if (reject && (!used_ptr || !used_cols)) {
-    set_error("mirec_sample_walk: reject=1 needs the used-id CSR");
+  if (reject && ((!used_ptr || !used_cols) && !used_bits)) {
+    set_error("mirec_sample_walk: reject=1 needs the used-id CSR or bitmap");
+    return -1;
+  }
+  if (used_bits && n_bits <= 0) {
+    set_error("mirec_sample_walk: bitmap needs n_bits > 0");
     return -1;
   }
   if (batch_keys * num > INT32_MAX) {
@@ -146,8 +294,14 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
   if (out_stride == 0) out_stride = batch_keys * num;
   int32_t* rejA = (int32_t*)ws;
   int32_t* rejB = rejA + batch_keys * num;
+  UsedSet u;
+  u.ptr = used_ptr;
+  u.cols = used_cols;
+  u.bits = used_bits;
+  u.nbits = n_bits;
+  u.words = used_bits ? (n_bits + 31) / 32 : 0;
   hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, (hipStream_t)stream,
-                     random_list, L, pr_dev, keys, n_keys, batch_keys, n_batches, num, used_ptr,
-                     used_cols, n_key_space, reject, out, out_stride, status_dev, rejA, rejB);
+                     random_list, L, pr_dev, keys, n_keys, batch_keys, n_batches, num, u,
+                     n_key_space, reject, out, out_stride, status_dev, rejA, rejB);
   return launch_status("mirec_sample_walk");
 }

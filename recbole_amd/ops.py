@@ -29,8 +29,10 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
                 used_ptr: torch.Tensor | None, used_cols: torch.Tensor | None, n_key_space: int,
                 reject: bool, batch_keys: int | None = None, n_batches: int = 1,
                 out: torch.Tensor | None = None, status: torch.Tensor | None = None,
-                ws: torch.Tensor | None = None, out_stride: int = 0) -> torch.Tensor:
-    """Bit-exact cyclic-walk negative sampling (sampler.py:82-154)."""
+                ws: torch.Tensor | None = None, out_stride: int = 0,
+                used_bits: torch.Tensor | None = None, n_bits: int = 0) -> torch.Tensor:
+    """Bit-exact cyclic-walk negative sampling (sampler.py:82-154). Membership
+    comes from `used_bits` (see used_bitmap) when given, else the CSR."""
     _dev(random_list, torch.int32, "random_list")
     _dev(pr_dev, torch.int64, "pr_dev")
     _dev(keys, torch.int64, "keys")
@@ -41,21 +43,39 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
         out = torch.empty(n_keys * num, dtype=torch.int64, device=keys.device)
     if status is None:
         status = torch.zeros(1, dtype=torch.int32, device=keys.device)
-    if reject:
+    if reject and used_bits is None:
         _dev(used_ptr, torch.int64, "used_ptr")
         _dev(used_cols, torch.int32, "used_cols")
+    if reject and used_bits is not None:
+        _dev(used_bits, torch.int32, "used_bits")
     wsz = lib().mirec_sample_walk_workspace_size(batch_keys, num)
     if ws is None or ws.numel() < wsz:
         ws = torch.empty(wsz, dtype=torch.uint8, device=keys.device)
+    bits = reject and used_bits is not None
     rc = lib().mirec_sample_walk(ptr(random_list), random_list.numel(), ptr(pr_dev), ptr(keys),
                                  n_keys, batch_keys, n_batches, num,
-                                 ptr(used_ptr) if reject else None,
-                                 ptr(used_cols) if reject else None, n_key_space,
+                                 ptr(used_ptr) if reject and not bits else None,
+                                 ptr(used_cols) if reject and not bits else None,
+                                 ptr(used_bits) if bits else None, n_bits if bits else 0,
+                                 n_key_space,
                                  1 if reject else 0, ptr(out), out_stride, ptr(status), ptr(ws),
                                  ws.numel(),
                                  stream_handle())
     check(rc, "mirec_sample_walk")
     return out
+
+
+def used_bitmap(used_ptr: torch.Tensor, used_cols: torch.Tensor, n_keys: int,
+                n_bits: int) -> torch.Tensor:
+    """Per-key used-id bitmap [n_keys, ceil(n_bits/32)] (int32 words) of a CSR."""
+    _dev(used_ptr, torch.int64, "used_ptr")
+    _dev(used_cols, torch.int32, "used_cols")
+    words = (n_bits + 31) // 32
+    bits = torch.empty(max(n_keys * words, 1), dtype=torch.int32, device=used_ptr.device)
+    rc = lib().mirec_used_bitmap_build(ptr(used_ptr), ptr(used_cols), n_keys, n_bits, ptr(bits),
+                                       stream_handle())
+    check(rc, "mirec_used_bitmap_build")
+    return bits
 
 
 # ---------------------------------------------------------------- K1 gather

@@ -23,11 +23,13 @@ random_pr by one round first; ids < 0 wrap around there).
 from __future__ import annotations
 
 import copy
+import os
 
 import numpy as np
 import torch
 
 from recbole_amd import ops
+from recbole_amd._native import lib
 
 
 class AbstractSampler(object):
@@ -91,6 +93,24 @@ class AbstractSampler(object):
     def _used_dev(self):
         return None, None
 
+    def _used_bits(self):
+        return None, 0
+
+    def check_status(self):
+        """Raise what the walk reported since the last check (one host sync):
+        -2 a key outside [0, n_users) (the reference raises ValueError), -3 a walk
+        that did not terminate (the reference would loop forever)."""
+        if self._pr_dev is None:
+            return
+        s = int(self._status.item())
+        if s == 0:
+            return
+        self._status.zero_()
+        if s == -2:
+            raise ValueError('user_id out of range in negative sampling')
+        raise RuntimeError('negative sampling did not terminate: a user has no free item the '
+                           'walk over random_list can reach')
+
     def _default_device(self):
         if self.device is not None:
             return self.device
@@ -110,9 +130,13 @@ class AbstractSampler(object):
             keys = keys.view(1)
         keys = keys.to(device=self.device, dtype=torch.int64).contiguous()
         up, uc = self._used_dev()
+        bits, n_bits = self._used_bits()
         reject = up is not None
-        return ops.sample_walk(self._rl_dev, self._pr_dev, keys, int(num), up, uc,
-                               self.n_users, reject, status=self._status)
+        out = ops.sample_walk(self._rl_dev, self._pr_dev, keys, int(num), up, uc,
+                              self.n_users, reject, status=self._status, used_bits=bits,
+                              n_bits=n_bits)
+        self.check_status()
+        return out
 
     def launch_batches(self, keys_dev, batch_keys, n_batches, num, out, out_stride=0, ws=None):
         """Walk `n_batches` consecutive batches in ONE kernel launch (the trainer's
@@ -121,10 +145,11 @@ class AbstractSampler(object):
         if self._rl_dev is None:
             self.to_device(keys_dev.device)
         up, uc = self._used_dev()
+        bits, n_bits = self._used_bits()
         return ops.sample_walk(self._rl_dev, self._pr_dev, keys_dev, int(num), up, uc,
                                self.n_users, up is not None, batch_keys=batch_keys,
                                n_batches=n_batches, out=out, status=self._status, ws=ws,
-                               out_stride=out_stride)
+                               out_stride=out_stride, used_bits=bits, n_bits=n_bits)
 
     def sample_by_user_ids(self, user_ids, num):
         """sampler.py:246-265: empty input returns None (the reference's IndexError
@@ -216,6 +241,19 @@ class Sampler(AbstractSampler):
                 torch.as_tensor(ptr, device=self.device),
                 torch.as_tensor(cols if len(cols) else np.zeros(1, np.int32), device=self.device))
         return self._used_dev_cache[key]
+
+    # the used sets as a [n_users, ceil(n_items/32)] bitmap when it fits this many
+    # bytes of HBM (one load per membership test); else the CSR binary search
+    BITMAP_BUDGET = int(os.environ.get('MIREC_SAMPLER_BITMAP_MB', '4096')) << 20
+
+    def _used_bits(self):
+        if lib().mirec_used_bitmap_bytes(self.n_users, self.n_items) > self.BITMAP_BUDGET:
+            return None, 0
+        key = (self.phase, self.device, 'bits')
+        if key not in self._used_dev_cache:
+            up, uc = self._used_dev()
+            self._used_dev_cache[key] = ops.used_bitmap(up, uc, self.n_users, self.n_items)
+        return self._used_dev_cache[key], self.n_items
 
     @property
     def used_ids(self):

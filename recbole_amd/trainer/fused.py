@@ -378,6 +378,7 @@ class FusedBPRTrainStep(object):
         self.sync_params()
         self.opt.advance(n_done)
         self.data.pr = 0
+        self.data.sampler.check_status()
         return [float(x) for x in self.loss_hist[:n_done].cpu().numpy()]
 
     def run_epoch(self):

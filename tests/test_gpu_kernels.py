@@ -23,22 +23,34 @@ def _walk_dev(rl, ptr, cols, dev):
             torch.as_tensor(np.asarray(cols if len(cols) else [0], np.int32), device=dev))
 
 
+def _membership(up, uc, n_users, n_bits, bits):
+    """Sampler membership argument: the CSR alone, or the bitmap built from it."""
+    from recbole_amd import ops
+    if not bits:
+        return {}
+    return dict(used_bits=ops.used_bitmap(up, uc, n_users, n_bits), n_bits=n_bits)
+
+
 # ---------------------------------------------------------------- K4 sampler
-def test_sampler_golden_vectors(dev):
+@pytest.mark.parametrize('bits', [False, True])
+def test_sampler_golden_vectors(dev, bits):
     from recbole_amd import ops
     for c in json.load(open(os.path.join(GOLDEN, 'sampler_walk.json'))):
         rl, up, uc = _walk_dev(c['random_list'], c['used_ptr'], c['used_cols'], dev)
+        mem = _membership(up, uc, c['n_users'], int(max(c['random_list'])) + 1, bits)
         pr = torch.zeros(1, dtype=torch.int64, device=dev)
         for b in c['batches']:
             keys = torch.as_tensor(b['keys'], dtype=torch.int64, device=dev)
-            out = ops.sample_walk(rl, pr, keys, b['num'], up, uc, c['n_users'], True)
+            out = ops.sample_walk(rl, pr, keys, b['num'], up, uc, c['n_users'], True, **mem)
             assert out.cpu().tolist() == b['out']
             assert int(pr.item()) == b['pr']
 
 
+@pytest.mark.parametrize('bits', [False, True])
 @pytest.mark.parametrize('n_items,n_users,K,num', [(1683, 944, 2048, 1), (26745, 3000, 512, 4),
-                                                   (50, 20, 3000, 7), (7, 3, 5, 9)])
-def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num):
+                                                   (50, 20, 3000, 7), (7, 3, 5, 9),
+                                                   (300, 100, 5000, 1), (70, 10, 700, 3)])
+def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num, bits):
     from recbole_amd import ops
     rng = np.random.default_rng(n_items + K)
     deg = np.minimum(rng.integers(0, max(2, n_items // 2), n_users), n_items // 2)
@@ -47,6 +59,7 @@ def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num):
     ptr, cols = cpu_ref.used_csr(n_users, u, i)
     rl = rng.permutation(np.arange(1, n_items))
     drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
+    mem = _membership(dup, duc, n_users, n_items, bits)
     pr_d = torch.zeros(1, dtype=torch.int64, device=dev)
     pr = 0
     for b in range(5):
@@ -55,12 +68,13 @@ def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num):
             keys[:] = keys[0]                       # single-key branch
         exp, pr = cpu_ref.c_sample_walk(rl, pr, keys, num, ptr, cols, n_users, True)
         got = ops.sample_walk(drl, pr_d, torch.as_tensor(keys, device=dev), num, dup, duc,
-                              n_users, True)
+                              n_users, True, **mem)
         assert np.array_equal(got.cpu().numpy(), exp)
         assert int(pr_d.item()) == pr
 
 
-def test_sampler_multi_batch_launch_equals_sequential(dev):
+@pytest.mark.parametrize('bits', [False, True])
+def test_sampler_multi_batch_launch_equals_sequential(dev, bits):
     from recbole_amd import ops
     rng = np.random.default_rng(11)
     n_users, n_items, B, T, nb = 500, 3000, 256, 4, 7
@@ -78,7 +92,8 @@ def test_sampler_multi_batch_launch_equals_sequential(dev):
     pr_d = torch.zeros(1, dtype=torch.int64, device=dev)
     out = torch.empty(len(keys) * T, dtype=torch.int64, device=dev)
     ops.sample_walk(drl, pr_d, torch.as_tensor(keys, device=dev), T, dup, duc, n_users, True,
-                    batch_keys=B, n_batches=nb, out=out)
+                    batch_keys=B, n_batches=nb, out=out,
+                    **_membership(dup, duc, n_users, n_items, bits))
     assert np.array_equal(out.cpu().numpy(), np.concatenate(exp))
     assert int(pr_d.item()) == pr
 
@@ -95,15 +110,45 @@ def test_repeatable_sampler_no_rejection(dev):
     assert np.array_equal(got.cpu().numpy(), exp) and int(pr_d.item()) == pr
 
 
-def test_sampler_livelock_reports_status(dev):
+@pytest.mark.parametrize('bits', [False, True])
+def test_sampler_livelock_reports_status(dev, bits):
     from recbole_amd import ops
     rl = np.array([1, 2, 3, 4])
     ptr, cols = cpu_ref.used_csr(2, np.array([0, 0, 0, 1, 1, 1]), np.array([1, 3, 4, 2, 3, 4]))
     drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.sample_walk(drl, torch.zeros(1, dtype=torch.int64, device=dev),
-                    torch.tensor([0, 1], device=dev), 1, dup, duc, 2, True, status=status)
+                    torch.tensor([0, 1], device=dev), 1, dup, duc, 2, True, status=status,
+                    **_membership(dup, duc, 2, 5, bits))
     assert int(status.item()) == -3
+
+
+def test_sampler_bad_key_status(dev):
+    from recbole_amd import ops
+    rl = np.arange(1, 20)
+    ptr, cols = cpu_ref.used_csr(3, np.array([0, 1]), np.array([1, 2]))
+    drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.sample_walk(drl, torch.zeros(1, dtype=torch.int64, device=dev),
+                    torch.tensor([0, 7], device=dev), 2, dup, duc, 3, True, status=status)
+    assert int(status.item()) == -2
+
+
+def test_used_bitmap_matches_csr(dev):
+    from recbole_amd import ops
+    rng = np.random.default_rng(3)
+    n_users, n_items = 37, 1000
+    u = rng.integers(0, n_users, 5000)
+    i = rng.integers(0, n_items, 5000)
+    ptr, cols = cpu_ref.used_csr(n_users, u, i)
+    _, dup, duc = _walk_dev([1], ptr, cols, dev)
+    bits = ops.used_bitmap(dup, duc, n_users, n_items).cpu().numpy().view(np.uint32)
+    words = (n_items + 31) // 32
+    dense = np.unpackbits(bits.reshape(n_users, words).view(np.uint8), axis=1,
+                          bitorder='little')[:, :n_items].astype(bool)
+    exp = np.zeros((n_users, n_items), bool)
+    exp[u, i] = True
+    assert np.array_equal(dense, exp)
 
 
 def test_sampler_api_mirror(dev):
