@@ -137,8 +137,9 @@ def cpu_baseline(train, step_obj, d, neg, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
-    ap.add_argument('--warmup', type=int, default=20)
+    # defaults are whole chunks (FusedBPRTrainStep.CHUNK = 64 steps per HIP graph)
+    ap.add_argument('--steps', type=int, default=256)
+    ap.add_argument('--warmup', type=int, default=64)
     ap.add_argument('--cpu-steps', type=int, default=20)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-eval', action='store_true')

@@ -139,7 +139,14 @@ int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
                                int64_t key_space, int32_t* perm, int32_t* uniq, int32_t* seg,
                                int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
 
-/* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :]  (fixed order)
+/* Look-ahead lists of the deferred Adam: for b < n_batches-1,
+ * out[b*stride ..) = uniq(b+1) \ uniq(b) ascending, n_out[b] its length, where
+ * uniq(b) = uniq[b*stride .. + n_uniq[b]) (the batched segment-sort layout);
+ * n_out[n_batches-1] = 0. */
+int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t stride,
+                          int64_t n_batches, int32_t* out, int32_t* n_out, void* stream);
+
+/* dense[uniq[u], :] +=sum_{i in seg[u]..seg[u+1]} rows[perm[i], :]  (fixed order)
  * — the dense-gradient form used by the autograd-compatible path. */
 int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
                                   const int32_t* uniq, const int32_t* seg,
@@ -157,13 +164,13 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
  * (+ dense_grad[row] when dense_grad != NULL; the grouped part may be omitted
  * with n_uniq_dev == NULL) (+ wd*p).  d in {4,16,32,64,128,256} floats per row
  * (any tensor whose numel % 4 == 0 can be viewed as [numel/4, 4]).
- * Per element (torch order):
- *   m = m + (1-b1)*(g-m);  v = v*b2 + (1-b2)*g*g;
- *   p = p - step_size * m / (sqrt(v)/bc2_sqrt + eps)
- * step_consts_dev[2*step_idx_dev[0] + {0,1}] = {step_size, bc2_sqrt} (float),
- * precomputed on the host in double like torch does; step_idx_dev is a device
- * counter (advanced by mirec_step_finish) so that a captured graph replays
- * successive optimizer steps.
+ * Per element (torch's order and rounding, see adam.hip):
+ *   g = fma(p, wd, g);  m = fma(1-b1, g-m, m);  v = fma((1-b2)*g, g, v*b2);
+ *   p = p + ((-step_size) * m) / (sqrt(v)/bc2_sqrt + eps)
+ * step_consts_dev (16-byte aligned) holds 4 floats per 0-based step index s:
+ * {step_size, bc2_sqrt, RN(1/bc2_sqrt), 0}, precomputed on the host in double
+ * like torch does; step s = step_idx_dev[0] is a device counter (advanced by
+ * mirec_step_finish) so that a captured graph replays successive steps.
  * ------------------------------------------------------------------------- */
 int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
                                const float* rows, const int32_t* perm,

@@ -20,11 +20,18 @@
 //   m  = fma(1-b1, g - m, m)              (exp_avg.lerp_(grad, 1-b1), weight < .5)
 //   v  = fma((1-b2) * g, g, v * b2)       (mul_(b2).addcmul_(g, g, value=1-b2))
 //   p  = p + ((-step_size) * m) / (sqrt(v) / bc2_sqrt + eps)   (addcdiv_)
-// This reproduces torch CPU's m, v and p bit-for-bit given the same sqrt; torch
-// CPU takes sqrt from the vendor vector math library (not always correctly
-// rounded), so p and v agree to an ulp there, exactly elsewhere.
-// step_size = lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t): a host table computed
-// in double, consts[2s], consts[2s+1] for the 0-based step index s.
+// Every other op is one IEEE-rounded fp32 operation (sqrt and / correctly
+// rounded). This reproduces torch CPU's m, v and p bit-for-bit given the same
+// sqrt; torch CPU takes sqrt from the vendor vector math library (not always
+// correctly rounded), so p agrees to an ulp there, exactly elsewhere.
+//
+// Host table (float32, 4 per 0-based step index s), computed in double like
+// torch: {step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t), rbc = RN(1/bc2_sqrt), 0}.
+// x / bc2_sqrt is evaluated as q = x*rbc; q + fma(-q, bc2_sqrt, x)*rbc (fma):
+// with rbc the correctly rounded reciprocal this is the correctly rounded
+// quotient (Markstein's theorem; checked exhaustively over two binades of x for
+// ~13k divisors of several beta2), i.e. bit-identical to IEEE division in 3
+// instead of ~11 instructions. x = +inf takes the IEEE division.
 #include "common.h"
 
 // No FMA contraction: every op rounds on its own, as in torch's op-by-op
@@ -43,6 +50,15 @@ struct AdamConsts {
   int lerp_small;  // 1 - beta1 < 0.5: lerp from m (torch's is_lerp_weight_small)
 };
 
+struct StepConsts {
+  float ss, bc2s, rbc;
+};
+
+__device__ __forceinline__ StepConsts step_consts(const float* __restrict__ consts, int s) {
+  const float4 c = reinterpret_cast<const float4*>(consts)[s];
+  return {c.x, c.y, c.z};
+}
+
 // Launch = a list of segments, each a contiguous block range over one table.
 // Streamed / flush: segment q = table q. Deferred: segment 2q = table q's
 // touched rows, 2q+1 = its look-ahead rows.
@@ -54,26 +70,28 @@ struct AdamTables {
 
 // One Adam step of one element. Shared by every schedule so the arithmetic is
 // the same instruction sequence wherever a step is applied.
-// The fused multiply-adds are where torch's vectorised CPU kernels fuse
-// (add with alpha, lerp, addcmul); every other op rounds on its own.
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float step_size,
-                                          float bc2s, const AdamConsts& k) {
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
+                                          const StepConsts& sc, const AdamConsts& k) {
   if (k.wd != 0.f) g = fmaf(p, k.wd, g);
   const float dlt = g - m;
   const float me = k.lerp_small ? fmaf(k.omb1, dlt, m) : fmaf(k.omb1m1, dlt, g);
   const float ve = fmaf(k.omb2 * g, g, v * k.b2);
-  const float den = sqrtf(ve) / bc2s + k.eps;
-  p = p + ((-step_size) * me) / den;
+  const float x = sqrtf(ve);
+  float q = x * sc.rbc;                       // x / bc2s, correctly rounded
+  q = fmaf(fmaf(-q, sc.bc2s, x), sc.rbc, q);
+  if (__builtin_expect(x == __builtin_inff(), 0)) q = x / sc.bc2s;
+  const float den = q + k.eps;
+  p = p + ((-sc.ss) * me) / den;
   m = me;
   v = ve;
 }
 
 __device__ __forceinline__ void adam_vec(float4& p, float4& m, float4& v, const float4& g,
-                                         float ss, float bc2s, const AdamConsts& k) {
-  adam_elem(p.x, m.x, v.x, g.x, ss, bc2s, k);
-  adam_elem(p.y, m.y, v.y, g.y, ss, bc2s, k);
-  adam_elem(p.z, m.z, v.z, g.z, ss, bc2s, k);
-  adam_elem(p.w, m.w, v.w, g.w, ss, bc2s, k);
+                                         const StepConsts& sc, const AdamConsts& k) {
+  adam_elem(p.x, m.x, v.x, g.x, sc, k);
+  adam_elem(p.y, m.y, v.y, g.y, sc, k);
+  adam_elem(p.z, m.z, v.z, g.z, sc, k);
+  adam_elem(p.w, m.w, v.w, g.w, sc, k);
 }
 
 // Replay steps [s0, s1) with a zero gradient (the exact per-step sequence).
@@ -81,7 +99,13 @@ __device__ __forceinline__ void adam_replay(float4& p, float4& m, float4& v, int
                                             const float* __restrict__ consts,
                                             const AdamConsts& k) {
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = s0; s < s1; ++s) adam_vec(p, m, v, z, consts[2 * s], consts[2 * s + 1], k);
+  for (int s = s0; s < s1; ++s) adam_vec(p, m, v, z, step_consts(consts, s), k);
+}
+
+__device__ __forceinline__ void adam_replay1(float& p, float& m, float& v, int s0, int s1,
+                                             const float* __restrict__ consts,
+                                             const AdamConsts& k) {
+  for (int s = s0; s < s1; ++s) adam_elem(p, m, v, 0.f, step_consts(consts, s), k);
 }
 
 __device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
@@ -92,13 +116,25 @@ __device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
   return si;
 }
 
-// Sum of the grouped contributions of row slot s for float4 column c, added in
-// perm order. Loads are issued 8 at a time (hot rows of a Zipf stream have
-// tens of contributions; a dependent chain of loads would serialise them);
-// the additions stay in order.
-__device__ __forceinline__ float4 grouped_grad(const mirec_adam_table& T, int s, int VPR, int c) {
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4* __restrict__ R4 = reinterpret_cast<const float4*>(T.rows);
+// Sum of the grouped contributions of row slot s, in perm order, for the W
+// consecutive floats starting at column c (W = 4: float4, W = 1: float).
+// Loads are issued 8 at a time (hot rows of a Zipf stream have tens of
+// contributions; a dependent chain of loads would serialise them); the
+// additions stay in order.
+template <typename V>
+__device__ __forceinline__ void vadd(V& a, const V& b);
+template <>
+__device__ __forceinline__ void vadd<float4>(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+template <>
+__device__ __forceinline__ void vadd<float>(float& a, const float& b) { a += b; }
+
+template <typename V>
+__device__ __forceinline__ V grouped_grad(const mirec_adam_table& T, int s, int VPR, int c) {
+  V g;
+  memset(&g, 0, sizeof(V));
+  const V* __restrict__ R = reinterpret_cast<const V*>(T.rows);
   const int32_t* __restrict__ perm = T.perm;
   int i = T.seg[s];
   const int i1 = T.seg[s + 1];
@@ -107,16 +143,13 @@ __device__ __forceinline__ float4 grouped_grad(const mirec_adam_table& T, int s,
     int32_t pi[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) pi[j] = perm[i + j];
-    float4 x[U];
+    V x[U];
 #pragma unroll
-    for (int j = 0; j < U; ++j) x[j] = R4[(int64_t)pi[j] * VPR + c];
+    for (int j = 0; j < U; ++j) x[j] = R[(int64_t)pi[j] * VPR + c];
 #pragma unroll
-    for (int j = 0; j < U; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
+    for (int j = 0; j < U; ++j) vadd(g, x[j]);
   }
-  for (; i < i1; ++i) {
-    const float4 x = R4[(int64_t)perm[i] * VPR + c];
-    g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-  }
+  for (; i < i1; ++i) vadd(g, R[(int64_t)perm[i] * VPR + c]);
   return g;
 }
 
@@ -155,9 +188,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
     slot[uniq[u] - lo] = u;
   __syncthreads();
 
-  const int st = step_base[0] + step_off;
-  const float ss = consts[2 * st];
-  const float bc2s = consts[2 * st + 1];
+  const StepConsts sc = step_consts(consts, step_base[0] + step_off);
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
 #pragma unroll 2
@@ -169,11 +200,8 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     if (T.dense_grad) g = reinterpret_cast<const float4*>(T.dense_grad)[off];
     const int s = slot[r - lo];
-    if (s >= 0) {
-      const float4 x = grouped_grad(T, s, VPR, c);
-      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-    }
-    adam_vec(p, m, v, g, ss, bc2s, k);
+    if (s >= 0) vadd(g, grouped_grad<float4>(T, s, VPR, c));
+    adam_vec(p, m, v, g, sc, k);
     reinterpret_cast<float4*>(P)[off] = p;
     reinterpret_cast<float4*>(M)[off] = m;
     reinterpret_cast<float4*>(V)[off] = v;
@@ -181,52 +209,46 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 }
 
 // ---------------------------------------------------------------- deferred
-// One thread per (row, float4 column); RPB rows per block.
+// One thread per (row, column): the replay of a row's skipped steps is a
+// serial chain per element, so one element per thread keeps the chain short.
+// RPB = 256 / D whole rows per block.
 //  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
 //               zero gradient, applies step s with its gradient; last = s+1.
-//  segment 2q+1 (look-ahead): row = ahead_uniq[u], the rows the NEXT batch reads,
-//               unless also touched now (binary search in the sorted uniq).
+//  segment 2q+1 (look-ahead): row = ahead_uniq[u], rows the NEXT batch reads
+//               and this one does not touch (the caller's set difference).
 //               Replays last..s (zero gradient); last = s+1 — so the next
 //               forward pass reads rows that are complete through step s.
-// The two lists of a table are disjoint after the membership test: no row is
-// written by two threads.
+// `last` is read by every thread of a row before the barrier and written
+// after it (a row of D >= 128 spans several waves).
 template <int D>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     const AdamTables tabs, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
-  constexpr int VPR = D / 4;
-  constexpr int RPB = kAdamThreads / VPR;           // rows per block
+  constexpr int RPB = kAdamThreads / D;             // rows per block
+  static_assert(kAdamThreads % D == 0, "row width");
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si >> 1];
   const bool ahead = si & 1;
-  const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
-  const int c = threadIdx.x % VPR;
-  const int nu = T.n_uniq[0];
-  int64_t row;
-  if (!ahead) {
-    if (u >= nu) return;
-    row = T.uniq[u];
-  } else {
-    if (u >= T.ahead_n_uniq[0]) return;
-    row = T.ahead_uniq[u];
-    int a = 0, b = nu;                              // lower_bound(uniq, row)
-    while (a < b) { const int mid = (a + b) >> 1; if (T.uniq[mid] < row) a = mid + 1; else b = mid; }
-    if (a < nu && T.uniq[a] == row) return;         // the touched segment owns it
-  }
+  const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / D;
+  const int c = threadIdx.x % D;
+  const bool valid = u < (ahead ? T.ahead_n_uniq[0] : T.n_uniq[0]);
   const int st = step_base[0] + step_off;
-  const int last = T.last[row];
-  const int64_t off = row * VPR + c;
-  float4 p = reinterpret_cast<const float4*>(T.p)[off];
-  float4 m = reinterpret_cast<const float4*>(T.m)[off];
-  float4 v = reinterpret_cast<const float4*>(T.v)[off];
-  adam_replay(p, m, v, last, st, consts, k);       // the zero-gradient steps it skipped
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (!ahead) g = grouped_grad(T, u, VPR, c);
-  adam_vec(p, m, v, g, consts[2 * st], consts[2 * st + 1], k);
-  reinterpret_cast<float4*>(T.p)[off] = p;
-  reinterpret_cast<float4*>(T.m)[off] = m;
-  reinterpret_cast<float4*>(T.v)[off] = v;
-  // every lane of this row read `last` above (same wave: VPR divides 64)
+  int64_t row = 0;
+  int last = st;
+  if (valid) {
+    row = ahead ? T.ahead_uniq[u] : T.uniq[u];
+    last = T.last[row];
+  }
+  __syncthreads();
+  if (!valid) return;
+  const int64_t off = row * D + c;
+  float p = T.p[off], m = T.m[off], v = T.v[off];
+  adam_replay1(p, m, v, last, st, consts, k);       // the zero-gradient steps it skipped
+  const float g = ahead ? 0.f : grouped_grad<float>(T, u, D, c);
+  adam_elem(p, m, v, g, step_consts(consts, st), k);
+  T.p[off] = p;
+  T.m[off] = m;
+  T.v[off] = v;
   if (c == 0) T.last[row] = st + 1;
 }
 
@@ -255,7 +277,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
     reinterpret_cast<float4*>(T.p)[off] = p;
     reinterpret_cast<float4*>(T.m)[off] = m;
     reinterpret_cast<float4*>(T.v)[off] = v;
-    if (c == 0) T.last[r] = target;
+    if (c == 0) T.last[r] = target;  // a row lies in one wave here (VPR <= 64)
   }
 }
 
@@ -273,6 +295,10 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                 double eps, double weight_decay, void* stream, const char* what) {
   if (n_tables < 1 || n_tables > kMaxTables || !tables || !consts || !step_base) {
     set_error("%s: bad arguments (n_tables=%d)", what, n_tables);
+    return -1;
+  }
+  if (((uintptr_t)consts & 15) != 0) {
+    set_error("%s: step constants must be 16-byte aligned", what);
     return -1;
   }
   if (d != 4 && d != 16 && d != 32 && d != 64 && d != 128 && d != 256) {
@@ -298,7 +324,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = kAdamThreads / VPR;
+      const int rpb = kAdamThreads / d;
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
@@ -309,6 +335,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       blocks += (t.n_rows + kAdamRows - 1) / kAdamRows;
     }
   }
+  (void)VPR;
   for (int q = tabs.n_seg; q <= 2 * kMaxTables; ++q) tabs.block_start[q] = blocks;
   if (blocks == 0) return 0;
   AdamConsts k;

@@ -249,3 +249,66 @@ extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const
                      (hipStream_t)stream, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows);
   return launch_status("mirec_segment_scatter_add_f32");
 }
+
+// ---------------------------------------------------------------------------
+// Look-ahead lists of the deferred Adam (adam.hip): for consecutive batches b,
+// b+1 of a chunk, out_b = uniq(b+1) \ uniq(b) in ascending order — the rows the
+// next forward pass reads that step b's Adam does not touch. One workgroup per
+// batch; uniq(b) is staged in LDS when it fits, membership by binary search.
+namespace mirec {
+
+constexpr int kDiffLds = 8192;
+
+__global__ __launch_bounds__(kSortThreads) void uniq_ahead_diff_kernel(
+    const int32_t* __restrict__ uniq, const int32_t* __restrict__ n_uniq, int64_t stride,
+    int64_t n_batches, int32_t* __restrict__ out, int32_t* __restrict__ n_out) {
+  __shared__ int32_t a_lds[kDiffLds];
+  __shared__ int scan_lds[kSortThreads / 64 + 1];
+  const int64_t b = blockIdx.x;
+  if (b + 1 >= n_batches) {                 // last batch of the chunk: nothing ahead
+    if (threadIdx.x == 0) n_out[b] = 0;
+    return;
+  }
+  const int32_t* __restrict__ A = uniq + b * stride;
+  const int32_t* __restrict__ Bv = uniq + (b + 1) * stride;
+  const int na = n_uniq[b], nb = n_uniq[b + 1];
+  const bool lds = na <= kDiffLds;
+  if (lds)
+    for (int i = threadIdx.x; i < na; i += kSortThreads) a_lds[i] = A[i];
+  __syncthreads();
+  const int32_t* S = lds ? a_lds : A;
+  int32_t* __restrict__ o = out + b * stride;
+  int base = 0;
+  for (int c0 = 0; c0 < nb; c0 += kSortThreads) {
+    const int i = c0 + threadIdx.x;
+    int f = 0;
+    int32_t x = 0;
+    if (i < nb) {
+      x = Bv[i];
+      int lo = 0, hi = na;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (S[mid] < x) lo = mid + 1; else hi = mid; }
+      f = (lo < na && S[lo] == x) ? 0 : 1;
+    }
+    int tot;
+    const int ex = block_exclusive_scan(f, scan_lds, &tot);
+    if (f) o[base + ex] = x;
+    base += tot;
+  }
+  if (threadIdx.x == 0) n_out[b] = base;
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t stride,
+                                     int64_t n_batches, int32_t* out, int32_t* n_out,
+                                     void* stream) {
+  if (!uniq || !n_uniq || !out || !n_out || stride <= 0 || n_batches < 0) {
+    mirec::set_error("mirec_uniq_ahead_diff: bad arguments");
+    return -1;
+  }
+  if (n_batches == 0) return 0;
+  hipLaunchKernelGGL(mirec::uniq_ahead_diff_kernel, dim3((unsigned)n_batches),
+                     dim3(mirec::kSortThreads), 0, (hipStream_t)stream, uniq, n_uniq, stride,
+                     n_batches, out, n_out);
+  return mirec::launch_status("mirec_uniq_ahead_diff");
+}

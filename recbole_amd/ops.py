@@ -206,6 +206,15 @@ def segment_sort_batched(keys: torch.Tensor, batch_n: int, key_space: int, perm,
     return ws
 
 
+def uniq_ahead_diff(uniq, n_uniq, stride: int, n_batches: int, out, n_out):
+    """out[b*stride..] = uniq(b+1) minus uniq(b) (batched segment-sort layout)."""
+    for n_, t_ in (("uniq", uniq), ("n_uniq", n_uniq), ("out", out), ("n_out", n_out)):
+        _dev(t_, torch.int32, n_)
+    rc = lib().mirec_uniq_ahead_diff(ptr(uniq), ptr(n_uniq), stride, n_batches, ptr(out),
+                                     ptr(n_out), stream_handle())
+    check(rc, "mirec_uniq_ahead_diff")
+
+
 def segment_scatter_add(rows: torch.Tensor, segs: Segments, dense: torch.Tensor) -> torch.Tensor:
     _dev(rows, torch.float32, "rows")
     _dev(dense, torch.float32, "dense")
@@ -248,8 +257,9 @@ def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None =
 def adam_tables(specs):
     """ctypes array of mirec_adam_table from dicts with keys p, m, v (2-D float32
     tables of one width) and optional rows + segs (grouped gradient), dense_grad,
-    last (int32 per-row step counts of the deferred schedule), ahead (Segments of
-    the next batch: rows the deferred schedule completes for the next forward)."""
+    last (int32 per-row step counts of the deferred schedule), ahead ((rows, count)
+    int32 device tensors: rows the next batch reads and this one does not touch,
+    completed by the deferred schedule for the next forward pass)."""
     from recbole_amd._native import AdamTable
     arr = (AdamTable * len(specs))()
     for t, s in zip(arr, specs):
@@ -266,7 +276,9 @@ def adam_tables(specs):
         if s.get("last") is not None:
             t.last = ptr(_dev(s["last"], torch.int32, "last"))
         if s.get("ahead") is not None:
-            t.ahead_uniq, t.ahead_n_uniq = ptr(s["ahead"].uniq), ptr(s["ahead"].n_uniq)
+            au, an = s["ahead"]
+            t.ahead_uniq = ptr(_dev(au, torch.int32, "ahead_uniq"))
+            t.ahead_n_uniq = ptr(_dev(an, torch.int32, "ahead_n_uniq"))
     return arr
 
 

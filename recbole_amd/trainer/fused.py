@@ -53,7 +53,7 @@ ADAM_MODES = ('deferred', 'streamed')
 class _Slot(object):
     """Buffers of one chunk of prepared batches."""
 
-    def __init__(self, C, B, T, dev):
+    def __init__(self, C, B, T, dev, ahead):
         KI = (1 + T) * B
         self.user_keys = torch.empty(C * B, dtype=torch.int64, device=dev)
         self.item_keys = torch.empty(C * KI, dtype=torch.int64, device=dev)
@@ -65,6 +65,11 @@ class _Slot(object):
         self.i_uniq = torch.empty(C * KI, dtype=torch.int32, device=dev)
         self.i_seg = torch.empty(C * (KI + 1), dtype=torch.int32, device=dev)
         self.i_nu = torch.zeros(C, dtype=torch.int32, device=dev)
+        if ahead:                    # deferred Adam: rows batch c+1 reads, batch c does not touch
+            self.u_ahead = torch.empty(C * B, dtype=torch.int32, device=dev)
+            self.u_nah = torch.zeros(C, dtype=torch.int32, device=dev)
+            self.i_ahead = torch.empty(C * KI, dtype=torch.int32, device=dev)
+            self.i_nah = torch.zeros(C, dtype=torch.int32, device=dev)
         self.ready = torch.cuda.Event()
         self.free = torch.cuda.Event()
         self.free_recorded = False
@@ -99,7 +104,8 @@ class FusedBPRTrainStep(object):
         self.gU = torch.empty(B, d, dtype=torch.float32, device=dev)
         self.gI = torch.empty((1 + T) * B, d, dtype=torch.float32, device=dev)
         self.loss_k = torch.empty(self.C * B, dtype=torch.float32, device=dev)
-        self.slots = [_Slot(self.C, B, T, dev), _Slot(self.C, B, T, dev)]
+        deferred = adam_mode == 'deferred'
+        self.slots = [_Slot(self.C, B, T, dev, deferred), _Slot(self.C, B, T, dev, deferred)]
         self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(B, T),
                                    dtype=torch.uint8, device=dev)
         self.sort_ws = None
@@ -150,6 +156,9 @@ class FusedBPRTrainStep(object):
             self.sort_ws = ops.segment_sort_batched(slot.item_keys[:nb * KI], KI, self.nI,
                                                     slot.i_perm, slot.i_uniq, slot.i_seg,
                                                     slot.i_nu, ws=self.sort_ws)
+            if self.adam_mode == 'deferred':
+                ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
+                ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
 
@@ -210,10 +219,10 @@ class FusedBPRTrainStep(object):
         t[1].seg = slot.i_seg.data_ptr() + 4 * c * (KI + 1)
         t[1].n_uniq = slot.i_nu.data_ptr() + 4 * c
         if self.adam_mode == 'deferred' and ahead:
-            t[0].ahead_uniq = slot.u_uniq.data_ptr() + 4 * (c + 1) * Bc
-            t[0].ahead_n_uniq = slot.u_nu.data_ptr() + 4 * (c + 1)
-            t[1].ahead_uniq = slot.i_uniq.data_ptr() + 4 * (c + 1) * KI
-            t[1].ahead_n_uniq = slot.i_nu.data_ptr() + 4 * (c + 1)
+            t[0].ahead_uniq = slot.u_ahead.data_ptr() + 4 * c * Bc
+            t[0].ahead_n_uniq = slot.u_nah.data_ptr() + 4 * c
+            t[1].ahead_uniq = slot.i_ahead.data_ptr() + 4 * c * KI
+            t[1].ahead_n_uniq = slot.i_nah.data_ptr() + 4 * c
         else:
             t[0].ahead_uniq = t[0].ahead_n_uniq = t[1].ahead_uniq = t[1].ahead_n_uniq = None
 

@@ -26,12 +26,23 @@ from recbole_amd import ops
 class FusedAdam(torch.optim.Optimizer):
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        # torch.optim.Adam's argument checks (optim/adam.py __init__)
+        if not 0.0 <= lr:
+            raise ValueError(f'Invalid learning rate: {lr}')
+        if not 0.0 <= eps:
+            raise ValueError(f'Invalid epsilon value: {eps}')
+        if not 0.0 <= betas[0] < 1.0:
+            raise ValueError(f'Invalid beta parameter at index 0: {betas[0]}')
+        if not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f'Invalid beta parameter at index 1: {betas[1]}')
+        if not 0.0 <= weight_decay:
+            raise ValueError(f'Invalid weight_decay value: {weight_decay}')
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                         maximize=False, foreach=None, capturable=False, differentiable=False,
                         fused=None)
         super().__init__(params, defaults)
         self.n_steps = 0            # optimizer steps taken (torch's state['step'])
-        self._consts = None         # device table [2 * window] of (step_size, bc2_sqrt)
+        self._consts = None         # device table [window, 4]: step_size, bc2_sqrt, 1/bc2_sqrt
         self._window_start = 0      # n_steps value at index 0 of the table
         self._step_idx = None       # device int32 cursor into the table
 
@@ -47,14 +58,19 @@ class FusedAdam(torch.optim.Optimizer):
         return st
 
     def step_constants(self, first_step: int, count: int):
-        """float32 [count, 2] of (lr/(1-b1^t), sqrt(1-b2^t)) for t = first_step..+count-1."""
+        """float32 [count, 4] of (lr/(1-b1^t), sqrt(1-b2^t), RN(1/that), 0) for
+        t = first_step..+count-1 (the K5 constant table, include/mirec.h)."""
         g = self.param_groups[0]
         lr, (b1, b2) = g['lr'], g['betas']
-        out = np.empty((count, 2), dtype=np.float32)
-        for j in range(count):
+        out = np.zeros((count, 4), dtype=np.float32)
+        for j in range(count):            # Python float pow, exactly as torch's step code
             t = float(first_step + j)
             out[j, 0] = lr / (1 - b1 ** t)
             out[j, 1] = (1 - b2 ** t) ** 0.5
+        # correctly rounded reciprocal: 1/x in double then one rounding to float
+        out[:, 2] = 1.0 / out[:, 1].astype(np.float64)
+        if count and not (out[:, 1] > 0).all():
+            raise ValueError(f'beta2={b2} too close to 1: sqrt(1 - beta2^t) rounds to 0 in fp32')
         return out
 
     def prepare_window(self, n_steps_ahead: int, device):

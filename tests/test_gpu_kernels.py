@@ -351,6 +351,15 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
 
     segs = [[ops.segment_sort(k.to(dev), sizes[q]) for q, (k, _) in enumerate(b)]
             for b in batches]
+    aheads = []                      # rows batch s+1 reads that batch s does not touch
+    for s in range(steps - 1):
+        row = []
+        for q in range(2):
+            a = np.setdiff1d(batches[s + 1][q][0].numpy(), batches[s][q][0].numpy())
+            row.append((torch.as_tensor(a.astype(np.int32) if len(a) else np.zeros(1, np.int32),
+                                        device=dev),
+                        torch.tensor([len(a)], dtype=torch.int32, device=dev)))
+        aheads.append(row)
     snaps = []
 
     def run(schedule, flush_at=(), check_ahead=False):
@@ -364,7 +373,7 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
             for q, (k, rows) in enumerate(batch):
                 specs.append(dict(p=P[q], m=M[q], v=V[q], rows=rows.to(dev), segs=segs[s][q],
                                   last=last[q],
-                                  ahead=segs[s + 1][q] if s + 1 < steps else None))
+                                  ahead=aheads[s][q] if s + 1 < steps else None))
             tabs = ops.adam_tables(specs)
             ops.adam_multi(tabs, d, consts, base, 0, schedule,
                            n_max_uniq=[b[0].numel() for b in batch], beta1=beta1,
@@ -414,6 +423,29 @@ def test_adam_matches_torch_cpu_rounding(dev):
     torch.testing.assert_close(st['exp_avg_sq'].cpu(), topt.state[ref]['exp_avg_sq'],
                                rtol=0, atol=0)
     torch.testing.assert_close(mine.detach().cpu(), ref.detach(), rtol=3e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize('stride,nb', [(2560, 9), (20000, 3)])
+def test_uniq_ahead_diff(dev, stride, nb):
+    from recbole_amd import ops
+    rng = np.random.default_rng(stride)
+    uniq = np.zeros(nb * stride, np.int32)
+    nu = np.zeros(nb, np.int32)
+    sets = []
+    for b in range(nb):
+        k = np.unique(rng.integers(0, stride, int(rng.integers(0, stride))))
+        sets.append(k)
+        uniq[b * stride:b * stride + len(k)] = k
+        nu[b] = len(k)
+    out = torch.full((nb * stride,), -7, dtype=torch.int32, device=dev)
+    n_out = torch.full((nb,), -7, dtype=torch.int32, device=dev)
+    ops.uniq_ahead_diff(torch.as_tensor(uniq, device=dev), torch.as_tensor(nu, device=dev),
+                        stride, nb, out, n_out)
+    o, n = out.cpu().numpy(), n_out.cpu().numpy()
+    for b in range(nb - 1):
+        exp = np.setdiff1d(sets[b + 1], sets[b])
+        assert n[b] == len(exp) and np.array_equal(o[b * stride:b * stride + n[b]], exp)
+    assert n[nb - 1] == 0
 
 
 def test_chunk_finish_matches_step_finish(dev):

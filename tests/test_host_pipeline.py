@@ -116,3 +116,24 @@ def test_fused_adam_constants_follow_torch():
     for j, t in enumerate([1.0, 2.0, 3.0]):
         assert c[j, 0] == np.float32(1e-3 / (1 - 0.9 ** t))
         assert c[j, 1] == np.float32((1 - 0.999 ** t) ** 0.5)
+        assert c[j, 2] == np.float32(1.0 / float(c[j, 1]))      # RN(1 / bc2_sqrt)
+    with pytest.raises(ValueError):
+        FusedAdam([p], betas=(0.9, 1.0))
+
+
+def test_reciprocal_division_is_correctly_rounded():
+    """K5 evaluates x / bc2_sqrt as q = x*r; q + fma(-q, d, x)*r with r = RN(1/d).
+    Check it against IEEE division on the actual divisors (numpy float32, the
+    fma emulated in float64: the residual is exact there; the last fma can
+    double-round only with probability ~2^-29 per case). The exhaustive check
+    (two binades of x, ~13k divisors, hardware fmaf) was run once offline."""
+    from recbole_amd.trainer.optim import FusedAdam
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(4))])
+    c = opt.step_constants(1, 3000)
+    rng = np.random.default_rng(0)
+    x = np.sqrt(rng.random(20000).astype(np.float32) * np.float32(1e-6))
+    for d, r in zip(c[::37, 1], c[::37, 2]):
+        q = x * r
+        e = (x.astype(np.float64) - q.astype(np.float64) * np.float64(d)).astype(np.float32)
+        q2 = (q.astype(np.float64) + e.astype(np.float64) * np.float64(r)).astype(np.float32)
+        assert np.array_equal(q2, x / d)

@@ -20,6 +20,6 @@ rm -f $OUT/summary.txt
 step smoke 300 python __graft_entry__.py smoke
 step gputests 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300
 if [ "${BENCH:-1}" = "1" ]; then
-  step bench 900 python bench.py --steps ${STEPS:-200} --warmup 20 ${BENCH_ARGS:-}
+  step bench 900 python bench.py ${BENCH_ARGS:-}
 fi
 exit 0
