@@ -68,6 +68,14 @@ struct AdamTables {
   int n_seg;
 };
 
+// x / bc2_sqrt, correctly rounded, for x = sqrt(v) >= 0 (header comment);
+// branch-free so the columns of a thread interleave. +inf / bc2_sqrt = +inf.
+__device__ __forceinline__ float div_bc2s(float x, const StepConsts& sc) {
+  const float q = x * sc.rbc;
+  const float r = fmaf(fmaf(-q, sc.bc2s, x), sc.rbc, q);
+  return x == __builtin_inff() ? x : r;
+}
+
 // One Adam step of one element. Shared by every schedule so the arithmetic is
 // the same instruction sequence wherever a step is applied.
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
@@ -76,36 +84,89 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   const float dlt = g - m;
   const float me = k.lerp_small ? fmaf(k.omb1, dlt, m) : fmaf(k.omb1m1, dlt, g);
   const float ve = fmaf(k.omb2 * g, g, v * k.b2);
-  const float x = sqrtf(ve);
-  float q = x * sc.rbc;                       // x / bc2s, correctly rounded
-  q = fmaf(fmaf(-q, sc.bc2s, x), sc.rbc, q);
-  if (__builtin_expect(x == __builtin_inff(), 0)) q = x / sc.bc2s;
-  const float den = q + k.eps;
+  const float den = div_bc2s(sqrtf(ve), sc) + k.eps;
   p = p + ((-sc.ss) * me) / den;
   m = me;
   v = ve;
 }
 
-__device__ __forceinline__ void adam_vec(float4& p, float4& m, float4& v, const float4& g,
-                                         const StepConsts& sc, const AdamConsts& k) {
-  adam_elem(p.x, m.x, v.x, g.x, sc, k);
-  adam_elem(p.y, m.y, v.y, g.y, sc, k);
-  adam_elem(p.z, m.z, v.z, g.z, sc, k);
-  adam_elem(p.w, m.w, v.w, g.w, sc, k);
+// adam_elem with g = 0, wd = 0 and 1-b1 < 0.5, rewritten with the same results:
+//   fma(1-b1, 0 - m, m) == fma(-(1-b1), m, m)   (0 - m == -m up to the sign of a
+//     zero, and a zero product added to m gives the same sum either way);
+//   fma((1-b2)*0, 0, v*b2) == v*b2              (adding +0 to v*b2 >= +0).
+__device__ __forceinline__ void adam_elem_zero(float& p, float& m, float& v, const StepConsts& sc,
+                                               const AdamConsts& k) {
+  const float me = fmaf(-k.omb1, m, m);
+  const float ve = v * k.b2;
+  const float den = div_bc2s(sqrtf(ve), sc) + k.eps;
+  p = p + ((-sc.ss) * me) / den;
+  m = me;
+  v = ve;
+}
+
+// Element-wise over the components of a float, float2 or float4.
+template <typename V> struct Lanes;
+template <> struct Lanes<float> {
+  static constexpr int n = 1;
+  __device__ static float& at(float& x, int) { return x; }
+  __device__ static float at(const float& x, int) { return x; }
+};
+template <> struct Lanes<float2> {
+  static constexpr int n = 2;
+  __device__ static float& at(float2& x, int i) { return i ? x.y : x.x; }
+  __device__ static float at(const float2& x, int i) { return i ? x.y : x.x; }
+};
+template <> struct Lanes<float4> {
+  static constexpr int n = 4;
+  __device__ static float& at(float4& x, int i) {
+    return i == 0 ? x.x : i == 1 ? x.y : i == 2 ? x.z : x.w;
+  }
+  __device__ static float at(const float4& x, int i) {
+    return i == 0 ? x.x : i == 1 ? x.y : i == 2 ? x.z : x.w;
+  }
+};
+
+template <typename V>
+__device__ __forceinline__ void adam_vec(V& p, V& m, V& v, const V& g, const StepConsts& sc,
+                                         const AdamConsts& k) {
+#pragma unroll
+  for (int i = 0; i < Lanes<V>::n; ++i)
+    adam_elem(Lanes<V>::at(p, i), Lanes<V>::at(m, i), Lanes<V>::at(v, i), Lanes<V>::at(g, i),
+              sc, k);
+}
+
+__device__ __forceinline__ int wave_min_i(int x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off, 64));
+  return x;
 }
 
 // Replay steps [s0, s1) with a zero gradient (the exact per-step sequence).
-__device__ __forceinline__ void adam_replay(float4& p, float4& m, float4& v, int s0, int s1,
+// The step loop runs over the wave's smallest s0, so the step index is
+// wave-uniform (scalar constant loads, one loop for all lanes); a lane applies
+// step s only from its own s0 on (one row per wave for d >= 128: no idle lanes).
+template <typename V>
+__device__ __forceinline__ void adam_replay(V& p, V& m, V& v, int s0, int s1,
                                             const float* __restrict__ consts,
                                             const AdamConsts& k) {
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = s0; s < s1; ++s) adam_vec(p, m, v, z, step_consts(consts, s), k);
-}
-
-__device__ __forceinline__ void adam_replay1(float& p, float& m, float& v, int s0, int s1,
-                                             const float* __restrict__ consts,
-                                             const AdamConsts& k) {
-  for (int s = s0; s < s1; ++s) adam_elem(p, m, v, 0.f, step_consts(consts, s), k);
+  const int lo = __builtin_amdgcn_readfirstlane(wave_min_i(s0));
+  if (k.wd == 0.f && k.lerp_small) {
+    for (int s = lo; s < s1; ++s) {
+      const StepConsts sc = step_consts(consts, s);
+      if (s >= s0) {
+#pragma unroll
+        for (int i = 0; i < Lanes<V>::n; ++i)
+          adam_elem_zero(Lanes<V>::at(p, i), Lanes<V>::at(m, i), Lanes<V>::at(v, i), sc, k);
+      }
+    }
+  } else {
+    V z;
+    memset(&z, 0, sizeof(V));
+    for (int s = lo; s < s1; ++s) {
+      const StepConsts sc = step_consts(consts, s);
+      if (s >= s0) adam_vec(p, m, v, z, sc, k);
+    }
+  }
 }
 
 __device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
@@ -126,6 +187,10 @@ __device__ __forceinline__ void vadd(V& a, const V& b);
 template <>
 __device__ __forceinline__ void vadd<float4>(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+template <>
+__device__ __forceinline__ void vadd<float2>(float2& a, const float2& b) {
+  a.x += b.x; a.y += b.y;
 }
 template <>
 __device__ __forceinline__ void vadd<float>(float& a, const float& b) { a += b; }
@@ -209,9 +274,9 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 }
 
 // ---------------------------------------------------------------- deferred
-// One thread per (row, column): the replay of a row's skipped steps is a
-// serial chain per element, so one element per thread keeps the chain short.
-// RPB = 256 / D whole rows per block.
+// Two columns per thread (float2: packed fp32 math, and a row's replay is a
+// serial chain per element, so few columns per thread keep the chain short).
+// RPB = 256 / (D/2) whole rows per block.
 //  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
 //               zero gradient, applies step s with its gradient; last = s+1.
 //  segment 2q+1 (look-ahead): row = ahead_uniq[u], rows the NEXT batch reads
@@ -219,18 +284,19 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 //               Replays last..s (zero gradient); last = s+1 — so the next
 //               forward pass reads rows that are complete through step s.
 // `last` is read by every thread of a row before the barrier and written
-// after it (a row of D >= 128 spans several waves).
+// after it (a row of D = 256 spans two waves).
 template <int D>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     const AdamTables tabs, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
-  constexpr int RPB = kAdamThreads / D;             // rows per block
-  static_assert(kAdamThreads % D == 0, "row width");
+  constexpr int VPR = D / 2;                        // float2 per row
+  constexpr int RPB = kAdamThreads / VPR;           // rows per block
+  static_assert(kAdamThreads % VPR == 0, "row width");
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si >> 1];
   const bool ahead = si & 1;
-  const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / D;
-  const int c = threadIdx.x % D;
+  const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
+  const int c = threadIdx.x % VPR;
   const bool valid = u < (ahead ? T.ahead_n_uniq[0] : T.n_uniq[0]);
   const int st = step_base[0] + step_off;
   int64_t row = 0;
@@ -240,15 +306,22 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     last = T.last[row];
   }
   __syncthreads();
+  const int64_t off = row * VPR + c;
+  float2 p = make_float2(0.f, 0.f), m = p, v = p;
+  if (valid) {
+    p = reinterpret_cast<const float2*>(T.p)[off];
+    m = reinterpret_cast<const float2*>(T.m)[off];
+    v = reinterpret_cast<const float2*>(T.v)[off];
+  }
+  // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop)
+  adam_replay(p, m, v, last, st, consts, k);
   if (!valid) return;
-  const int64_t off = row * D + c;
-  float p = T.p[off], m = T.m[off], v = T.v[off];
-  adam_replay1(p, m, v, last, st, consts, k);       // the zero-gradient steps it skipped
-  const float g = ahead ? 0.f : grouped_grad<float>(T, u, D, c);
-  adam_elem(p, m, v, g, step_consts(consts, st), k);
-  T.p[off] = p;
-  T.m[off] = m;
-  T.v[off] = v;
+  float2 g = make_float2(0.f, 0.f);
+  if (!ahead) g = grouped_grad<float2>(T, u, VPR, c);
+  adam_vec(p, m, v, g, step_consts(consts, st), k);
+  reinterpret_cast<float2*>(T.p)[off] = p;
+  reinterpret_cast<float2*>(T.m)[off] = m;
+  reinterpret_cast<float2*>(T.v)[off] = v;
   if (c == 0) T.last[row] = st + 1;
 }
 
@@ -266,18 +339,26 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
   const int target = step_base[0] + step_off;
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
-  for (int64_t r = lo + rsub; r < hi; r += RPP) {
-    const int last = T.last[r];
-    if (last >= target) continue;
+  // wave-uniform trip count (adam_replay's step loop runs over the whole wave)
+  for (int64_t base = lo; base < hi; base += RPP) {
+    const int64_t r = base + rsub;
+    const bool valid = r < hi;
+    const int last = valid ? min(T.last[r], target) : target;
+    const bool work = last < target;
     const int64_t off = r * VPR + c;
-    float4 p = reinterpret_cast<const float4*>(T.p)[off];
-    float4 m = reinterpret_cast<const float4*>(T.m)[off];
-    float4 v = reinterpret_cast<const float4*>(T.v)[off];
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
+    if (work) {
+      p = reinterpret_cast<const float4*>(T.p)[off];
+      m = reinterpret_cast<const float4*>(T.m)[off];
+      v = reinterpret_cast<const float4*>(T.v)[off];
+    }
     adam_replay(p, m, v, last, target, consts, k);
-    reinterpret_cast<float4*>(T.p)[off] = p;
-    reinterpret_cast<float4*>(T.m)[off] = m;
-    reinterpret_cast<float4*>(T.v)[off] = v;
-    if (c == 0) T.last[r] = target;  // a row lies in one wave here (VPR <= 64)
+    if (work) {
+      reinterpret_cast<float4*>(T.p)[off] = p;
+      reinterpret_cast<float4*>(T.m)[off] = m;
+      reinterpret_cast<float4*>(T.v)[off] = v;
+      if (c == 0) T.last[r] = target;  // a row lies in one wave here (VPR <= 64)
+    }
   }
 }
 
@@ -324,7 +405,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = kAdamThreads / d;
+      const int rpb = kAdamThreads / (d / 2);
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
