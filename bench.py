@@ -77,16 +77,36 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
                                                               adam_mode=adam_mode)
 
 
-def roofline(step, events, uniq, d):
-    """Roofline of the dominant model-side kernel from the per-launch HIP events.
+def pmc_bytes(substr):
+    """HBM bytes per launch of the kernel whose name contains `substr`, from the
+    newest committed PMC summary (profiles/*_pmc.json, tools/summarize_prof.py:
+    FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for k, v in data.items():
+        if substr in k:
+            return v['hbm_bytes_per_launch'], os.path.basename(files[-1])
+    return None, None
 
-    Algorithmic bytes per launch (fp32 rows of d floats, R = d*4 bytes):
-      adam/streamed  6 * (n_users + n_items) * R          (read+write p, m, v of every row)
-      adam/deferred  sum over tables of 6*u*R + c*R + 20*u + 4*c
-                     (touched rows u: p, m, v r+w, last r+w, uniq, seg; contributions
-                     c: grouped gradient rows + perm)
-      bpr            (B + (1+T)B) * R (embedding rows) + (B + (1+T)B) * R (gradients)
-                     + (B + (1+T)B) * 8 (ids) + B * 4 (losses)
+
+ADAM_FLOPS = 13      # IEEE fp32 ops per element per Adam step in torch's formula (see DESIGN.md)
+VALU_PEAK_TFLOPS = 157.3   # MI355X fp32 vector peak (MI355X_MICROARCH.md)
+
+
+def roofline(step, events, uniq, d, M):
+    """Rooflines from the per-launch HIP events of an eager window of M steps
+    that starts right after a flush and ends with one (every row of both tables
+    is advanced exactly M Adam steps by the window's K5 launches).
+
+    K5 dense Adam (dominant; fp32 VALU-bound: sqrt and two divisions per element):
+      FLOPs = (n_users + n_items) * d * M * 13 over the window's deferred + flush
+      launches. 13 = lerp (sub + fma) 3, v (mul + mul + fma) 4, sqrt 1, / 1, + eps 1,
+      step * m 1, / 1, + p 1 (sqrt and division counted as one op each).
+    K3 BPR (HBM view): bytes per launch = 2*(B+(1+T)B)*d*4 (rows read + gradient
+      rows written) + 8*(B+(1+T)B) (ids) + 4*B (losses).
     """
     per = {}
     for name, a, b in events:
@@ -94,29 +114,43 @@ def roofline(step, events, uniq, d):
     kernels_us = {k: round(float(np.mean(v)) * 1e6, 2) for k, v in per.items()}
     R, B, T = d * 4, step.B, step.times
     rowsI = (1 + T) * B
-    if step.adam_mode == 'streamed':
-        adam_bytes = 6 * (step.nU + step.nI) * R
-        adam_formula = '6 * (n_users + n_items) * d * 4 (read+write p, m, v of every row)'
-        adam_name = f'K5 adam_multi_kernel<{d}> (streamed dense Adam, user+item tables)'
-    else:
-        u = torch.stack(uniq).double().mean(0).cpu().numpy()
-        adam_bytes = float(6 * (u[0] + u[1]) * R + (B + rowsI) * R + 20 * (u[0] + u[1])
-                           + 4 * (B + rowsI))
-        adam_formula = (f'6*u*d*4 + c*d*4 + 20*u + 4*c summed over tables; mean touched rows '
-                        f'u = {u[0]:.1f} users + {u[1]:.1f} items, c = {B} + {rowsI}')
-        adam_name = f'K5 adam_deferred_kernel<{d}> (deferred dense Adam, user+item tables)'
     bpr_bytes = 2 * (B + rowsI) * R + (B + rowsI) * 8 + B * 4
-    cands = {'adam': (adam_name, adam_bytes, adam_formula),
-             'bpr': (f'K3 bpr_fwd_bwd<{d}>', bpr_bytes,
-                     '2*(B+(1+T)B)*d*4 + 8*(B+(1+T)B) + 4*B')}
-    top = max(cands, key=lambda k: kernels_us.get(k, 0.0))
-    name, nbytes, formula = cands[top]
-    t = kernels_us[top] * 1e-6
-    gbs = nbytes / t / 1e9
-    return ({'kernel': name, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
-             'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
-             'bytes_per_launch': round(nbytes), 'avg_launch_us': kernels_us[top],
-             'bytes_formula': formula}, kernels_us)
+    t_bpr = kernels_us['bpr'] * 1e-6
+    tb, _ = pmc_bytes(f'bpr_fwd_bwd_kernel<{d}>')
+    bpr = {'kernel': f'K3 bpr_fwd_bwd<{d}>', 'bound': 'hbm', 'traffic': tb,
+           'achieved': round(bpr_bytes / t_bpr / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+           'frac': round(bpr_bytes / t_bpr / 1e9 / HBM_PEAK_GBS, 4),
+           'bytes_per_launch': bpr_bytes, 'avg_launch_us': kernels_us['bpr']}
+    t_adam = sum(per.get('adam', [])) + sum(per.get('flush', []))
+    flops = (step.nU + step.nI) * d * M * ADAM_FLOPS
+    tf = flops / t_adam / 1e12
+    name = ('K5 deferred dense Adam: adam_deferred_kernel<%d> x %d + adam_flush_kernel<%d> x %d'
+            % (d, len(per.get('adam', [])), d, len(per.get('flush', []))))
+    if step.adam_mode == 'streamed':
+        name = f'K5 adam_multi_kernel<{d}> x {len(per.get("adam", []))} (streamed dense Adam)'
+    adam = {'kernel': name, 'bound': 'valu', 'achieved': round(tf, 2),
+            'peak': VALU_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(tf / VALU_PEAK_TFLOPS, 4),
+            'traffic': None, 'flops_per_window': flops, 'window_steps': M,
+            'window_kernel_us': round(t_adam * 1e6, 1),
+            'us_per_step': round(t_adam * 1e6 / M, 2),
+            'flops_formula': '(n_users + n_items) * d * steps * 13'}
+    nd, nf = len(per.get('adam', [])), len(per.get('flush', []))
+    if step.adam_mode == 'deferred':
+        bd, src = pmc_bytes(f'adam_deferred_kernel<{d}>')
+        bf, _ = pmc_bytes(f'adam_flush_kernel<{d}>')
+        if bd is not None and bf is not None:
+            adam.update({'traffic': int(nd * bd + nf * bf), 'traffic_unit': 'HBM bytes per window',
+                         'traffic_source': src,
+                         'traffic_note': 'PMC FETCH_SIZE x2 + WRITE_SIZE per launch x launches; '
+                                         'streamed dense Adam moves 6*(nU+nI)*d*4 = %d per step'
+                                         % (6 * (step.nU + step.nI) * R)})
+    if step.adam_mode == 'streamed':           # memory-bound: HBM view is the binding one
+        by = 6 * (step.nU + step.nI) * R * M
+        gbs = by / t_adam / 1e9
+        adam.update({'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
+                     'bytes_formula': '6 * (n_users + n_items) * d * 4 per step'})
+    return adam, bpr, kernels_us
 
 
 def cpu_baseline(train, step_obj, d, neg, steps):
@@ -163,7 +197,8 @@ def main():
                                                            adam_mode=args.adam_mode)
     setup_s = time.time() - t_setup
     nb = step.begin_epoch()
-    K, W, M = args.steps, args.warmup, 32
+    K, W = args.steps, args.warmup
+    M = step.C - (W + K) % step.C          # measurement window: up to the next chunk end
     if W + K + M > nb:
         raise SystemExit(f'steps+warmup exceed one epoch ({nb} batches)')
     step.run_batches(0, W)
@@ -187,7 +222,9 @@ def main():
     # Per-kernel HIP events around each model-side launch, on the stream it runs
     # on, over M further steps launched eagerly behind a spin kernel so the
     # events bracket kernel time only (not host enqueue gaps).
-    torch.cuda._sleep(int(5e6))
+    # spin long enough (~2.4k cycles/us) to cover the host's enqueue of the whole
+    # window (~5 eager launches per step), so the events bracket kernel time only
+    torch.cuda._sleep(int(2.4e3 * 400 * M))
     step.kernel_events, step.kernel_uniq = [], []
     step.run_batches(W + K, W + K + M)
     torch.cuda.synchronize()
@@ -195,7 +232,7 @@ def main():
     step.kernel_events = None
     losses = step.end_epoch(W + K + M)
     assert all(np.isfinite(losses)), 'non-finite loss'
-    roof, kernels_us = roofline(step, events, uniq, d)
+    roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M)
     positives = K * step.B * world
     result = {
         'metric': 'train positives/sec (+neg) per node',
@@ -218,6 +255,7 @@ def main():
                        train.dataset.inter_num), 'parallelism': 'single' if world == 1
                    else f'replicas{world}'},
         'roofline': roof,
+        'roofline_bpr': roof_bpr,
         'kernels_us': kernels_us,
         'adam_mode': step.adam_mode,
         'setup_s': round(setup_s, 1),

@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS="--steps ${STEPS:-100} --warmup 20 --no-cpu-baseline ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline ${BENCH_ARGS:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace rc=$?"; exit 3; }
 echo trace-ok; tail -1 $OUT/trace.log | cut -c1-300
