@@ -12,9 +12,12 @@ A step = one batch: K4 sampler walk -> K3 fused BPR fwd/bwd -> K2 grouping ->
 K5 dense Adam over every row of both tables -> loss bookkeeping. Inputs are
 resident in HBM before the timed region.
 
-Prints ONE JSON line (rank 0). With --gpus N>1 (torchrun) each rank trains an
-independent replica on its own GPU ("replicas only" in round 1: the table
-sharding with an RCCL exchange is the next step).
+Prints ONE JSON line (rank 0). With --gpus N>1 (torchrun, one rank per GPU) the
+step is data parallel: each optimizer step consumes a global batch of N x 512
+positives, rank g computes K3 on its 512, one RCCL all-gather over xGMI exchanges
+the contribution rows, and every rank applies the same dense Adam to its replica of
+the tables — bit-identical to one GPU running the global batch (weak scaling: the
+per-GPU batch is fixed; value = global positives / max-over-ranks time).
 """
 from __future__ import annotations
 
@@ -54,7 +57,8 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
     return u[order], i[order], n_users + 1, n_items + 1
 
 
-def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred'):
+def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
+                   dist=None):
     from recbole_amd.config import Config
     from recbole_amd.data import data_preparation
     from recbole_amd.data.dataset import Dataset
@@ -74,7 +78,7 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
     return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train,
-                                                              adam_mode=adam_mode)
+                                                              adam_mode=adam_mode, dist=dist)
 
 
 def pmc_bytes(substr):
@@ -193,8 +197,8 @@ def main():
 
     d, neg = 128, 4
     t_setup = time.time()
-    config, train, test, model, opt, step = build_workload(dev, d=d, neg=neg,
-                                                           adam_mode=args.adam_mode)
+    config, train, test, model, opt, step = build_workload(
+        dev, d=d, neg=neg, adam_mode=args.adam_mode, dist=tdist.group.WORLD if dist else None)
     setup_s = time.time() - t_setup
     nb = step.begin_epoch()
     K, W = args.steps, args.warmup
@@ -233,7 +237,7 @@ def main():
     losses = step.end_epoch(W + K + M)
     assert all(np.isfinite(losses)), 'non-finite loss'
     roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M)
-    positives = K * step.B * world
+    positives = K * step.Bg                    # global batch = world x 512 positives
     result = {
         'metric': 'train positives/sec (+neg) per node',
         'value': round(positives / elapsed, 1),
@@ -251,9 +255,10 @@ def main():
                                'PAD), ~20M interactions RO_RS 0.8/0.1/0.1, embedding 128, '
                                '4 uniform negatives, 512 positives (2,048 rows) per step, '
                                'dense Adam',
-                   'global_batch': step.B * world, 'train_interactions': int(
+                   'global_batch': step.Bg, 'per_gpu_batch': step.B, 'train_interactions': int(
                        train.dataset.inter_num), 'parallelism': 'single' if world == 1
-                   else f'replicas{world}'},
+                   else f'dp{world} (replicated tables, RCCL all-gather of contribution rows)',
+                   'exchange_graph': bool(step.use_graph)},
         'roofline': roof,
         'roofline_bpr': roof_bpr,
         'kernels_us': kernels_us,

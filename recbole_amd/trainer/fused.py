@@ -46,44 +46,59 @@ import torch
 
 from recbole_amd import ops
 from recbole_amd._native import AdamTable, check, lib
+from recbole_amd.trainer.exchange import ExchangeLayout
 
 ADAM_MODES = ('deferred', 'streamed')
 
 
 class _Slot(object):
-    """Buffers of one chunk of prepared batches."""
+    """Buffers of one chunk of prepared batches (global-batch keys and groupings;
+    for G > 1 also this rank's local key slices)."""
 
-    def __init__(self, C, B, T, dev, ahead):
-        KI = (1 + T) * B
-        self.user_keys = torch.empty(C * B, dtype=torch.int64, device=dev)
+    def __init__(self, C, B, T, G, dev, ahead):
+        Bg = G * B
+        KI = (1 + T) * Bg
+        self.user_keys = torch.empty(C * Bg, dtype=torch.int64, device=dev)
         self.item_keys = torch.empty(C * KI, dtype=torch.int64, device=dev)
-        self.u_perm = torch.empty(C * B, dtype=torch.int32, device=dev)
-        self.u_uniq = torch.empty(C * B, dtype=torch.int32, device=dev)
-        self.u_seg = torch.empty(C * (B + 1), dtype=torch.int32, device=dev)
+        if G > 1:
+            self.lu = torch.empty(C * B, dtype=torch.int64, device=dev)
+            self.li = torch.empty(C * (1 + T) * B, dtype=torch.int64, device=dev)
+        self.u_perm = torch.empty(C * Bg, dtype=torch.int32, device=dev)
+        self.u_uniq = torch.empty(C * Bg, dtype=torch.int32, device=dev)
+        self.u_seg = torch.empty(C * (Bg + 1), dtype=torch.int32, device=dev)
         self.u_nu = torch.zeros(C, dtype=torch.int32, device=dev)
         self.i_perm = torch.empty(C * KI, dtype=torch.int32, device=dev)
         self.i_uniq = torch.empty(C * KI, dtype=torch.int32, device=dev)
         self.i_seg = torch.empty(C * (KI + 1), dtype=torch.int32, device=dev)
         self.i_nu = torch.zeros(C, dtype=torch.int32, device=dev)
         if ahead:                    # deferred Adam: rows batch c+1 reads, batch c does not touch
-            self.u_ahead = torch.empty(C * B, dtype=torch.int32, device=dev)
+            self.u_ahead = torch.empty(C * Bg, dtype=torch.int32, device=dev)
             self.u_nah = torch.zeros(C, dtype=torch.int32, device=dev)
             self.i_ahead = torch.empty(C * KI, dtype=torch.int32, device=dev)
             self.i_nah = torch.zeros(C, dtype=torch.int32, device=dev)
         self.ready = torch.cuda.Event()
         self.free = torch.cuda.Event()
         self.free_recorded = False
-        self.chunk = None            # (first batch, n batches, batch size)
+        self.chunk = None            # (first global batch, n batches, global batch size)
         self.graph = None            # HIP graph of a full chunk's model-side steps
 
 
 class FusedBPRTrainStep(object):
-    """Device buffers and launch sequence of the fused pairwise train step."""
+    """Device buffers and launch sequence of the fused pairwise train step.
+
+    Data parallel over G ranks (`dist` = a torch.distributed process group, or None
+    for one GPU): one optimizer step consumes a GLOBAL batch of G*B positives, rank g
+    runs K3 on positives [g*B, (g+1)*B) of it, one all-gather (RCCL over xGMI)
+    exchanges the packed contribution rows (trainer/exchange.py), and every rank
+    applies the same dense Adam to its replica of the tables. The walk and the K2
+    grouping of the global batch are computed on every rank (cheap, on the prep
+    stream), so each rank's result is bit-identical to ONE GPU running the global
+    batch. A ragged last batch is computed whole on every rank (no exchange)."""
 
     CHUNK = 64
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
-                 adam_mode='deferred'):
+                 adam_mode='deferred', dist=None):
         if adam_mode not in ADAM_MODES:
             raise ValueError(f'adam_mode must be one of {ADAM_MODES}, got {adam_mode!r}')
         self.model = model
@@ -91,49 +106,66 @@ class FusedBPRTrainStep(object):
         self.data = train_data
         (self.pU, self.nU), (self.pI, self.nI) = model.fused_embedding_tables()
         self.device = self.pU.device
-        self.B = train_data.step                   # positives per batch
+        self.B = train_data.step                   # positives per batch per rank
         self.times = train_data.times              # negatives per positive
         self.uid_field = train_data.uid_field
         self.iid_field = train_data.iid_field
         self.C = chunk or self.CHUNK
         self.use_graph = use_graph
         self.adam_mode = adam_mode
-        B, T, d = self.B, self.times, self.pU.shape[1]
+        self.group = dist
+        if dist is not None:
+            import torch.distributed as tdist
+            self.G, self.rank = tdist.get_world_size(dist), tdist.get_rank(dist)
+            self._backend = str(tdist.get_backend(dist))
+            if self._backend != 'nccl':        # host-staged collectives cannot be captured
+                self.use_graph = use_graph = False
+        else:
+            self.G, self.rank, self._backend = 1, 0, None
+        B, T, G, d = self.B, self.times, self.G, self.pU.shape[1]
+        self.Bg = G * B                            # positives per optimizer step
         self.d = d
         dev = self.device
-        self.gU = torch.empty(B, d, dtype=torch.float32, device=dev)
-        self.gI = torch.empty((1 + T) * B, d, dtype=torch.float32, device=dev)
-        self.loss_k = torch.empty(self.C * B, dtype=torch.float32, device=dev)
+        self.layout = ExchangeLayout(G, B, T, d)
+        # packed exchange rows [G, R, d]; with G = 1 (or a ragged global batch) the
+        # same memory holds [user rows | item rows] of the whole batch
+        self.xbuf = torch.empty(max(G * self.layout.R, self.Bg * (2 + T)) * d,
+                                dtype=torch.float32, device=dev)
+        self.loss_k = torch.empty(self.C * self.Bg, dtype=torch.float32, device=dev)
         deferred = adam_mode == 'deferred'
-        self.slots = [_Slot(self.C, B, T, dev, deferred), _Slot(self.C, B, T, dev, deferred)]
-        self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(B, T),
+        self.slots = [_Slot(self.C, B, T, G, dev, deferred) for _ in range(2)]
+        self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(self.Bg, T),
                                    dtype=torch.uint8, device=dev)
         self.sort_ws = None
         self.prep_stream = torch.cuda.Stream(device=dev)
         self.loss_hist = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.consts = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.consts = torch.zeros(4, dtype=torch.float32, device=dev)
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
         self.kernel_events = None   # list -> (name, start, end) HIP events (bench.py)
         self.kernel_uniq = []       # per eager step: [touched users, touched items]
         self.opt._ensure_state(self.pU)
         self.opt._ensure_state(self.pI)
         self._tables = (AdamTable * 2)()
-        if adam_mode == 'deferred':
+        if deferred:
             self.lastU = torch.zeros(self.nU, dtype=torch.int32, device=dev)
             self.lastI = torch.zeros(self.nI, dtype=torch.int32, device=dev)
-            self._n_max = (ctypes.c_int64 * 2)(B, (1 + T) * B)
+        self._n_max = (ctypes.c_int64 * 2)(self.Bg, (1 + T) * self.Bg)
         g = self.opt.param_groups[0]
         self._adam_args = (g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'])
         self._fill_tables()
 
     # ------------------------------------------------------------------ data side
     def _chunks(self):
+        """(first global batch, batches, global batch size) per chunk."""
         n = self._users.numel()
-        full = n // self.B
-        out = [(b0, min(self.C, full - b0), self.B) for b0 in range(0, full, self.C)]
-        if n % self.B:
-            out.append((full, 1, n % self.B))
+        full = n // self.Bg
+        out = [(b0, min(self.C, full - b0), self.Bg) for b0 in range(0, full, self.C)]
+        if n % self.Bg:
+            out.append((full, 1, n % self.Bg))
         return out
+
+    def _sharded(self, Bc):
+        return self.G > 1 and Bc == self.Bg
 
     def _prepare(self, slot, chunk):
         b0, nb, Bc = chunk
@@ -142,7 +174,7 @@ class FusedBPRTrainStep(object):
         if slot.free_recorded:
             self.prep_stream.wait_event(slot.free)
         with torch.cuda.stream(self.prep_stream):
-            s0 = b0 * self.B
+            s0 = b0 * self.Bg
             users = slot.user_keys[:nb * Bc]
             users.copy_(self._users[s0:s0 + nb * Bc])
             keys = slot.item_keys[:nb * KI].view(nb, 1 + T, Bc)
@@ -156,6 +188,14 @@ class FusedBPRTrainStep(object):
             self.sort_ws = ops.segment_sort_batched(slot.item_keys[:nb * KI], KI, self.nI,
                                                     slot.i_perm, slot.i_uniq, slot.i_seg,
                                                     slot.i_nu, ws=self.sort_ws)
+            if self._sharded(Bc):
+                lay, g, B = self.layout, self.rank, self.B
+                slot.lu[:nb * B].view(nb, B).copy_(lay.local_users(users, g))
+                slot.li[:nb * (1 + T) * B].view(nb, 1 + T, B).copy_(
+                    lay.local_items(slot.item_keys[:nb * KI], g))
+                up, ip = slot.u_perm[:nb * Bc], slot.i_perm[:nb * KI]
+                up.copy_(lay.user_rows(up))
+                ip.copy_(lay.item_rows(ip))
             if self.adam_mode == 'deferred':
                 ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
                 ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
@@ -172,7 +212,6 @@ class FusedBPRTrainStep(object):
                                                stU['exp_avg_sq'].data_ptr(), self.nU)
         t[1].p, t[1].m, t[1].v, t[1].n_rows = (self.pI.data_ptr(), stI['exp_avg'].data_ptr(),
                                                stI['exp_avg_sq'].data_ptr(), self.nI)
-        t[0].rows, t[1].rows = self.gU.data_ptr(), self.gI.data_ptr()
         t[0].dense_grad = t[1].dense_grad = None
         if self.adam_mode == 'deferred':
             t[0].last, t[1].last = self.lastU.data_ptr(), self.lastI.data_ptr()
@@ -190,26 +229,41 @@ class FusedBPRTrainStep(object):
         ev.append((name, e0, e1))
 
     def _step(self, slot, c, Bc, stream, step_off, ahead):
-        """Model-side kernels of batch c of `slot` (batch size Bc) as optimizer
+        """Model-side work of global batch c of `slot` (Bc positives) as optimizer
         step step_idx + step_off; every pointer is relative to the slot or a
-        persistent buffer (graph-capturable). `ahead`: batch c+1 of the slot
-        runs next, so the deferred Adam also completes the rows it reads."""
-        T = self.times
+        persistent buffer (graph-capturable). `ahead`: batch c+1 of the slot runs
+        next, so the deferred Adam also completes the rows it reads."""
+        T, d = self.times, self.d
         KI = (1 + T) * Bc
-        user_p = slot.user_keys.data_ptr() + 8 * c * Bc
-        keys_p = slot.item_keys.data_ptr() + 8 * c * KI
         L = lib()
         st = stream.cuda_stream
-        loss_p = self.loss_k.data_ptr() + 4 * c * self.B
+        sharded = self._sharded(Bc)
+        x0 = self.xbuf.data_ptr()
+        loss_p = self.loss_k.data_ptr() + 4 * c * self.Bg
+        if sharded:
+            lay, B = self.layout, self.B
+            user_p = slot.lu.data_ptr() + 8 * c * B
+            keys_p = slot.li.data_ptr() + 8 * c * (1 + T) * B
+            mine = x0 + 4 * self.rank * lay.R * d
+            n_pos, gU, gI = B, mine, mine + 4 * lay.item0 * d
+            bpr_loss = mine + 4 * lay.loss0 * d
+            rowsU = rowsI = x0
+        else:
+            user_p = slot.user_keys.data_ptr() + 8 * c * Bc
+            keys_p = slot.item_keys.data_ptr() + 8 * c * KI
+            n_pos, gU, gI, bpr_loss = Bc, x0, x0 + 4 * Bc * d, loss_p
+            rowsU, rowsI = gU, gI
 
         def bpr():
             check(L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
-                                          self.nI, self.d, user_p, keys_p, keys_p + 8 * Bc, Bc,
-                                          T, 1e-10, self._grad_scale(Bc), loss_p, None, None,
-                                          self.gU.data_ptr(), self.gI.data_ptr(), st),
-                  'mirec_bpr_fwd_bwd_f32')
+                                          self.nI, d, user_p, keys_p, keys_p + 8 * n_pos,
+                                          n_pos, T, 1e-10, self._grad_scale(Bc), bpr_loss,
+                                          None, None, gU, gI, st), 'mirec_bpr_fwd_bwd_f32')
         self._record('bpr', stream, bpr)
+        if sharded:
+            self._record('exchange', stream, lambda: self._exchange(c))
         t = self._tables
+        t[0].rows, t[1].rows = rowsU, rowsI
         t[0].perm = slot.u_perm.data_ptr() + 4 * c * Bc
         t[0].uniq = slot.u_uniq.data_ptr() + 4 * c * Bc
         t[0].seg = slot.u_seg.data_ptr() + 4 * c * (Bc + 1)
@@ -228,21 +282,35 @@ class FusedBPRTrainStep(object):
 
         if self.adam_mode == 'deferred':
             def adam():
-                check(L.mirec_adam_deferred_f32(t, 2, self._n_max, self.d, self.consts.data_ptr(),
+                check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
                                                 self.step_idx.data_ptr(), step_off,
                                                 *self._adam_args, st), 'mirec_adam_deferred_f32')
         else:
             def adam():
-                check(L.mirec_adam_multi_f32(t, 2, self.d, self.consts.data_ptr(),
+                check(L.mirec_adam_multi_f32(t, 2, d, self.consts.data_ptr(),
                                              self.step_idx.data_ptr(), step_off,
                                              *self._adam_args, st), 'mirec_adam_multi_f32')
         self._record('adam', stream, adam)
         if self.kernel_events is not None:       # rows touched, for the bench's byte count
             self.kernel_uniq.append(torch.stack([slot.u_nu[c], slot.i_nu[c]]))
 
+    def _exchange(self, c):
+        """All-gather the packed contribution rows of every rank (RCCL over xGMI),
+        then lay the G*B losses out in global positive order for chunk_finish."""
+        import torch.distributed as tdist
+        lay = self.layout
+        full = self.xbuf[:self.G * lay.R * self.d]
+        parts = list(full.view(self.G, -1).unbind(0))
+        if self._backend == 'nccl':            # RCCL: in place, one collective
+            tdist.all_gather_into_tensor(full, parts[self.rank], group=self.group)
+        else:                                  # gloo (CPU-staged; tests): list form
+            tdist.all_gather(parts, parts[self.rank].clone(), group=self.group)
+        self.loss_k[c * self.Bg:(c + 1) * self.Bg].view(self.G, self.B).copy_(
+            lay.gathered_losses(full.view(self.G, lay.R, self.d)))
+
     def _finish(self, c0, n_steps, Bc, stream):
         """Losses of batches c0..c0+n_steps of the slot -> loss_hist; step_idx += n."""
-        rc = lib().mirec_chunk_finish(self.loss_k.data_ptr() + 4 * c0 * self.B, Bc, self.B,
+        rc = lib().mirec_chunk_finish(self.loss_k.data_ptr() + 4 * c0 * self.Bg, Bc, self.Bg,
                                       n_steps, float(Bc * self.times),
                                       self.loss_hist.data_ptr(), self.step_idx.data_ptr(),
                                       stream.cuda_stream)
@@ -260,6 +328,7 @@ class FusedBPRTrainStep(object):
         self._record('flush', stream, flush)
 
     def _grad_scale(self, Bc):
+        """1 / (rows of the GLOBAL batch): the reference's .mean() over the batch."""
         R = Bc * self.times
         if getattr(self, '_gs_R', None) != R:
             self._gs_R = R
@@ -273,8 +342,8 @@ class FusedBPRTrainStep(object):
             cap.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=cap):
                 for c in range(self.C):
-                    self._step(slot, c, self.B, cap, c, c + 1 < self.C)
-                self._finish(0, self.C, self.B, cap)
+                    self._step(slot, c, self.Bg, cap, c, c + 1 < self.C)
+                self._finish(0, self.C, self.Bg, cap)
                 self._flush(cap)
             torch.cuda.current_stream(self.device).wait_stream(cap)
             slot.graph = g
@@ -283,7 +352,7 @@ class FusedBPRTrainStep(object):
     # ------------------------------------------------------------------ epoch API
     def begin_epoch(self):
         """Shuffle (reference order of RNG use), stage the epoch's Adam constants,
-        and start preparing the first chunks; returns the number of batches."""
+        and start preparing the first chunks; returns the number of (global) batches."""
         data = self.data
         if data.shuffle:
             data._shuffle()                     # randperm (CPU RNG) + device reorder
@@ -292,7 +361,7 @@ class FusedBPRTrainStep(object):
         self._items = inter[self.iid_field]
         if not self._users.is_cuda:
             raise RuntimeError('fused train step needs the train table on the GPU')
-        self.n_batches = nb = math.ceil(self._users.numel() / self.B)
+        self.n_batches = nb = math.ceil(self._users.numel() / self.Bg)
         table = self.opt.step_constants(self.opt.n_steps + 1, max(nb, 1)).reshape(-1)
         if self.consts.numel() < table.size:   # persistent buffers (graph-captured pointers)
             self.consts = torch.zeros(table.size, dtype=torch.float32, device=self.device)
@@ -311,8 +380,17 @@ class FusedBPRTrainStep(object):
             self.lastU.zero_()
             self.lastI.zero_()
         if self.use_graph and nb >= self.C:
-            for s in self.slots:                # capture up front: capture synchronizes
-                self._graph_for(s)
+            try:
+                for s in self.slots:            # capture up front: capture synchronizes
+                    self._graph_for(s)
+            except RuntimeError:
+                if self.G == 1:
+                    raise
+                # collectives that cannot be captured: replay the steps eagerly
+                torch.cuda.synchronize(self.device)
+                self.use_graph = False
+                for s in self.slots:
+                    s.graph = None
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
         self._plan = self._chunks()
         self._next_chunk = 0
@@ -343,9 +421,9 @@ class FusedBPRTrainStep(object):
         self._cur = k
 
     def run_batches(self, b_start, b_end):
-        """Enqueue batches [b_start, b_end) in order (no host sync). Whole chunks
-        replay their captured graph; partial chunks launch eagerly, one step and
-        one loss bookkeeping launch at a time, flushing when a chunk completes."""
+        """Enqueue global batches [b_start, b_end) in order (no host sync). Whole
+        chunks replay their captured graph; partial chunks launch eagerly, one step
+        and one loss bookkeeping launch at a time, flushing when a chunk completes."""
         stream = torch.cuda.current_stream(self.device)
         b = b_start
         while b < b_end:
@@ -354,7 +432,7 @@ class FusedBPRTrainStep(object):
             self._enter_chunk(k, stream)
             slot = self.slots[k % 2]
             c0, c1 = b - b0, min(nb, b_end - b0)
-            if (self.use_graph and c0 == 0 and c1 == nb == self.C and Bc == self.B
+            if (self.use_graph and c0 == 0 and c1 == nb == self.C and Bc == self.Bg
                     and self.kernel_events is None):
                 self._graph_for(slot).replay()
             else:
@@ -369,7 +447,7 @@ class FusedBPRTrainStep(object):
         self.run_batches(b, b + 1)
 
     def _chunk_of(self, b):
-        full = self._users.numel() // self.B
+        full = self._users.numel() // self.Bg
         if b >= full:
             return len(self._plan) - 1
         return b // self.C
