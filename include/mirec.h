@@ -168,7 +168,8 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
  *   g = fma(p, wd, g);  m = fma(1-b1, g-m, m);  v = fma((1-b2)*g, g, v*b2);
  *   p = p + ((-step_size) * m) / (sqrt(v)/bc2_sqrt + eps)
  * step_consts_dev (16-byte aligned) holds 4 floats per 0-based step index s:
- * {step_size, bc2_sqrt, RN(1/bc2_sqrt), 0}, precomputed on the host in double
+ * {step_size, bc2_sqrt, RN(1/bc2_sqrt), step_size*bc2_sqrt*(1+2^-20) rounded up},
+ * precomputed on the host in double
  * like torch does; step s = step_idx_dev[0] is a device counter (advanced by
  * mirec_step_finish) so that a captured graph replays successive steps.
  * ------------------------------------------------------------------------- */

@@ -26,7 +26,8 @@
 // correctly rounded), so p agrees to an ulp there, exactly elsewhere.
 //
 // Host table (float32, 4 per 0-based step index s), computed in double like
-// torch: {step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t), rbc = RN(1/bc2_sqrt), 0}.
+// torch: {step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t), rbc = RN(1/bc2_sqrt),
+// kq = step_size*bc2_sqrt*(1+2^-20) rounded up (p_update_vanishes)}.
 // x / bc2_sqrt is evaluated as q = x*rbc; q + fma(-q, bc2_sqrt, x)*rbc (fma):
 // with rbc the correctly rounded reciprocal this is the correctly rounded
 // quotient (Markstein's theorem; checked exhaustively over two binades of x for
@@ -51,12 +52,32 @@ struct AdamConsts {
 };
 
 struct StepConsts {
-  float ss, bc2s, rbc;
+  float ss, bc2s, rbc, kq;  // kq >= step_size * bc2_sqrt * (1 + 2^-20), rounded up
 };
 
 __device__ __forceinline__ StepConsts step_consts(const float* __restrict__ consts, int s) {
   const float4 c = reinterpret_cast<const float4*>(consts)[s];
-  return {c.x, c.y, c.z};
+  return {c.x, c.y, c.z, c.w};
+}
+
+// Zero-gradient step whose p update provably rounds away: with me, ve the new
+// moments, the increment q = RN(RN(-ss*me) / den), den = RN(RN(RN(sqrt(ve))/bc2s)
+// + eps) >= sqrt(ve)(1-u)^3/bc2s, so |q| <= kq*|me|/sqrt(ve) (u = 2^-24; kq holds
+// the (1+u)^2/(1-u)^3 margin). If that bound is below ulp(p)/4, RN(p + q) == p
+// (the nearest other float is at least ulp(p)/2 away, also below a power of two).
+// Tested without sqrt or division as (kq*|me| * 2^(26-e))^2 < 0.999*ve, where
+// p = f*2^e, f in [0.5, 1): the power-of-two scaling is exact, the two roundings
+// of the left side and the 0.999 cover the rest. Only for normal |p| >= 2^-60
+// and ve >= 2^-100 (no denormal scaling error can matter there).
+// me == 0 (a row never touched, or whose momentum underflowed): q = -0 / den with
+// den >= eps > 0, and p + (-0) == p for every p, zeros included.
+__device__ __forceinline__ bool p_update_vanishes(float p, float me, float ve,
+                                                  const StepConsts& sc, float eps) {
+  const uint32_t ex = (__float_as_uint(p) >> 23) & 0xffu;       // biased exponent
+  const float scale = __uint_as_float((279u - ex) << 23);        // 2^(152-ex) = 2^(26-e)
+  const float t = (sc.kq * fabsf(me)) * scale;
+  return (me == 0.f && eps > 0.f) ||
+         (ex >= 67u && ex < 255u && ve >= 0x1p-100f && t * t < 0.999f * ve);
 }
 
 // Launch = a list of segments, each a contiguous block range over one table.
@@ -151,12 +172,43 @@ __device__ __forceinline__ void adam_replay(V& p, V& m, V& v, int s0, int s1,
                                             const AdamConsts& k) {
   const int lo = __builtin_amdgcn_readfirstlane(wave_min_i(s0));
   if (k.wd == 0.f && k.lerp_small) {
+    // Long-idle rows: once every p update of the wave provably rounds away
+    // (p_update_vanishes), a step only moves m and v. The test runs every step
+    // while it holds and every 4th step while it does not; a skipped step gives
+    // exactly the bits the full step would.
+    bool skipping = false;
+    constexpr int N = Lanes<V>::n;
     for (int s = lo; s < s1; ++s) {
       const StepConsts sc = step_consts(consts, s);
-      if (s >= s0) {
+      const bool act = s >= s0;
+      float me[N], ve[N];
 #pragma unroll
-        for (int i = 0; i < Lanes<V>::n; ++i)
-          adam_elem_zero(Lanes<V>::at(p, i), Lanes<V>::at(m, i), Lanes<V>::at(v, i), sc, k);
+      for (int i = 0; i < N; ++i) {
+        me[i] = fmaf(-k.omb1, Lanes<V>::at(m, i), Lanes<V>::at(m, i));
+        ve[i] = Lanes<V>::at(v, i) * k.b2;
+      }
+      bool vanish = false;
+      if (skipping || ((s - lo) & 3) == 0) {
+        bool mine = true;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+          mine = mine && p_update_vanishes(Lanes<V>::at(p, i), me[i], ve[i], sc, k.eps);
+        vanish = __all(!act || mine);
+      }
+      skipping = vanish;
+      if (!vanish && act) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const float den = div_bc2s(sqrtf(ve[i]), sc) + k.eps;
+          Lanes<V>::at(p, i) = Lanes<V>::at(p, i) + ((-sc.ss) * me[i]) / den;
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          Lanes<V>::at(m, i) = me[i];
+          Lanes<V>::at(v, i) = ve[i];
+        }
       }
     }
   } else {
@@ -297,28 +349,31 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   const bool ahead = si & 1;
   const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
-  const bool valid = u < (ahead ? T.ahead_n_uniq[0] : T.n_uniq[0]);
+  // Dependent-load chain kept to three levels: (count, row id) -> (last, p, m,
+  // v, the row's gradient contributions) -> replay + step. The block barrier
+  // that orders every thread's read of `last` before the row's write sits at
+  // the end, so no thread leaves early.
+  const int n = ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
   const int st = step_base[0] + step_off;
+  const bool valid = u < n;
   int64_t row = 0;
   int last = st;
+  float2 p = make_float2(0.f, 0.f), m = p, v = p, g = p;
   if (valid) {
     row = ahead ? T.ahead_uniq[u] : T.uniq[u];
+    const int64_t off = row * VPR + c;
     last = T.last[row];
-  }
-  __syncthreads();
-  const int64_t off = row * VPR + c;
-  float2 p = make_float2(0.f, 0.f), m = p, v = p;
-  if (valid) {
     p = reinterpret_cast<const float2*>(T.p)[off];
     m = reinterpret_cast<const float2*>(T.m)[off];
     v = reinterpret_cast<const float2*>(T.v)[off];
+    if (!ahead) g = grouped_grad<float2>(T, u, VPR, c);
   }
   // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop)
   adam_replay(p, m, v, last, st, consts, k);
-  if (!valid) return;
-  float2 g = make_float2(0.f, 0.f);
-  if (!ahead) g = grouped_grad<float2>(T, u, VPR, c);
   adam_vec(p, m, v, g, step_consts(consts, st), k);
+  __syncthreads();
+  if (!valid) return;
+  const int64_t off = row * VPR + c;
   reinterpret_cast<float2*>(T.p)[off] = p;
   reinterpret_cast<float2*>(T.m)[off] = m;
   reinterpret_cast<float2*>(T.v)[off] = v;

@@ -69,6 +69,12 @@ class FusedAdam(torch.optim.Optimizer):
             out[j, 1] = (1 - b2 ** t) ** 0.5
         # correctly rounded reciprocal: 1/x in double then one rounding to float
         out[:, 2] = 1.0 / out[:, 1].astype(np.float64)
+        # bound of the zero-gradient skip test (adam.hip p_update_vanishes):
+        # step_size * bc2_sqrt * (1 + 2^-20), rounded up to float
+        kq = out[:, 0].astype(np.float64) * out[:, 1].astype(np.float64) * (1 + 2.0 ** -20)
+        kq32 = kq.astype(np.float32)
+        out[:, 3] = np.where(kq32.astype(np.float64) < kq,
+                             np.nextafter(kq32, np.float32(np.inf)), kq32)
         if count and not (out[:, 1] > 0).all():
             raise ValueError(f'beta2={b2} too close to 1: sqrt(1 - beta2^t) rounds to 0 in fp32')
         return out

@@ -399,6 +399,47 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
             assert torch.equal(a, b), (a - b).abs().max()
 
 
+@pytest.mark.parametrize('lr', [1e-3, 3e-2])
+def test_adam_deferred_long_idle_rows_bitwise(dev, lr):
+    """Rows idle for hundreds of steps (where the deferred replay stops updating p
+    once its increments provably round away) end bit-identical to the streamed
+    dense Adam that updates them every step."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(11)
+    d, sizes, steps = 128, (40, 72), 420
+    init = [(torch.randn(n, d, generator=g) * s) for n, s in zip(sizes, (0.1, 3e-3))]
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(1))], lr=lr)
+    consts = torch.from_numpy(opt.step_constants(1, steps).reshape(-1)).to(dev)
+    hot = 6
+    keys = []
+    for s in range(steps):
+        ks = [torch.arange(n) if s == 0 else torch.randint(0, hot, (5,), generator=g)
+              for n in sizes]
+        keys.append([(k, torch.randn(k.numel(), d, generator=g) * 1e-2) for k in ks])
+    segs = [[ops.segment_sort(k.to(dev), sizes[q]) for q, (k, _) in enumerate(b)] for b in keys]
+
+    def run(schedule):
+        P = [x.clone().to(dev) for x in init]
+        M = [torch.zeros_like(x) for x in P]
+        V = [torch.zeros_like(x) for x in P]
+        last = [torch.zeros(x.shape[0], dtype=torch.int32, device=dev) for x in P]
+        base = torch.zeros(1, dtype=torch.int32, device=dev)
+        for s in range(steps):
+            tabs = ops.adam_tables([dict(p=P[q], m=M[q], v=V[q], rows=keys[s][q][1].to(dev),
+                                         segs=segs[s][q], last=last[q]) for q in range(2)])
+            ops.adam_multi(tabs, d, consts, base, 0, schedule,
+                           n_max_uniq=[k.numel() for k, _ in keys[s]])
+            base += 1
+        if schedule == 'deferred':
+            ops.adam_multi(tabs, d, consts, base, 0, 'flush')
+        return [t.cpu() for t in P + M + V]
+
+    ref, got = run('streamed'), run('deferred')
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b), (a - b).abs().max()
+
+
 def test_adam_matches_torch_cpu_rounding(dev):
     """m and v agree with torch CPU's Adam to the bit (same fma pattern); p to
     the ulp the CPU's vector sqrt may differ by."""

@@ -58,7 +58,7 @@ def main():
         return float(np.median(ts))
 
     print(f"streamed      : {timeit(lambda: ops.adam_multi(tabs, d, consts, base, 0)):8.2f} us")
-    for gap in (0, 1, 8, 32, 63, 127):
+    for gap in (0, 1, 8, 32, 63, 127, 511):
         def prep(gap=gap):
             base.fill_(1000)
             for x in last:
