@@ -105,7 +105,10 @@ __device__ __forceinline__ void load_user_operand(const float* __restrict__ Uq, 
 }
 
 template <int D, int KC>
-__global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
+#ifndef MIREC_FS_WAVES_PER_EU
+#define MIREC_FS_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU) void fullsort_topk_kernel(
     const float* __restrict__ Uq, int64_t nq, const float* __restrict__ EI, int64_t I,
     const int64_t* __restrict__ hist_ptr, const int32_t* __restrict__ hist_cols,
     const int64_t* __restrict__ pos_ptr, const int32_t* __restrict__ pos_cols, int K,
@@ -219,7 +222,12 @@ __global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
     // partner's K-th best already has K better items, so it can never reach the
     // final (merged) top-K: filter with the stronger of the two thresholds.
     thr = fmaxf(thr, __shfl_xor(thr, 32, 64));
+#ifdef MIREC_FS_NO_TOPK   // profiling variant (tools/build_variant.sh): MFMA + mask only
+    thr = fmaxf(thr, best);
+    if (false) {
+#else
     if (__any(best > thr)) {             // wave-uniform: rare once the lists fill up
+#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -238,6 +246,9 @@ __global__ __launch_bounds__(kFsThreads) void fullsort_topk_kernel(
     cur ^= 1;
   }
 
+#ifdef MIREC_FS_NO_TOPK
+  ts[0] = thr;   // keep the scores live in the profiling variant
+#endif
   // merge the two item halves of each user: lane j takes lane j+32's list
 #pragma unroll
   for (int t = 0; t < KC; ++t) {

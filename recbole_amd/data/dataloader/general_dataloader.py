@@ -296,3 +296,16 @@ class GeneralFullDataLoader(NegSampleMixin):
 
     def get_user_len_list(self):
         return np.full(self.pr_end, self.dataset.item_num)
+
+    def device_csr(self, device):
+        """(uids, hist_ptr, hist_cols, pos_ptr, pos_cols) resident on `device`,
+        uploaded once per loader (the fused evaluator's inputs; history and
+        positives do not change between evaluations)."""
+        key = str(device)
+        cache = self.__dict__.setdefault('_device_csr', {})
+        if key not in cache:
+            up = lambda a: torch.as_tensor(a, device=device)
+            hist_cols = self.hist_cols if len(self.hist_cols) else np.zeros(1, np.int32)
+            cache[key] = (torch.as_tensor(self.uid_list, dtype=torch.int64, device=device),
+                          up(self.hist_ptr), up(hist_cols), up(self.pos_ptr), up(self.pos_cols))
+        return cache[key]

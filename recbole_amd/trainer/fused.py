@@ -482,12 +482,7 @@ def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20):
     reduction (evaluators.py:122-141)."""
     dev = model.fused_item_table().device
     K = max(topk_evaluator.topk)
-    uids = torch.as_tensor(eval_data.uid_list, dtype=torch.int64, device=dev)
-    hist_ptr = torch.as_tensor(eval_data.hist_ptr, device=dev)
-    hist_cols = torch.as_tensor(eval_data.hist_cols if len(eval_data.hist_cols)
-                                else np.zeros(1, np.int32), device=dev)
-    pos_ptr = torch.as_tensor(eval_data.pos_ptr, device=dev)
-    pos_cols = torch.as_tensor(eval_data.pos_cols, device=dev)
+    uids, hist_ptr, hist_cols, pos_ptr, pos_cols = eval_data.device_csr(dev)
     EI = model.fused_item_table().contiguous()
     n = uids.numel()
     flags = torch.empty(n, K, dtype=torch.uint8, device=dev)
