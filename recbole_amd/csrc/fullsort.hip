@@ -105,10 +105,14 @@ __device__ __forceinline__ void load_user_operand(const float* __restrict__ Uq, 
 }
 
 template <int D, int KC>
+// Two waves per SIMD (<= 256 VGPRs, no spills for D <= 128): the second wave's
+// VALU top-K work overlaps the first one's MFMAs — measured 1.43x over one wave
+// per SIMD at C2 (21.6 -> 15.0 ms). D = 256 keeps one (its user operand alone
+// takes 128 VGPRs).
 #ifndef MIREC_FS_WAVES_PER_EU
-#define MIREC_FS_WAVES_PER_EU 1
+#define MIREC_FS_WAVES_PER_EU(D) ((D) <= 128 ? 2 : 1)
 #endif
-__global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU) void fullsort_topk_kernel(
+__global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort_topk_kernel(
     const float* __restrict__ Uq, int64_t nq, const float* __restrict__ EI, int64_t I,
     const int64_t* __restrict__ hist_ptr, const int32_t* __restrict__ hist_cols,
     const int64_t* __restrict__ pos_ptr, const int32_t* __restrict__ pos_cols, int K,

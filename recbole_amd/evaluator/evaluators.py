@@ -8,7 +8,7 @@ import numpy as np
 import torch
 from torch.nn.utils.rnn import pad_sequence
 
-from recbole_amd.evaluator.metrics import metrics_dict
+from recbole_amd.evaluator.metrics import metrics_dict, topk_metric_rows
 
 topk_metrics = {m.lower(): m for m in ['Hit', 'Recall', 'MRR', 'Precision', 'NDCG', 'MAP']}
 loss_metrics = {m.lower(): m for m in ['AUC', 'RMSE', 'MAE', 'LOGLOSS']}
@@ -74,7 +74,7 @@ class TopKEvaluator(BaseEvaluator):
         """Metric reduction from the [n_users, max(topk)] positive matrix
         (evaluators.py:78-141)."""
         out = {}
-        vals = np.stack([metrics_dict[m.lower()](pos_idx, pos_len_list) for m in self.metrics],
+        vals = np.stack([topk_metric_rows(m.lower(), pos_idx, pos_len_list) for m in self.metrics],
                         axis=0).mean(axis=1)
         for m, v in zip(self.metrics, vals):
             for k in self.topk:

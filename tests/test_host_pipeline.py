@@ -137,3 +137,18 @@ def test_reciprocal_division_is_correctly_rounded():
         e = (x.astype(np.float64) - q.astype(np.float64) * np.float64(d)).astype(np.float32)
         q2 = (q.astype(np.float64) + e.astype(np.float64) * np.float64(r)).astype(np.float32)
         assert np.array_equal(q2, x / d)
+
+
+def test_metric_pattern_tables_equal_direct_formulas():
+    """The pattern-table path of the top-K metrics (many users, small K) gives the
+    same float64 rows as the direct vectorised formulas, incl. empty positive sets."""
+    from recbole_amd.evaluator import metrics as M
+    rng = np.random.default_rng(5)
+    for K in (1, 3, 10):
+        pos_idx = rng.random((20000, K)) < 0.3
+        pos_len = rng.integers(0, 3 * K, 20000)
+        for name in ('hit', 'mrr', 'precision', 'recall', 'ndcg', 'map'):
+            with np.errstate(all='ignore'):
+                a = M.metrics_dict[name](pos_idx, pos_len)
+                b = M.topk_metric_rows(name, pos_idx, pos_len)
+            assert np.array_equal(a, b, equal_nan=True), (K, name)
