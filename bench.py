@@ -157,6 +157,38 @@ def roofline(step, events, uniq, d, M):
     return adam, bpr, kernels_us
 
 
+def gather_throughput(step, d, neg, B=65536, reps=20):
+    """north_star's gather roofline at the throughput setting of SURVEY.md §8d
+    (B = 65,536 positives, C2 tables): K3 alone — (2+T) row gathers per positive
+    and the per-contribution gradient rows written — HIP events per launch.
+    Bytes per launch = 2*(B + (1+T)B)*d*4 (rows read + gradient rows written)
+    + 8*(B + (1+T)B) (ids) + 4*B (losses)."""
+    from recbole_amd import ops
+    dev = step.device
+    g = torch.Generator(device='cpu').manual_seed(7)
+    user = torch.randint(0, step.nU, (B,), generator=g).to(dev)
+    pos = torch.randint(1, step.nI, (B,), generator=g).to(dev)
+    negs = torch.randint(1, step.nI, (neg * B,), generator=g).to(dev)
+    out = {}
+    ops.bpr_fwd_bwd(step.pU.detach(), step.pI.detach(), user, pos, negs, neg, out=out)
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ops.bpr_fwd_bwd(step.pU.detach(), step.pI.detach(), user, pos, negs, neg, out=out)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e-3)
+    t = float(np.median(ts))
+    rows = B + (1 + neg) * B
+    nbytes = 2 * rows * d * 4 + rows * 8 + B * 4
+    gbs = nbytes / t / 1e9
+    return {'kernel': f'K3 bpr_fwd_bwd<{d}> at B={B} positives', 'bound': 'hbm',
+            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes,
+            'launch_us': round(t * 1e6, 1), 'positives_per_s': round(B / t, 1)}
+
+
 def cpu_baseline(train, step_obj, d, neg, steps):
     from oracle import cpu_baseline as cb
     users = train.dataset.inter_feat['user_id'].cpu().numpy()
@@ -279,6 +311,8 @@ def main():
         result['eval'] = {'metric': 'full-sort eval users/sec', 'value': round(n_users / e_dt, 1),
                           'users': n_users, 'seconds': round(e_dt, 4),
                           'flops_per_user': 2 * step.nI * d}
+    if rank == 0 and not args.no_eval:
+        result['gather_throughput'] = gather_throughput(step, d, neg)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(train, step, d, neg, args.cpu_steps)
     if rank == 0:
