@@ -230,6 +230,74 @@ def bpr_train_steps(model: BPRCPU, batches, lr=1e-3, weight_decay=0.0):
 
 
 # --------------------------------------------------------------------------
+# LightGCN  (recbole/model/general_recommender/lightgcn.py:32-180)
+# --------------------------------------------------------------------------
+def lightgcn_norm_adj(inter_rows, inter_cols, n_users, n_items):
+    """get_norm_adj_mat (lightgcn.py:71-104) with scipy + torch CPU. The
+    reference fills a dok_matrix through the private dok._update (:89), which
+    the container's scipy lacks; the same dict of (row, col) -> 1 is written
+    here through a CSR with duplicates reset to 1. Then, as written:
+    sumArr = (A > 0).sum(1); diag = sumArr + 1e-7; D^-1/2 * A * D^-1/2 (float64
+    from the float64 diag), coo, torch.sparse FloatTensor."""
+    import scipy.sparse as sp
+    N = n_users + n_items
+    r = np.asarray(inter_rows, dtype=np.int64)
+    c = np.asarray(inter_cols, dtype=np.int64) + n_users
+    rows = np.concatenate([r, c])
+    cols = np.concatenate([c, r])
+    A = sp.coo_matrix((np.ones(len(rows), dtype=np.float32), (rows, cols)), shape=(N, N)).tocsr()
+    A.data[:] = 1.0
+    sumArr = (A > 0).sum(axis=1)
+    diag = np.array(sumArr.flatten())[0] + 1e-7
+    diag = np.power(diag, -0.5)
+    D = sp.diags(diag)
+    L = sp.coo_matrix(D * A * D)
+    i = torch.LongTensor(np.array([L.row, L.col]))
+    return torch.sparse_coo_tensor(i, torch.FloatTensor(L.data), torch.Size(L.shape))
+
+
+class LightGCNCPU(torch.nn.Module):
+    """LightGCN forward / calculate_loss / full_sort_predict on torch CPU
+    (lightgcn.py:106-180) with BPRLoss + EmbLoss (loss.py:23-84)."""
+
+    def __init__(self, n_users, n_items, d, n_layers, reg_weight, norm_adj, init=True):
+        super().__init__()
+        self.n_users, self.n_items, self.n_layers = n_users, n_items, n_layers
+        self.reg_weight = reg_weight
+        self.user_embedding = torch.nn.Embedding(n_users, d)
+        self.item_embedding = torch.nn.Embedding(n_items, d)
+        self.norm_adj_matrix = norm_adj
+        if init:
+            torch.nn.init.xavier_uniform_(self.user_embedding.weight.data)
+            torch.nn.init.xavier_uniform_(self.item_embedding.weight.data)
+
+    def forward(self):
+        all_e = torch.cat([self.user_embedding.weight, self.item_embedding.weight], dim=0)
+        embs = [all_e]
+        for _ in range(self.n_layers):
+            all_e = torch.sparse.mm(self.norm_adj_matrix, all_e)
+            embs.append(all_e)
+        out = torch.mean(torch.stack(embs, dim=1), dim=1)
+        return torch.split(out, [self.n_users, self.n_items])
+
+    def calculate_loss(self, user, pos, neg, gamma=1e-10):
+        ua, ia = self.forward()
+        u, p, n = ua[user], ia[pos], ia[neg]
+        ps = torch.mul(u, p).sum(dim=1)
+        ns = torch.mul(u, n).sum(dim=1)
+        mf = -torch.log(gamma + torch.sigmoid(ps - ns)).mean()
+        emb = torch.zeros(1)
+        for e in (self.user_embedding(user), self.item_embedding(pos), self.item_embedding(neg)):
+            emb += torch.norm(e, p=2)
+        emb /= neg.shape[0]
+        return mf + self.reg_weight * emb
+
+    def full_sort_predict(self, user):
+        ua, ia = self.forward()
+        return torch.matmul(ua[user], ia.transpose(0, 1)).view(-1)
+
+
+# --------------------------------------------------------------------------
 # Full-sort evaluation (trainer.py:328-353, evaluators.py:53-141)
 # --------------------------------------------------------------------------
 def full_sort_pos_idx(scores: torch.Tensor, hist: list, pos: list, K: int):

@@ -22,6 +22,17 @@ LIB_PATH = os.environ.get("MIREC_LIB", os.path.join(_HERE, "_lib", "libmirec.so"
 _P = c_void_p
 
 
+class RowsRef(ctypes.Structure):
+    """struct mirec_rows_ref (include/mirec.h)."""
+    _fields_ = [('lo', _P), ('hi', _P), ('split', c_int64)]
+
+
+class SpmmEpilogue(ctypes.Structure):
+    """struct mirec_spmm_epilogue (include/mirec.h)."""
+    _fields_ = [('add', RowsRef), ('add_scale', c_float), ('y', RowsRef), ('acc_in', RowsRef),
+                ('acc_out', RowsRef), ('acc_scale', c_float)]
+
+
 class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
@@ -55,6 +66,8 @@ SIGNATURES = {
     "mirec_adam_sparse_grad_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, _P, _P,
                                            c_int64, _P, _P, _P, c_double, c_double, c_double,
                                            c_double, _P]),
+    "mirec_adam_flat_f32": (c_int, [_P, _P, _P, c_int64, _P, _P, _P, c_double, c_double,
+                                    c_double, c_double, _P]),
     "mirec_adam_multi_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
     "mirec_adam_deferred_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, _P, c_int32, _P,
@@ -67,9 +80,14 @@ SIGNATURES = {
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
                                         c_int32, _P, _P, _P, _P]),
     "mirec_score_matrix_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P]),
+    "mirec_spmm_csr_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
+                                   _P, _P, c_int64, _P, ctypes.POINTER(RowsRef),
+                                   ctypes.POINTER(SpmmEpilogue), _P]),
+    "mirec_gather_sqnorm_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P]),
+    "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class NativeError(RuntimeError):

@@ -557,3 +557,48 @@ extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t 
   return mirec_adam_multi_f32(&t, 1, d, step_consts_dev, step_idx_dev, 0, beta1, beta2, eps,
                               weight_decay, stream);
 }
+
+namespace mirec {
+
+// Flat form: any number of elements (biases, [n,1] first-order tables, MLP
+// weights whose numel is not a multiple of 4), dense gradient, same adam_elem.
+__global__ __launch_bounds__(kAdamThreads) void adam_flat_kernel(
+    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int64_t n,
+    const float* __restrict__ g, const float* __restrict__ consts,
+    const int32_t* __restrict__ step_idx, AdamConsts k) {
+  const StepConsts sc = step_consts(consts, step_idx[0]);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, mm, vv, g[i], sc, k);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_adam_flat_f32(float* p, float* m, float* v, int64_t n,
+                                   const float* grad, const float* step_consts_dev,
+                                   const int32_t* step_idx_dev, double beta1, double beta2,
+                                   double eps, double weight_decay, void* stream) {
+  if (n == 0) return 0;
+  if (!p || !m || !v || !grad || !step_consts_dev || !step_idx_dev || n < 0) {
+    set_error("mirec_adam_flat_f32: bad arguments");
+    return -1;
+  }
+  AdamConsts k;
+  k.omb1 = (float)(1.0 - beta1);
+  k.omb1m1 = k.omb1 - 1.0f;
+  k.lerp_small = fabsf(k.omb1) < 0.5f;
+  k.b2 = (float)beta2;
+  k.omb2 = (float)(1.0 - beta2);
+  k.eps = (float)eps;
+  k.wd = (float)weight_decay;
+  int64_t blocks = (n + kAdamThreads - 1) / kAdamThreads;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0,
+                     (hipStream_t)stream, p, m, v, n, grad, step_consts_dev, step_idx_dev, k);
+  return launch_status("mirec_adam_flat_f32");
+}

@@ -7,6 +7,9 @@ the wrong device or a missing library raises.
 """
 from __future__ import annotations
 
+import ctypes
+
+import numpy as np
 import torch
 
 from recbole_amd._native import NativeError, check, lib, ptr, stream_handle
@@ -234,17 +237,22 @@ def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None =
         _dev(t_, torch.float32, n_)
     _dev(step_consts, torch.float32, "step_consts")
     _dev(step_idx, torch.int32, "step_idx")
-    if p.dim() == 2 and p.shape[1] in (16, 32, 64, 128, 256):
-        n_rows, d = p.shape
-    elif p.numel() % 4 == 0:
-        n_rows, d = p.numel() // 4, 4
-        if segs is not None:
-            raise ValueError("grouped gradients need a 2-D table")
-    else:
-        raise NotImplementedError(f"adam_step: parameter of shape {tuple(p.shape)} "
-                                  f"(numel % 4 != 0) is not supported by the fused kernel")
     if dense_grad is not None:
         _dev(dense_grad, torch.float32, "dense_grad")
+    if p.dim() == 2 and p.shape[1] in (16, 32, 64, 128, 256):
+        n_rows, d = p.shape
+    elif segs is not None:
+        raise ValueError("grouped gradients need a 2-D table of width 16..256")
+    elif p.numel() % 4 == 0:
+        n_rows, d = p.numel() // 4, 4
+    else:
+        if dense_grad is None:
+            raise ValueError("adam_step: a flat parameter needs a dense gradient")
+        rc = lib().mirec_adam_flat_f32(ptr(p), ptr(m), ptr(v), p.numel(), ptr(dense_grad),
+                                       ptr(step_consts), ptr(step_idx), beta1, beta2, eps,
+                                       weight_decay, stream_handle())
+        check(rc, "mirec_adam_flat_f32")
+        return
     rc = lib().mirec_adam_sparse_grad_f32(
         ptr(p), ptr(m), ptr(v), n_rows, d, ptr(rows),
         ptr(segs.perm) if segs else None, ptr(segs.uniq) if segs else None,
@@ -354,4 +362,117 @@ def score_matrix(Uq, EI, out=None):
     rc = lib().mirec_score_matrix_f32(ptr(Uq), Uq.shape[0], ptr(EI), EI.shape[0], Uq.shape[1],
                                       ptr(out), stream_handle())
     check(rc, "mirec_score_matrix_f32")
+    return out
+
+
+# ---------------------------------------------------------------- K7 graph propagation
+def _rows_ref(t):
+    """mirec_rows_ref from None, a [n, d] tensor, or a (lo, hi) pair of row blocks."""
+    from recbole_amd._native import RowsRef
+    if t is None:
+        return RowsRef(None, None, 0)
+    if isinstance(t, tuple):
+        lo, hi = t
+        _dev(lo, torch.float32, "rows.lo")
+        _dev(hi, torch.float32, "rows.hi")
+        return RowsRef(ptr(lo), ptr(hi), lo.shape[0])
+    _dev(t, torch.float32, "rows")
+    return RowsRef(ptr(t), None, t.shape[0])
+
+
+def _rows_n(t):
+    if t is None:
+        return None
+    if isinstance(t, tuple):
+        return t[0].shape[0] + t[1].shape[0], t[0].shape[1]
+    return t.shape[0], t.shape[1]
+
+
+class SpmmPlan:
+    """Device CSR of a square sparse matrix plus the K7 load-balancing plan:
+    every row is cut into units of at most `piece` nonzeros (include/mirec.h)."""
+
+    def __init__(self, row_ptr: np.ndarray, cols: np.ndarray, vals: np.ndarray, device,
+                 piece: int = 256):
+        row_ptr = np.asarray(row_ptr, dtype=np.int64)
+        n = len(row_ptr) - 1
+        deg = np.diff(row_ptr)
+        n_units_row = np.maximum(1, -(-deg // piece))
+        first_unit = np.concatenate([[0], np.cumsum(n_units_row)])
+        n_units = int(first_unit[-1])
+        unit_row = np.repeat(np.arange(n, dtype=np.int32), n_units_row)
+        k_in_row = np.arange(n_units, dtype=np.int64) - first_unit[:-1][unit_row]
+        unit_beg = row_ptr[:-1][unit_row] + k_in_row * piece
+        split = n_units_row > 1
+        unit_slot = np.full(n_units, -1, dtype=np.int32)
+        in_split = split[unit_row]
+        unit_slot[in_split] = np.arange(int(in_split.sum()), dtype=np.int32)
+        fix_row = np.nonzero(split)[0].astype(np.int32)
+        fix_ptr = np.concatenate([[0], np.cumsum(n_units_row[split])]).astype(np.int32)
+        self.n_rows, self.nnz, self.piece = n, int(row_ptr[-1]), piece
+        self.n_units, self.n_fix, self.n_slots = n_units, len(fix_row), int(fix_ptr[-1])
+        T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=device)
+        self.row_ptr, self.cols, self.vals = T(row_ptr), T(cols.astype(np.int32)), \
+            T(vals.astype(np.float32))
+        self.unit_row, self.unit_beg, self.unit_slot = T(unit_row), T(unit_beg), T(unit_slot)
+        self.fix_row, self.fix_ptr = T(fix_row), T(fix_ptr)
+        self._partial = {}
+
+    def partial(self, d, device):
+        if self.n_slots == 0:
+            return None
+        if d not in self._partial:
+            self._partial[d] = torch.empty(self.n_slots, d, dtype=torch.float32, device=device)
+        return self._partial[d]
+
+
+def spmm_csr(plan: SpmmPlan, x, y=None, add=None, add_scale: float = 1.0, acc_in=None,
+             acc_out=None, acc_scale: float = 1.0):
+    """One K7 launch: y = A @ x (+ add_scale*add); Y = y; ACC_OUT = (ACC_IN + y)*acc_scale.
+    Each operand is None, a [n, d] tensor or a (lo, hi) pair of row blocks."""
+    from recbole_amd._native import SpmmEpilogue
+    n, d = _rows_n(x)
+    if n != plan.n_rows:
+        raise ValueError(f"spmm_csr: x has {n} rows, the matrix {plan.n_rows}")
+    for name, t in (("y", y), ("add", add), ("acc_in", acc_in), ("acc_out", acc_out)):
+        if t is not None and _rows_n(t) != (n, d):
+            raise ValueError(f"spmm_csr: {name} shape {_rows_n(t)} != {(n, d)}")
+    if y is None and acc_out is None:
+        raise ValueError("spmm_csr: nothing to write")
+    dev = plan.row_ptr.device
+    part = plan.partial(d, dev)
+    ep = SpmmEpilogue(_rows_ref(add), add_scale, _rows_ref(y), _rows_ref(acc_in),
+                      _rows_ref(acc_out), acc_scale)
+    xr = _rows_ref(x)
+    rc = lib().mirec_spmm_csr_f32(ptr(plan.row_ptr), ptr(plan.cols), ptr(plan.vals), plan.n_rows,
+                                  d, ptr(plan.unit_row), ptr(plan.unit_beg), ptr(plan.unit_slot),
+                                  plan.n_units, plan.piece, ptr(plan.fix_row), ptr(plan.fix_ptr),
+                                  plan.n_fix, ptr(part), ctypes.byref(xr), ctypes.byref(ep),
+                                  stream_handle())
+    check(rc, "mirec_spmm_csr_f32")
+
+
+def gather_sqnorm(table, idx, out=None):
+    """out[i] = ||table[idx[i]]||^2 (EmbLoss, loss.py:79-84)."""
+    _dev(table, torch.float32, "table")
+    _dev(idx, torch.int64, "idx")
+    if out is None:
+        out = torch.empty(idx.numel(), dtype=torch.float32, device=table.device)
+    rc = lib().mirec_gather_sqnorm_f32(ptr(table), table.shape[0], table.shape[1], ptr(idx),
+                                       idx.numel(), ptr(out), stream_handle())
+    check(rc, "mirec_gather_sqnorm_f32")
+    return out
+
+
+def gather_scale_rows(table, idx, scale_dev, out=None):
+    """out[i, :] = scale_dev[0] * table[idx[i], :]."""
+    _dev(table, torch.float32, "table")
+    _dev(idx, torch.int64, "idx")
+    _dev(scale_dev, torch.float32, "scale")
+    if out is None:
+        out = torch.empty(idx.numel(), table.shape[1], dtype=torch.float32, device=table.device)
+    rc = lib().mirec_gather_scale_rows_f32(ptr(table), table.shape[0], table.shape[1], ptr(idx),
+                                           idx.numel(), ptr(scale_dev), ptr(out),
+                                           stream_handle())
+    check(rc, "mirec_gather_scale_rows_f32")
     return out

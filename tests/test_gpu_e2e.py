@@ -44,7 +44,7 @@ def _pipeline(tmp_path, **over):
     init_seed(config['seed'], config['reproducibility'])
     ds = create_dataset(config)
     train, valid, test = data_preparation(config, ds)
-    model = get_model('BPR')(config, train).to(config['device'])
+    model = get_model(cd['model'])(config, train).to(config['device'])
     return config, train, valid, test, model
 
 
