@@ -329,6 +329,63 @@ int mirec_gather_scale_rows_f32(const float* table, int64_t n_rows, int32_t d,
                                 const int64_t* idx, int64_t n, const float* scale_dev,
                                 float* out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * K8  Context-aware fields + factorization machine (DeepFM's embedding side).
+ * Replaces ContextRecommender.embed_input_fields / concat_embed_input_fields
+ *   (recbole/model/abstract_recommender.py:199-412), FMEmbedding
+ *   (model/layers.py:121-144), BaseFactorizationMachine (:147-171),
+ *   FMFirstOrderLinear (:905-1062) and DeepFM's y_fm (context_aware_recommender/
+ *   deepfm.py:58-70), with their autograd backward.
+ * fields_dev: DEVICE array of n_fields descriptors in concat order
+ *   (token fields, then token_seq fields, then float fields):
+ *   kind 0 token:     row = ids[b] + offset of the shared token table;
+ *   kind 1 token_seq: ids [B, seq_len] into the field's own table, masked mean
+ *                     sum(e * (id != 0)) / (count + 1e-8);
+ *   kind 2 float:     e = table[offset] * vals[b].
+ *   table1 is the matching first-order table (width 1, same rows).
+ * Forward:  concat[b, f*d + k] = e_bfk;  keys[b] = token row (kind 0, if keys);
+ *   y_fm[b] = (sum float w*x + sum token w + sum token_seq masked w) + bias[0]
+ *             + 0.5 * sum_k ((sum_f e_bfk)^2 - sum_f e_bfk^2).
+ * Backward (g_concat may be NULL): ge = g_concat + g_fm[b] * (S_bk - e_bfk);
+ *   token: grad[b*grad_ld + k] = ge, grad1[b*grad1_ld] = g_fm[b];
+ *   token_seq: grad[(b*L + t)*d + k] = mask * ge / (count + 1e-8), grad1[b*L+t] = mask*g_fm[b];
+ *   float: grad[b*grad_ld + k] = ge * x_b, grad1[b*grad1_ld] = g_fm[b] * x_b
+ *          (column-sum them over b).
+ * 1 <= d <= 64.
+ * ------------------------------------------------------------------------- */
+typedef struct mirec_ctx_field {
+  int32_t kind;
+  int32_t seq_len;
+  const int64_t* ids;
+  const float* vals;
+  int64_t offset;
+  const float* table;
+  const float* table1;
+  int64_t n_rows;
+  float* grad;
+  float* grad1;
+  int64_t* keys;
+  int64_t grad_ld;   /* row stride (floats) of grad for kinds 0 and 2 */
+  int64_t grad1_ld;  /* stride of grad1 for kinds 0 and 2 */
+} mirec_ctx_field;
+
+int mirec_ctx_fm_fwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields, int64_t B,
+                         int32_t d, const float* bias, float* concat, float* y_fm, void* stream);
+int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields, int64_t B,
+                         int32_t d, const float* concat, const float* g_concat,
+                         const float* g_fm, void* stream);
+
+/* sigmoid + nn.BCELoss (DeepFM.forward / calculate_loss, deepfm.py:66-73):
+ * z = y_fm + y_deep (y_deep may be NULL); prob = sigmoid(z);
+ * loss[b] = (t-1)*max(log(1-p),-100) - t*max(log p,-100)  (mean = sum/B);
+ * dz[b] = grad_scale*(p-t)/max((1-p)p, 1e-12) * (1-p)*p. Any output may be NULL;
+ * label may be NULL when only prob is requested. */
+int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* label, int64_t B,
+                          float grad_scale, float* prob, float* loss, float* dz, void* stream);
+
+/* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
+int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -298,6 +298,104 @@ class LightGCNCPU(torch.nn.Module):
 
 
 # --------------------------------------------------------------------------
+# DeepFM  (recbole/model/context_aware_recommender/deepfm.py:26-73 with
+# ContextRecommender abstract_recommender.py:151-412, FMEmbedding /
+# BaseFactorizationMachine / FMFirstOrderLinear / MLPLayers layers.py)
+# --------------------------------------------------------------------------
+class _FMEmb(torch.nn.Module):
+    def __init__(self, n, d):
+        super().__init__()
+        self.embedding = torch.nn.Embedding(n, d)
+
+
+class _FirstOrder(torch.nn.Module):
+    def __init__(self, tok_dims, seq_dims, n_float):
+        super().__init__()
+        if tok_dims:
+            self.token_embedding_table = _FMEmb(int(sum(tok_dims)), 1)
+        if n_float:
+            self.float_embedding_table = torch.nn.Embedding(n_float, 1)
+        if seq_dims:
+            self.token_seq_embedding_table = torch.nn.ModuleList(
+                [torch.nn.Embedding(n, 1) for n in seq_dims])
+        self.bias = torch.nn.Parameter(torch.zeros((1,)))
+
+
+class DeepFMCPU(torch.nn.Module):
+    """Same module tree (state_dict keys) as the reference DeepFM; forward as
+    written there, on torch CPU. tok/seq/float = ordered field-name lists."""
+
+    def __init__(self, tok, tok_dims, seq, seq_dims, flt, d, hidden, dropout):
+        super().__init__()
+        self.tok, self.seq, self.flt, self.d = tok, seq, flt, d
+        self.offsets = np.array((0, *np.cumsum(tok_dims)[:-1]), dtype=np.int64) if tok else None
+        if tok:
+            self.token_embedding_table = _FMEmb(int(sum(tok_dims)), d)
+        if flt:
+            self.float_embedding_table = torch.nn.Embedding(len(flt), d)
+        if seq:
+            self.token_seq_embedding_table = torch.nn.ModuleList(
+                [torch.nn.Embedding(n, d) for n in seq_dims])
+        self.first_order_linear = _FirstOrder(tok_dims, seq_dims, len(flt))
+        sizes = [d * (len(tok) + len(seq) + len(flt))] + list(hidden)
+        mods = []
+        for a, b in zip(sizes[:-1], sizes[1:]):
+            mods += [torch.nn.Dropout(dropout), torch.nn.Linear(a, b), torch.nn.ReLU()]
+        self.mlp_layers = torch.nn.Module()
+        self.mlp_layers.mlp_layers = torch.nn.Sequential(*mods)
+        self.deep_predict_layer = torch.nn.Linear(sizes[-1], 1)
+
+    def _seq_mean(self, table, ids):
+        mask = (ids != 0).float()
+        cnt = torch.sum(mask, dim=1, keepdim=True)
+        e = table(ids)
+        s = torch.sum(e * mask.unsqueeze(2).expand_as(e), dim=1)
+        return torch.div(s, cnt + torch.FloatTensor([1e-8])).unsqueeze(1)
+
+    def forward(self, inter):
+        parts = []
+        if self.tok:
+            ids = torch.cat([inter[n].unsqueeze(1) for n in self.tok], dim=1)
+            parts.append(self.token_embedding_table.embedding(
+                ids + ids.new_tensor(self.offsets).unsqueeze(0)))
+        if self.seq:
+            parts.append(torch.cat([self._seq_mean(t, inter[n]) for t, n in
+                                    zip(self.token_seq_embedding_table, self.seq)], dim=1))
+        xf = None
+        if self.flt:
+            xf = torch.cat([inter[n].float().unsqueeze(1) for n in self.flt], dim=1)
+            idx = torch.arange(0, xf.shape[1]).unsqueeze(0).expand_as(xf).long()
+            parts.append(torch.mul(self.float_embedding_table(idx), xf.unsqueeze(2)))
+        allE = torch.cat(parts, dim=1)
+        B = allE.shape[0]
+        fo = self.first_order_linear
+        tot = []
+        if self.flt:
+            idx = torch.arange(0, xf.shape[1]).unsqueeze(0).expand_as(xf).long()
+            tot.append(torch.sum(torch.mul(fo.float_embedding_table(idx), xf.unsqueeze(2)),
+                                 dim=1, keepdim=True))
+        if self.tok:
+            tot.append(torch.sum(fo.token_embedding_table.embedding(
+                ids + ids.new_tensor(self.offsets).unsqueeze(0)), dim=1, keepdim=True))
+        if self.seq:
+            res = []
+            for t, n in zip(fo.token_seq_embedding_table, self.seq):
+                m = (inter[n] != 0).float()
+                e = t(inter[n])
+                res.append(torch.sum(e * m.unsqueeze(2).expand_as(e), dim=1, keepdim=True))
+            tot.append(torch.sum(torch.cat(res, dim=1), dim=1, keepdim=True))
+        first = torch.sum(torch.cat(tot, dim=1), dim=1) + fo.bias
+        sq_sum = torch.sum(allE, dim=1) ** 2
+        sum_sq = torch.sum(allE ** 2, dim=1)
+        fm = 0.5 * torch.sum(sq_sum - sum_sq, dim=1, keepdim=True)
+        y_deep = self.deep_predict_layer(self.mlp_layers.mlp_layers(allE.view(B, -1)))
+        return torch.sigmoid(first + fm + y_deep).squeeze()
+
+    def calculate_loss(self, inter, label):
+        return torch.nn.BCELoss()(self.forward(inter), label)
+
+
+# --------------------------------------------------------------------------
 # Full-sort evaluation (trainer.py:328-353, evaluators.py:53-141)
 # --------------------------------------------------------------------------
 def full_sort_pos_idx(scores: torch.Tensor, hist: list, pos: list, K: int):

@@ -33,6 +33,14 @@ class SpmmEpilogue(ctypes.Structure):
                 ('acc_out', RowsRef), ('acc_scale', c_float)]
 
 
+class CtxField(ctypes.Structure):
+    """struct mirec_ctx_field (include/mirec.h)."""
+    _fields_ = [('kind', c_int32), ('seq_len', c_int32), ('ids', _P), ('vals', _P),
+                ('offset', c_int64), ('table', _P), ('table1', _P), ('n_rows', c_int64),
+                ('grad', _P), ('grad1', _P), ('keys', _P), ('grad_ld', c_int64),
+                ('grad1_ld', c_int64)]
+
+
 class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
@@ -83,6 +91,10 @@ SIGNATURES = {
     "mirec_spmm_csr_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
                                    _P, _P, c_int64, _P, ctypes.POINTER(RowsRef),
                                    ctypes.POINTER(SpmmEpilogue), _P]),
+    "mirec_ctx_fm_fwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P]),
+    "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P]),
+    "mirec_sigmoid_bce_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
+    "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
     "mirec_gather_sqnorm_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P]),
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }

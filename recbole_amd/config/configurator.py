@@ -23,7 +23,8 @@ from logging import getLogger
 import torch
 import yaml
 
-from recbole_amd.config.defaults import DATASET_DEFAULTS, MODEL_DEFAULTS, OVERALL, SAMPLE, TYPE_PRESETS
+from recbole_amd.config.defaults import (DATASET_DEFAULTS, MODEL_DEFAULTS, OVERALL, SAMPLE,
+                                         TYPE_DATASET_PRESETS, TYPE_PRESETS)
 from recbole_amd.evaluator import group_metrics, individual_metrics
 from recbole_amd.utils import EvaluatorType, InputType, ModelType, get_model
 
@@ -132,6 +133,7 @@ class Config(object):
         preset = TYPE_PRESETS.get(model_class.type)
         if preset:
             d.update(preset)
+        d.update(TYPE_DATASET_PRESETS.get((model_class.type, dataset), {}))
         return d
 
     # ------------------------------------------------------------------ derived

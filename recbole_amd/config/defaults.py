@@ -61,6 +61,15 @@ MODEL_DEFAULTS = {
     'DeepFM': dict(embedding_size=10, mlp_hidden_size=[128, 128, 128], dropout_prob=0.2),
 }
 
+# quick_start_config/context-aware_ml-100k.yaml, applied after the type preset
+TYPE_DATASET_PRESETS = {
+    (ModelType.CONTEXT, 'ml-100k'): dict(
+        threshold={'rating': 4},
+        load_col={'inter': ['user_id', 'item_id', 'rating', 'timestamp'],
+                  'user': ['user_id', 'age', 'gender', 'occupation'],
+                  'item': ['item_id', 'release_year', 'class']}),
+}
+
 TYPE_PRESETS = {
     ModelType.SEQUENTIAL: dict(eval_setting='TO_LS,full'),
     ModelType.CONTEXT: dict(eval_setting='RO_RS', group_by_user=False, training_neg_sample_num=0,

@@ -1,0 +1,248 @@
+// K8 — context-aware field embedding + factorization machine + BCE, fused.
+//
+// Restates, for one batch of samples (recbole/model/...):
+//   ContextRecommender.embed_input_fields / concat_embed_input_fields
+//     (abstract_recommender.py:286-412): token fields through one offset table
+//     (FMEmbedding, layers.py:121-144), token_seq fields as masked means
+//     sum(mask*e) / (cnt + 1e-8) (:231-272), float fields as E_f[j] * x_j
+//     (:199-214); concatenated [token | token_seq | float] along the field axis;
+//   FMFirstOrderLinear.forward (layers.py:1029-1062): sum of the first-order
+//     weights (float: w_j*x_j, token: w[id], token_seq: sum of masked w) + bias;
+//   BaseFactorizationMachine(reduce_sum=True) (layers.py:147-171):
+//     0.5 * sum_k ((sum_f e_fk)^2 - sum_f e_fk^2);
+//   DeepFM.forward's y_fm = first_order + fm (deepfm.py:58-70);
+//   sigmoid + nn.BCELoss (mean) and their autograd backward.
+// The MLP of DeepFM stays a chain of library GEMMs (torch.nn.Linear on
+// hipBLASLt); this kernel produces its input (the concatenated field rows) and
+// consumes its input gradient.
+//
+// Layout: one group of LPS = pow2 >= d lanes per sample (lane k owns column k of
+// every field row; 64/LPS samples per wave). Field rows of d = 16 floats are one
+// 64-B segment per gather. Backward writes per-contribution gradient rows
+// (field-major) for the K2 grouping / scatter or the compact Adam — no dense
+// gradient of the (up to 33 M-row) table is formed here.
+#include "common.h"
+
+namespace mirec {
+
+constexpr int kCtxThreads = 256;
+
+template <int LPS>
+__device__ __forceinline__ float group_sum(float x) {
+#pragma unroll
+  for (int off = LPS / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__device__ __forceinline__ int64_t clamp_row(int64_t r, int64_t n) {
+  return r < 0 ? 0 : (r >= n ? n - 1 : r);
+}
+
+// Forward: concat[b, f*d + k], keys of token fields, y_fm[b].
+template <int LPS>
+__global__ __launch_bounds__(kCtxThreads) void ctx_fm_fwd_kernel(
+    const mirec_ctx_field* __restrict__ fields, int n_fields, int64_t B, int d,
+    const float* __restrict__ bias, float* __restrict__ concat, float* __restrict__ y_fm) {
+  constexpr int SPW = 64 / LPS;
+  const int lane = threadIdx.x & 63;
+  const int k = lane % LPS;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t b = wave * SPW + lane / LPS;
+  if (b >= B) return;   // whole groups exit together; no cross-group shuffles below
+  const bool col = k < d;
+  const int64_t F = n_fields;
+  float S = 0.f, Q = 0.f;
+  float fo_float = 0.f, fo_tok = 0.f, fo_seq = 0.f;
+  for (int f = 0; f < n_fields; ++f) {
+    const mirec_ctx_field fd = fields[f];
+    float e = 0.f;
+    if (fd.kind == 0) {
+      const int64_t r = clamp_row(fd.ids[b] + fd.offset, fd.n_rows);
+      if (col) e = fd.table[r * d + k];
+      fo_tok += fd.table1[r];
+      if (fd.keys && k == 0) fd.keys[b] = r;
+    } else if (fd.kind == 1) {
+      const int64_t* ids = fd.ids + b * fd.seq_len;
+      float sum = 0.f, cnt = 0.f, w = 0.f;
+      for (int t = 0; t < fd.seq_len; ++t) {
+        const int64_t id = ids[t];
+        const float msk = id != 0 ? 1.f : 0.f;
+        const int64_t r = clamp_row(id, fd.n_rows);
+        if (col) sum += fd.table[r * d + k] * msk;
+        w += fd.table1[r] * msk;
+        cnt += msk;
+      }
+      e = sum / (cnt + 1e-8f);
+      fo_seq += w;
+    } else {
+      const float x = fd.vals[b];
+      if (col) e = fd.table[fd.offset * d + k] * x;
+      fo_float += fd.table1[fd.offset] * x;
+    }
+    if (col) concat[(b * F + f) * d + k] = e;
+    S += e;
+    Q += e * e;
+  }
+  const float fm = 0.5f * group_sum<LPS>(col ? S * S - Q : 0.f);
+  if (k == 0) y_fm[b] = ((fo_float + fo_tok) + fo_seq) + bias[0] + fm;
+}
+
+// Backward. g_concat: dL/d concat [B, F*d] (may be NULL = 0); g_fm: dL/d y_fm [B].
+// grad_e = g_concat + g_fm * (S_k - e) (d fm / d e_fk = S_k - e_fk).
+template <int LPS>
+__global__ __launch_bounds__(kCtxThreads) void ctx_fm_bwd_kernel(
+    const mirec_ctx_field* __restrict__ fields, int n_fields, int64_t B, int d,
+    const float* __restrict__ concat, const float* __restrict__ g_concat,
+    const float* __restrict__ g_fm) {
+  constexpr int SPW = 64 / LPS;
+  const int lane = threadIdx.x & 63;
+  const int k = lane % LPS;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t b = wave * SPW + lane / LPS;
+  if (b >= B) return;
+  const bool col = k < d;
+  const int64_t F = n_fields;
+  float S = 0.f;
+  if (col)
+    for (int f = 0; f < n_fields; ++f) S += concat[(b * F + f) * d + k];
+  const float gf = g_fm[b];
+  for (int f = 0; f < n_fields; ++f) {
+    const mirec_ctx_field fd = fields[f];
+    float ge = 0.f;
+    if (col) {
+      const int64_t c = (b * F + f) * d + k;
+      ge = (g_concat ? g_concat[c] : 0.f) + gf * (S - concat[c]);
+    }
+    if (fd.kind == 0) {
+      if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge;
+      if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf;
+    } else if (fd.kind == 1) {
+      const int64_t* ids = fd.ids + b * fd.seq_len;
+      float cnt = 0.f;
+      for (int t = 0; t < fd.seq_len; ++t) cnt += ids[t] != 0 ? 1.f : 0.f;
+      const float gm = ge / (cnt + 1e-8f);
+      for (int t = 0; t < fd.seq_len; ++t) {
+        const float msk = ids[t] != 0 ? 1.f : 0.f;
+        if (col && fd.grad) fd.grad[(b * fd.seq_len + t) * d + k] = gm * msk;
+        if (k == 0 && fd.grad1) fd.grad1[b * fd.seq_len + t] = gf * msk;
+      }
+    } else {
+      const float x = fd.vals[b];
+      if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge * x;
+      if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf * x;
+    }
+  }
+}
+
+// z = y_fm + y_deep; p = sigmoid(z); loss_b = -(t*max(log p,-100) + (1-t)*max(log(1-p),-100))
+// (torch BCELoss), dz_b = grad_scale * (p - t) / max((1-p)*p, 1e-12) * (1-p) * p
+// (BCELoss backward then sigmoid backward, torch's op order).
+__global__ __launch_bounds__(256) void sigmoid_bce_kernel(const float* __restrict__ y_fm,
+                                                          const float* __restrict__ y_deep,
+                                                          const float* __restrict__ label,
+                                                          int64_t B, float grad_scale,
+                                                          float* __restrict__ prob,
+                                                          float* __restrict__ loss,
+                                                          float* __restrict__ dz) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    const float z = y_fm[b] + (y_deep ? y_deep[b] : 0.f);
+    const float p = 1.f / (1.f + expf(-z));
+    const float t = label ? label[b] : 0.f;
+    if (prob) prob[b] = p;
+    if (loss) {
+      const float lp = fmaxf(logf(p), -100.f);
+      const float l1p = fmaxf(logf(1.f - p), -100.f);
+      loss[b] = (t - 1.f) * l1p - t * lp;
+    }
+    if (dz) {
+      const float gp = grad_scale * (p - t) / fmaxf((1.f - p) * p, 1e-12f);
+      dz[b] = gp * (1.f - p) * p;
+    }
+  }
+}
+
+// out[j] = sum_i x[i*m + j] for i = 0..n-1 in order (column sums; float-field
+// and bias gradients). One thread per column, fixed order.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int64_t n,
+                                                     int64_t m, float* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  float s = 0.f;
+  for (int64_t i = 0; i < n; ++i) s += x[i * m + j];
+  out[j] = s;
+}
+
+static unsigned ctx_grid(int64_t B, int lps) {
+  const int64_t spb = (kCtxThreads / 64) * (64 / lps);
+  return (unsigned)((B + spb - 1) / spb);
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+#define MIREC_CTX_DISPATCH(KERNEL, ...)                                                       \
+  do {                                                                                        \
+    hipStream_t st = (hipStream_t)stream;                                                     \
+    if (d <= 4)                                                                               \
+      hipLaunchKernelGGL(KERNEL<4>, dim3(ctx_grid(B, 4)), dim3(kCtxThreads), 0, st, __VA_ARGS__);   \
+    else if (d <= 8)                                                                          \
+      hipLaunchKernelGGL(KERNEL<8>, dim3(ctx_grid(B, 8)), dim3(kCtxThreads), 0, st, __VA_ARGS__);   \
+    else if (d <= 16)                                                                         \
+      hipLaunchKernelGGL(KERNEL<16>, dim3(ctx_grid(B, 16)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+    else if (d <= 32)                                                                         \
+      hipLaunchKernelGGL(KERNEL<32>, dim3(ctx_grid(B, 32)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+    else                                                                                      \
+      hipLaunchKernelGGL(KERNEL<64>, dim3(ctx_grid(B, 64)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+  } while (0)
+
+extern "C" int mirec_ctx_fm_fwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields,
+                                    int64_t B, int32_t d, const float* bias, float* concat,
+                                    float* y_fm, void* stream) {
+  if (B == 0) return 0;
+  if (!fields_dev || n_fields <= 0 || B < 0 || d < 1 || d > 64 || !bias || !concat || !y_fm) {
+    set_error("mirec_ctx_fm_fwd_f32: bad arguments (1 <= d <= 64)");
+    return -1;
+  }
+  MIREC_CTX_DISPATCH(ctx_fm_fwd_kernel, fields_dev, n_fields, B, d, bias, concat, y_fm);
+  return launch_status("mirec_ctx_fm_fwd_f32");
+}
+
+extern "C" int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields,
+                                    int64_t B, int32_t d, const float* concat,
+                                    const float* g_concat, const float* g_fm, void* stream) {
+  if (B == 0) return 0;
+  if (!fields_dev || n_fields <= 0 || B < 0 || d < 1 || d > 64 || !concat || !g_fm) {
+    set_error("mirec_ctx_fm_bwd_f32: bad arguments (1 <= d <= 64)");
+    return -1;
+  }
+  MIREC_CTX_DISPATCH(ctx_fm_bwd_kernel, fields_dev, n_fields, B, d, concat, g_concat, g_fm);
+  return launch_status("mirec_ctx_fm_bwd_f32");
+}
+
+extern "C" int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* label,
+                                     int64_t B, float grad_scale, float* prob, float* loss,
+                                     float* dz, void* stream) {
+  if (B == 0) return 0;
+  if (!y_fm || B < 0 || (!label && (loss || dz))) {
+    set_error("mirec_sigmoid_bce_f32: bad arguments (loss / dz need labels)");
+    return -1;
+  }
+  int64_t blocks = (B + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(sigmoid_bce_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, y_fm, y_deep, label, B, grad_scale, prob, loss, dz);
+  return launch_status("mirec_sigmoid_bce_f32");
+}
+
+extern "C" int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream) {
+  if (m == 0) return 0;
+  if (!x || !out || n < 0 || m < 0) {
+    set_error("mirec_colsum_f32: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, n, m, out);
+  return launch_status("mirec_colsum_f32");
+}

@@ -13,14 +13,16 @@ from recbole_amd.utils import ModelType
 
 def create_dataset(config):
     model_type = config['MODEL_TYPE']
-    if model_type in (ModelType.GENERAL, ModelType.TRADITIONAL):
+    if model_type in (ModelType.GENERAL, ModelType.TRADITIONAL, ModelType.CONTEXT):
         return Dataset(config)
     raise NotImplementedError(f'model type {model_type} datasets are not part of this build yet')
 
 
 def get_data_loader(name, config, neg_sample_args):
     model_type = config['MODEL_TYPE']
-    if model_type not in (ModelType.GENERAL, ModelType.TRADITIONAL):
+    # Context{DataLoader,NegSampleDataLoader,FullDataLoader} are the General ones
+    # under another name (context_dataloader.py:20-43)
+    if model_type not in (ModelType.GENERAL, ModelType.TRADITIONAL, ModelType.CONTEXT):
         raise NotImplementedError(f'model type {model_type} loaders are not part of this build yet')
     strategy = neg_sample_args['strategy']
     if strategy == 'none':

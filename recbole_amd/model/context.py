@@ -1,0 +1,208 @@
+"""Autograd wrappers of the K8 kernels (csrc/context.hip) for ContextRecommender.
+
+_CtxFMFn:      field embeddings of a batch -> (concat [B, F, d], y_fm [B]) where
+               y_fm = first-order term + FM second-order term; backward gives the
+               dense gradients nn.Embedding(sparse=False) would (zero tables +
+               K2-grouped, fixed-order scatter of the per-contribution rows).
+_SigmoidBCEFn: mean BCE of sigmoid(y_fm + y_deep) (deepfm.py:66-73).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from recbole_amd import ops
+from recbole_amd._native import CtxField, check, lib, ptr, stream_handle
+
+TOKEN, TOKEN_SEQ, FLOAT = 0, 1, 2
+
+
+class FieldLayout:
+    """The concat-order field list of a ContextRecommender: (kind, name, index)
+    with index = token field number / token_seq field number / float column."""
+
+    def __init__(self, token_names, seq_names, float_names, token_offsets):
+        self.token_names = list(token_names)
+        self.seq_names = list(seq_names)
+        self.float_names = list(float_names)
+        self.token_offsets = [int(x) for x in token_offsets] if len(token_names) else []
+        self.n_fields = len(self.token_names) + len(self.seq_names) + len(self.float_names)
+
+
+def _col(interaction, name, dtype):
+    t = interaction[name]
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    return t.contiguous()
+
+
+def build_fields(layout, interaction, tables, grads=None):
+    """ctypes array of mirec_ctx_field (host) + the tensors it points at.
+    tables: dict T, T1, Ef, Ef1, seq (list), seq1 (list) of weight tensors."""
+    arr = (CtxField * layout.n_fields)()
+    keep = []
+    f = 0
+    for i, name in enumerate(layout.token_names):
+        ids = _col(interaction, name, torch.int64)
+        keep.append(ids)
+        fd = arr[f]
+        fd.kind, fd.seq_len, fd.ids, fd.offset = TOKEN, 1, ptr(ids), layout.token_offsets[i]
+        fd.table, fd.table1, fd.n_rows = ptr(tables['T']), ptr(tables['T1']), tables['T'].shape[0]
+        if grads is not None:
+            d = tables['T'].shape[1]
+            fd.grad = ptr(grads['T']) + 4 * i * grads['B'] * d
+            fd.grad1 = ptr(grads['T1']) + 4 * i * grads['B']
+            fd.keys = ptr(grads['keys']) + 8 * i * grads['B']
+            fd.grad_ld, fd.grad1_ld = d, 1
+        f += 1
+    for i, name in enumerate(layout.seq_names):
+        ids = _col(interaction, name, torch.int64)
+        keep.append(ids)
+        fd = arr[f]
+        fd.kind, fd.seq_len, fd.ids = TOKEN_SEQ, ids.shape[1], ptr(ids)
+        fd.table, fd.table1 = ptr(tables['seq'][i]), ptr(tables['seq1'][i])
+        fd.n_rows = tables['seq'][i].shape[0]
+        if grads is not None:
+            fd.grad, fd.grad1 = ptr(grads['seq'][i]), ptr(grads['seq1'][i])
+        f += 1
+    n_float = len(layout.float_names)
+    for j, name in enumerate(layout.float_names):
+        vals = _col(interaction, name, torch.float32).view(-1)
+        keep.append(vals)
+        fd = arr[f]
+        fd.kind, fd.seq_len, fd.vals, fd.offset = FLOAT, 1, ptr(vals), j
+        fd.table, fd.table1 = ptr(tables['Ef']), ptr(tables['Ef1'])
+        fd.n_rows = tables['Ef'].shape[0]
+        if grads is not None:
+            d = tables['Ef'].shape[1]
+            fd.grad = ptr(grads['Ef']) + 4 * j * d
+            fd.grad1 = ptr(grads['Ef1']) + 4 * j
+            fd.grad_ld, fd.grad1_ld = n_float * d, n_float
+        f += 1
+    return arr, keep
+
+
+def _upload(arr, device):
+    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return raw.to(device)
+
+
+def ctx_fm_forward(layout, interaction, tables, B, d, bias, keys=None):
+    dev = bias.device
+    arr, keep = build_fields(layout, interaction, tables)
+    if keys is not None:
+        for i in range(len(layout.token_names)):
+            arr[i].keys = ptr(keys) + 8 * i * B
+    fields_dev = _upload(arr, dev)
+    concat = torch.empty(B, layout.n_fields, d, dtype=torch.float32, device=dev)
+    y_fm = torch.empty(B, dtype=torch.float32, device=dev)
+    rc = lib().mirec_ctx_fm_fwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(bias), ptr(concat),
+                                    ptr(y_fm), stream_handle())
+    check(rc, "mirec_ctx_fm_fwd_f32")
+    keep.append(fields_dev)
+    return concat, y_fm, keep
+
+
+class _CtxFMFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, layout, interaction, T, T1, Ef, Ef1, bias, *seq_tables):
+        ns = len(layout.seq_names)
+        seq, seq1 = list(seq_tables[:ns]), list(seq_tables[ns:])
+        d = (T if T is not None else (Ef if Ef is not None else seq[0])).shape[1]
+        B = interaction.length
+        tables = {'T': T, 'T1': T1, 'Ef': Ef, 'Ef1': Ef1, 'seq': seq, 'seq1': seq1}
+        tables = {k: (v.detach() if isinstance(v, torch.Tensor) else
+                      [x.detach() for x in v] if isinstance(v, list) else v)
+                  for k, v in tables.items()}
+        keys = torch.empty(len(layout.token_names) * B, dtype=torch.int64, device=bias.device)
+        concat, y_fm, _ = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
+        ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
+        ctx.save_for_backward(concat, keys)
+        return concat, y_fm
+
+    @staticmethod
+    def backward(ctx, g_concat, g_fm):
+        concat, keys = ctx.saved_tensors
+        layout, tables, B, d = ctx.layout, ctx.tables, ctx.B, ctx.d
+        dev = concat.device
+        nt, ns, nf = len(layout.token_names), len(layout.seq_names), len(layout.float_names)
+        if g_fm is None:
+            g_fm = torch.zeros(B, dtype=torch.float32, device=dev)
+        g_fm = g_fm.contiguous()
+        E = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)
+        seq_ids = [_col(ctx.interaction, n, torch.int64) for n in layout.seq_names]
+        grads = {'B': B, 'keys': keys,
+                 'T': E(nt * B, d) if nt else None, 'T1': E(nt * B, 1) if nt else None,
+                 'Ef': E(B, nf * d) if nf else None, 'Ef1': E(B, nf) if nf else None,
+                 'seq': [E(ids.numel(), d) for ids in seq_ids],
+                 'seq1': [E(ids.numel(), 1) for ids in seq_ids]}
+        arr, keep = build_fields(layout, ctx.interaction, tables, grads)
+        fields_dev = _upload(arr, dev)
+        gc = None if g_concat is None else g_concat.contiguous()
+        rc = lib().mirec_ctx_fm_bwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(concat),
+                                        ptr(gc), ptr(g_fm), stream_handle())
+        check(rc, "mirec_ctx_fm_bwd_f32")
+        dT = dT1 = dEf = dEf1 = None
+        if nt:
+            T = tables['T']
+            segs = ops.segment_sort(keys, T.shape[0])
+            dT = ops.segment_scatter_add(grads['T'], segs, torch.zeros_like(T))
+            dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))
+        if nf:
+            dEf = torch.empty_like(tables['Ef'])
+            check(lib().mirec_colsum_f32(ptr(grads['Ef']), B, nf * d, ptr(dEf), stream_handle()),
+                  "mirec_colsum_f32")
+            dEf1 = torch.empty_like(tables['Ef1'])
+            check(lib().mirec_colsum_f32(ptr(grads['Ef1']), B, nf, ptr(dEf1), stream_handle()),
+                  "mirec_colsum_f32")
+        dbias = torch.empty(1, dtype=torch.float32, device=dev)
+        check(lib().mirec_colsum_f32(ptr(g_fm), B, 1, ptr(dbias), stream_handle()),
+              "mirec_colsum_f32")
+        dseq, dseq1 = [], []
+        for i, ids in enumerate(seq_ids):
+            segs = ops.segment_sort(ids.view(-1), tables['seq'][i].shape[0])
+            dseq.append(ops.segment_scatter_add(grads['seq'][i], segs,
+                                                torch.zeros_like(tables['seq'][i])))
+            dseq1.append(ops.segment_scatter_add(grads['seq1'][i], segs,
+                                                 torch.zeros_like(tables['seq1'][i])))
+        del keep
+        return (None, None, dT, dT1, dEf, dEf1, dbias, *dseq, *dseq1)
+
+
+class _SigmoidBCEFn(torch.autograd.Function):
+    """nn.BCELoss()(sigmoid(y_fm + y_deep), label) (deepfm.py:45, 66-73)."""
+
+    @staticmethod
+    def forward(ctx, y_fm, y_deep, label):
+        B = y_fm.numel()
+        yd = y_deep.detach().reshape(-1).contiguous()
+        lab = label.detach().to(torch.float32).contiguous()
+        loss_b = torch.empty(B, dtype=torch.float32, device=y_fm.device)
+        dz = torch.empty(B, dtype=torch.float32, device=y_fm.device)
+        gs = float(np.float32(1.0) / np.float32(B))
+        rc = lib().mirec_sigmoid_bce_f32(ptr(y_fm.detach().contiguous()), ptr(yd), ptr(lab), B, gs,
+                                         None, ptr(loss_b), ptr(dz), stream_handle())
+        check(rc, "mirec_sigmoid_bce_f32")
+        ctx.save_for_backward(dz)
+        ctx.deep_shape = y_deep.shape
+        return ops.fixed_sum(loss_b).view(()) / B
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        dz = dz * g
+        return dz, dz.view(ctx.deep_shape), None
+
+
+def sigmoid_prob(y_fm, y_deep):
+    """sigmoid(y_fm + y_deep) on the device (DeepFM.forward's output)."""
+    B = y_fm.numel()
+    yd = None if y_deep is None else y_deep.detach().reshape(-1).contiguous()
+    prob = torch.empty(B, dtype=torch.float32, device=y_fm.device)
+    rc = lib().mirec_sigmoid_bce_f32(ptr(y_fm.detach().contiguous()), ptr(yd), None, B, 1.0,
+                                     ptr(prob), None, None, stream_handle())
+    check(rc, "mirec_sigmoid_bce_f32")
+    return prob

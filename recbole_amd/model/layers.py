@@ -1,0 +1,150 @@
+"""Layers used by the context-aware path (mirror of recbole/model/layers.py:30-171,
+905-1062). Same module structure, parameter names and construction order as the
+reference, so checkpoints interoperate and the CPU-generator draws of module
+construction and init line up.
+
+The DeepFM hot path does not call FMEmbedding / FMFirstOrderLinear /
+BaseFactorizationMachine forward: ContextRecommender runs all three in the
+fused K8 kernel (csrc/context.hip) over these modules' weights. Their forward
+methods remain, in torch ops, for user code that composes them directly.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn.init import normal_
+
+from recbole_amd.utils import FeatureType
+
+
+def activation_layer(activation_name='relu', emb_dim=None):
+    """layers.py:89-118."""
+    if activation_name is None:
+        return None
+    if isinstance(activation_name, str):
+        name = activation_name.lower()
+        if name == 'sigmoid':
+            return nn.Sigmoid()
+        if name == 'tanh':
+            return nn.Tanh()
+        if name == 'relu':
+            return nn.ReLU()
+        if name == 'leakyrelu':
+            return nn.LeakyReLU()
+        if name == 'none':
+            return None
+        raise NotImplementedError(f'activation function {activation_name} is not implemented')
+    if issubclass(activation_name, nn.Module):
+        return activation_name()
+    raise NotImplementedError(f'activation function {activation_name} is not implemented')
+
+
+class MLPLayers(nn.Module):
+    """[Dropout -> Linear -> (BatchNorm) -> activation] per layer (layers.py:30-86)."""
+
+    def __init__(self, layers, dropout=0., activation='relu', bn=False, init_method=None):
+        super().__init__()
+        self.layers = layers
+        self.dropout = dropout
+        self.activation = activation
+        self.use_bn = bn
+        self.init_method = init_method
+        mods = []
+        for input_size, output_size in zip(self.layers[:-1], self.layers[1:]):
+            mods.append(nn.Dropout(p=self.dropout))
+            mods.append(nn.Linear(input_size, output_size))
+            if self.use_bn:
+                mods.append(nn.BatchNorm1d(num_features=output_size))
+            act = activation_layer(self.activation, output_size)
+            if act is not None:
+                mods.append(act)
+        self.mlp_layers = nn.Sequential(*mods)
+        if self.init_method is not None:
+            self.apply(self.init_weights)
+
+    def init_weights(self, module):
+        if isinstance(module, nn.Linear):
+            if self.init_method == 'norm':
+                normal_(module.weight.data, 0, 0.01)
+            if module.bias is not None:
+                module.bias.data.fill_(0.0)
+
+    def forward(self, input_feature):
+        return self.mlp_layers(input_feature)
+
+
+class FMEmbedding(nn.Module):
+    """One table for all token fields, field f's ids shifted by offsets[f]
+    (layers.py:121-144)."""
+
+    def __init__(self, field_dims, offsets, embed_dim):
+        super().__init__()
+        self.embedding = nn.Embedding(int(sum(field_dims)), embed_dim)
+        self.offsets = offsets
+
+    def forward(self, input_x):
+        input_x = input_x + input_x.new_tensor(self.offsets).unsqueeze(0)
+        return self.embedding(input_x)
+
+
+class BaseFactorizationMachine(nn.Module):
+    """0.5 * ((sum_f e)^2 - sum_f e^2), summed over the embedding axis when
+    reduce_sum (layers.py:147-171)."""
+
+    def __init__(self, reduce_sum=True):
+        super().__init__()
+        self.reduce_sum = reduce_sum
+
+    def forward(self, input_x):
+        square_of_sum = torch.sum(input_x, dim=1) ** 2
+        sum_of_square = torch.sum(input_x ** 2, dim=1)
+        output = square_of_sum - sum_of_square
+        if self.reduce_sum:
+            output = torch.sum(output, dim=1, keepdim=True)
+        return 0.5 * output
+
+
+def _split_fields(config, dataset):
+    """Token / token_seq / float field names and sizes in dataset.fields() order,
+    the label skipped (abstract_recommender.py:185-200, layers.py:913-928)."""
+    label = config['LABEL_FIELD']
+    tok, tok_dims, seq, seq_dims, flt, flt_dims = [], [], [], [], [], []
+    for name in dataset.fields():
+        if name == label:
+            continue
+        ftype = dataset.field2type[name]
+        if ftype == FeatureType.TOKEN:
+            tok.append(name)
+            tok_dims.append(dataset.num(name))
+        elif ftype == FeatureType.TOKEN_SEQ:
+            seq.append(name)
+            seq_dims.append(dataset.num(name))
+        else:
+            flt.append(name)
+            flt_dims.append(dataset.num(name))
+    return tok, tok_dims, seq, seq_dims, flt, flt_dims
+
+
+class FMFirstOrderLinear(nn.Module):
+    """First-order weights of every field + a bias (layers.py:905-1062)."""
+
+    def __init__(self, config, dataset, output_dim=1):
+        super().__init__()
+        self.field_names = dataset.fields()
+        self.LABEL = config['LABEL_FIELD']
+        self.device = config['device']
+        (self.token_field_names, self.token_field_dims, self.token_seq_field_names,
+         self.token_seq_field_dims, self.float_field_names,
+         self.float_field_dims) = _split_fields(config, dataset)
+        if len(self.token_field_dims) > 0:
+            self.token_field_offsets = np.array((0, *np.cumsum(self.token_field_dims)[:-1]),
+                                                dtype=np.int64)
+            self.token_embedding_table = FMEmbedding(self.token_field_dims,
+                                                     self.token_field_offsets, output_dim)
+        if len(self.float_field_dims) > 0:
+            self.float_embedding_table = nn.Embedding(int(np.sum(self.float_field_dims)),
+                                                      output_dim)
+        if len(self.token_seq_field_dims) > 0:
+            self.token_seq_embedding_table = nn.ModuleList()
+            for dim in self.token_seq_field_dims:
+                self.token_seq_embedding_table.append(nn.Embedding(dim, output_dim))
+        self.bias = nn.Parameter(torch.zeros((output_dim,)), requires_grad=True)
