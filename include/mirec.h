@@ -83,6 +83,12 @@ int mirec_gather_rows(const void* table, int64_t n_rows, int64_t row_bytes,
 int mirec_gather_rows_i32idx(const void* table, int64_t n_rows, int64_t row_bytes,
                              const int32_t* idx, int64_t n, void* out, void* stream);
 
+/* Sliding-window gather (SequentialDataLoader.augmentation,
+ * recbole/data/dataloader/sequential_dataloader.py:95-127, on the device):
+ * out[i, t] = col[start[i] + t] for t < len[i], else 0 (elements of 4 or 8 bytes). */
+int mirec_window_gather(const void* col, int32_t elem_bytes, const int64_t* start,
+                        const int64_t* len, int64_t n, int32_t L, void* out, void* stream);
+
 /* ---------------------------------------------------------------------------
  * K3  Fused BPR forward + backward.
  * Replaces BPR.calculate_loss (recbole/model/general_recommender/bpr.py:74-83),
@@ -385,6 +391,38 @@ int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* l
 
 /* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
 int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K9  Sequential recommender (SASRec) embedding block and sampled softmax.
+ * seq_embed_ln replaces the input block of SASRec.forward
+ *   (recbole/model/sequential_recommender/sasrec.py:107-117):
+ *   out[r] = LayerNorm(item_table[item_seq[r]] + pos_table[r % L]) (gamma, beta, eps),
+ *   r = b*L + t over [B, L]; mean / rstd [B*L] saved for the backward.
+ * Backward: dx[r] = LayerNorm input gradient (may be NULL); ditem[r] = dx[r], or 0
+ *   where item_seq[r] == 0 (nn.Embedding(padding_idx=0)); part_gamma / part_beta
+ *   [mirec_seq_embed_ln_partials(B*L), d] per-block partial sums of g*xhat and g,
+ *   to be finished by mirec_colsum_f32 (fixed order). d in {32,64,128,256}.
+ * sampled_softmax (the C3 configuration's loss, a build extension; pinned by the
+ *   oracle's torch restatement): per sequence b, logits over [pos[b],
+ *   neg[j*B + b] for j < n_neg] (the sampler's layout), loss[b] =
+ *   logsumexp - logit_0, g_seq[b] = grad_scale * (sum_j p_j E_j - E_0),
+ *   g_items rows [(1+n_neg)*B, d]: row b = grad_scale*(p_0 - 1)*s_b,
+ *   row j*B + b = grad_scale*p_j*s_b. d in {64,128,256}, n_neg <= 4095.
+ * ------------------------------------------------------------------------- */
+int mirec_seq_embed_ln_fwd_f32(const float* item_table, int64_t n_items, const float* pos_table,
+                               const int64_t* item_seq, int64_t B, int32_t L, int32_t d,
+                               const float* gamma, const float* beta, float eps, float* out,
+                               float* mean, float* rstd, void* stream);
+int64_t mirec_seq_embed_ln_partials(int64_t n_rows);
+int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const float* pos_table,
+                               const int64_t* item_seq, int64_t B, int32_t L, int32_t d,
+                               const float* gamma, const float* mean, const float* rstd,
+                               const float* grad_out, float* dx, float* ditem,
+                               float* part_gamma, float* part_beta, void* stream);
+int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table, int64_t n_items,
+                              int32_t d, const int64_t* pos, const int64_t* neg, int64_t B,
+                              int32_t n_neg, float grad_scale, float* loss, float* g_seq,
+                              float* g_items, void* stream);
 
 #ifdef __cplusplus
 }

@@ -396,6 +396,129 @@ class DeepFMCPU(torch.nn.Module):
 
 
 # --------------------------------------------------------------------------
+# Sequential data + SASRec  (recbole/data/dataset/sequential_dataset.py:43-112,
+# data/dataloader/sequential_dataloader.py:95-127, model/sequential_recommender/
+# sasrec.py:25-158, model/layers.py:338-552)
+# --------------------------------------------------------------------------
+def seq_augmentation(uids_sorted, max_len):
+    """prepare_data_augmentation's loop as written (:72-85) over rows already
+    sorted by (user, time): (uid_list, (start, stop) per sample, target_index)."""
+    uid_list, index, target = [], [], []
+    last_uid, seq_start = None, 0
+    for i, uid in enumerate(uids_sorted):
+        if last_uid != uid:
+            last_uid = uid
+            seq_start = i
+        else:
+            if i - seq_start > max_len:
+                seq_start += 1
+            uid_list.append(uid)
+            index.append((seq_start, i))
+            target.append(i)
+    return uid_list, index, target
+
+
+def leave_one_out_index(group_keys, leave_one_num):
+    """dataset.py:1249-1256 (_grouped_index) + :1317-1337, as written."""
+    groups = {}
+    for i, k in enumerate(group_keys):
+        groups.setdefault(k, []).append(i)
+    nxt = [[] for _ in range(leave_one_num + 1)]
+    for index in groups.values():
+        tot = len(index)
+        legal = min(leave_one_num, tot - 1)
+        pr = tot - legal
+        nxt[0].extend(index[:pr])
+        for i in range(legal):
+            nxt[-legal + i].append(index[pr])
+            pr += 1
+    return nxt
+
+
+class _MHA(torch.nn.Module):
+    def __init__(self, h, d, eps):
+        super().__init__()
+        self.h, self.hd = h, d // h
+        self.query, self.key, self.value = (torch.nn.Linear(d, d), torch.nn.Linear(d, d),
+                                            torch.nn.Linear(d, d))
+        self.dense = torch.nn.Linear(d, d)
+        self.LayerNorm = torch.nn.LayerNorm(d, eps=eps)
+
+    def _t(self, x):
+        return x.view(*(x.size()[:-1] + (self.h, self.hd))).permute(0, 2, 1, 3)
+
+    def forward(self, x, mask):
+        import math
+        q, k, v = self._t(self.query(x)), self._t(self.key(x)), self._t(self.value(x))
+        sc = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(self.hd) + mask
+        p = torch.softmax(sc, dim=-1)
+        c = torch.matmul(p, v).permute(0, 2, 1, 3).contiguous()
+        c = c.view(*(c.size()[:-2] + (self.h * self.hd,)))
+        return self.LayerNorm(self.dense(c) + x)
+
+
+class _FF(torch.nn.Module):
+    def __init__(self, d, inner, eps):
+        super().__init__()
+        self.dense_1, self.dense_2 = torch.nn.Linear(d, inner), torch.nn.Linear(inner, d)
+        self.LayerNorm = torch.nn.LayerNorm(d, eps=eps)
+
+    def forward(self, x):
+        import math
+        h = self.dense_1(x)
+        h = h * 0.5 * (1.0 + torch.erf(h / math.sqrt(2.0)))
+        return self.LayerNorm(self.dense_2(h) + x)
+
+
+class _TL(torch.nn.Module):
+    def __init__(self, h, d, inner, eps):
+        super().__init__()
+        self.multi_head_attention = _MHA(h, d, eps)
+        self.feed_forward = _FF(d, inner, eps)
+
+
+class SASRecCPU(torch.nn.Module):
+    """SASRec with dropout 0 (the reference's module tree: state_dict keys match),
+    forward / losses as written in sasrec.py:107-158 on torch CPU. loss 'SSM' is
+    the build's sampled softmax: CE over logits [pos | negs] with target 0."""
+
+    def __init__(self, n_items, L, d, n_layers, n_heads, inner, eps):
+        super().__init__()
+        self.item_embedding = torch.nn.Embedding(n_items, d, padding_idx=0)
+        self.position_embedding = torch.nn.Embedding(L, d)
+        self.trm_encoder = torch.nn.Module()
+        self.trm_encoder.layer = torch.nn.ModuleList([_TL(n_heads, d, inner, eps)
+                                                      for _ in range(n_layers)])
+        self.LayerNorm = torch.nn.LayerNorm(d, eps=eps)
+
+    def forward(self, item_seq, item_len):
+        pos = torch.arange(item_seq.size(1)).unsqueeze(0).expand_as(item_seq)
+        x = self.LayerNorm(self.item_embedding(item_seq) + self.position_embedding(pos))
+        am = (item_seq > 0).long().unsqueeze(1).unsqueeze(2)
+        n = item_seq.size(1)
+        sub = (torch.triu(torch.ones((1, n, n)), diagonal=1) == 0).unsqueeze(1).long()
+        mask = (1.0 - (am * sub).float()) * -10000.0
+        for layer in self.trm_encoder.layer:
+            x = layer.feed_forward(layer.multi_head_attention(x, mask))
+        idx = (item_len - 1).view(-1, 1, 1).expand(-1, -1, x.shape[-1])
+        return x.gather(dim=1, index=idx).squeeze(1)
+
+    def calculate_loss(self, item_seq, item_len, pos, neg=None, loss_type='CE'):
+        s = self.forward(item_seq, item_len)
+        W = self.item_embedding.weight
+        if loss_type == 'BPR':
+            ps = torch.sum(s * self.item_embedding(pos), dim=-1)
+            ns = torch.sum(s * self.item_embedding(neg), dim=-1)
+            return -torch.log(1e-10 + torch.sigmoid(ps - ns)).mean()
+        if loss_type == 'SSM':
+            B = s.shape[0]
+            items = torch.cat([pos.view(1, B), neg.view(-1, B)], dim=0).T     # [B, 1+N]
+            logits = (s.unsqueeze(1) * self.item_embedding(items)).sum(-1)
+            return torch.nn.functional.cross_entropy(logits, torch.zeros(B, dtype=torch.long))
+        return torch.nn.functional.cross_entropy(torch.matmul(s, W.T), pos)
+
+
+# --------------------------------------------------------------------------
 # Full-sort evaluation (trainer.py:328-353, evaluators.py:53-141)
 # --------------------------------------------------------------------------
 def full_sort_pos_idx(scores: torch.Tensor, hist: list, pos: list, K: int):

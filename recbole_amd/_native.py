@@ -59,6 +59,7 @@ SIGNATURES = {
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
     "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
+    "mirec_window_gather": (c_int, [_P, c_int32, _P, _P, c_int64, c_int32, _P, _P]),
     "mirec_gather_rows_i32idx": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
                                       c_int32, c_float, c_float, _P, _P, _P, _P, _P, _P]),
@@ -95,6 +96,13 @@ SIGNATURES = {
     "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P]),
     "mirec_sigmoid_bce_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
     "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
+    "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
+                                           _P, c_float, _P, _P, _P, _P]),
+    "mirec_seq_embed_ln_partials": (c_int64, [c_int64]),
+    "mirec_seq_embed_ln_bwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
+                                           _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mirec_sampled_softmax_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32,
+                                          c_float, _P, _P, _P, _P]),
     "mirec_gather_sqnorm_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P]),
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }

@@ -152,7 +152,8 @@ class Config(object):
                 if c['MODEL_TYPE'] == ModelType.SEQUENTIAL and c['training_neg_sample_num'] > 0:
                     raise ValueError('training_neg_sample_num should be 0 when the loss_type is CE')
                 c['MODEL_INPUT_TYPE'] = InputType.POINTWISE
-            elif c['loss_type'] in ['BPR']:
+            elif c['loss_type'] in ['BPR', 'SSM']:
+                # SSM: sampled softmax over neg_sample_num negatives (build extension)
                 c['MODEL_INPUT_TYPE'] = InputType.PAIRWISE
         else:
             raise ValueError("Either Model has attr 'input_type',or arg 'loss_type' should exist in config.")

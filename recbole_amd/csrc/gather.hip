@@ -78,3 +78,44 @@ extern "C" int mirec_gather_rows_i32idx(const void* table, int64_t n_rows, int64
                                         const int32_t* idx, int64_t n, void* out, void* stream) {
   return gather_impl<int32_t>(table, n_rows, row_bytes, idx, n, out, (hipStream_t)stream);
 }
+
+// Sliding-window gather for the sequential loaders (SequentialDataLoader.augmentation,
+// recbole/data/dataloader/sequential_dataloader.py:95-127, computed on the device):
+// out[i, t] = col[start[i] + t] for t < len[i], else 0; elements of 4 or 8 bytes.
+namespace mirec {
+
+template <typename T>
+__global__ __launch_bounds__(256) void window_gather_kernel(const T* __restrict__ col,
+                                                            const int64_t* __restrict__ start,
+                                                            const int64_t* __restrict__ len,
+                                                            int64_t n, int L, T* __restrict__ out) {
+  const int64_t total = n * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / L;
+    const int t = (int)(e - i * L);
+    out[e] = t < len[i] ? col[start[i] + t] : T(0);
+  }
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_window_gather(const void* col, int32_t elem_bytes, const int64_t* start,
+                                   const int64_t* len, int64_t n, int32_t L, void* out,
+                                   void* stream) {
+  if (n == 0) return 0;
+  if (!col || !start || !len || !out || n < 0 || L <= 0 || (elem_bytes != 4 && elem_bytes != 8)) {
+    set_error("mirec_window_gather: bad arguments");
+    return -1;
+  }
+  int64_t g = (n * L + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  hipStream_t st = (hipStream_t)stream;
+  if (elem_bytes == 8)
+    hipLaunchKernelGGL(window_gather_kernel<int64_t>, dim3((unsigned)g), dim3(256), 0, st,
+                       (const int64_t*)col, start, len, n, L, (int64_t*)out);
+  else
+    hipLaunchKernelGGL(window_gather_kernel<int32_t>, dim3((unsigned)g), dim3(256), 0, st,
+                       (const int32_t*)col, start, len, n, L, (int32_t*)out);
+  return launch_status("mirec_window_gather");
+}

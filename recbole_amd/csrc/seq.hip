@@ -1,0 +1,315 @@
+// K9 — sequential recommender (SASRec) embedding side and sampled softmax.
+//
+// K9a  seq_embed_ln: restates the input block of SASRec.forward
+//   (recbole/model/sequential_recommender/sasrec.py:107-117):
+//     x[b,t] = item_embedding[item_seq[b,t]] + position_embedding[t]
+//     y[b,t] = LayerNorm(x[b,t]) = (x - mean) * rstd * gamma + beta
+//   and its autograd backward: dx = rstd * (g*gamma - mean(g*gamma)
+//   - xhat * mean(g*gamma*xhat)); dgamma = sum g*xhat, dbeta = sum g (per-block
+//   partials in a fixed order, then a fixed-order column sum); the item rows'
+//   gradient is returned per contribution for the K2 grouping (row 0 = the
+//   padding_idx row receives none, nn.Embedding(padding_idx=0)).
+// K9b  sampled softmax over [positive | N negatives] per sequence (the C3
+//   config's loss, a build extension — the reference has BPR and full CE only):
+//     logit_j = <s_b, E[item_bj]>, loss_b = logsumexp_j(logit) - logit_0,
+//     dS_b = scale * (sum_j p_j E_j - E_0), dE_bj = scale * (p_j - [j==0]) s_b.
+//   One wave per sequence, ONE pass over the N+1 rows: an online (running-max)
+//   softmax accumulates sum_j p_j E_j while the rows stream in; the logits stay
+//   in LDS for the row gradients, which need only s_b (no second gather).
+//
+// Layout: D/4 lanes per row (float4 per lane), 64/(D/4) rows per wave for K9a.
+#include "common.h"
+
+namespace mirec {
+
+template <int LPR>
+__device__ __forceinline__ float lane_group_sum(float x) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__device__ __forceinline__ float sum4(float4 a) { return (a.x + a.y) + (a.z + a.w); }
+
+constexpr int kLnRowsPerBlock = 64;   // K9a backward partial-sum chunk (fixed)
+
+template <int D>
+__global__ __launch_bounds__(256) void seq_embed_ln_fwd_kernel(
+    const float* __restrict__ E, int64_t n_items, const float* __restrict__ P,
+    const int64_t* __restrict__ seq, int64_t n_rows, int L, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ out,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int LPR = D / 4, GPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane % LPR;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t r = wave * GPW + g;
+  if (r >= n_rows) return;
+  int64_t id = seq[r];
+  id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
+  const int t = (int)(r % L);
+  const float4 e = reinterpret_cast<const float4*>(E + id * D)[l];
+  const float4 p = reinterpret_cast<const float4*>(P + (int64_t)t * D)[l];
+  float4 x = make_float4(e.x + p.x, e.y + p.y, e.z + p.z, e.w + p.w);
+  const float mean = lane_group_sum<LPR>(sum4(x)) * (1.0f / D);
+  float4 c = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+  const float var = lane_group_sum<LPR>(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) *
+                    (1.0f / D);
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+  const float4 bt = reinterpret_cast<const float4*>(beta)[l];
+  float4 y;
+  y.x = c.x * rstd * gm.x + bt.x;
+  y.y = c.y * rstd * gm.y + bt.y;
+  y.z = c.z * rstd * gm.z + bt.z;
+  y.w = c.w * rstd * gm.w + bt.w;
+  reinterpret_cast<float4*>(out + r * D)[l] = y;
+  if (l == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+// Block = 4 waves over kLnRowsPerBlock consecutive rows; writes dx rows, the
+// item-row gradient (0 for padding id 0) and the block's partial dgamma / dbeta.
+template <int D>
+__global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
+    const float* __restrict__ E, int64_t n_items, const float* __restrict__ P,
+    const int64_t* __restrict__ seq, int64_t n_rows, int L, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const float* __restrict__ gy, float* __restrict__ dx, float* __restrict__ ditem,
+    float* __restrict__ part_gamma, float* __restrict__ part_beta) {
+  constexpr int LPR = D / 4, GPW = 64 / LPR;
+  __shared__ float4 red_g[4 * GPW][LPR];
+  __shared__ float4 red_b[4 * GPW][LPR];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane / LPR, l = lane % LPR;
+  const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+  float4 ag = make_float4(0.f, 0.f, 0.f, 0.f), ab = ag;
+  const int64_t base = (int64_t)blockIdx.x * kLnRowsPerBlock;
+  for (int i = w * GPW + g; i < kLnRowsPerBlock; i += 4 * GPW) {
+    const int64_t r = base + i;
+    if (r >= n_rows) break;
+    int64_t id = seq[r];
+    const bool pad = id == 0;
+    id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
+    const int t = (int)(r % L);
+    const float4 e = reinterpret_cast<const float4*>(E + id * D)[l];
+    const float4 p = reinterpret_cast<const float4*>(P + (int64_t)t * D)[l];
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float4 xh;
+    xh.x = (e.x + p.x - mean) * rstd;
+    xh.y = (e.y + p.y - mean) * rstd;
+    xh.z = (e.z + p.z - mean) * rstd;
+    xh.w = (e.w + p.w - mean) * rstd;
+    const float4 gv = reinterpret_cast<const float4*>(gy + r * D)[l];
+    const float4 gg = make_float4(gv.x * gm.x, gv.y * gm.y, gv.z * gm.z, gv.w * gm.w);
+    const float m1 = lane_group_sum<LPR>(sum4(gg)) * (1.0f / D);
+    const float m2 =
+        lane_group_sum<LPR>(gg.x * xh.x + gg.y * xh.y + gg.z * xh.z + gg.w * xh.w) *
+        (1.0f / D);
+    float4 o;
+    o.x = rstd * (gg.x - m1 - xh.x * m2);
+    o.y = rstd * (gg.y - m1 - xh.y * m2);
+    o.z = rstd * (gg.z - m1 - xh.z * m2);
+    o.w = rstd * (gg.w - m1 - xh.w * m2);
+    if (dx) reinterpret_cast<float4*>(dx + r * D)[l] = o;
+    if (ditem)
+      reinterpret_cast<float4*>(ditem + r * D)[l] = pad ? make_float4(0.f, 0.f, 0.f, 0.f) : o;
+    ag.x += gv.x * xh.x;
+    ag.y += gv.y * xh.y;
+    ag.z += gv.z * xh.z;
+    ag.w += gv.w * xh.w;
+    ab.x += gv.x;
+    ab.y += gv.y;
+    ab.z += gv.z;
+    ab.w += gv.w;
+  }
+  red_g[w * GPW + g][l] = ag;
+  red_b[w * GPW + g][l] = ab;
+  __syncthreads();
+  if (threadIdx.x < LPR) {
+    float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
+    for (int q = 0; q < 4 * GPW; ++q) {
+      const float4 a = red_g[q][threadIdx.x], b = red_b[q][threadIdx.x];
+      sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
+      sb.x += b.x; sb.y += b.y; sb.z += b.z; sb.w += b.w;
+    }
+    reinterpret_cast<float4*>(part_gamma + (int64_t)blockIdx.x * D)[threadIdx.x] = sg;
+    reinterpret_cast<float4*>(part_beta + (int64_t)blockIdx.x * D)[threadIdx.x] = sb;
+  }
+}
+
+// K9b. items: pos [B] and negs [N*B] (layout j*B + b, the sampler's).
+template <int D>
+__global__ __launch_bounds__(256) void sampled_softmax_kernel(
+    const float* __restrict__ S, const float* __restrict__ E, int64_t n_items,
+    const int64_t* __restrict__ pos, const int64_t* __restrict__ neg, int64_t B, int N,
+    float scale, float* __restrict__ loss, float* __restrict__ gS, float* __restrict__ gI) {
+  extern __shared__ float lds_logits[];   // (N+1) per wave
+  constexpr int V = D / 64;   // floats per lane (D in {64, 128, 256})
+  const int lane = threadIdx.x & 63;
+  const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (b >= B) return;
+  float s[V], acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    s[v] = S[b * D + v * 64 + lane];
+    acc[v] = 0.f;
+  }
+  // every lane writes the same value to its wave's slot and reads only what it
+  // wrote itself: no cross-lane ordering is involved
+  float* lg = lds_logits + (threadIdx.x >> 6) * (N + 1);
+  float m = -__builtin_inff(), lsum = 0.f, l0 = 0.f;
+  float e0[V];
+  for (int j = 0; j <= N; ++j) {
+    int64_t id = j == 0 ? pos[b] : neg[(int64_t)(j - 1) * B + b];
+    id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
+    float row[V];
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      row[v] = E[id * D + v * 64 + lane];
+      dot = fmaf(s[v], row[v], dot);
+    }
+    dot = wave_sum(dot);
+    lg[j] = dot;
+    if (j == 0) l0 = dot;
+    const float mn = fmaxf(m, dot);
+    const float cold = expf(m - mn), cnew = expf(dot - mn);
+    lsum = lsum * cold + cnew;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      acc[v] = acc[v] * cold + cnew * row[v];
+      if (j == 0) e0[v] = row[v];
+    }
+    m = mn;
+  }
+  const float lse = m + logf(lsum);
+  if (lane == 0) loss[b] = lse - l0;
+  const float inv = 1.f / lsum;
+#pragma unroll
+  for (int v = 0; v < V; ++v) gS[b * D + v * 64 + lane] = scale * (acc[v] * inv - e0[v]);
+  for (int j = 0; j <= N; ++j) {
+    const float p = expf(lg[j] - lse);
+    const float c = scale * (p - (j == 0 ? 1.f : 0.f));
+    float* out = gI + ((j == 0 ? b : (int64_t)j * B + b)) * D;
+#pragma unroll
+    for (int v = 0; v < V; ++v) out[v * 64 + lane] = c * s[v];
+  }
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_seq_embed_ln_fwd_f32(const float* item_table, int64_t n_items,
+                                          const float* pos_table, const int64_t* item_seq,
+                                          int64_t B, int32_t L, int32_t d, const float* gamma,
+                                          const float* beta, float eps, float* out, float* mean,
+                                          float* rstd, void* stream) {
+  const int64_t n = B * L;
+  if (n == 0) return 0;
+  if (!item_table || !pos_table || !item_seq || !gamma || !beta || !out || !mean || !rstd ||
+      B < 0 || L <= 0 || n_items <= 0) {
+    set_error("mirec_seq_embed_ln_fwd_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_LNF(DD)                                                                        \
+  case DD: {                                                                                 \
+    constexpr int GPW = 64 / (DD / 4);                                                       \
+    const int64_t waves = (n + GPW - 1) / GPW;                                               \
+    hipLaunchKernelGGL(seq_embed_ln_fwd_kernel<DD>, dim3((unsigned)((waves + 3) / 4)),       \
+                       dim3(256), 0, st, item_table, n_items, pos_table, item_seq, n, L,     \
+                       gamma, beta, eps, out, mean, rstd);                                   \
+  } break;
+  switch (d) {
+    MIREC_LNF(32)
+    MIREC_LNF(64)
+    MIREC_LNF(128)
+    MIREC_LNF(256)
+    default:
+      set_error("mirec_seq_embed_ln_fwd_f32: hidden size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_LNF
+  return launch_status("mirec_seq_embed_ln_fwd_f32");
+}
+
+extern "C" int64_t mirec_seq_embed_ln_partials(int64_t n_rows) {
+  return (n_rows + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
+}
+
+extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items,
+                                          const float* pos_table, const int64_t* item_seq,
+                                          int64_t B, int32_t L, int32_t d, const float* gamma,
+                                          const float* mean, const float* rstd,
+                                          const float* grad_out, float* dx, float* ditem,
+                                          float* part_gamma, float* part_beta, void* stream) {
+  const int64_t n = B * L;
+  if (n == 0) return 0;
+  if (!item_table || !pos_table || !item_seq || !gamma || !mean || !rstd || !grad_out ||
+      !part_gamma || !part_beta || B < 0 || L <= 0 || n_items <= 0) {
+    set_error("mirec_seq_embed_ln_bwd_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grd((unsigned)mirec_seq_embed_ln_partials(n));
+#define MIREC_LNB(DD)                                                                        \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(seq_embed_ln_bwd_kernel<DD>, grd, dim3(256), 0, st, item_table,       \
+                       n_items, pos_table, item_seq, n, L, gamma, mean, rstd, grad_out, dx,  \
+                       ditem, part_gamma, part_beta);                                        \
+    break;
+  switch (d) {
+    MIREC_LNB(32)
+    MIREC_LNB(64)
+    MIREC_LNB(128)
+    MIREC_LNB(256)
+    default:
+      set_error("mirec_seq_embed_ln_bwd_f32: hidden size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_LNB
+  return launch_status("mirec_seq_embed_ln_bwd_f32");
+}
+
+extern "C" int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table,
+                                         int64_t n_items, int32_t d, const int64_t* pos,
+                                         const int64_t* neg, int64_t B, int32_t n_neg,
+                                         float grad_scale, float* loss, float* g_seq,
+                                         float* g_items, void* stream) {
+  if (B == 0) return 0;
+  if (!seq_out || !item_table || !pos || (n_neg > 0 && !neg) || !loss || !g_seq || !g_items ||
+      B < 0 || n_neg < 0 || n_items <= 0) {
+    set_error("mirec_sampled_softmax_f32: bad arguments");
+    return -1;
+  }
+  const dim3 grd((unsigned)((B + 3) / 4));
+  const size_t lds = (size_t)4 * (n_neg + 1) * sizeof(float);
+  if (lds > 64 * 1024) {
+    set_error("mirec_sampled_softmax_f32: %d negatives exceed the LDS logit buffer", n_neg);
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  switch (d) {
+    case 64:
+      hipLaunchKernelGGL(sampled_softmax_kernel<64>, grd, dim3(256), lds, st, seq_out,
+                         item_table, n_items, pos, neg, B, n_neg, grad_scale, loss, g_seq, g_items);
+      break;
+    case 128:
+      hipLaunchKernelGGL(sampled_softmax_kernel<128>, grd, dim3(256), lds, st, seq_out,
+                         item_table, n_items, pos, neg, B, n_neg, grad_scale, loss, g_seq, g_items);
+      break;
+    case 256:
+      hipLaunchKernelGGL(sampled_softmax_kernel<256>, grd, dim3(256), lds, st, seq_out,
+                         item_table, n_items, pos, neg, B, n_neg, grad_scale, loss, g_seq, g_items);
+      break;
+    default:
+      set_error("mirec_sampled_softmax_f32: hidden size %d not in {64,128,256}", d);
+      return -1;
+  }
+  return launch_status("mirec_sampled_softmax_f32");
+}

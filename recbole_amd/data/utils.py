@@ -6,13 +6,19 @@ from logging import getLogger
 from recbole_amd.config import EvalSetting
 from recbole_amd.data.dataloader import (GeneralDataLoader, GeneralFullDataLoader,
                                          GeneralNegSampleDataLoader)
+from recbole_amd.data.dataloader.sequential_dataloader import (SequentialDataLoader,
+                                                               SequentialFullDataLoader,
+                                                               SequentialNegSampleDataLoader)
 from recbole_amd.data.dataset import Dataset
+from recbole_amd.data.sequential_dataset import SequentialDataset
 from recbole_amd.sampler import RepeatableSampler, Sampler
 from recbole_amd.utils import ModelType
 
 
 def create_dataset(config):
     model_type = config['MODEL_TYPE']
+    if model_type == ModelType.SEQUENTIAL:
+        return SequentialDataset(config)
     if model_type in (ModelType.GENERAL, ModelType.TRADITIONAL, ModelType.CONTEXT):
         return Dataset(config)
     raise NotImplementedError(f'model type {model_type} datasets are not part of this build yet')
@@ -20,6 +26,10 @@ def create_dataset(config):
 
 def get_data_loader(name, config, neg_sample_args):
     model_type = config['MODEL_TYPE']
+    if model_type == ModelType.SEQUENTIAL:
+        strategy = neg_sample_args['strategy']
+        return {'none': SequentialDataLoader, 'by': SequentialNegSampleDataLoader,
+                'full': SequentialFullDataLoader}[strategy]
     # Context{DataLoader,NegSampleDataLoader,FullDataLoader} are the General ones
     # under another name (context_dataloader.py:20-43)
     if model_type not in (ModelType.GENERAL, ModelType.TRADITIONAL, ModelType.CONTEXT):

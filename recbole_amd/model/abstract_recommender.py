@@ -113,3 +113,24 @@ class ContextRecommender(AbstractRecommender):
     def concat_embed_input_fields(self, interaction):
         """[B, num_feature_field, d] (abstract_recommender.py:356-363)."""
         return self.fm_fields(interaction)[0]
+
+
+class SequentialRecommender(AbstractRecommender):
+    """abstract_recommender.py:97-121."""
+    type = ModelType.SEQUENTIAL
+
+    def __init__(self, config, dataset):
+        super().__init__()
+        self.USER_ID = config['USER_ID_FIELD']
+        self.ITEM_ID = config['ITEM_ID_FIELD']
+        self.ITEM_SEQ = self.ITEM_ID + config['LIST_SUFFIX']
+        self.ITEM_SEQ_LEN = config['ITEM_LIST_LENGTH_FIELD']
+        self.POS_ITEM_ID = self.ITEM_ID
+        self.NEG_ITEM_ID = config['NEG_PREFIX'] + self.ITEM_ID
+        self.max_seq_length = config['MAX_ITEM_LIST_LENGTH']
+        self.n_items = dataset.num(self.ITEM_ID)
+
+    def gather_indexes(self, output, gather_index):
+        """Vectors at the given positions over a minibatch (:117-121)."""
+        gather_index = gather_index.view(-1, 1, 1).expand(-1, -1, output.shape[-1])
+        return output.gather(dim=1, index=gather_index).squeeze(1)

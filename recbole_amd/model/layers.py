@@ -8,6 +8,9 @@ BaseFactorizationMachine forward: ContextRecommender runs all three in the
 fused K8 kernel (csrc/context.hip) over these modules' weights. Their forward
 methods remain, in torch ops, for user code that composes them directly.
 """
+import copy
+import math
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -148,3 +151,106 @@ class FMFirstOrderLinear(nn.Module):
             for dim in self.token_seq_field_dims:
                 self.token_seq_embedding_table.append(nn.Embedding(dim, output_dim))
         self.bias = nn.Parameter(torch.zeros((output_dim,)), requires_grad=True)
+
+
+class MultiHeadAttention(nn.Module):
+    """layers.py:338-407 (same parameters and op sequence; library GEMMs)."""
+
+    def __init__(self, n_heads, hidden_size, hidden_dropout_prob, attn_dropout_prob,
+                 layer_norm_eps):
+        super().__init__()
+        if hidden_size % n_heads != 0:
+            raise ValueError(f'The hidden size ({hidden_size}) is not a multiple of the number '
+                             f'of attention heads ({n_heads})')
+        self.num_attention_heads = n_heads
+        self.attention_head_size = int(hidden_size / n_heads)
+        self.all_head_size = self.num_attention_heads * self.attention_head_size
+        self.query = nn.Linear(hidden_size, self.all_head_size)
+        self.key = nn.Linear(hidden_size, self.all_head_size)
+        self.value = nn.Linear(hidden_size, self.all_head_size)
+        self.attn_dropout = nn.Dropout(attn_dropout_prob)
+        self.dense = nn.Linear(hidden_size, hidden_size)
+        self.LayerNorm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
+        self.out_dropout = nn.Dropout(hidden_dropout_prob)
+
+    def transpose_for_scores(self, x):
+        x = x.view(*(x.size()[:-1] + (self.num_attention_heads, self.attention_head_size)))
+        return x.permute(0, 2, 1, 3)
+
+    def forward(self, input_tensor, attention_mask):
+        q = self.transpose_for_scores(self.query(input_tensor))
+        k = self.transpose_for_scores(self.key(input_tensor))
+        v = self.transpose_for_scores(self.value(input_tensor))
+        scores = torch.matmul(q, k.transpose(-1, -2))
+        scores = scores / math.sqrt(self.attention_head_size)
+        scores = scores + attention_mask
+        probs = nn.Softmax(dim=-1)(scores)
+        probs = self.attn_dropout(probs)
+        ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
+        ctx = ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
+        hidden = self.out_dropout(self.dense(ctx))
+        return self.LayerNorm(hidden + input_tensor)
+
+
+class FeedForward(nn.Module):
+    """layers.py:410-461."""
+
+    def __init__(self, hidden_size, inner_size, hidden_dropout_prob, hidden_act, layer_norm_eps):
+        super().__init__()
+        self.dense_1 = nn.Linear(hidden_size, inner_size)
+        self.intermediate_act_fn = self.get_hidden_act(hidden_act)
+        self.dense_2 = nn.Linear(inner_size, hidden_size)
+        self.LayerNorm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
+        self.dropout = nn.Dropout(hidden_dropout_prob)
+
+    def get_hidden_act(self, act):
+        return {'gelu': self.gelu, 'relu': nn.functional.relu, 'swish': self.swish,
+                'tanh': torch.tanh, 'sigmoid': torch.sigmoid}[act]
+
+    def gelu(self, x):
+        return x * 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+    def swish(self, x):
+        return x * torch.sigmoid(x)
+
+    def forward(self, input_tensor):
+        hidden = self.dense_2(self.intermediate_act_fn(self.dense_1(input_tensor)))
+        hidden = self.dropout(hidden)
+        return self.LayerNorm(hidden + input_tensor)
+
+
+class TransformerLayer(nn.Module):
+    """layers.py:464-490."""
+
+    def __init__(self, n_heads, hidden_size, intermediate_size, hidden_dropout_prob,
+                 attn_dropout_prob, hidden_act, layer_norm_eps):
+        super().__init__()
+        self.multi_head_attention = MultiHeadAttention(n_heads, hidden_size, hidden_dropout_prob,
+                                                       attn_dropout_prob, layer_norm_eps)
+        self.feed_forward = FeedForward(hidden_size, intermediate_size, hidden_dropout_prob,
+                                        hidden_act, layer_norm_eps)
+
+    def forward(self, hidden_states, attention_mask):
+        return self.feed_forward(self.multi_head_attention(hidden_states, attention_mask))
+
+
+class TransformerEncoder(nn.Module):
+    """layers.py:493-552 (n_layers deep copies of one TransformerLayer)."""
+
+    def __init__(self, n_layers=2, n_heads=2, hidden_size=64, inner_size=256,
+                 hidden_dropout_prob=0.5, attn_dropout_prob=0.5, hidden_act='gelu',
+                 layer_norm_eps=1e-12):
+        super().__init__()
+        layer = TransformerLayer(n_heads, hidden_size, inner_size, hidden_dropout_prob,
+                                 attn_dropout_prob, hidden_act, layer_norm_eps)
+        self.layer = nn.ModuleList([copy.deepcopy(layer) for _ in range(n_layers)])
+
+    def forward(self, hidden_states, attention_mask, output_all_encoded_layers=True):
+        out = []
+        for layer_module in self.layer:
+            hidden_states = layer_module(hidden_states, attention_mask)
+            if output_all_encoded_layers:
+                out.append(hidden_states)
+        if not output_all_encoded_layers:
+            out.append(hidden_states)
+        return out

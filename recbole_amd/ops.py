@@ -105,6 +105,22 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None
     return out
 
 
+def window_gather(col: torch.Tensor, start: torch.Tensor, length: torch.Tensor, L: int,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i, t] = col[start[i] + t] if t < length[i] else 0 (sequence windows)."""
+    _dev(start, torch.int64, "start")
+    _dev(length, torch.int64, "length")
+    if not col.is_cuda or not col.is_contiguous():
+        raise NativeError("window_gather: col must be a contiguous GPU tensor")
+    n = start.numel()
+    if out is None:
+        out = torch.empty(n, L, dtype=col.dtype, device=col.device)
+    rc = lib().mirec_window_gather(ptr(col), col.element_size(), ptr(start), ptr(length), n, L,
+                                   ptr(out), stream_handle())
+    check(rc, "mirec_window_gather")
+    return out
+
+
 # ---------------------------------------------------------------- K3 BPR
 def bpr_fwd_bwd(EU, EI, user, pos, neg, times: int, gamma: float = 1e-10,
                 grad_scale: float | None = None, grads: bool = True, scores: bool = False,

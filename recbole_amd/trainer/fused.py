@@ -494,3 +494,24 @@ def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20):
                           pos_ptr=pos_ptr[s:e + 1], pos_cols=pos_cols, out=o)
     pos_idx = flags.cpu().numpy().astype(bool)
     return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
+
+
+def fused_seq_full_sort_eval(model, eval_data, topk_evaluator):
+    """Trainer.evaluate for SequentialFullDataLoader (trainer.py:328-353 with
+    sequential_dataloader.py:318-345: pad column masked, the target swapped to
+    the front, no history mask) on K6: per batch, the sequence representations
+    are ranked against every item with the target as the only positive."""
+    dev = model.fused_item_table().device
+    K = max(topk_evaluator.topk)
+    EI = model.fused_item_table().contiguous()
+    flags = []
+    for interaction, _, _, _, _ in eval_data:
+        inter = interaction.to(dev)
+        Uq = model.fused_query_vectors(inter).detach().contiguous()
+        n = Uq.shape[0]
+        pos_ptr = torch.arange(n + 1, dtype=torch.int64, device=dev)
+        pos_cols = inter[eval_data.iid_field].to(torch.int32).contiguous()
+        o = ops.fullsort_topk(Uq, EI, K, pos_ptr=pos_ptr, pos_cols=pos_cols)
+        flags.append(o['pos_flags'])
+    pos_idx = torch.cat(flags).cpu().numpy().astype(bool)
+    return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
