@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 3
+#define MIREC_ABI_VERSION 4
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -128,7 +128,8 @@ int mirec_sum_f32(const float* x, int64_t n, float* out, void* stream);
  * K2  Segment sort: group contribution rows by table row id, deterministic.
  * Replaces the index_add in torch's embedding_dense_backward for
  *   nn.Embedding(sparse=False) (bpr.py:40-41; trainer.py:170).
- * Stable sort of (keys[c], c): perm[i] = c sorted by (key, c);
+ * Stable sort of (keys[c], c): perm[i] = c sorted by (key, c); one workgroup in LDS
+ * up to 8,192 keys, a device-wide 4-bit LSD radix sort above (single batch);
  *   uniq[u] = distinct keys ascending, seg[u]..seg[u+1] their slice of perm,
  *   *n_uniq_dev = number of distinct keys. Keys must lie in [0, key_space).
  * ------------------------------------------------------------------------- */
@@ -152,12 +153,17 @@ int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
 int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t stride,
                           int64_t n_batches, int32_t* out, int32_t* n_out, void* stream);
 
-/* dense[uniq[u], :] +=sum_{i in seg[u]..seg[u+1]} rows[perm[i], :]  (fixed order)
- * — the dense-gradient form used by the autograd-compatible path. */
+/* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
+ * dense-gradient form used by the autograd-compatible path. n = number of
+ * contributions (seg[n_uniq] <= n). The sorted contributions are summed in chunks
+ * of 32 positions in a fixed order (hot rows are split over many lane groups and
+ * their partials added in chunk order by a fixup pass): deterministic, no atomics.
+ * Workspace: mirec_segment_scatter_add_workspace_size(n, d). 1 <= d <= 256. */
+size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d);
 int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
                                   const int32_t* uniq, const int32_t* seg,
-                                  const int32_t* n_uniq_dev, int64_t n_max_uniq,
-                                  float* dense, int64_t n_rows, void* stream);
+                                  const int32_t* n_uniq_dev, int64_t n, float* dense,
+                                  int64_t n_rows, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K5  Dense Adam over every row, with the gradient supplied in compact form.

@@ -70,8 +70,9 @@ SIGNATURES = {
     "mirec_segment_sort_batched": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
+    "mirec_segment_scatter_add_workspace_size": (c_size_t, [c_int64, c_int32]),
     "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
-                                              c_int64, _P]),
+                                              c_int64, _P, c_size_t, _P]),
     "mirec_adam_sparse_grad_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, _P, _P,
                                            c_int64, _P, _P, _P, c_double, c_double, c_double,
                                            c_double, _P]),
@@ -107,7 +108,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class NativeError(RuntimeError):

@@ -183,6 +183,316 @@ __global__ __launch_bounds__(256) void segment_scatter_add_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large single-batch sorts (n > kLdsMax: the autograd paths of the context and
+// sequential models group 10^5..10^6 contributions per step). Device-wide
+// stable LSD radix sort, 4-bit digits, one tile of kRadixTile keys per block:
+//   upsweep   per-tile digit histogram            -> hist[digit * n_tiles + tile]
+//   scan      exclusive scan of hist (digit-major) -> global destination bases
+//   downsweep stable in-tile ranking (blocked layout, per-thread digit counts
+//             scanned digit-major in LDS) -> scatter of (key, index)
+// then segments: per-tile head-flag counts -> scan -> uniq / seg writes.
+constexpr int kRadixThreads = 256;
+constexpr int kRadixIpt = 8;
+constexpr int kRadixTile = kRadixThreads * kRadixIpt;
+constexpr int kRadixBins = 16;
+
+__global__ __launch_bounds__(kRadixThreads) void radix_init_kernel(
+    const int64_t* __restrict__ keys, int n, int32_t* __restrict__ k32, int32_t* __restrict__ v32) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    k32[i] = (int32_t)keys[i];
+    v32[i] = i;
+  }
+}
+
+// per-thread digit counts of the thread's kRadixIpt consecutive keys -> cnt[bin][t]
+__device__ __forceinline__ void tile_counts(const int32_t* __restrict__ k, int n, int base,
+                                            int shift, int* cnt, int32_t* my, int* nmy) {
+  const int t = threadIdx.x;
+  int c[kRadixBins];
+#pragma unroll
+  for (int b = 0; b < kRadixBins; ++b) c[b] = 0;
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < kRadixIpt; ++j) {
+    const int i = base + t * kRadixIpt + j;
+    if (i < n) {
+      my[j] = k[i];
+      const int dg = (my[j] >> shift) & (kRadixBins - 1);
+#pragma unroll
+      for (int b = 0; b < kRadixBins; ++b) c[b] += (dg == b) ? 1 : 0;
+      ++m;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < kRadixBins; ++b) cnt[b * kRadixThreads + t] = c[b];
+  *nmy = m;
+}
+
+__global__ __launch_bounds__(kRadixThreads) void radix_upsweep_kernel(
+    const int32_t* __restrict__ k, int n, int shift, int n_tiles, int32_t* __restrict__ hist) {
+  __shared__ int cnt[kRadixBins * kRadixThreads];
+  int32_t my[kRadixIpt];
+  int nmy;
+  tile_counts(k, n, blockIdx.x * kRadixTile, shift, cnt, my, &nmy);
+  __syncthreads();
+  if (threadIdx.x < kRadixBins) {
+    int s = 0;
+    for (int t = 0; t < kRadixThreads; ++t) s += cnt[threadIdx.x * kRadixThreads + t];
+    hist[threadIdx.x * n_tiles + blockIdx.x] = s;
+  }
+}
+
+// exclusive scan of a[0..m) in place (one block), a[m] = total
+__global__ __launch_bounds__(1024) void scan_exclusive_kernel(int32_t* __restrict__ a, int m) {
+  __shared__ int lds[1024 / 64 + 1];
+  int run = 0;
+  for (int c0 = 0; c0 < m; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    const int x = i < m ? a[i] : 0;
+    int tot;
+    const int ex = block_exclusive_scan(x, lds, &tot);
+    if (i < m) a[i] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) a[m] = run;
+}
+
+__global__ __launch_bounds__(kRadixThreads) void radix_downsweep_kernel(
+    const int32_t* __restrict__ k, const int32_t* __restrict__ v, int n, int shift, int n_tiles,
+    const int32_t* __restrict__ hist, int32_t* __restrict__ ko, int32_t* __restrict__ vo) {
+  __shared__ int cnt[kRadixBins * kRadixThreads];
+  __shared__ int part[kRadixThreads / 64 + 1];
+  __shared__ int bin_start[kRadixBins];
+  int32_t my[kRadixIpt];
+  int nmy;
+  const int base = blockIdx.x * kRadixTile;
+  tile_counts(k, n, base, shift, cnt, my, &nmy);
+  __syncthreads();
+  // exclusive scan of cnt (bin-major, 4096 entries): 16 per thread, then a block scan
+  const int t = threadIdx.x;
+  int loc[kRadixBins];
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < kRadixBins; ++j) {
+    loc[j] = s;
+    s += cnt[t * kRadixBins + j];
+  }
+  int tot;
+  const int ex = block_exclusive_scan(s, part, &tot);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRadixBins; ++j) cnt[t * kRadixBins + j] = ex + loc[j];
+  __syncthreads();
+  if (t < kRadixBins) bin_start[t] = cnt[t * kRadixThreads];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRadixIpt; ++j) {
+    if (j < nmy) {
+      const int dg = (my[j] >> shift) & (kRadixBins - 1);
+      int before = 0;
+#pragma unroll
+      for (int q = 0; q < kRadixIpt; ++q) before += (q < j && ((my[q] >> shift) & (kRadixBins - 1)) == dg) ? 1 : 0;
+      const int local = cnt[dg * kRadixThreads + t] - bin_start[dg] + before;
+      const int dst = hist[dg * n_tiles + blockIdx.x] + local;
+      const int i = base + t * kRadixIpt + j;
+      ko[dst] = my[j];
+      vo[dst] = v[i];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kRadixThreads) void seg_count_kernel(const int32_t* __restrict__ k,
+                                                                  int n,
+                                                                  int32_t* __restrict__ tcnt) {
+  __shared__ int part[kRadixThreads / 64 + 1];
+  const int base = blockIdx.x * kRadixTile;
+  int f = 0;
+  for (int j = 0; j < kRadixIpt; ++j) {
+    const int i = base + threadIdx.x * kRadixIpt + j;
+    if (i < n) f += (i == 0 || k[i - 1] != k[i]) ? 1 : 0;
+  }
+  int tot;
+  (void)block_exclusive_scan(f, part, &tot);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kRadixThreads) void seg_write_kernel(
+    const int32_t* __restrict__ k, int n, int n_tiles, const int32_t* __restrict__ tbase,
+    int32_t* __restrict__ uniq, int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq) {
+  __shared__ int part[kRadixThreads / 64 + 1];
+  const int base = blockIdx.x * kRadixTile;
+  int f = 0;
+  for (int j = 0; j < kRadixIpt; ++j) {
+    const int i = base + threadIdx.x * kRadixIpt + j;
+    if (i < n) f += (i == 0 || k[i - 1] != k[i]) ? 1 : 0;
+  }
+  int tot;
+  int o = tbase[blockIdx.x] + block_exclusive_scan(f, part, &tot);
+  for (int j = 0; j < kRadixIpt; ++j) {
+    const int i = base + threadIdx.x * kRadixIpt + j;
+    if (i < n && (i == 0 || k[i - 1] != k[i])) {
+      uniq[o] = k[i];
+      seg[o] = i;
+      ++o;
+    }
+  }
+  if (blockIdx.x == n_tiles - 1 && threadIdx.x == 0) {
+    const int total = tbase[n_tiles];
+    seg[total] = n;
+    n_uniq[0] = total;
+  }
+}
+
+static size_t radix_ws_bytes(int64_t n) {
+  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
+  return (size_t)4 * (size_t)n * sizeof(int32_t) +
+         (size_t)(kRadixBins * tiles + 1 + tiles + 1) * sizeof(int32_t) + 256;
+}
+
+static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* perm,
+                              int32_t* uniq, int32_t* seg, int32_t* n_uniq, void* ws,
+                              hipStream_t st) {
+  const int tiles = (n + kRadixTile - 1) / kRadixTile;
+  int32_t* kA = (int32_t*)ws;
+  int32_t* vA = kA + n;
+  int32_t* kB = vA + n;
+  int32_t* vB = kB + n;
+  int32_t* hist = vB + n;                       // kRadixBins * tiles + 1
+  int32_t* tcnt = hist + kRadixBins * tiles + 1;  // tiles + 1
+  int g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(radix_init_kernel, dim3(g), dim3(256), 0, st, keys, n, kA, vA);
+  const int passes = nbits == 0 ? 0 : (nbits + 3) / 4;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 4 * p;
+    hipLaunchKernelGGL(radix_upsweep_kernel, dim3(tiles), dim3(kRadixThreads), 0, st, kA, n,
+                       shift, tiles, hist);
+    hipLaunchKernelGGL(scan_exclusive_kernel, dim3(1), dim3(1024), 0, st, hist,
+                       kRadixBins * tiles);
+    hipLaunchKernelGGL(radix_downsweep_kernel, dim3(tiles), dim3(kRadixThreads), 0, st, kA, vA,
+                       n, shift, tiles, hist, kB, vB);
+    int32_t* t = kA; kA = kB; kB = t;
+    t = vA; vA = vB; vB = t;
+  }
+  {
+    const int rc = hip_status(
+        hipMemcpyAsync(perm, vA, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st),
+        "mirec_segment_sort (perm copy)");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(seg_count_kernel, dim3(tiles), dim3(kRadixThreads), 0, st, kA, n, tcnt);
+  hipLaunchKernelGGL(scan_exclusive_kernel, dim3(1), dim3(1024), 0, st, tcnt, tiles);
+  hipLaunchKernelGGL(seg_write_kernel, dim3(tiles), dim3(kRadixThreads), 0, st, kA, n, tiles,
+                     tcnt, uniq, seg, n_uniq);
+  return launch_status("mirec_segment_sort (radix)");
+}
+
+// ---------------------------------------------------------------------------
+// Chunked segmented scatter-add (hot rows: a Zipf head row may own 10^4..10^5
+// contributions, far too many for one wave to sum serially). The sorted
+// contribution positions are cut into chunks of kScatChunk; a group of G lanes
+// per chunk sums runs of equal segment in position order. A segment wholly
+// inside a chunk is added to dense directly; a segment crossing chunk
+// boundaries leaves a tail partial in its first chunk and head partials in the
+// following ones, which the fixup kernel (one owner per segment: the boundary
+// it first crosses) adds in chunk order. Deterministic, no float atomics.
+constexpr int kScatChunk = 32;
+
+__device__ __forceinline__ int seg_of(const int32_t* __restrict__ seg, int nu, int p) {
+  int lo = 0, hi = nu - 1;   // largest u with seg[u] <= p
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg[mid] <= p) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <int G, int DMAX>
+__global__ __launch_bounds__(256) void scatter_chunks_kernel(
+    const float* __restrict__ rows, int d, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ n_uniq_dev, float* __restrict__ dense, int64_t n_rows,
+    float* __restrict__ head, float* __restrict__ tail, int n_chunks) {
+  const int nu = n_uniq_dev[0];
+  const int n = seg[nu];
+  const int lane = threadIdx.x & 63;
+  const int gi = lane / G, l = lane % G;
+  const int c = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64) * (64 / G) + gi;
+  if (c >= n_chunks || nu == 0) return;
+  const int p0 = c * kScatChunk;
+  if (p0 >= n) return;
+  const int p1 = min(n, p0 + kScatChunk);
+  constexpr int MAXC = DMAX / G;    // columns per lane, d <= DMAX
+  float acc[MAXC];
+  int u = seg_of(seg, nu, p0);
+  int s0 = seg[u], e = seg[u + 1];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+  auto flush = [&](void) {
+    const bool started_before = s0 < p0;
+    const bool ends_after = e > p1;
+    float* dst = nullptr;
+    if (!started_before && !ends_after) {
+      const int64_t row = uniq[u];
+      if (row >= 0 && row < n_rows) dst = dense + row * d;
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int col = l + j * G;
+        if (dst && col < d) dst[col] += acc[j];
+      }
+      return;
+    }
+    dst = (started_before ? head : tail) + (int64_t)c * d;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int col = l + j * G;
+      if (col < d) dst[col] = acc[j];
+    }
+  };
+  for (int p = p0; p < p1; ++p) {
+    if (p == e) {
+      flush();
+      ++u;
+      s0 = e;
+      e = seg[u + 1];
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+    }
+    const float* r = rows + (int64_t)perm[p] * d;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int col = l + j * G;
+      if (col < d) acc[j] += r[col];
+    }
+  }
+  flush();
+}
+
+__global__ __launch_bounds__(256) void scatter_fixup_kernel(
+    int d, const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ n_uniq_dev, float* __restrict__ dense, int64_t n_rows,
+    const float* __restrict__ head, const float* __restrict__ tail, int n_chunks) {
+  const int nu = n_uniq_dev[0];
+  const int n = seg[nu];
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64) + 1;  // boundary
+  if (b >= n_chunks || nu == 0) return;
+  const int q = b * kScatChunk;
+  if (q >= n) return;
+  const int u = seg_of(seg, nu, q);
+  const int s0 = seg[u], e = seg[u + 1];
+  if (s0 == q || s0 < (b - 1) * kScatChunk) return;   // not crossing, or not the owner
+  const int kend = (e - 1) / kScatChunk;
+  const int64_t row = uniq[u];
+  if (row < 0 || row >= n_rows) return;
+  for (int col = lane; col < d; col += 64) {
+    float s = tail[(int64_t)(b - 1) * d + col];
+    for (int k = b; k <= kend; ++k) s += head[(int64_t)k * d + col];
+    dense[row * d + col] += s;
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -190,7 +500,7 @@ using namespace mirec;
 extern "C" size_t mirec_segment_sort_workspace_size(int64_t n, int64_t key_space) {
   (void)key_space;
   if (n <= kLdsMax) return 256;
-  return (size_t)4 * (size_t)n * sizeof(int32_t) + 256;
+  return radix_ws_bytes(n);
 }
 
 extern "C" int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
@@ -211,6 +521,13 @@ extern "C" int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_
     return launch_status("mirec_segment_sort");
   }
   const int64_t n_batches = (n + batch_n - 1) / batch_n;
+  if (n_batches == 1 && n > kLdsMax) {
+    if (!ws || ws_bytes < radix_ws_bytes(n)) {
+      set_error("mirec_segment_sort: workspace %zu < %zu", ws_bytes, radix_ws_bytes(n));
+      return -1;
+    }
+    return radix_segment_sort(keys, (int)n, nb, perm, uniq, seg, n_uniq_dev, ws, st);
+  }
   if (batch_n <= kLdsMax) {
     hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)n_batches), dim3(kSortThreads), 0, st,
                        keys, n, (int)batch_n, nb, perm, uniq, seg, n_uniq_dev);
@@ -234,19 +551,47 @@ extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_sp
                                     n_uniq_dev, ws, ws_bytes, stream);
 }
 
+extern "C" size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d) {
+  const int64_t chunks = (n + kScatChunk - 1) / kScatChunk;
+  return (size_t)2 * (size_t)chunks * (size_t)(d > 0 ? d : 1) * sizeof(float) + 256;
+}
+
 extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
                                              const int32_t* uniq, const int32_t* seg,
-                                             const int32_t* n_uniq_dev, int64_t n_max_uniq,
-                                             float* dense, int64_t n_rows, void* stream) {
-  if (n_max_uniq == 0) return 0;
-  if (!rows || !perm || !uniq || !seg || !n_uniq_dev || !dense || d <= 0 || n_max_uniq < 0) {
-    set_error("mirec_segment_scatter_add_f32: bad arguments");
+                                             const int32_t* n_uniq_dev, int64_t n, float* dense,
+                                             int64_t n_rows, void* ws, size_t ws_bytes,
+                                             void* stream) {
+  if (n == 0) return 0;
+  if (!rows || !perm || !uniq || !seg || !n_uniq_dev || !dense || d <= 0 || d > 256 || n < 0 ||
+      n > INT32_MAX) {
+    set_error("mirec_segment_scatter_add_f32: bad arguments (1 <= d <= 256)");
     return -1;
   }
-  int64_t g = (n_max_uniq + 3) / 4;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(segment_scatter_add_kernel, dim3((unsigned)g), dim3(256), 0,
-                     (hipStream_t)stream, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows);
+  if (!ws || ws_bytes < mirec_segment_scatter_add_workspace_size(n, d)) {
+    set_error("mirec_segment_scatter_add_f32: workspace too small");
+    return -1;
+  }
+  const int chunks = (int)((n + kScatChunk - 1) / kScatChunk);
+  float* head = (float*)ws;
+  float* tail = head + (int64_t)chunks * d;
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_SCAT(GG, DM)                                                                    \
+  {                                                                                          \
+    const int64_t groups_per_block = 4 * (64 / GG);                                          \
+    hipLaunchKernelGGL((scatter_chunks_kernel<GG, DM>),                                       \
+                       dim3((unsigned)((chunks + groups_per_block - 1) / groups_per_block)),  \
+                       dim3(256), 0, st, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows, \
+                       head, tail, chunks);                                                   \
+  }
+  if (d <= 4) MIREC_SCAT(4, 4)
+  else if (d <= 16) MIREC_SCAT(16, 16)
+  else if (d <= 32) MIREC_SCAT(32, 32)
+  else if (d <= 64) MIREC_SCAT(64, 64)
+  else MIREC_SCAT(64, 256)
+#undef MIREC_SCAT
+  if (chunks > 1)
+    hipLaunchKernelGGL(scatter_fixup_kernel, dim3((unsigned)((chunks - 1 + 3) / 4)), dim3(256),
+                       0, st, d, uniq, seg, n_uniq_dev, dense, n_rows, head, tail, chunks);
   return launch_status("mirec_segment_scatter_add_f32");
 }
 

@@ -234,12 +234,30 @@ def uniq_ahead_diff(uniq, n_uniq, stride: int, n_batches: int, out, n_out):
     check(rc, "mirec_uniq_ahead_diff")
 
 
+_SCATTER_WS = {}
+
+
+def _scatter_ws(device, nbytes):
+    """Per-device scratch of the chunked scatter (stream-ordered reuse: every
+    launch on the stream finishes with it before the next one starts)."""
+    key = str(device)
+    buf = _SCATTER_WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+        _SCATTER_WS[key] = buf
+    return buf
+
+
 def segment_scatter_add(rows: torch.Tensor, segs: Segments, dense: torch.Tensor) -> torch.Tensor:
     _dev(rows, torch.float32, "rows")
     _dev(dense, torch.float32, "dense")
-    rc = lib().mirec_segment_scatter_add_f32(ptr(rows), rows.shape[1], ptr(segs.perm),
-                                             ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq),
-                                             segs.n, ptr(dense), dense.shape[0], stream_handle())
+    d = rows.shape[1]
+    wsz = lib().mirec_segment_scatter_add_workspace_size(segs.n, d)
+    ws = _scatter_ws(rows.device, wsz)
+    rc = lib().mirec_segment_scatter_add_f32(ptr(rows), d, ptr(segs.perm), ptr(segs.uniq),
+                                             ptr(segs.seg), ptr(segs.n_uniq), segs.n, ptr(dense),
+                                             dense.shape[0], ptr(ws), ws.numel(),
+                                             stream_handle())
     check(rc, "mirec_segment_scatter_add_f32")
     return dense
 

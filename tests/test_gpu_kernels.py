@@ -586,3 +586,30 @@ def test_score_matrix(dev, nq, I, d):
     got = ops.score_matrix(torch.as_tensor(U, device=dev), torch.as_tensor(E, device=dev)).cpu()
     exp = torch.as_tensor(U.astype(np.float64) @ E.astype(np.float64).T).float()
     torch.testing.assert_close(got, exp, rtol=RTOL, atol=1e-4)
+
+
+@pytest.mark.parametrize('n,key_space,d', [(9000, 50, 16), (206_000, 3_000_001, 128),
+                                           (53_248, 33_000_026, 1), (100_000, 7, 64),
+                                           (30_000, 1 << 24, 10)])
+def test_large_segment_sort_and_hot_row_scatter(dev, n, key_space, d):
+    """Device-wide radix path of K2 (n > 8,192) and the chunked scatter: stable
+    grouping identical to numpy's stable argsort; dense sums vs index_add with
+    Zipf-hot rows (one row owns a large share of the contributions)."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(n)
+    keys = np.minimum(rng.zipf(1.1, n), key_space) - 1
+    keys = keys.astype(np.int64)
+    segs = ops.segment_sort(torch.as_tensor(keys, device=dev), key_space)
+    nu = int(segs.n_uniq.item())
+    order = np.argsort(keys, kind='stable')
+    u, first = np.unique(keys[order], return_index=True)
+    assert nu == len(u)
+    assert np.array_equal(segs.perm[:n].cpu().numpy(), order)
+    assert np.array_equal(segs.uniq[:nu].cpu().numpy(), u)
+    assert np.array_equal(segs.seg[:nu + 1].cpu().numpy(), np.r_[first, n])
+    rows = torch.randn(n, d, generator=torch.Generator().manual_seed(1))
+    n_rows = int(keys.max()) + 1
+    exp = torch.zeros(n_rows, d, dtype=torch.float64).index_add_(
+        0, torch.as_tensor(keys), rows.double())
+    got = ops.segment_scatter_add(rows.to(dev), segs, torch.zeros(n_rows, d, device=dev))
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-4, atol=2e-3)

@@ -1,0 +1,360 @@
+"""Per-configuration measurements of the model rows of SURVEY.md §8 beyond the
+C2 headline (bench.py): one JSON line per configuration, 1 GPU.
+
+  C3  SASRec, Amazon-Books shape: I = 3,000,000 (+PAD), L = 50, d = 128, 2 layers,
+      2 heads, inner 256, 100 uniform negatives per sequence from the device walk
+      (RepeatableSampler, K4), sampled-softmax loss (K9b), dense Adam over every
+      parameter (the reference's optim.Adam on nn.Embedding(sparse=False)).
+      Unit: sequences/s; dominant-kernel rooflines from HIP events.
+  C4  DeepFM, Criteo shape: 13 float + 26 token fields, vocabularies summing to
+      33,000,000 (10M, 8M, 5M, 4M, 3M, then geometric down to 3), Zipf(1.1) ids,
+      d = 16, MLP 624-128-128-128-1 (dropout 0.2), BCE, B = 2,048, dense Adam.
+      Unit: samples/s.
+  C5  LightGCN, 10M users x 5M items, 100M edges (Zipf items, Zipf-like user
+      degrees), d = 256, 2 layers: propagation (K7) once, then full-sort top-10
+      (K6) of a bounded sample of users against all 5M items. Unit: users/s.
+
+Synthetic data (seeded numpy PCG64 / torch generators), random init. Each step is
+the Trainer's generic step: zero_grad -> calculate_loss -> backward -> FusedAdam.
+Usage: python tools/bench_models.py [--configs C3,C4,C5] [--steps K] [--warmup W]
+       [--scale S] (S < 1 shrinks the tables / graph for a quick run).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3   # fp32 MFMA / vector peak
+
+
+class StubDataset:
+    """The dataset surface a model constructor reads (fields / field2type / num)."""
+
+    def __init__(self, types, nums, uid=None, iid=None):
+        self.field2type = dict(types)
+        self._num = dict(nums)
+        self.uid_field, self.iid_field = uid, iid
+
+    def fields(self, ftype=None, source=None):
+        return [f for f in self.field2type if ftype is None or self.field2type[f] in ftype]
+
+    def num(self, field):
+        return self._num[field]
+
+
+def _timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _event_time(fn, reps=10):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e-3)
+    return float(np.median(ts))
+
+
+def _zipf_ids(rng, a, n, vmax):
+    """Zipf(a) ranks clipped to [1, vmax] (id 0 is [PAD])."""
+    return np.minimum(rng.zipf(a, n), vmax).astype(np.int64)
+
+
+# ----------------------------------------------------------------------------- C4
+def c4_vocab(total=33_000_000):
+    big = [10_000_000, 8_000_000, 5_000_000, 4_000_000, 3_000_000]
+    rest = total - sum(big)
+    r = 0.55
+    w = r ** np.arange(21)
+    sizes = np.maximum(np.round(w / w.sum() * rest).astype(np.int64), 3)
+    sizes[0] += rest - sizes.sum()
+    return big + sizes.tolist()
+
+
+def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
+    from recbole_amd.config import Config
+    from recbole_amd.model.context_aware_recommender import DeepFM
+    from recbole_amd.model.context import _CtxFMFn
+    from recbole_amd.trainer.optim import FusedAdam
+    from recbole_amd.data.interaction import Interaction
+    from recbole_amd.utils import FeatureType
+    vocab = [max(3, int(v * scale)) for v in c4_vocab()]
+    types = {'label': FeatureType.FLOAT}
+    nums = {'label': 1}
+    for j in range(13):
+        types[f'I{j}'], nums[f'I{j}'] = FeatureType.FLOAT, 1
+    for j, v in enumerate(vocab):
+        types[f'C{j}'], nums[f'C{j}'] = FeatureType.TOKEN, v + 1      # + [PAD]
+    config = Config(model='DeepFM', dataset='criteo-synth', config_dict={
+        'embedding_size': d, 'load_col': None, 'state': 'ERROR', 'data_path': ROOT})
+    config['device'] = dev
+    torch.manual_seed(2020)
+    model = DeepFM(config, StubDataset(types, nums)).to(dev)
+    rng = np.random.default_rng(2020)
+    batches = []
+    for _ in range(n_batches):
+        cols = {'label': torch.as_tensor((rng.random(B) < 0.256).astype(np.float32))}
+        for j in range(13):
+            x = rng.lognormal(0.0, 2.0, B)
+            cols[f'I{j}'] = torch.as_tensor(((x - x.min()) / (x.max() - x.min())).astype(
+                np.float32))
+        for j, v in enumerate(vocab):
+            cols[f'C{j}'] = torch.as_tensor(_zipf_ids(rng, 1.1, B, v))
+        batches.append(Interaction(cols).to(dev))
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    it = [0]
+
+    def step():
+        b = batches[it[0] % n_batches]
+        it[0] += 1
+        opt.zero_grad()
+        loss = model.calculate_loss(b)
+        loss.backward()
+        opt.step()
+
+    t = _timed(step, steps, warmup)
+    V = sum(nums[f'C{j}'] for j in range(26))
+    # dominant kernel: dense Adam over the [V, 16] token table (K5, HBM-bound):
+    # algorithmic bytes per step = p, m, v, g read + p, m, v written = 7 * V * d * 4
+    T = model.token_embedding_table.embedding.weight
+    st = opt._ensure_state(T)
+    g = torch.zeros_like(T)
+    from recbole_amd import ops
+    consts, idx = opt.prepare_window(1, dev)
+    ta = _event_time(lambda: ops.adam_step(T.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
+                                           dense_grad=g))
+    adam_bytes = 7 * T.numel() * 4
+    # K8 forward on one batch: rows read (26 token rows of d floats + 26 first-order
+    # weights + 26 ids + 13 floats) + concat written (39 * d) + y_fm
+    b0 = batches[0]
+    Tw, T1, Ef, Ef1, bias, seq, seq1 = model._fm_params()
+    tk = _event_time(lambda: _CtxFMFn.apply(model.field_layout, b0, Tw, T1, Ef, Ef1, bias))
+    k8_bytes = B * (26 * (d * 4 + 4 + 8) + 13 * 4 + 39 * d * 4 + 4)
+    return {
+        'config': 'C4', 'metric': 'train samples/s', 'value': round(B / t, 1),
+        'unit': 'samples/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
+        'workload': f'DeepFM Criteo-shape: 13 float + 26 token fields, vocab {V:,} '
+                    f'(incl. PADs), d={d}, MLP 624-128-128-128-1, dropout 0.2, BCE, dense Adam',
+        'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) ids, log-normal floats, seeded)',
+        'roofline': {'kernel': 'K5 dense Adam over the [V,16] token table (adam_multi_kernel<16>)',
+                     'bound': 'hbm', 'achieved': round(adam_bytes / ta / 1e9, 1),
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(adam_bytes / ta / 1e9 / HBM_PEAK_GBS, 4),
+                     'bytes_per_launch': adam_bytes, 'launch_us': round(ta * 1e6, 1)},
+        'k8_fwd': {'kernel': 'K8 ctx_fm_fwd (field gather + first order + FM)',
+                   'bound': 'hbm', 'achieved': round(k8_bytes / tk / 1e9, 1),
+                   'unit': 'GB/s', 'bytes_per_launch': k8_bytes,
+                   'launch_us_incl_host': round(tk * 1e6, 1)},
+    }
+
+
+# ----------------------------------------------------------------------------- C3
+def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_batches=8):
+    from recbole_amd import ops
+    from recbole_amd.config import Config
+    from recbole_amd.data.interaction import Interaction
+    from recbole_amd.model.sequential_recommender import SASRec
+    from recbole_amd.trainer.optim import FusedAdam
+    from recbole_amd.utils import FeatureType
+    n_items = max(1000, int(3_000_000 * scale)) + 1
+    config = Config(model='SASRec', dataset='books-synth', config_dict={
+        'hidden_size': d, 'inner_size': 256, 'n_layers': 2, 'n_heads': 2,
+        'MAX_ITEM_LIST_LENGTH': L, 'loss_type': 'SSM', 'training_neg_sample_num': n_neg,
+        'state': 'ERROR', 'data_path': ROOT})
+    config['device'] = dev
+    torch.manual_seed(2020)
+    model = SASRec(config, StubDataset({'item_id': FeatureType.TOKEN},
+                                       {'item_id': n_items})).to(dev)
+    rng = np.random.default_rng(2020)
+    batches = []
+    for _ in range(n_batches):
+        lens = np.minimum(rng.poisson(20, B) + 4, L).astype(np.int64)
+        seq = np.zeros((B, L), dtype=np.int64)
+        ids = _zipf_ids(rng, 1.1, int(lens.sum()), n_items - 1)
+        mask = np.arange(L)[None, :] < lens[:, None]
+        seq[mask] = ids
+        batches.append(Interaction({
+            'item_id_list': torch.as_tensor(seq), 'item_length': torch.as_tensor(lens),
+            'item_id': torch.as_tensor(_zipf_ids(rng, 1.1, B, n_items - 1)),
+            'user_id': torch.as_tensor(rng.integers(1, 1_000_000, B))}).to(dev))
+    random_list = torch.as_tensor(rng.permutation(np.arange(1, n_items)).astype(np.int32),
+                                  device=dev)
+    pr = torch.zeros(1, dtype=torch.int64, device=dev)
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    it = [0]
+
+    def step():
+        b = batches[it[0] % n_batches]
+        it[0] += 1
+        neg = ops.sample_walk(random_list, pr, b['user_id'], n_neg, None, None, 1_000_000, False)
+        b.interaction['neg_item_id'] = neg
+        opt.zero_grad()
+        loss = model.calculate_loss(b)
+        loss.backward()
+        opt.step()
+
+    t = _timed(step, steps, warmup)
+    from recbole_amd.model.sequential_recommender.sasrec import _SampledSoftmaxFn
+    b0 = batches[0]
+    S = torch.randn(B, d, device=dev)
+    W = model.item_embedding.weight
+    neg = ops.sample_walk(random_list, pr, b0['user_id'], n_neg, None, None, 1_000_000, False)
+    tk = _event_time(lambda: _SampledSoftmaxFn.apply(S, W, b0['item_id'], neg))
+    k9_bytes = B * (1 + n_neg) * (d * 4 + 8 + d * 4) + B * d * 4 * 2
+    st = opt._ensure_state(W)
+    g = torch.zeros_like(W)
+    consts, idx = opt.prepare_window(1, dev)
+    ta = _event_time(lambda: ops.adam_step(W.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
+                                           dense_grad=g))
+    adam_bytes = 7 * W.numel() * 4
+    flops = 86.3e6 * B    # transformer fwd+bwd per sequence
+    return {
+        'config': 'C3', 'metric': 'train sequences/s', 'value': round(B / t, 1),
+        'unit': 'sequences/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
+        'workload': f'SASRec Amazon-Books-shape: {n_items:,} items (incl. PAD), L={L}, d={d}, '
+                    f'2 layers x 2 heads, inner 256, sampled softmax over {n_neg} walk '
+                    f'negatives, dense Adam',
+        'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) items, Poisson(20)+4 lengths, seeded)',
+        'transformer_tflops_at_step_rate': round(flops / t / 1e12, 2),
+        'roofline': {'kernel': 'K5 dense Adam over the [I,128] item table (adam_multi_kernel<128>)',
+                     'bound': 'hbm', 'achieved': round(adam_bytes / ta / 1e9, 1),
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(adam_bytes / ta / 1e9 / HBM_PEAK_GBS, 4),
+                     'bytes_per_launch': adam_bytes, 'launch_us': round(ta * 1e6, 1)},
+        'k9b': {'kernel': f'K9b sampled_softmax<{d}> ({n_neg} negatives)', 'bound': 'hbm',
+                'achieved': round(k9_bytes / tk / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': k9_bytes,
+                'launch_us_incl_host': round(tk * 1e6, 1)},
+    }
+
+
+# ----------------------------------------------------------------------------- C5
+def make_c5_graph(n_users, n_items, nnz, seed=2020):
+    """Distinct (user, item) edges: user degrees Zipf-like (min 1), items Zipf(1.0)."""
+    rng = np.random.default_rng(seed)
+    w = 1.0 / np.arange(1, n_users + 1) ** 0.6
+    deg = np.maximum(1, np.round(w / w.sum() * nnz)).astype(np.int64)
+    deg = np.minimum(deg, n_items // 2)
+    u = np.repeat(rng.permutation(np.arange(1, n_users + 1)), deg[rng.permutation(n_users)])
+    p = 1.0 / np.arange(1, n_items + 1)
+    cdf = np.cumsum(p / p.sum())
+    i = np.searchsorted(cdf, rng.random(len(u))).astype(np.int64) + 1
+    i = np.minimum(i, n_items)
+    key = np.unique(u * (n_items + 1) + i)
+    return key // (n_items + 1), key % (n_items + 1)
+
+
+def bench_c5(dev, scale=1.0, d=256, n_layers=2, K=10, sample_users=131072):
+    from recbole_amd import ops
+    from recbole_amd.model.general_recommender.lightgcn import norm_adj_csr, propagate
+    U = int(10_000_000 * scale) + 1
+    I = int(5_000_000 * scale) + 1
+    t0 = time.perf_counter()
+    u, i = make_c5_graph(U - 1, I - 1, int(100_000_000 * scale))
+    print(f'C5: {len(u):,} edges generated ({time.perf_counter() - t0:.0f} s)', file=sys.stderr,
+          flush=True)
+    rp, cols, vals = norm_adj_csr(u, i, U, I)
+    print(f'C5: normalised adjacency built ({time.perf_counter() - t0:.0f} s)', file=sys.stderr,
+          flush=True)
+    plan = ops.SpmmPlan(rp, cols, vals, device=dev)
+    setup = time.perf_counter() - t0
+    g = torch.Generator(device=dev).manual_seed(2020)
+    EU = torch.randn(U, d, generator=g, device=dev) * 0.01
+    EI = torch.randn(I, d, generator=g, device=dev) * 0.01
+    out_u, out_i = torch.empty_like(EU), torch.empty_like(EI)
+    tmp = [torch.empty(U + I, d, device=dev)]
+    propagate(plan, EU, EI, n_layers, out_u, out_i, tmp)      # warm-up
+    torch.cuda.synchronize()
+    tp = _event_time(lambda: propagate(plan, EU, EI, n_layers, out_u, out_i, tmp), reps=3)
+    # K7 algorithmic bytes per layer: per nonzero col+val (8 B) + the gathered row
+    # (d*4 B); per row the output write (d*4) and the accumulator read/write
+    nnz2 = int(rp[-1])
+    per_layer = nnz2 * (8 + d * 4) + (U + I) * (d * 4 * 3) + (U + I + 1) * 8
+    # full-sort sample: users 1..n, history = their training edges, 1 positive each
+    n = min(sample_users, U - 1)
+    users = torch.arange(1, n + 1, device=dev)
+    up = rp[:U + 1]
+    hist_ptr = torch.as_tensor((up[1:n + 2] - up[1]).astype(np.int64), device=dev)
+    hist_cols = torch.as_tensor((cols[up[1]:up[n + 1]].astype(np.int64) - U).astype(np.int32),
+                                device=dev)
+    rng = np.random.default_rng(7)
+    pos_cols = torch.as_tensor(rng.integers(1, I, n).astype(np.int32), device=dev)
+    pos_ptr = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    Uq = ops.gather_rows(out_u, users)
+    o = {}
+    run = lambda: ops.fullsort_topk(Uq, out_i, K, hist_ptr=hist_ptr, hist_cols=hist_cols,
+                                    pos_ptr=pos_ptr, pos_cols=pos_cols, out=o)
+    run()
+    torch.cuda.synchronize()
+    tf = _event_time(run, reps=3)
+    flops = 2.0 * n * I * d
+    return {
+        'config': 'C5', 'metric': 'full-sort eval users/s', 'value': round(n / tf, 1),
+        'unit': 'users/s', 'users_timed': n,
+        'workload': f'LightGCN {U - 1:,} users x {I - 1:,} items, {len(u):,} edges, d={d}, '
+                    f'{n_layers} layers; full-sort top-{K} vs all items with history mask',
+        'dtype': 'fp32', 'data': 'synthetic (Zipf items, Zipf-like user degrees, seeded)',
+        'setup_s': round(setup, 1),
+        'roofline': {'kernel': f'K6 fullsort_topk<{d}> (fp32 MFMA 32x32x2)', 'bound': 'mfma',
+                     'achieved': round(flops / tf / 1e12, 2), 'peak': FP32_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': round(flops / tf / 1e12 / FP32_PEAK_TFLOPS, 4),
+                     'flops_per_launch': flops, 'launch_ms': round(tf * 1e3, 2)},
+        'propagation': {'kernel': f'K7 spmm_units_kernel<{d}> x {n_layers} layers',
+                        'bound': 'hbm', 'ms': round(tp * 1e3, 2),
+                        'achieved': round(n_layers * per_layer / tp / 1e9, 1),
+                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': round(n_layers * per_layer / tp / 1e9 / HBM_PEAK_GBS, 4),
+                        'bytes_per_layer': per_layer, 'nnz': nnz2},
+        'full_pass_s_estimate': round((U - 1) / (n / tf) + tp, 1),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--configs', default='C3,C4,C5')
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--scale', type=float, default=1.0)
+    ap.add_argument('--out', default=None)
+    args = ap.parse_args()
+    dev = torch.device('cuda', 0)
+    res = []
+    for c in args.configs.split(','):
+        if c == 'C3':
+            r = bench_c3(dev, args.steps, args.warmup, args.scale)
+        elif c == 'C4':
+            r = bench_c4(dev, args.steps, args.warmup, args.scale)
+        elif c == 'C5':
+            r = bench_c5(dev, args.scale)
+        else:
+            raise SystemExit(f'unknown config {c}')
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        torch.cuda.empty_cache()
+    if args.out:
+        with open(args.out, 'w') as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()
