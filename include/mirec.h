@@ -156,7 +156,7 @@ int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t st
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of
  * contributions (seg[n_uniq] <= n). The sorted contributions are summed in chunks
- * of 32 positions in a fixed order (hot rows are split over many lane groups and
+ * of 128 positions in a fixed order (hot rows are split over many lane groups and
  * their partials added in chunk order by a fixup pass): deterministic, no atomics.
  * Workspace: mirec_segment_scatter_add_workspace_size(n, d). 1 <= d <= 256. */
 size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d);
@@ -164,6 +164,12 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
                                   const int32_t* uniq, const int32_t* seg,
                                   const int32_t* n_uniq_dev, int64_t n, float* dense,
                                   int64_t n_rows, void* ws, size_t ws_bytes, void* stream);
+/* Compact form: out[u, :] = sum of segment u's contributions (u < n_uniq), the same
+ * chunked fixed-order summation; out needs n rows. Lets K5 take each touched row's
+ * gradient as one row (hot Zipf rows would otherwise be summed serially in K5). */
+int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,
+                             const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq_dev,
+                             int64_t n, float* out, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K5  Dense Adam over every row, with the gradient supplied in compact form.
@@ -234,6 +240,7 @@ int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32
  * gradient; last[r] = s + 1. Look-ahead: rows in ahead_uniq (the rows the
  * next batch's forward pass reads) and not in uniq replay steps last[r]..s with
  * a zero gradient; last[r] = s + 1 — so the next forward reads complete rows.
+ * A row with last[r] > s (already complete through s) is left unchanged.
  * n_max_uniq[q] (host array) bounds table q's n_uniq and ahead count (grid
  * size). dense_grad must be NULL. Rows never touched lag until
  * mirec_adam_flush_f32. */

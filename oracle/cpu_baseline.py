@@ -65,3 +65,83 @@ def time_bpr_steps(users, items, used_ptr, used_cols, random_list, n_users, n_it
         one(b)
     dt = time.perf_counter() - t0
     return steps * B / dt, dt, torch.get_num_threads()
+
+
+class _EmptySets(object):
+    def __getitem__(self, k):
+        return set()
+
+
+def _cpu_batch(inter):
+    return {k: v.cpu() for k, v in inter.interaction.items()}
+
+
+def time_deepfm_steps(batches, tok, tok_dims, flt, d, hidden, steps=3, warmup=1, lr=1e-3,
+                      threads=None, dropout=0.2):
+    """C4: DeepFM.calculate_loss + backward + optim.Adam on torch CPU (dense
+    gradients of every table, as the reference). Returns (samples/s, s, threads)."""
+    if threads:
+        torch.set_num_threads(threads)
+    model = cpu_ref.DeepFMCPU(tok, tok_dims, [], [], flt, d, hidden, dropout)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]
+
+    def one(b):
+        opt.zero_grad()
+        loss = model.calculate_loss(b, b['label'])
+        loss.item()
+        loss.backward()
+        opt.step()
+
+    for b in cb[:warmup]:
+        one(b)
+    t0 = time.perf_counter()
+    for b in cb[warmup:warmup + steps]:
+        one(b)
+    dt = time.perf_counter() - t0
+    B = len(cb[0]['label'])
+    return steps * B / dt, dt, torch.get_num_threads()
+
+
+def time_sasrec_steps(batches, random_list, n_items, L, d, n_neg, steps=3, warmup=1, lr=1e-3,
+                      threads=None):
+    """C3: RepeatableSampler walk (numpy restatement, no rejection) + SASRec forward
+    + sampled softmax + backward + optim.Adam on torch CPU. Returns (seq/s, s, threads)."""
+    if threads:
+        torch.set_num_threads(threads)
+    model = cpu_ref.SASRecCPU(n_items, L, d, 2, 2, 256, 1e-12)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    walk = cpu_ref.NumpyWalk(random_list, _EmptySets())     # RepeatableSampler: no rejection
+    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]
+
+    def one(b):
+        neg = torch.as_tensor(walk.sample_by_key_ids(b['user_id'].numpy(), n_neg))
+        opt.zero_grad()
+        loss = model.calculate_loss(b['item_id_list'], b['item_length'], b['item_id'], neg,
+                                    'SSM')
+        loss.item()
+        loss.backward()
+        opt.step()
+
+    for b in cb[:warmup]:
+        one(b)
+    t0 = time.perf_counter()
+    for b in cb[warmup:warmup + steps]:
+        one(b)
+    dt = time.perf_counter() - t0
+    return steps * len(cb[0]['item_id']) / dt, dt, torch.get_num_threads()
+
+
+def time_full_sort_users(user_e, item_e, n_users, K=10, batch=256, threads=None):
+    """C5 scorer as the reference runs it on the CPU (trainer.py:328-353 +
+    evaluators.py:53-76): scores = U[u] @ I^T, pad column -inf, topk, for
+    n_users users in batches. Returns (users/s, s, threads)."""
+    if threads:
+        torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    for s in range(0, n_users, batch):
+        sc = torch.matmul(user_e[s:s + batch], item_e.T)
+        sc[:, 0] = -np.inf
+        torch.topk(torch.flip(sc, dims=[-1]), K, dim=-1)
+    dt = time.perf_counter() - t0
+    return n_users / dt, dt, torch.get_num_threads()

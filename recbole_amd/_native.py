@@ -70,6 +70,8 @@ SIGNATURES = {
     "mirec_segment_sort_batched": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
+    "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,
+                                         _P]),
     "mirec_segment_scatter_add_workspace_size": (c_size_t, [c_int64, c_int32]),
     "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
                                               c_int64, _P, c_size_t, _P]),

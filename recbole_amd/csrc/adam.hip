@@ -368,11 +368,14 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     v = reinterpret_cast<const float2*>(T.v)[off];
     if (!ahead) g = grouped_grad<float2>(T, u, VPR, c);
   }
-  // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop)
+  // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop);
+  // a row already complete through st (last > st: a repeated look-ahead of the
+  // same step) is left as it is
   adam_replay(p, m, v, last, st, consts, k);
-  adam_vec(p, m, v, g, step_consts(consts, st), k);
+  const bool fresh = last <= st;
+  if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
   __syncthreads();
-  if (!valid) return;
+  if (!valid || !fresh) return;
   const int64_t off = row * VPR + c;
   reinterpret_cast<float2*>(T.p)[off] = p;
   reinterpret_cast<float2*>(T.m)[off] = m;

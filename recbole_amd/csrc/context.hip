@@ -162,15 +162,28 @@ __global__ __launch_bounds__(256) void sigmoid_bce_kernel(const float* __restric
   }
 }
 
-// out[j] = sum_i x[i*m + j] for i = 0..n-1 in order (column sums; float-field
-// and bias gradients). One thread per column, fixed order.
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int64_t n,
-                                                     int64_t m, float* __restrict__ out) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
+// out[j] = sum_i x[i*m + j] (column sums; float-field, bias, position and
+// LayerNorm gradients). One 1024-thread block per tile of CB columns: thread
+// (c, r) sums rows r, r + RG, ... (RG = 1024 / CB row groups, coalesced across c),
+// then the RG partials of a column are added in r order. Fixed order,
+// independent of timing.
+template <int CB>
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ x, int64_t n,
+                                                      int64_t m, float* __restrict__ out) {
+  constexpr int RG = 1024 / CB;
+  __shared__ float part[RG][CB + 1];
+  const int c = threadIdx.x % CB, r = threadIdx.x / CB;
+  const int64_t j = (int64_t)blockIdx.x * CB + c;
   float s = 0.f;
-  for (int64_t i = 0; i < n; ++i) s += x[i * m + j];
-  out[j] = s;
+  if (j < m)
+    for (int64_t i = r; i < n; i += RG) s += x[i * m + j];
+  part[r][c] = s;
+  __syncthreads();
+  if (r == 0 && j < m) {
+    float t = 0.f;
+    for (int q = 0; q < RG; ++q) t += part[q][c];
+    out[j] = t;
+  }
 }
 
 static unsigned ctx_grid(int64_t B, int lps) {
@@ -242,7 +255,14 @@ extern "C" int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out
     set_error("mirec_colsum_f32: bad arguments");
     return -1;
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, n, m, out);
+  hipStream_t st = (hipStream_t)stream;
+  if (m >= 64)
+    hipLaunchKernelGGL(colsum_kernel<64>, dim3((unsigned)((m + 63) / 64)), dim3(1024), 0, st, x,
+                       n, m, out);
+  else if (m >= 8)
+    hipLaunchKernelGGL(colsum_kernel<8>, dim3((unsigned)((m + 7) / 8)), dim3(1024), 0, st, x, n,
+                       m, out);
+  else
+    hipLaunchKernelGGL(colsum_kernel<1>, dim3((unsigned)m), dim3(1024), 0, st, x, n, m, out);
   return launch_status("mirec_colsum_f32");
 }

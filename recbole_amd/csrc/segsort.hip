@@ -397,7 +397,7 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
 // boundaries leaves a tail partial in its first chunk and head partials in the
 // following ones, which the fixup kernel (one owner per segment: the boundary
 // it first crosses) adds in chunk order. Deterministic, no float atomics.
-constexpr int kScatChunk = 32;
+constexpr int kScatChunk = 128;
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ seg, int nu, int p) {
   int lo = 0, hi = nu - 1;   // largest u with seg[u] <= p
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
     const float* __restrict__ rows, int d, const int32_t* __restrict__ perm,
     const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ n_uniq_dev, float* __restrict__ dense, int64_t n_rows,
-    float* __restrict__ head, float* __restrict__ tail, int n_chunks) {
+    float* __restrict__ head, float* __restrict__ tail, int n_chunks, int compact) {
   const int nu = n_uniq_dev[0];
   const int n = seg[nu];
   const int lane = threadIdx.x & 63;
@@ -424,59 +424,76 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
   if (p0 >= n) return;
   const int p1 = min(n, p0 + kScatChunk);
   constexpr int MAXC = DMAX / G;    // columns per lane, d <= DMAX
-  float acc[MAXC];
   int u = seg_of(seg, nu, p0);
-  int s0 = seg[u], e = seg[u + 1];
+  int p = p0;
+  while (p < p1) {
+    const int s0 = seg[u], e = seg[u + 1];
+    const int q1 = min(e, p1);
+    float acc[MAXC];
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
-  auto flush = [&](void) {
-    const bool started_before = s0 < p0;
-    const bool ends_after = e > p1;
-    float* dst = nullptr;
-    if (!started_before && !ends_after) {
-      const int64_t row = uniq[u];
-      if (row >= 0 && row < n_rows) dst = dense + row * d;
+    for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+    // one run of equal segment: loads issued 4 positions ahead of the adds
+    for (; p + 4 <= q1; p += 4) {
+      int pr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) pr[t] = perm[p + t];
+      float v[4][MAXC];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) {
+          const int col = l + j * G;
+          v[t][j] = col < d ? rows[(int64_t)pr[t] * d + col] : 0.f;
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) acc[j] += v[t][j];
+    }
+    for (; p < q1; ++p) {
+      const float* r = rows + (int64_t)perm[p] * d;
 #pragma unroll
       for (int j = 0; j < MAXC; ++j) {
         const int col = l + j * G;
-        if (dst && col < d) dst[col] += acc[j];
+        if (col < d) acc[j] += r[col];
       }
-      return;
     }
-    dst = (started_before ? head : tail) + (int64_t)c * d;
+    const bool started_before = s0 < p0;
+    const bool ends_after = e > p1;
+    float* dst;
+    if (!started_before && !ends_after) {
+      const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
+      dst = (row >= 0 && row < n_rows) ? dense + row * d : nullptr;
 #pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int col = l + j * G;
-      if (col < d) dst[col] = acc[j];
-    }
-  };
-  for (int p = p0; p < p1; ++p) {
-    if (p == e) {
-      flush();
-      ++u;
-      s0 = e;
-      e = seg[u + 1];
+      for (int j = 0; j < MAXC; ++j) {
+        const int col = l + j * G;
+        if (dst && col < d) {
+          if (compact) dst[col] = acc[j]; else dst[col] += acc[j];
+        }
+      }
+    } else {
+      dst = (started_before ? head : tail) + (int64_t)c * d;
 #pragma unroll
-      for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+      for (int j = 0; j < MAXC; ++j) {
+        const int col = l + j * G;
+        if (col < d) dst[col] = acc[j];
+      }
     }
-    const float* r = rows + (int64_t)perm[p] * d;
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const int col = l + j * G;
-      if (col < d) acc[j] += r[col];
-    }
+    ++u;
   }
-  flush();
 }
 
+// One 256-thread block per boundary; the owner block of a crossing segment
+// sums its partials with KL = 256 / CW lanes per column (k = kl, kl + KL, ...),
+// combined in kl order: deterministic.
 __global__ __launch_bounds__(256) void scatter_fixup_kernel(
     int d, const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ n_uniq_dev, float* __restrict__ dense, int64_t n_rows,
-    const float* __restrict__ head, const float* __restrict__ tail, int n_chunks) {
+    const float* __restrict__ head, const float* __restrict__ tail, int n_chunks, int compact) {
+  __shared__ float red[256];
   const int nu = n_uniq_dev[0];
   const int n = seg[nu];
-  const int lane = threadIdx.x & 63;
-  const int b = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64) + 1;  // boundary
+  const int b = blockIdx.x + 1;   // boundary
   if (b >= n_chunks || nu == 0) return;
   const int q = b * kScatChunk;
   if (q >= n) return;
@@ -484,12 +501,27 @@ __global__ __launch_bounds__(256) void scatter_fixup_kernel(
   const int s0 = seg[u], e = seg[u + 1];
   if (s0 == q || s0 < (b - 1) * kScatChunk) return;   // not crossing, or not the owner
   const int kend = (e - 1) / kScatChunk;
-  const int64_t row = uniq[u];
+  const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
   if (row < 0 || row >= n_rows) return;
-  for (int col = lane; col < d; col += 64) {
-    float s = tail[(int64_t)(b - 1) * d + col];
-    for (int k = b; k <= kend; ++k) s += head[(int64_t)k * d + col];
-    dense[row * d + col] += s;
+  int cw = 1;
+  while (cw < d && cw < 256) cw <<= 1;
+  const int KL = 256 / cw;
+  const int col0 = threadIdx.x % cw, kl = threadIdx.x / cw;
+  for (int cb = 0; cb < d; cb += cw) {
+    const int col = cb + col0;
+    float s = 0.f;
+    if (col < d) {
+      if (kl == 0) s = tail[(int64_t)(b - 1) * d + col];
+      for (int k = b + kl; k <= kend; k += KL) s += head[(int64_t)k * d + col];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (kl == 0 && col < d) {
+      float t = red[col0];
+      for (int z = 1; z < KL; ++z) t += red[z * cw + col0];
+      if (compact) dense[row * d + col] = t; else dense[row * d + col] += t;
+    }
+    __syncthreads();
   }
 }
 
@@ -556,11 +588,9 @@ extern "C" size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d)
   return (size_t)2 * (size_t)chunks * (size_t)(d > 0 ? d : 1) * sizeof(float) + 256;
 }
 
-extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
-                                             const int32_t* uniq, const int32_t* seg,
-                                             const int32_t* n_uniq_dev, int64_t n, float* dense,
-                                             int64_t n_rows, void* ws, size_t ws_bytes,
-                                             void* stream) {
+static int scatter_impl(const float* rows, int32_t d, const int32_t* perm, const int32_t* uniq,
+                        const int32_t* seg, const int32_t* n_uniq_dev, int64_t n, float* dense,
+                        int64_t n_rows, void* ws, size_t ws_bytes, int compact, void* stream) {
   if (n == 0) return 0;
   if (!rows || !perm || !uniq || !seg || !n_uniq_dev || !dense || d <= 0 || d > 256 || n < 0 ||
       n > INT32_MAX) {
@@ -581,7 +611,7 @@ extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const
     hipLaunchKernelGGL((scatter_chunks_kernel<GG, DM>),                                       \
                        dim3((unsigned)((chunks + groups_per_block - 1) / groups_per_block)),  \
                        dim3(256), 0, st, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows, \
-                       head, tail, chunks);                                                   \
+                       head, tail, chunks, compact);                                          \
   }
   if (d <= 4) MIREC_SCAT(4, 4)
   else if (d <= 16) MIREC_SCAT(16, 16)
@@ -590,9 +620,26 @@ extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const
   else MIREC_SCAT(64, 256)
 #undef MIREC_SCAT
   if (chunks > 1)
-    hipLaunchKernelGGL(scatter_fixup_kernel, dim3((unsigned)((chunks - 1 + 3) / 4)), dim3(256),
-                       0, st, d, uniq, seg, n_uniq_dev, dense, n_rows, head, tail, chunks);
+    hipLaunchKernelGGL(scatter_fixup_kernel, dim3((unsigned)(chunks - 1)), dim3(256),
+                       0, st, d, uniq, seg, n_uniq_dev, dense, n_rows, head, tail, chunks,
+                       compact);
   return launch_status("mirec_segment_scatter_add_f32");
+}
+
+extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* perm,
+                                             const int32_t* uniq, const int32_t* seg,
+                                             const int32_t* n_uniq_dev, int64_t n, float* dense,
+                                             int64_t n_rows, void* ws, size_t ws_bytes,
+                                             void* stream) {
+  return scatter_impl(rows, d, perm, uniq, seg, n_uniq_dev, n, dense, n_rows, ws, ws_bytes, 0,
+                      stream);
+}
+
+extern "C" int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,
+                                        const int32_t* uniq, const int32_t* seg,
+                                        const int32_t* n_uniq_dev, int64_t n, float* out,
+                                        void* ws, size_t ws_bytes, void* stream) {
+  return scatter_impl(rows, d, perm, uniq, seg, n_uniq_dev, n, out, n, ws, ws_bytes, 1, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -118,8 +118,16 @@ class _CtxFMFn(torch.autograd.Function):
                       [x.detach() for x in v] if isinstance(v, list) else v)
                   for k, v in tables.items()}
         keys = torch.empty(len(layout.token_names) * B, dtype=torch.int64, device=bias.device)
+        h = getattr(T, '_mirec_deferred', None) if T is not None else None
+        if h is not None:                     # deferred Adam: complete the rows read
+            off = torch.as_tensor(layout.token_offsets, dtype=torch.int64, device=bias.device)
+            keys.view(len(layout.token_names), B).copy_(
+                torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
+                + off.unsqueeze(1))
+            h.catch_up(T, keys)
         concat, y_fm, _ = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
         ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
+        ctx.deferred_T = T if h is not None else None
         ctx.save_for_backward(concat, keys)
         return concat, y_fm
 
@@ -149,7 +157,10 @@ class _CtxFMFn(torch.autograd.Function):
         if nt:
             T = tables['T']
             segs = ops.segment_sort(keys, T.shape[0])
-            dT = ops.segment_scatter_add(grads['T'], segs, torch.zeros_like(T))
+            if ctx.deferred_T is not None:    # compact rows to the deferred optimizer
+                ctx.deferred_T._mirec_deferred.stash(ctx.deferred_T, grads['T'], keys)
+            else:
+                dT = ops.segment_scatter_add(grads['T'], segs, torch.zeros_like(T))
             dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))
         if nf:
             dEf = torch.empty_like(tables['Ef'])

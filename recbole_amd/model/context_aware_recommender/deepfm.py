@@ -52,3 +52,8 @@ class DeepFM(ContextRecommender):
 
     def predict(self, interaction):
         return self.forward(interaction)
+
+    def deferred_tables(self):
+        """Tables the trainer may run on the deferred K5 schedule (only rows a
+        batch reads are touched; the first-order [V, 1] table stays dense)."""
+        return [self.token_embedding_table.embedding.weight] if self.token_field_names else []

@@ -35,6 +35,10 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         d = E.shape[1]
         dev = E.device
         seq = item_seq.contiguous()
+        h = getattr(E, '_mirec_deferred', None)
+        if h is not None:                     # deferred Adam: complete the rows read
+            h.catch_up(E, seq.view(-1))
+        ctx.deferred = h is not None
         out = torch.empty(B, L, d, dtype=torch.float32, device=dev)
         mean = torch.empty(B * L, dtype=torch.float32, device=dev)
         rstd = torch.empty(B * L, dtype=torch.float32, device=dev)
@@ -63,8 +67,12 @@ class _SeqEmbedLNFn(torch.autograd.Function):
                                               ptr(rstd), ptr(g.contiguous()), ptr(dx),
                                               ptr(ditem), ptr(pg), ptr(pb), stream_handle())
         check(rc, "mirec_seq_embed_ln_bwd_f32")
-        dE = ops.segment_scatter_add(ditem, ops.segment_sort(seq.view(-1), E.shape[0]),
-                                     torch.zeros_like(E))
+        if ctx.deferred:
+            E._mirec_deferred.stash(E, ditem, seq.view(-1))
+            dE = None
+        else:
+            dE = ops.segment_scatter_add(ditem, ops.segment_sort(seq.view(-1), E.shape[0]),
+                                         torch.zeros_like(E))
         dP = torch.zeros_like(P)
         check(lib().mirec_colsum_f32(ptr(dx), B, L * d, ptr(dP), stream_handle()),
               "mirec_colsum_f32")
@@ -77,6 +85,23 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         return dE, dP, dgamma, dbeta, None, None
 
 
+def _catch_up(ctx, E, items):
+    h = getattr(E, '_mirec_deferred', None)
+    ctx.deferred_E = E if h is not None else None
+    if h is not None:                         # deferred Adam: complete the rows read
+        h.catch_up(E, items.contiguous())
+
+
+def _item_grad(ctx, gI, items):
+    """Dense item-table gradient, or the compact rows handed to the deferred
+    optimizer (then autograd gets None)."""
+    if ctx.deferred_E is not None:
+        ctx.deferred_E._mirec_deferred.stash(ctx.deferred_E, gI, items)
+        return None
+    return ops.segment_scatter_add(gI, ops.segment_sort(items, ctx.nI),
+                                   torch.zeros((ctx.nI, gI.shape[1]), device=gI.device))
+
+
 class _SeqBPRFn(torch.autograd.Function):
     """BPRLoss(<s_r, E[pos_r]>, <s_r, E[neg_r]>) over R rows (K3 with the
     sequence outputs as the 'user' table, row r = user r)."""
@@ -85,6 +110,7 @@ class _SeqBPRFn(torch.autograd.Function):
     def forward(ctx, S, E, pos, neg):
         R = S.shape[0]
         rows = torch.arange(R, dtype=torch.int64, device=S.device)
+        _catch_up(ctx, E, torch.cat([pos, neg]))
         o = ops.bpr_fwd_bwd(S.detach().contiguous(), E.detach(), rows, pos.contiguous(),
                             neg.contiguous(), times=1, grads=True)
         ctx.save_for_backward(torch.cat([pos, neg]), o['gU'], o['gI'])
@@ -94,9 +120,7 @@ class _SeqBPRFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         items, gS, gI = ctx.saved_tensors
-        dE = ops.segment_scatter_add(gI, ops.segment_sort(items, ctx.nI),
-                                     torch.zeros((ctx.nI, gI.shape[1]), device=gI.device))
-        return gS * g, dE * g, None, None
+        return gS * g, _item_grad(ctx, gI * g, items), None, None
 
 
 class _SampledSoftmaxFn(torch.autograd.Function):
@@ -110,6 +134,7 @@ class _SampledSoftmaxFn(torch.autograd.Function):
         loss = torch.empty(B, dtype=torch.float32, device=dev)
         gS = torch.empty(B, d, dtype=torch.float32, device=dev)
         gI = torch.empty((1 + N) * B, d, dtype=torch.float32, device=dev)
+        _catch_up(ctx, E, torch.cat([pos, neg]))
         scale = float(torch.tensor(1.0) / torch.tensor(float(B)))
         rc = lib().mirec_sampled_softmax_f32(ptr(S.detach().contiguous()), ptr(E.detach()),
                                              E.shape[0], d, ptr(pos.contiguous()),
@@ -123,9 +148,7 @@ class _SampledSoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         items, gS, gI = ctx.saved_tensors
-        dE = ops.segment_scatter_add(gI, ops.segment_sort(items, ctx.nI),
-                                     torch.zeros((ctx.nI, gI.shape[1]), device=gI.device))
-        return gS * g, dE * g, None, None
+        return gS * g, _item_grad(ctx, gI * g, items), None, None
 
 
 class SASRec(SequentialRecommender):
@@ -211,9 +234,20 @@ class SASRec(SequentialRecommender):
                             interaction[self.ITEM_ID])
 
     def full_sort_predict(self, interaction):
+        self._sync_items()
         seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
         return ops.score_matrix(seq_output.detach().contiguous(),
                                 self.item_embedding.weight.detach())
+
+    def deferred_tables(self):
+        """The item table on the deferred K5 schedule when every read of it is a
+        row gather (BPR / SSM losses); CE reads the whole table every step."""
+        return [] if self.loss_type == 'CE' else [self.item_embedding.weight]
+
+    def _sync_items(self):
+        h = getattr(self.item_embedding.weight, '_mirec_deferred', None)
+        if h is not None:
+            h.flush()
 
     # ------------------------------------------------------------------ fused eval hooks
     def fused_query_vectors(self, interaction):
@@ -221,4 +255,5 @@ class SASRec(SequentialRecommender):
         return self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
 
     def fused_item_table(self):
+        self._sync_items()
         return self.item_embedding.weight.detach()

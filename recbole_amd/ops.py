@@ -262,6 +262,26 @@ def segment_scatter_add(rows: torch.Tensor, segs: Segments, dense: torch.Tensor)
     return dense
 
 
+def segment_reduce(rows: torch.Tensor, segs: Segments):
+    """(compact [n, d] with row u = sum of segment u's contributions, identity
+    Segments over it with the same uniq / n_uniq) — each touched table row's
+    gradient as one row for K5."""
+    _dev(rows, torch.float32, "rows")
+    n, d = segs.n, rows.shape[1]
+    out = torch.empty(max(n, 1), d, dtype=torch.float32, device=rows.device)
+    ws = _scatter_ws(rows.device, lib().mirec_segment_scatter_add_workspace_size(n, d))
+    rc = lib().mirec_segment_reduce_f32(ptr(rows), d, ptr(segs.perm), ptr(segs.uniq),
+                                        ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out), ptr(ws),
+                                        ws.numel(), stream_handle())
+    check(rc, "mirec_segment_reduce_f32")
+    ident = Segments.__new__(Segments)
+    ident.n = n
+    ident.perm = torch.arange(max(n, 1), dtype=torch.int32, device=rows.device)
+    ident.seg = torch.arange(max(n, 1) + 1, dtype=torch.int32, device=rows.device)
+    ident.uniq, ident.n_uniq, ident.ws = segs.uniq, segs.n_uniq, segs.ws
+    return out, ident
+
+
 # ---------------------------------------------------------------- K5 Adam
 def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None = None,
               dense_grad=None, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):

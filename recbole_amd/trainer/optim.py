@@ -111,8 +111,13 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        params = [p for p in self._params() if p.grad is not None]
+        deferred = getattr(self, '_deferred', {})
+        params = [p for p in self._params() if p.grad is not None and p not in deferred]
+        for p in deferred:
+            self._deferred_step(p)
         if not params:
+            if deferred:
+                self.n_steps += 1
             return loss
         dev = params[0].device
         consts, idx = self.prepare_window(1, dev)
@@ -126,8 +131,148 @@ class FusedAdam(torch.optim.Optimizer):
     def advance(self, n: int):
         self.n_steps += n
 
+    # ------------------------------------------------------------------ deferred tables
+    # Embedding tables read sparsely through the autograd path (DeepFM's token
+    # table, SASRec's item table) can run the deferred schedule of K5 instead of a
+    # dense update: the model's autograd Functions (a) call catch_up() on the rows
+    # a forward pass reads, which replays their skipped zero-gradient steps, and
+    # (b) stash() the per-contribution gradient rows + their keys instead of
+    # returning a dense gradient. step() then groups the stashed contributions
+    # (K2) and applies the deferred step to the touched rows only; untouched rows
+    # lag and are completed by flush() (window end, epoch end, state_dict()). The
+    # result is bit-identical to the dense Adam the reference runs over every row.
+    def enable_deferred(self, params, window: int = 256):
+        """Run the deferred schedule for these 2-D parameters (width 4..256)."""
+        params = list(params)
+        if not params:
+            return
+        dev = params[0].device
+        if not hasattr(self, '_deferred'):
+            self._deferred = {}
+            self._zero_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._dummy_i32 = torch.zeros(2, dtype=torch.int32, device=dev)
+            self._dummy_f32 = torch.zeros(4, dtype=torch.float32, device=dev)
+        for p in params:
+            if p.dim() != 2 or p.shape[1] not in (4, 16, 32, 64, 128, 256) or not p.is_cuda:
+                continue
+            self._ensure_state(p)
+            self._deferred[p] = {'last': torch.zeros(p.shape[0], dtype=torch.int32,
+                                                     device=p.device),
+                                 'window': window, 't0': None, 'consts': None, 'stash': []}
+            p._mirec_deferred = self
+
+    def _dstate(self, p):
+        ds = self._deferred[p]
+        if ds['t0'] is None:                  # open a window at the current step
+            ds['t0'] = self.n_steps
+            ds['consts'] = torch.as_tensor(
+                self.step_constants(self.n_steps + 1, ds['window']).reshape(-1),
+                device=p.device)
+            ds['last'].zero_()
+        return ds
+
+    def _dtable(self, p, ds, **kw):
+        st = self.state[p]
+        spec = {'p': p.data, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'last': ds['last']}
+        spec.update(kw)
+        return ops.adam_tables([spec])
+
+    def catch_up(self, p, keys):
+        """Make the rows `keys` (int64, any order / duplicates) current before a
+        forward pass reads them; returns their K2 grouping."""
+        segs = ops.segment_sort(keys.contiguous(), p.shape[0])
+        ds = self._dstate(p)
+        r = self.n_steps - ds['t0']
+        if r > 0:
+            class _Z:
+                perm = uniq = seg = self._dummy_i32
+                n_uniq = self._zero_i32
+            tab = self._dtable(p, ds, rows=self._dummy_f32, segs=_Z,
+                               ahead=(segs.uniq, segs.n_uniq))
+            ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, r - 1,
+                           schedule='deferred', n_max_uniq=[keys.numel()],
+                           **self._group_args())
+        return segs
+
+    def stash(self, p, rows, keys):
+        """Per-contribution gradient rows [n, d] for the table rows `keys` [n]."""
+        self._deferred[p]['stash'].append((rows, keys))
+
+    def _flush_table(self, p, ds, target):
+        if ds['t0'] is None or target <= 0:
+            return
+        tab = self._dtable(p, ds)
+        ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, target,
+                       schedule='flush', **self._group_args())
+
+    def flush(self):
+        """Complete every row of every deferred table (after it, p / m / v equal
+        the dense schedule's)."""
+        for p, ds in getattr(self, '_deferred', {}).items():
+            if ds['t0'] is not None:
+                self._flush_table(p, ds, self.n_steps - ds['t0'])
+
+    def _combine_stash(self, p, stash):
+        """One summed gradient row per touched table row. Each source (one autograd
+        Function's contributions) is grouped and reduced on its own, in chunked
+        fixed order; several sources are then added row-wise in source order —
+        the same sums the dense path forms (a dense gradient per Function, added
+        by autograd), so both schedules stay bit-identical."""
+        n_rows = p.shape[0]
+        parts = []
+        for rows, keys in stash:
+            segs = ops.segment_sort(keys.contiguous(), n_rows)
+            parts.append(ops.segment_reduce(rows.contiguous(), segs))
+        if len(parts) == 1:
+            rows, segs = parts[0]
+            return rows, segs, segs.n
+        # second level: key = the table row of each compact row, sentinel n_rows
+        # beyond a source's n_uniq (dropped after the sort: it is the last group)
+        keys, rows = [], []
+        for cr, cs in parts:
+            idx = torch.arange(cs.n, device=p.device)
+            keys.append(torch.where(idx < cs.n_uniq.long(), cs.uniq[:cs.n].long(),
+                                    torch.full_like(idx, n_rows)))
+            rows.append(cr[:cs.n])
+        keys, rows = torch.cat(keys), torch.cat(rows)
+        segs = ops.segment_sort(keys, n_rows + 1)
+        last = segs.uniq.gather(0, (segs.n_uniq.long() - 1).clamp(min=0))
+        segs.n_uniq.sub_((last == n_rows).to(torch.int32))
+        rows, segs = ops.segment_reduce(rows, segs)
+        return rows, segs, segs.n
+
+    def _deferred_step(self, p):
+        ds = self._deferred[p]
+        stash, ds['stash'] = ds['stash'], []
+        if not stash and p.grad is None:      # table not in this step's graph: skipped
+            if ds['t0'] is not None:
+                self._flush_table(p, ds, self.n_steps - ds['t0'])
+                ds['t0'] = None
+            return
+        ds = self._dstate(p)
+        r = self.n_steps - ds['t0']
+        if stash:
+            rows, segs, n_keys = self._combine_stash(p, stash)
+        if p.grad is not None:                # a dense contribution too: stream every row
+            self._flush_table(p, ds, r)
+            st = self.state[p]
+            kw = {'rows': rows.contiguous(), 'segs': segs} if stash else {}
+            ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], ds['consts'],
+                          self._zero_i32 + r, dense_grad=p.grad.contiguous(),
+                          **kw, **self._group_args())
+            ds['last'].fill_(r + 1)
+        else:
+            tab = self._dtable(p, ds, rows=rows.contiguous(), segs=segs)
+            ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, r,
+                           schedule='deferred', n_max_uniq=[n_keys],
+                           **self._group_args())
+        if r + 1 >= ds['window']:             # window full: complete every row
+            self._flush_table(p, ds, r + 1)
+            ds['t0'] = None
+
     # ------------------------------------------------------------------ (de)serialise
     def state_dict(self):
+        self.flush()
         params = self._params()
         state = {}
         for i, p in enumerate(params):
@@ -145,6 +290,9 @@ class FusedAdam(torch.optim.Optimizer):
         return {'state': state, 'param_groups': groups}
 
     def load_state_dict(self, state_dict):
+        for ds in getattr(self, '_deferred', {}).values():
+            ds['t0'] = None                   # loaded rows are complete: new window
+            ds['stash'] = []
         params = self._params()
         for g, sg in zip(self.param_groups, state_dict['param_groups']):
             for key, v in sg.items():

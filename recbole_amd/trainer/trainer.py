@@ -79,6 +79,12 @@ class Trainer(AbstractTrainer):
         self.best_valid_result = None
         self.train_loss_dict = dict()
         self.optimizer = self._build_optimizer(self.model.parameters())
+        if (isinstance(self.optimizer, FusedAdam) and config['adam_mode'] != 'streamed'
+                and hasattr(self.model, 'deferred_tables')):
+            # sparsely read embedding tables on the deferred K5 schedule (optim.py)
+            self.optimizer.enable_deferred(self.model.deferred_tables())
+            # any state_dict() of the model sees complete rows
+            self.model.register_state_dict_pre_hook(lambda *a, **k: self.optimizer.flush())
         self.eval_type = config['eval_type']
         self.evaluator = ProxyEvaluator(config)
         self.item_tensor = None
@@ -154,13 +160,19 @@ class Trainer(AbstractTrainer):
             if self.clip_grad_norm:
                 clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
             self.optimizer.step()
+        self._sync_params()
         return total_loss
 
     def _valid_epoch(self, valid_data, show_progress=False):
         valid_result = self.evaluate(valid_data, load_best_model=False, show_progress=show_progress)
         return calculate_valid_score(valid_result, self.valid_metric), valid_result
 
+    def _sync_params(self):
+        if isinstance(self.optimizer, FusedAdam):
+            self.optimizer.flush()
+
     def _save_checkpoint(self, epoch):
+        self._sync_params()
         state = {
             'config': dict(self.config.final_config_dict) if hasattr(self.config, 'final_config_dict')
             else self.config,
@@ -281,6 +293,7 @@ class Trainer(AbstractTrainer):
             checkpoint = torch.load(checkpoint_file, weights_only=False)
             self.model.load_state_dict(checkpoint['state_dict'])
             self.logger.info(f'Loading model structure and parameters from {checkpoint_file}')
+        self._sync_params()
         self.model.eval()
         topk = self.evaluator.topk_evaluator
         if (eval_data.dl_type == DataLoaderType.FULL and self.config['fused_eval'] is not False

@@ -81,6 +81,8 @@ def test_train_steps_match_oracle(tmp_path):
         lr_.backward()
         opt.step()
         np.testing.assert_allclose(loss.item(), lr_.item(), rtol=1e-4)
+    assert trainer.optimizer._deferred            # the token table ran deferred
+    trainer.optimizer.flush()                     # complete the rows no batch touched last
     refp = dict(ref.named_parameters())
     for name, p in model.named_parameters():
         torch.testing.assert_close(p.detach().cpu(), refp[name].detach(), rtol=1e-3, atol=2e-5,

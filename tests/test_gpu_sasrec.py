@@ -127,6 +127,7 @@ def test_sasrec_train_and_eval(tmp_path):
         lr_.backward()
         opt.step()
         np.testing.assert_allclose(loss.item(), lr_.item(), rtol=1e-4)
+    trainer.optimizer.flush()
     refp = dict(ref.named_parameters())
     for name, p in model.named_parameters():
         torch.testing.assert_close(p.detach().cpu(), refp[name].detach(), rtol=1e-3, atol=2e-5,

@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # fp32 MFMA / vector peak
+CPU_BASELINE = True
 
 
 class StubDataset:
@@ -150,7 +151,19 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
     Tw, T1, Ef, Ef1, bias, seq, seq1 = model._fm_params()
     tk = _event_time(lambda: _CtxFMFn.apply(model.field_layout, b0, Tw, T1, Ef, Ef1, bias))
     k8_bytes = B * (26 * (d * 4 + 4 + 8) + 13 * 4 + 39 * d * 4 + 4)
+    cpu = None
+    if CPU_BASELINE:
+        from oracle import cpu_baseline as cb
+        thr = min(16, os.cpu_count() or 1)
+        sps, dt, used = cb.time_deepfm_steps(batches, [f'C{j}' for j in range(26)],
+                                             [nums[f'C{j}'] for j in range(26)],
+                                             [f'I{j}' for j in range(13)], d, [128, 128, 128],
+                                             steps=3, threads=thr)
+        cpu = {'value': round(sps, 1), 'unit': 'samples/s', 'cores': used, 'kind': 'port',
+               'sample': f'3 C4 steps of the oracle restatement on torch CPU (DeepFMCPU + dense '
+                         f'optim.Adam over every table), {dt:.1f} s'}
     return {
+        'cpu_baseline': cpu,
         'config': 'C4', 'metric': 'train samples/s', 'value': round(B / t, 1),
         'unit': 'samples/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
         'workload': f'DeepFM Criteo-shape: 13 float + 26 token fields, vocab {V:,} '
@@ -228,7 +241,17 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
                                            dense_grad=g))
     adam_bytes = 7 * W.numel() * 4
     flops = 86.3e6 * B    # transformer fwd+bwd per sequence
+    cpu = None
+    if CPU_BASELINE:
+        from oracle import cpu_baseline as cb
+        thr = min(16, os.cpu_count() or 1)
+        sps, dt, used = cb.time_sasrec_steps(batches, random_list.cpu().numpy(), n_items, L, d,
+                                             n_neg, steps=2, threads=thr)
+        cpu = {'value': round(sps, 1), 'unit': 'sequences/s', 'cores': used, 'kind': 'port',
+               'sample': f'2 C3 steps of the oracle restatement on torch CPU (numpy walk, '
+                         f'SASRecCPU + sampled softmax, dense optim.Adam), {dt:.1f} s'}
     return {
+        'cpu_baseline': cpu,
         'config': 'C3', 'metric': 'train sequences/s', 'value': round(B / t, 1),
         'unit': 'sequences/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
         'workload': f'SASRec Amazon-Books-shape: {n_items:,} items (incl. PAD), L={L}, d={d}, '
@@ -308,7 +331,18 @@ def bench_c5(dev, scale=1.0, d=256, n_layers=2, K=10, sample_users=131072):
     torch.cuda.synchronize()
     tf = _event_time(run, reps=3)
     flops = 2.0 * n * I * d
+    cpu = None
+    if CPU_BASELINE:
+        from oracle import cpu_baseline as cb
+        thr = min(16, os.cpu_count() or 1)
+        nc = 512
+        ups, dt, used = cb.time_full_sort_users(Uq[:nc].cpu(), out_i.cpu(), nc, K=K,
+                                                threads=thr)
+        cpu = {'value': round(ups, 1), 'unit': 'users/s', 'cores': used, 'kind': 'port',
+               'sample': f'{nc} users ranked on torch CPU as the reference does (U[u] @ I^T, '
+                         f'pad mask, flip + topk), {dt:.1f} s'}
     return {
+        'cpu_baseline': cpu,
         'config': 'C5', 'metric': 'full-sort eval users/s', 'value': round(n / tf, 1),
         'unit': 'users/s', 'users_timed': n,
         'workload': f'LightGCN {U - 1:,} users x {I - 1:,} items, {len(u):,} edges, d={d}, '
@@ -336,7 +370,10 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--scale', type=float, default=1.0)
     ap.add_argument('--out', default=None)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
+    global CPU_BASELINE
+    CPU_BASELINE = not args.no_cpu_baseline
     dev = torch.device('cuda', 0)
     res = []
     for c in args.configs.split(','):
