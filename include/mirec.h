@@ -156,7 +156,7 @@ int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t st
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of
  * contributions (seg[n_uniq] <= n). The sorted contributions are summed in chunks
- * of 128 positions in a fixed order (hot rows are split over many lane groups and
+ * of 32 (d > 16) or 64 positions in a fixed order (hot rows are split over many lane groups and
  * their partials added in chunk order by a fixup pass): deterministic, no atomics.
  * Workspace: mirec_segment_scatter_add_workspace_size(n, d). 1 <= d <= 256. */
 size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d);

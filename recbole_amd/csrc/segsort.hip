@@ -391,13 +391,16 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
 // ---------------------------------------------------------------------------
 // Chunked segmented scatter-add (hot rows: a Zipf head row may own 10^4..10^5
 // contributions, far too many for one wave to sum serially). The sorted
-// contribution positions are cut into chunks of kScatChunk; a group of G lanes
+// contribution positions are cut into chunks of scat_chunk(d); a group of G lanes
 // per chunk sums runs of equal segment in position order. A segment wholly
 // inside a chunk is added to dense directly; a segment crossing chunk
 // boundaries leaves a tail partial in its first chunk and head partials in the
 // following ones, which the fixup kernel (one owner per segment: the boundary
 // it first crosses) adds in chunk order. Deterministic, no float atomics.
-constexpr int kScatChunk = 128;
+// positions per chunk: short chunks for wide rows (more lane groups in flight),
+// longer ones for narrow rows; the workspace is sized for the smallest
+__host__ __device__ __forceinline__ int scat_chunk(int d) { return d <= 16 ? 64 : 32; }
+constexpr int kScatChunkMin = 32;
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ seg, int nu, int p) {
   int lo = 0, hi = nu - 1;   // largest u with seg[u] <= p
@@ -420,9 +423,10 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
   const int gi = lane / G, l = lane % G;
   const int c = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64) * (64 / G) + gi;
   if (c >= n_chunks || nu == 0) return;
-  const int p0 = c * kScatChunk;
+  const int CH = scat_chunk(d);
+  const int p0 = c * CH;
   if (p0 >= n) return;
-  const int p1 = min(n, p0 + kScatChunk);
+  const int p1 = min(n, p0 + CH);
   constexpr int MAXC = DMAX / G;    // columns per lane, d <= DMAX
   int u = seg_of(seg, nu, p0);
   int p = p0;
@@ -495,12 +499,13 @@ __global__ __launch_bounds__(256) void scatter_fixup_kernel(
   const int n = seg[nu];
   const int b = blockIdx.x + 1;   // boundary
   if (b >= n_chunks || nu == 0) return;
-  const int q = b * kScatChunk;
+  const int CH = scat_chunk(d);
+  const int q = b * CH;
   if (q >= n) return;
   const int u = seg_of(seg, nu, q);
   const int s0 = seg[u], e = seg[u + 1];
-  if (s0 == q || s0 < (b - 1) * kScatChunk) return;   // not crossing, or not the owner
-  const int kend = (e - 1) / kScatChunk;
+  if (s0 == q || s0 < (b - 1) * CH) return;   // not crossing, or not the owner
+  const int kend = (e - 1) / CH;
   const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
   if (row < 0 || row >= n_rows) return;
   int cw = 1;
@@ -584,7 +589,7 @@ extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_sp
 }
 
 extern "C" size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d) {
-  const int64_t chunks = (n + kScatChunk - 1) / kScatChunk;
+  const int64_t chunks = (n + kScatChunkMin - 1) / kScatChunkMin;
   return (size_t)2 * (size_t)chunks * (size_t)(d > 0 ? d : 1) * sizeof(float) + 256;
 }
 
@@ -601,7 +606,7 @@ static int scatter_impl(const float* rows, int32_t d, const int32_t* perm, const
     set_error("mirec_segment_scatter_add_f32: workspace too small");
     return -1;
   }
-  const int chunks = (int)((n + kScatChunk - 1) / kScatChunk);
+  const int chunks = (int)((n + scat_chunk(d) - 1) / scat_chunk(d));
   float* head = (float*)ws;
   float* tail = head + (int64_t)chunks * d;
   hipStream_t st = (hipStream_t)stream;
@@ -613,7 +618,8 @@ static int scatter_impl(const float* rows, int32_t d, const int32_t* perm, const
                        dim3(256), 0, st, rows, d, perm, uniq, seg, n_uniq_dev, dense, n_rows, \
                        head, tail, chunks, compact);                                          \
   }
-  if (d <= 4) MIREC_SCAT(4, 4)
+  if (d == 1) MIREC_SCAT(1, 1)
+  else if (d <= 4) MIREC_SCAT(4, 4)
   else if (d <= 16) MIREC_SCAT(16, 16)
   else if (d <= 32) MIREC_SCAT(32, 32)
   else if (d <= 64) MIREC_SCAT(64, 64)

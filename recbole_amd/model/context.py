@@ -124,7 +124,9 @@ class _CtxFMFn(torch.autograd.Function):
             keys.view(len(layout.token_names), B).copy_(
                 torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
                 + off.unsqueeze(1))
-            h.catch_up(T, keys)
+            ctx.segs = h.catch_up(T, keys)
+        else:
+            ctx.segs = None
         concat, y_fm, _ = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
         ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
         ctx.deferred_T = T if h is not None else None
@@ -156,9 +158,9 @@ class _CtxFMFn(torch.autograd.Function):
         dT = dT1 = dEf = dEf1 = None
         if nt:
             T = tables['T']
-            segs = ops.segment_sort(keys, T.shape[0])
+            segs = ctx.segs if ctx.segs is not None else ops.segment_sort(keys, T.shape[0])
             if ctx.deferred_T is not None:    # compact rows to the deferred optimizer
-                ctx.deferred_T._mirec_deferred.stash(ctx.deferred_T, grads['T'], keys)
+                ctx.deferred_T._mirec_deferred.stash(ctx.deferred_T, grads['T'], keys, segs)
             else:
                 dT = ops.segment_scatter_add(grads['T'], segs, torch.zeros_like(T))
             dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))

@@ -153,6 +153,45 @@ class FMFirstOrderLinear(nn.Module):
         self.bias = nn.Parameter(torch.zeros((output_dim,)), requires_grad=True)
 
 
+class _SplitKLinearFn(torch.autograd.Function):
+    """nn.Linear whose weight gradient dW = dY^T X over K = batch*positions rows is
+    formed as a batched GEMM over C row blocks, then summed: the library picks a
+    32x32-tile kernel for the single [out, K] x [K, in] product, which leaves most
+    CUs idle at K = 10^5 (SASRec on C3); C blocks give C times the tiles."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return nn.functional.linear(x, W, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        n_in, n_out = W.shape[1], W.shape[0]
+        x2 = x.reshape(-1, n_in)
+        g2 = gy.reshape(-1, n_out)
+        K = x2.shape[0]
+        C = 1
+        while K % (2 * C) == 0 and K // (2 * C) >= 2048 and C < 64:
+            C *= 2
+        dx = torch.matmul(gy, W)
+        if C > 1:
+            dW = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2),
+                           x2.view(C, K // C, n_in)).sum(0)
+        else:
+            dW = g2.t().mm(x2)
+        db = g2.sum(0) if ctx.has_b else None
+        return dx, dW, db
+
+
+def linear(module, x):
+    """module(x), with the split-K weight gradient for tall GPU inputs."""
+    if x.is_cuda and x.requires_grad and x.numel() // x.shape[-1] >= 16384:
+        return _SplitKLinearFn.apply(x, module.weight, module.bias)
+    return module(x)
+
+
 class MultiHeadAttention(nn.Module):
     """layers.py:338-407 (same parameters and op sequence; library GEMMs)."""
 
@@ -178,9 +217,9 @@ class MultiHeadAttention(nn.Module):
         return x.permute(0, 2, 1, 3)
 
     def forward(self, input_tensor, attention_mask):
-        q = self.transpose_for_scores(self.query(input_tensor))
-        k = self.transpose_for_scores(self.key(input_tensor))
-        v = self.transpose_for_scores(self.value(input_tensor))
+        q = self.transpose_for_scores(linear(self.query, input_tensor))
+        k = self.transpose_for_scores(linear(self.key, input_tensor))
+        v = self.transpose_for_scores(linear(self.value, input_tensor))
         scores = torch.matmul(q, k.transpose(-1, -2))
         scores = scores / math.sqrt(self.attention_head_size)
         scores = scores + attention_mask
@@ -188,7 +227,7 @@ class MultiHeadAttention(nn.Module):
         probs = self.attn_dropout(probs)
         ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
         ctx = ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
-        hidden = self.out_dropout(self.dense(ctx))
+        hidden = self.out_dropout(linear(self.dense, ctx))
         return self.LayerNorm(hidden + input_tensor)
 
 
@@ -214,7 +253,7 @@ class FeedForward(nn.Module):
         return x * torch.sigmoid(x)
 
     def forward(self, input_tensor):
-        hidden = self.dense_2(self.intermediate_act_fn(self.dense_1(input_tensor)))
+        hidden = linear(self.dense_2, self.intermediate_act_fn(linear(self.dense_1, input_tensor)))
         hidden = self.dropout(hidden)
         return self.LayerNorm(hidden + input_tensor)
 

@@ -36,8 +36,7 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         dev = E.device
         seq = item_seq.contiguous()
         h = getattr(E, '_mirec_deferred', None)
-        if h is not None:                     # deferred Adam: complete the rows read
-            h.catch_up(E, seq.view(-1))
+        ctx.segs = h.catch_up(E, seq.view(-1)) if h is not None else None
         ctx.deferred = h is not None
         out = torch.empty(B, L, d, dtype=torch.float32, device=dev)
         mean = torch.empty(B * L, dtype=torch.float32, device=dev)
@@ -68,7 +67,7 @@ class _SeqEmbedLNFn(torch.autograd.Function):
                                               ptr(ditem), ptr(pg), ptr(pb), stream_handle())
         check(rc, "mirec_seq_embed_ln_bwd_f32")
         if ctx.deferred:
-            E._mirec_deferred.stash(E, ditem, seq.view(-1))
+            E._mirec_deferred.stash(E, ditem, seq.view(-1), ctx.segs)
             dE = None
         else:
             dE = ops.segment_scatter_add(ditem, ops.segment_sort(seq.view(-1), E.shape[0]),
@@ -88,15 +87,15 @@ class _SeqEmbedLNFn(torch.autograd.Function):
 def _catch_up(ctx, E, items):
     h = getattr(E, '_mirec_deferred', None)
     ctx.deferred_E = E if h is not None else None
-    if h is not None:                         # deferred Adam: complete the rows read
-        h.catch_up(E, items.contiguous())
+    # deferred Adam: complete the rows read (grouping reused by the backward)
+    ctx.segs = h.catch_up(E, items.contiguous()) if h is not None else None
 
 
 def _item_grad(ctx, gI, items):
     """Dense item-table gradient, or the compact rows handed to the deferred
     optimizer (then autograd gets None)."""
     if ctx.deferred_E is not None:
-        ctx.deferred_E._mirec_deferred.stash(ctx.deferred_E, gI, items)
+        ctx.deferred_E._mirec_deferred.stash(ctx.deferred_E, gI, items, ctx.segs)
         return None
     return ops.segment_scatter_add(gI, ops.segment_sort(items, ctx.nI),
                                    torch.zeros((ctx.nI, gI.shape[1]), device=gI.device))

@@ -194,9 +194,10 @@ class FusedAdam(torch.optim.Optimizer):
                            **self._group_args())
         return segs
 
-    def stash(self, p, rows, keys):
-        """Per-contribution gradient rows [n, d] for the table rows `keys` [n]."""
-        self._deferred[p]['stash'].append((rows, keys))
+    def stash(self, p, rows, keys, segs=None):
+        """Per-contribution gradient rows [n, d] for the table rows `keys` [n]
+        (segs: their K2 grouping when the caller already has it)."""
+        self._deferred[p]['stash'].append((rows, keys, segs))
 
     def _flush_table(self, p, ds, target):
         if ds['t0'] is None or target <= 0:
@@ -220,8 +221,9 @@ class FusedAdam(torch.optim.Optimizer):
         by autograd), so both schedules stay bit-identical."""
         n_rows = p.shape[0]
         parts = []
-        for rows, keys in stash:
-            segs = ops.segment_sort(keys.contiguous(), n_rows)
+        for rows, keys, segs in stash:
+            if segs is None:
+                segs = ops.segment_sort(keys.contiguous(), n_rows)
             parts.append(ops.segment_reduce(rows.contiguous(), segs))
         if len(parts) == 1:
             rows, segs = parts[0]

@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # fp32 MFMA / vector peak
 CPU_BASELINE = True
+ADAM_MODE = 'deferred'
 
 
 class StubDataset:
@@ -53,13 +54,19 @@ class StubDataset:
         return self._num[field]
 
 
-def _timed(fn, steps, warmup):
+def _timed(fn, steps, warmup, opt=None):
+    """Mean wall time per step over `steps` steps; with a deferred optimizer the
+    flush that completes every row is inside the timed region (no work skipped)."""
     for _ in range(warmup):
         fn()
+    if opt is not None:
+        opt.flush()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
+    if opt is not None:
+        opt.flush()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps
 
@@ -123,6 +130,8 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
             cols[f'C{j}'] = torch.as_tensor(_zipf_ids(rng, 1.1, B, v))
         batches.append(Interaction(cols).to(dev))
     opt = FusedAdam(model.parameters(), lr=1e-3)
+    if ADAM_MODE == 'deferred':
+        opt.enable_deferred(model.deferred_tables())
     it = [0]
 
     def step():
@@ -133,7 +142,7 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
         loss.backward()
         opt.step()
 
-    t = _timed(step, steps, warmup)
+    t = _timed(step, steps, warmup, opt)
     V = sum(nums[f'C{j}'] for j in range(26))
     # dominant kernel: dense Adam over the [V, 16] token table (K5, HBM-bound):
     # algorithmic bytes per step = p, m, v, g read + p, m, v written = 7 * V * d * 4
@@ -164,6 +173,7 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                          f'optim.Adam over every table), {dt:.1f} s'}
     return {
         'cpu_baseline': cpu,
+        'adam_mode': ADAM_MODE,
         'config': 'C4', 'metric': 'train samples/s', 'value': round(B / t, 1),
         'unit': 'samples/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
         'workload': f'DeepFM Criteo-shape: 13 float + 26 token fields, vocab {V:,} '
@@ -214,6 +224,8 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
                                   device=dev)
     pr = torch.zeros(1, dtype=torch.int64, device=dev)
     opt = FusedAdam(model.parameters(), lr=1e-3)
+    if ADAM_MODE == 'deferred':
+        opt.enable_deferred(model.deferred_tables())
     it = [0]
 
     def step():
@@ -226,7 +238,7 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
         loss.backward()
         opt.step()
 
-    t = _timed(step, steps, warmup)
+    t = _timed(step, steps, warmup, opt)
     from recbole_amd.model.sequential_recommender.sasrec import _SampledSoftmaxFn
     b0 = batches[0]
     S = torch.randn(B, d, device=dev)
@@ -252,6 +264,7 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
                          f'SASRecCPU + sampled softmax, dense optim.Adam), {dt:.1f} s'}
     return {
         'cpu_baseline': cpu,
+        'adam_mode': ADAM_MODE,
         'config': 'C3', 'metric': 'train sequences/s', 'value': round(B / t, 1),
         'unit': 'sequences/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
         'workload': f'SASRec Amazon-Books-shape: {n_items:,} items (incl. PAD), L={L}, d={d}, '
@@ -371,9 +384,11 @@ def main():
     ap.add_argument('--scale', type=float, default=1.0)
     ap.add_argument('--out', default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
     args = ap.parse_args()
-    global CPU_BASELINE
+    global CPU_BASELINE, ADAM_MODE
     CPU_BASELINE = not args.no_cpu_baseline
+    ADAM_MODE = args.adam_mode
     dev = torch.device('cuda', 0)
     res = []
     for c in args.configs.split(','):
