@@ -156,7 +156,7 @@ int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t st
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of
  * contributions (seg[n_uniq] <= n). The sorted contributions are summed in chunks
- * of 32 (d > 16) or 64 positions in a fixed order (hot rows are split over many lane groups and
+ * of 32 (8 when d = 1) positions in a fixed order (hot rows are split over many lane groups and
  * their partials added in chunk order by a fixup pass): deterministic, no atomics.
  * Workspace: mirec_segment_scatter_add_workspace_size(n, d). 1 <= d <= 256. */
 size_t mirec_segment_scatter_add_workspace_size(int64_t n, int32_t d);
@@ -309,10 +309,11 @@ int mirec_score_matrix_f32(const float* Uq, int64_t nq, const float* EI, int64_t
  * Per row r (nonzeros in ascending CSR order):
  *   y = sum_j vals[j] * X[cols[j]];  if add: y += add_scale * ADD[r];
  *   if y: Y[r] = y;  if acc_out: ACC_OUT[r] = (ACC_IN[r] (0 if absent) + y) * acc_scale.
- * Load balance: the host plan (recbole_amd/model/general_recommender/lightgcn.py
- *   `spmm_plan`) cuts row r into ceil(deg/piece) units (at least one);
- *   unit u covers nonzeros [unit_beg[u], min(unit_beg[u]+piece, row_ptr[r+1])) of
- *   row unit_row[u]; unit_slot[u] = -1 when it is the row's only unit, else the
+ * Load balance: the host plan (recbole_amd/ops.py `SpmmPlan`) cuts row r into
+ *   min(ceil(deg/piece), 1024) units of near-equal length (at least one);
+ *   unit u covers nonzeros [unit_beg[u], unit_beg[u+1]) of row unit_row[u]
+ *   (unit_beg has n_units+1 entries, the last = nnz; piece = the base unit length,
+ *   informational); unit_slot[u] = -1 when it is the row's only unit, else the
  *   row of `partial` [n_slots, d] it writes; fix_row[f] / fix_ptr[f..f+1] list the
  *   split rows and their slots, summed in slot order (deterministic).
  * d in {32, 64, 128, 256}; Y / ACC_OUT must not alias X.

@@ -21,7 +21,8 @@
 // two weight gradients directly.
 //
 // Work decomposition (load balance under Zipf degrees): the host plan cuts every
-// row into units of at most `piece` nonzeros. A unit is handled by a group of
+// row into near-equal units of about `piece` nonzeros, at most 1024 per row (a
+// hub item of a Zipf graph has millions of edges). A unit is handled by a group of
 // D/4 lanes (one float4 of the row per lane; 64/(D/4) rows per wave). Rows of
 // one unit apply the epilogue directly; the units of a longer row write their
 // partial sums to `partial` and a second kernel adds them in unit order and
@@ -99,11 +100,11 @@ __global__ __launch_bounds__(256) void spmm_units_kernel(
     if (u < n_units) {
       r = unit_row[u];
       b = unit_beg[u];
-      const int64_t re = row_ptr[r + 1];
-      e = b + piece < re ? b + piece : re;
+      e = unit_beg[u + 1];   // units tile each row in order: the next one starts here
       slot = unit_slot[u];
     }
     const int len = (int)(e - b);
+    (void)piece;
     int maxlen = len;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, off, 64));

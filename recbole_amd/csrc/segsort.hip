@@ -399,8 +399,8 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
 // it first crosses) adds in chunk order. Deterministic, no float atomics.
 // positions per chunk: short chunks for wide rows (more lane groups in flight),
 // longer ones for narrow rows; the workspace is sized for the smallest
-__host__ __device__ __forceinline__ int scat_chunk(int d) { return d <= 16 ? 64 : 32; }
-constexpr int kScatChunkMin = 32;
+__host__ __device__ __forceinline__ int scat_chunk(int d) { return d == 1 ? 8 : 32; }
+constexpr int kScatChunkMin = 8;
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ seg, int nu, int p) {
   int lo = 0, hi = nu - 1;   // largest u with seg[u] <= p

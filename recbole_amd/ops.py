@@ -447,16 +447,20 @@ class SpmmPlan:
     every row is cut into units of at most `piece` nonzeros (include/mirec.h)."""
 
     def __init__(self, row_ptr: np.ndarray, cols: np.ndarray, vals: np.ndarray, device,
-                 piece: int = 256):
+                 piece: int = 256, max_units: int = 1024):
         row_ptr = np.asarray(row_ptr, dtype=np.int64)
         n = len(row_ptr) - 1
         deg = np.diff(row_ptr)
-        n_units_row = np.maximum(1, -(-deg // piece))
+        # hub rows (a Zipf head item has millions of edges) are cut into at most
+        # max_units units so the fixup of their partials stays short
+        n_units_row = np.minimum(np.maximum(1, -(-deg // piece)), max_units)
         first_unit = np.concatenate([[0], np.cumsum(n_units_row)])
         n_units = int(first_unit[-1])
         unit_row = np.repeat(np.arange(n, dtype=np.int32), n_units_row)
         k_in_row = np.arange(n_units, dtype=np.int64) - first_unit[:-1][unit_row]
-        unit_beg = row_ptr[:-1][unit_row] + k_in_row * piece
+        # near-equal split of row r's deg nonzeros over its units
+        unit_beg = row_ptr[:-1][unit_row] + (k_in_row * deg[unit_row]) // n_units_row[unit_row]
+        unit_beg = np.concatenate([unit_beg, [row_ptr[-1]]])
         split = n_units_row > 1
         unit_slot = np.full(n_units, -1, dtype=np.int32)
         in_split = split[unit_row]

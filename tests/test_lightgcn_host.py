@@ -28,9 +28,11 @@ def test_spmm_plan_covers_every_nonzero_once():
     cols = rng.integers(0, len(deg), rp[-1])
     plan = ops.SpmmPlan(rp, cols, np.ones(rp[-1], np.float32), device='cpu', piece=16)
     ur, ub, us = plan.unit_row.numpy(), plan.unit_beg.numpy(), plan.unit_slot.numpy()
+    assert len(ub) == len(ur) + 1 and ub[-1] == rp[-1]
     seen = np.zeros(rp[-1], dtype=int)
-    for r, b in zip(ur, ub):
-        seen[b:min(b + 16, rp[r + 1])] += 1
+    for u, r in enumerate(ur):
+        assert rp[r] <= ub[u] <= ub[u + 1] <= rp[r + 1] and ub[u + 1] - ub[u] <= 16
+        seen[ub[u]:ub[u + 1]] += 1
     assert (seen == 1).all()
     assert set(ur.tolist()) == set(range(len(deg)))       # empty rows still get a unit
     fr, fp = plan.fix_row.numpy(), plan.fix_ptr.numpy()
@@ -38,3 +40,15 @@ def test_spmm_plan_covers_every_nonzero_once():
     for k, r in enumerate(fr):
         assert sorted(us[ur == r].tolist()) == list(range(fp[k], fp[k + 1]))
     assert (us[~np.isin(ur, fr)] == -1).all()
+
+
+def test_spmm_plan_caps_units_of_hub_rows():
+    from recbole_amd import ops
+    deg = np.r_[3, 100_000, 5]
+    rp = np.r_[0, np.cumsum(deg)]
+    plan = ops.SpmmPlan(rp, np.zeros(rp[-1], np.int64), np.ones(rp[-1], np.float32),
+                        device='cpu', piece=16, max_units=64)
+    ur, ub = plan.unit_row.numpy(), plan.unit_beg.numpy()
+    assert (ur == 1).sum() == 64 and plan.n_fix == 1
+    sizes = np.diff(ub)[ur == 1]
+    assert sizes.sum() == 100_000 and sizes.max() - sizes.min() <= 1
