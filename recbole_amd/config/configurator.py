@@ -176,7 +176,9 @@ class Config(object):
     def _init_device(self):
         c = self.final_config_dict
         use_gpu = c['use_gpu']
-        if use_gpu and 'CUDA_VISIBLE_DEVICES' not in os.environ and c.get('n_gpus', 1) == 1:
+        # one process per GPU under torchrun (WORLD_SIZE > 1) picks its own device
+        if (use_gpu and 'CUDA_VISIBLE_DEVICES' not in os.environ
+                and int(os.environ.get('WORLD_SIZE', '1')) == 1):
             os.environ['CUDA_VISIBLE_DEVICES'] = str(c['gpu_id'])
         c['device'] = torch.device('cuda' if torch.cuda.is_available() and use_gpu else 'cpu')
 

@@ -19,7 +19,7 @@ OVERALL = dict(
     valid_metric='MRR@10', eval_batch_size=4096, loss_decimal_place=4,
     metric_decimal_place=4,
     # MI355X build extensions
-    n_gpus=1, fused_train=True, fused_eval=True, train_graph=True, profile=False,
+    n_gpus=None, fused_train=True, fused_eval=True, train_graph=True, profile=False,
     adam_mode='deferred',
 )
 

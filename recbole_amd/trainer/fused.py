@@ -475,23 +475,28 @@ class FusedBPRTrainStep(object):
         return self.end_epoch()
 
 
-def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20):
+def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, dp=None):
     """Trainer.evaluate for a FULL loader (trainer.py:355-412) on K6: scores,
     pad/history mask, top-K and positive flags in one kernel per user batch; only
     the [n_users, K] positive matrix returns to the host for the metric
-    reduction (evaluators.py:122-141)."""
+    reduction (evaluators.py:122-141). With a DataParallelStep `dp` every rank ranks
+    its contiguous block of users and one all-gather assembles the flags in user
+    order (trainer/dist.py) — the metrics of one GPU."""
     dev = model.fused_item_table().device
     K = max(topk_evaluator.topk)
     uids, hist_ptr, hist_cols, pos_ptr, pos_cols = eval_data.device_csr(dev)
     EI = model.fused_item_table().contiguous()
     n = uids.numel()
-    flags = torch.empty(n, K, dtype=torch.uint8, device=dev)
-    for s in range(0, n, user_batch):
-        e = min(n, s + user_batch)
+    lo, hi, blk = dp.user_block(n) if dp is not None else (0, n, n)
+    flags = torch.empty(max(hi - lo, 0), K, dtype=torch.uint8, device=dev)
+    for s in range(lo, hi, user_batch):
+        e = min(hi, s + user_batch)
         Uq = model.fused_user_vectors(uids[s:e]).contiguous()
-        o = {'pos_flags': flags[s:e]}
+        o = {'pos_flags': flags[s - lo:e - lo]}
         ops.fullsort_topk(Uq, EI, K, hist_ptr=hist_ptr[s:e + 1], hist_cols=hist_cols,
                           pos_ptr=pos_ptr[s:e + 1], pos_cols=pos_cols, out=o)
+    if dp is not None:
+        flags = dp.gather_rows(flags, n, blk)
     pos_idx = flags.cpu().numpy().astype(bool)
     return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
 
