@@ -119,14 +119,47 @@ class FusedAdam(torch.optim.Optimizer):
             if deferred:
                 self.n_steps += 1
             return loss
-        dev = params[0].device
-        consts, idx = self.prepare_window(1, dev)
-        for p in params:
-            st = self._ensure_state(p)
-            ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
-                          dense_grad=p.grad.contiguous(), **self._group_args())
+        self._dense_step(params)
         self.n_steps += 1
         return loss
+
+    def _dense_step(self, params, window=256):
+        """One Adam step of parameters with dense gradients: the step constants come
+        from a window uploaded once per `window` steps, and parameters of one row width
+        share a launch (up to 4 tables per K5 launch; [numel/4, 4] views for the
+        rest, the flat kernel for numel % 4 != 0) — few launches and no per-step
+        host-to-device copy."""
+        dev = params[0].device
+        w = getattr(self, '_dwin', None)
+        if (w is None or w['dev'] != dev or not 0 <= self.n_steps - w['t0'] < w['W']):
+            w = self._dwin = {
+                'dev': dev, 't0': self.n_steps, 'W': window,
+                'consts': torch.as_tensor(
+                    self.step_constants(self.n_steps + 1, window).reshape(-1), device=dev),
+                'idx': torch.arange(window, dtype=torch.int32, device=dev),
+                'zero': torch.zeros(1, dtype=torch.int32, device=dev)}
+        r = self.n_steps - w['t0']
+        groups, flat = {}, []
+        for p in params:
+            st = self._ensure_state(p)
+            g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+            if p.dim() == 2 and p.shape[1] in (16, 32, 64, 128, 256):
+                d, view = p.shape[1], (lambda t: t)
+            elif p.numel() % 4 == 0:
+                d, view = 4, (lambda t: t.view(-1, 4))
+            else:
+                flat.append((p, st, g))
+                continue
+            groups.setdefault(d, []).append({'p': view(p.data), 'm': view(st['exp_avg']),
+                                             'v': view(st['exp_avg_sq']),
+                                             'dense_grad': view(g)})
+        for d, specs in groups.items():
+            for i in range(0, len(specs), 4):
+                ops.adam_multi(ops.adam_tables(specs[i:i + 4]), d, w['consts'], w['zero'], r,
+                               schedule='streamed', **self._group_args())
+        for p, st, g in flat:
+            ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], w['consts'],
+                          w['idx'][r:r + 1], dense_grad=g, **self._group_args())
 
     def advance(self, n: int):
         self.n_steps += n
@@ -292,6 +325,7 @@ class FusedAdam(torch.optim.Optimizer):
         return {'state': state, 'param_groups': groups}
 
     def load_state_dict(self, state_dict):
+        self._dwin = None
         for ds in getattr(self, '_deferred', {}).values():
             ds['t0'] = None                   # loaded rows are complete: new window
             ds['stash'] = []
