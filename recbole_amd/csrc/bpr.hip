@@ -1,4 +1,4 @@
-// K3 — fused BPR forward + backward, one wavefront per positive.
+// K3 — fused BPR forward + backward, D/4 lanes per positive.
 //
 // Restates BPR.calculate_loss (recbole/model/general_recommender/bpr.py:74-83)
 // and BPRLoss (recbole/model/loss.py:43-49) plus the autograd backward torch
@@ -51,6 +51,22 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, int lane, co
   }
 }
 
+template <int LPR>
+__device__ __forceinline__ float group_sum(float x) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
+  return ((a.x * b.x + a.y * b.y) + a.z * b.z) + a.w * b.w;
+}
+
+// D/4 lanes per positive (one float4 of every row per lane: 16-B loads, a 512-B
+// row of D = 128 is one half-wave access), 64/(D/4) positives per wave. The
+// negatives are gathered NB at a time with all their loads issued before the
+// first reduction, so a positive costs ~2 dependent memory round trips instead
+// of one per negative.
 template <int D>
 __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     const float* __restrict__ EU, int64_t nU, const float* __restrict__ EI, int64_t nI,
@@ -58,76 +74,75 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     const int64_t* __restrict__ neg, int64_t B, int times, float gamma, float grad_scale,
     float* __restrict__ loss_k, float* __restrict__ pos_score, float* __restrict__ neg_score,
     float* __restrict__ gU, float* __restrict__ gI) {
-  constexpr int E = RowVec<D>::E;
-  constexpr int ACT = RowVec<D>::ACT;
+  constexpr int LPR = D / 4;
+  constexpr int GPW = 64 / LPR;
+  constexpr int NB = 4;
   const int lane = threadIdx.x & 63;
-  const int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (k >= B) return;  // whole wave exits together
-  const bool act = lane < ACT;
+  const int g = lane / LPR;
+  const int l = lane - g * LPR;
+  const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
+  if (k >= B) return;  // whole lane group exits together (shuffles stay in the group)
 
   int64_t uid = user[k], pid = pos[k];
   uid = uid < 0 ? 0 : (uid >= nU ? nU - 1 : uid);
   pid = pid < 0 ? 0 : (pid >= nI ? nI - 1 : pid);
-  RowVec<D> u, p;
-  if (act) {
-    load_row<D>(EU + uid * D, lane, u);
-    load_row<D>(EI + pid * D, lane, p);
-  } else {
+  const float4 u = reinterpret_cast<const float4*>(EU + uid * D)[l];
+  const float4 p = reinterpret_cast<const float4*>(EI + pid * D)[l];
+  int64_t nid[NB];
 #pragma unroll
-    for (int e = 0; e < E; ++e) { u.x[e] = 0.f; p.x[e] = 0.f; }
+  for (int q = 0; q < NB; ++q) {
+    int64_t id = q < times ? neg[(int64_t)q * B + k] : 0;
+    nid[q] = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
   }
-  float part = 0.f;
-#pragma unroll
-  for (int e = 0; e < E; ++e) part += u.x[e] * p.x[e];
-  const float sp = wave_sum(part);
-
-  float gu[E], gp[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) { gu[e] = 0.f; gp[e] = 0.f; }
+  const float sp = group_sum<LPR>(dot4(u, p));
+  float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gp = gu;
   float lsum = 0.f;
   const float ng = -grad_scale;
-
-  // software-pipeline the negative rows: load row j+1 while reducing row j
-  RowVec<D> n_cur, n_nxt;
-  auto load_neg = [&](int j, RowVec<D>& dst) {
-    int64_t nid = neg[(int64_t)j * B + k];
-    nid = nid < 0 ? 0 : (nid >= nI ? nI - 1 : nid);
-    if (act) load_row<D>(EI + nid * D, lane, dst);
-    else {
+  for (int j0 = 0; j0 < times; j0 += NB) {
+    float4 n[NB];
 #pragma unroll
-      for (int e = 0; e < E; ++e) dst.x[e] = 0.f;
+    for (int q = 0; q < NB; ++q)
+      n[q] = j0 + q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    // ids of the next group in flight under this group's arithmetic
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int j = j0 + NB + q;
+      int64_t id = j < times ? neg[(int64_t)j * B + k] : 0;
+      nid[q] = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
     }
-  };
-  if (times > 0) load_neg(0, n_cur);
-  for (int j = 0; j < times; ++j) {
-    if (j + 1 < times) load_neg(j + 1, n_nxt);
-    float pn = 0.f;
+    float sn[NB];
 #pragma unroll
-    for (int e = 0; e < E; ++e) pn += u.x[e] * n_cur.x[e];
-    const float sn = wave_sum(pn);
-    const float x = sp - sn;
-    const float s = 1.f / (1.f + expf(-x));
-    const float gs = gamma + s;
-    lsum += -logf(gs);
-    const float g = ng / gs;
-    const float dx = (g * (1.f - s)) * s;
-    float gn[E];
+    for (int q = 0; q < NB; ++q) sn[q] = group_sum<LPR>(dot4(u, n[q]));
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      gu[e] += dx * p.x[e] - dx * n_cur.x[e];
-      gp[e] += dx * u.x[e];
-      gn[e] = -dx * u.x[e];
+    for (int q = 0; q < NB; ++q) {
+      const int j = j0 + q;
+      if (j < times) {
+        const float x = sp - sn[q];
+        const float s = 1.f / (1.f + expf(-x));
+        const float gs = gamma + s;
+        lsum += -logf(gs);
+        const float gg = ng / gs;
+        const float dx = (gg * (1.f - s)) * s;
+        gu.x += dx * p.x - dx * n[q].x;
+        gu.y += dx * p.y - dx * n[q].y;
+        gu.z += dx * p.z - dx * n[q].z;
+        gu.w += dx * p.w - dx * n[q].w;
+        gp.x += dx * u.x;
+        gp.y += dx * u.y;
+        gp.z += dx * u.z;
+        gp.w += dx * u.w;
+        const int64_t r = (int64_t)j * B + k;
+        if (gI)
+          reinterpret_cast<float4*>(gI + (B + r) * D)[l] =
+              make_float4(-dx * u.x, -dx * u.y, -dx * u.z, -dx * u.w);
+        if (neg_score && l == 0) neg_score[r] = sn[q];
+      }
     }
-    const int64_t r = (int64_t)j * B + k;
-    if (gI && act) store_row<D>(gI + (B + r) * D, lane, gn);
-    if (neg_score && lane == 0) neg_score[r] = sn;
-    n_cur = n_nxt;
   }
-  if (act) {
-    if (gU) store_row<D>(gU + k * D, lane, gu);
-    if (gI) store_row<D>(gI + k * D, lane, gp);
-  }
-  if (lane == 0) {
+  if (gU) reinterpret_cast<float4*>(gU + k * D)[l] = gu;
+  if (gI) reinterpret_cast<float4*>(gI + k * D)[l] = gp;
+  if (l == 0) {
     if (loss_k) loss_k[k] = lsum;
     if (pos_score) pos_score[k] = sp;
   }
@@ -199,11 +214,12 @@ extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* E
     return -1;
   }
   const dim3 blk(256);
-  const dim3 grd((unsigned)((B + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define MIREC_BPR_CASE(DD)                                                                    \
   case DD:                                                                                    \
-    hipLaunchKernelGGL(bpr_fwd_bwd_kernel<DD>, grd, blk, 0, st, EU, nU, EI, nI, user, pos,    \
+    hipLaunchKernelGGL(bpr_fwd_bwd_kernel<DD>,                                                \
+                       dim3((unsigned)((B + 4 * (256 / DD) - 1) / (4 * (256 / DD)))), blk, 0, \
+                       st, EU, nU, EI, nI, user, pos,                                         \
                        neg, B, times, gamma, grad_scale, loss_k, pos_score, neg_score, gU, gI); \
     break;
   switch (d) {
