@@ -433,6 +433,16 @@ int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const f
                                const float* gamma, const float* mean, const float* rstd,
                                const float* grad_out, float* dx, float* ditem,
                                float* part_gamma, float* part_beta, void* stream);
+/* K9c: sampled evaluation (uni-N) of a sequential model — rank[q] = number of the
+ * m sampled items neg[q*m .. q*m+m) (row-major: the sampler's per-row walk order)
+ * whose score <seq_out[q], E[i]> is greater than or equal to the positive's (exact
+ * ties — sampled copies of the positive item — counted ahead of it; torch.topk
+ * leaves their order unspecified). pos_idx[q, r] = (rank[q] == r) for r < K — Trainer.evaluate's
+ * repeat / sample_collect / topk sequence (trainer.py:384-409, abstract_evaluator.py
+ * :65-75) for one positive per query. d in {32,64,128,256}. */
+int mirec_rank_of_pos_f32(const float* seq_out, const float* item_table, int64_t n_items,
+                          int32_t d, const int64_t* pos, const int64_t* neg, int64_t n, int32_t m,
+                          int32_t* rank, void* stream);
 int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table, int64_t n_items,
                               int32_t d, const int64_t* pos, const int64_t* neg, int64_t B,
                               int32_t n_neg, float grad_scale, float* loss, float* g_seq,

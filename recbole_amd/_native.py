@@ -106,6 +106,8 @@ SIGNATURES = {
                                            _P, _P, _P, _P, _P, _P, _P, _P]),
     "mirec_sampled_softmax_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32,
                                           c_float, _P, _P, _P, _P]),
+    "mirec_rank_of_pos_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32, _P,
+                                      _P]),
     "mirec_gather_sqnorm_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P]),
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }

@@ -313,3 +313,82 @@ extern "C" int mirec_sampled_softmax_f32(const float* seq_out, const float* item
   }
   return launch_status("mirec_sampled_softmax_f32");
 }
+
+// K9c — sampled evaluation of a sequential model (uni-N, the fork's validation):
+// rank of the positive among [pos | N sampled items] per query, i.e. the number
+// of sampled items whose score is greater or equal (a sampled copy of the positive
+// item ties it exactly; torch.topk leaves the order of ties unspecified, this
+// counts them ahead of the positive — the pessimistic order). Replaces
+// the repeat x (1+N) of every sequence through the whole model (predict on each
+// copy) + sample_collect + topk of Trainer.evaluate for these loaders.
+namespace mirec {
+
+template <int D>
+__global__ __launch_bounds__(256) void rank_of_pos_kernel(
+    const float* __restrict__ S, const float* __restrict__ E, int64_t n_items,
+    const int64_t* __restrict__ pos, const int64_t* __restrict__ neg, int64_t n, int m,
+    int32_t* __restrict__ rank) {
+  constexpr int LPR = D / 4, GPW = 64 / LPR, NB = 4;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane % LPR;
+  const int64_t q = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
+  if (q >= n) return;
+  const float4 s = reinterpret_cast<const float4*>(S + q * D)[l];
+  auto row = [&](int64_t id) {
+    id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
+    return reinterpret_cast<const float4*>(E + id * D)[l];
+  };
+  auto dot = [&](const float4& e) {   // explicit fma chain: every call site rounds alike
+    float x = fmaf(s.w, e.w, fmaf(s.z, e.z, fmaf(s.y, e.y, s.x * e.x)));
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+  };
+  const float sp = dot(row(pos[q]));
+  const int64_t* nq = neg + q * (int64_t)m;
+  int cnt = 0;
+  for (int j0 = 0; j0 < m; j0 += NB) {
+    float4 e[NB];
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+      e[t] = j0 + t < m ? row(nq[j0 + t]) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const float sc = dot(e[t]);
+      cnt += (j0 + t < m && sc >= sp) ? 1 : 0;
+    }
+  }
+  if (l == 0) rank[q] = cnt;
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_rank_of_pos_f32(const float* seq_out, const float* item_table,
+                                     int64_t n_items, int32_t d, const int64_t* pos,
+                                     const int64_t* neg, int64_t n, int32_t m, int32_t* rank,
+                                     void* stream) {
+  if (n == 0) return 0;
+  if (!seq_out || !item_table || !pos || (m > 0 && !neg) || !rank || n < 0 || m < 0 ||
+      n_items <= 0) {
+    set_error("mirec_rank_of_pos_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_ROP(DD)                                                                         \
+  case DD:                                                                                    \
+    hipLaunchKernelGGL(rank_of_pos_kernel<DD>,                                                \
+                       dim3((unsigned)((n + 4 * (256 / DD) - 1) / (4 * (256 / DD)))),          \
+                       dim3(256), 0, st, seq_out, item_table, n_items, pos, neg, n, m, rank);  \
+    break;
+  switch (d) {
+    MIREC_ROP(32)
+    MIREC_ROP(64)
+    MIREC_ROP(128)
+    MIREC_ROP(256)
+    default:
+      set_error("mirec_rank_of_pos_f32: hidden size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_ROP
+  return launch_status("mirec_rank_of_pos_f32");
+}

@@ -520,3 +520,46 @@ def fused_seq_full_sort_eval(model, eval_data, topk_evaluator):
         flags.append(o['pos_flags'])
     pos_idx = torch.cat(flags).cpu().numpy().astype(bool)
     return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
+
+
+def fused_seq_sampled_eval(model, eval_data, topk_evaluator):
+    """Trainer.evaluate for SequentialNegSampleDataLoader in evaluation (uni-N, this
+    fork's validation, data/utils.py:86-88): the reference repeats every sequence
+    1+N times through the whole model (predict on each copy) and ranks the padded
+    score rows with topk (trainer.py:384-409, abstract_evaluator.py:65-75). Here each
+    sequence is encoded once and K9c counts the sampled items that beat the
+    positive; pos_idx[q, r] = (rank[q] == r). The negatives are the ones the
+    RepeatableSampler's per-row walk would draw (sample_by_user_ids(uid, N) for row
+    after row, no rejection): the next N values of the walk, row by row, taken with
+    one device gather; the walk pointer advances by rows x N exactly as it would."""
+    from recbole_amd._native import check, lib, ptr, stream_handle
+    sampler = eval_data.sampler
+    dev = model.fused_item_table().device
+    EI = model.fused_item_table().contiguous()
+    K = max(topk_evaluator.topk)
+    m = eval_data.neg_sample_by
+    sampler.to_device(dev)
+    L = sampler.random_list_length
+    ranks = []
+    for start in range(0, eval_data.pr_end, eval_data.step):
+        inter = eval_data.augmentation(slice(start, start + eval_data.step)).to(dev)
+        uids = inter[eval_data.uid_field]
+        n = uids.numel()
+        if n == 0:
+            continue
+        mn, mx = int(uids.min()), int(uids.max())
+        if mn < 0 or mx >= sampler.n_users:
+            raise ValueError(f'user_id [{mn if mn < 0 else mx}] not exist.')
+        idx = (sampler._pr_dev + torch.arange(n * m, device=dev)) % L
+        neg = sampler._rl_dev[idx].to(torch.int64)
+        sampler._pr_dev.copy_((sampler._pr_dev + n * m) % L)
+        S = model.fused_query_vectors(inter).detach().contiguous()
+        pos = inter[eval_data.iid_field].to(torch.int64).contiguous()
+        rank = torch.empty(n, dtype=torch.int32, device=dev)
+        rc = lib().mirec_rank_of_pos_f32(ptr(S), ptr(EI), EI.shape[0], EI.shape[1], ptr(pos),
+                                         ptr(neg), n, m, ptr(rank), stream_handle())
+        check(rc, 'mirec_rank_of_pos_f32')
+        ranks.append(rank)
+    rank = torch.cat(ranks) if ranks else torch.zeros(0, dtype=torch.int32, device=dev)
+    pos_idx = (rank.unsqueeze(1) == torch.arange(K, device=dev).unsqueeze(0)).cpu().numpy()
+    return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())

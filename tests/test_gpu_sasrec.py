@@ -150,3 +150,69 @@ def test_run_recbole_sasrec(tmp_path):
         'load_col': {'inter': ['user_id', 'item_id', 'timestamp']}, 'show_progress': False,
         'MAX_ITEM_LIST_LENGTH': 12, 'training_neg_sample_num': 0})
     assert 0.0 <= res['test_result']['hit@10'] <= 1.0
+
+
+def test_fused_sampled_eval_matches_generic(tmp_path):
+    """uni1000 validation (the fork's switch): K9c rank-of-positive on one encoding
+    per sequence vs the reference sequence (1+N copies through predict, flip + topk)
+    row by row: the same negatives (the per-row walk), and the positive's top-K
+    position equal where no sampled item ties it; where copies of the positive item
+    tie it exactly (torch.topk leaves their order unspecified) the generic position
+    lies in [#greater, #greater-or-equal] and K9c reports #greater-or-equal. Then
+    the full fused evaluation leaves the walk pointer where the generic one does."""
+    from recbole_amd._native import lib, ptr, stream_handle
+    from recbole_amd.trainer import Trainer
+    config, train, valid, test, model = _pipeline(tmp_path)
+    tr = Trainer(config, model)
+    for b in list(train)[:3]:
+        tr.optimizer.zero_grad()
+        model.calculate_loss(b).backward()
+        tr.optimizer.step()
+    model.eval()
+    dev = config['device']
+    sm = valid.sampler
+    sm.to_device(dev)
+    L, m, K = sm.random_list_length, valid.neg_sample_by, 10
+    pr_start = sm.random_pr
+    ties = 0
+    with torch.no_grad():
+        for start in range(0, valid.pr_end, valid.step):
+            pr0 = sm.random_pr
+            valid.pr = start
+            b = valid._next_batch_data()
+            items = b['item_id'].view(-1, 1 + m)
+            sc = model.predict(b.to(dev)).view(-1, 1 + m)
+            _, ti = torch.topk(torch.flip(sc, dims=[-1]), K)
+            sm.random_pr = pr0
+            inter = valid.augmentation(slice(start, start + valid.step)).to(dev)
+            n = inter['user_id'].numel()
+            idx = (sm._pr_dev + torch.arange(n * m, device=dev)) % L
+            neg = sm._rl_dev[idx].to(torch.int64)
+            sm._pr_dev.copy_((sm._pr_dev + n * m) % L)
+            assert torch.equal(neg.view(n, m).cpu(), items[:, 1:].cpu())
+            S = model.fused_query_vectors(inter).contiguous()
+            E = model.item_embedding.weight.detach()
+            rank = torch.empty(n, dtype=torch.int32, device=dev)
+            lib().mirec_rank_of_pos_f32(ptr(S), ptr(E), E.shape[0], E.shape[1],
+                                        ptr(inter['item_id'].contiguous()), ptr(neg), n, m,
+                                        ptr(rank), stream_handle())
+            for r in range(n):
+                g = sc[r]
+                gt, ge = int((g[1:] > g[0]).sum()), int((g[1:] >= g[0]).sum())
+                hit = (ti[r] >= m).nonzero()
+                gpos = int(hit[0]) if len(hit) else None
+                # the two paths encode the sequence in different batches: scores may
+                # differ by rounding, so near-ties of OTHER items may fall either way
+                other = items[r, 1:] != items[r, 0]
+                near = int((((g[1:] - g[0]).abs() <= 1e-5 * g[0].abs() + 1e-6) & other).sum())
+                assert abs(int(rank[r]) - ge) <= near, (int(rank[r]), gt, ge, near)
+                if gt == ge and near == 0:
+                    assert gpos == (ge if ge < K else None)
+                else:
+                    ties += 1
+                    assert gpos is None or gt <= gpos <= ge
+    pr_generic = sm.random_pr
+    sm.random_pr = pr_start
+    valid.pr = 0
+    tr.evaluate(valid, load_best_model=False)           # the fused path end to end
+    assert sm.random_pr == pr_generic
