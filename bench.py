@@ -214,6 +214,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-eval', action='store_true')
     ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
+    # diagnostic: rows per step (default 2,048 = 512 positives x 4 negatives, C2)
+    ap.add_argument('--batch-rows', type=int, default=2048)
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -230,7 +232,8 @@ def main():
     d, neg = 128, 4
     t_setup = time.time()
     config, train, test, model, opt, step = build_workload(
-        dev, d=d, neg=neg, adam_mode=args.adam_mode, dist=tdist.group.WORLD if dist else None)
+        dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode,
+        dist=tdist.group.WORLD if dist else None)
     setup_s = time.time() - t_setup
     nb = step.begin_epoch()
     K, W = args.steps, args.warmup

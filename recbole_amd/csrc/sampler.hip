@@ -62,6 +62,81 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* lds, int* total) {
   return before + pre;
 }
 
+// Refill rounds of one batch: the i-th rejected slot (ascending) takes the i-th
+// next walk value, until no slot is rejected. The reference loops until done;
+// on adversarial inputs (a key whose free ids all sit outside the walk
+// positions its slots can reach) that never ends, so give up after a bound and
+// set `livelock`. Called by every thread of the block; `cur` holds the nrej
+// pending slots, `nxt` is scratch of the same capacity.
+template <class KeyOf>
+__device__ __forceinline__ void walk_refill(const int32_t* __restrict__ rl, int64_t L,
+                                            int64_t& pr, const UsedSet& used, KeyOf key_of,
+                                            int64_t* __restrict__ bout, int32_t* cur,
+                                            int32_t* nxt, int32_t nrej,
+                                            int (*scan_lds)[kSampThreads / 64 + 1],
+                                            int32_t* wl, int64_t* pr_lds, int& livelock) {
+  const int lane = threadIdx.x & 63;
+  int64_t rounds = 0;
+  const int64_t max_rounds = 4 * L + 1024;
+  int sel = 0;
+  while (nrej > 64) {                       // wide rounds: whole block
+    if (++rounds > max_rounds) { livelock = 1; break; }
+    int32_t nnew = 0;
+    for (int32_t base = 0; base < nrej; base += kSampThreads) {
+      const int32_t i = base + threadIdx.x;
+      int rej = 0;
+      int32_t t = 0;
+      if (i < nrej) {
+        t = cur[i];
+        int64_t pos = pr + i;
+        if (pos >= L) pos %= L;
+        const int32_t v = rl[pos];
+        bout[t] = v;
+        rej = is_used(used, key_of(t), v) ? 1 : 0;
+      }
+      int tot;
+      const int excl = block_flag_scan(rej, scan_lds[sel], &tot);
+      sel ^= 1;
+      if (rej) nxt[nnew + excl] = t;
+      nnew += tot;
+    }
+    pr = (pr + nrej) % L;
+    int32_t* tmp = cur; cur = nxt; nxt = tmp;
+    nrej = nnew;
+    __syncthreads();
+  }
+  if (nrej > 0 && !livelock) {              // tail: one wave, no block barriers
+    if (threadIdx.x < 64) {
+      int n = nrej;
+      int64_t p = pr;
+      int32_t t = lane < n ? cur[lane] : 0;
+      int ll = 0;
+      while (n > 0) {
+        if (++rounds > max_rounds) { ll = 1; break; }
+        int rej = 0;
+        if (lane < n) {
+          int64_t pos = p + lane;
+          if (pos >= L) pos %= L;
+          const int32_t v = rl[pos];
+          bout[t] = v;
+          rej = is_used(used, key_of(t), v) ? 1 : 0;
+        }
+        const uint64_t m = __ballot(rej);
+        if (rej) wl[__popcll(m & ((1ull << lane) - 1ull))] = t;
+        __builtin_amdgcn_wave_barrier();
+        p = (p + n) % L;
+        n = __popcll(m);
+        t = lane < n ? wl[lane] : 0;
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) { *pr_lds = p; scan_lds[1][kSampThreads / 64] = ll; }
+    }
+    __syncthreads();
+    pr = *pr_lds;
+    livelock = scan_lds[1][kSampThreads / 64];
+  }
+}
+
 __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
     const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
@@ -74,7 +149,6 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
   __shared__ int32_t key_lds[kKeyLds];
   __shared__ int32_t wl[64];
   __shared__ int64_t pr_lds;
-  const int lane = threadIdx.x & 63;
   int64_t pr = pr_dev[0] % L;
   int bad_key = 0;
   int livelock = 0;
@@ -143,75 +217,121 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     pr = (pr + total) % L;
     __syncthreads();
 
-    // ---- refill rounds: the i-th rejected slot takes the i-th next walk value.
-    // The reference loops until no slot is rejected; on adversarial inputs
-    // (a user whose free items all sit outside the walk positions its slots
-    // can reach) that never ends. Give up after a bound and report -3.
-    int64_t rounds = 0;
-    const int64_t max_rounds = 4 * L + 1024;
-    int sel = 0;
-    while (nrej > 64) {                       // wide rounds: whole block
-      if (++rounds > max_rounds) { livelock = 1; break; }
-      int32_t nnew = 0;
-      for (int32_t base = 0; base < nrej; base += kSampThreads) {
-        const int32_t i = base + threadIdx.x;
-        int rej = 0;
-        int32_t t = 0;
-        if (i < nrej) {
-          t = cur[i];
-          int64_t pos = pr + i;
-          if (pos >= L) pos %= L;
-          const int32_t v = rl[pos];
-          bout[t] = v;
-          rej = is_used(used, key_of(t), v) ? 1 : 0;
-        }
-        int tot;
-        const int excl = block_flag_scan(rej, scan_lds[sel], &tot);
-        sel ^= 1;
-        if (rej) nxt[nnew + excl] = t;
-        nnew += tot;
-      }
-      pr = (pr + nrej) % L;
-      int32_t* tmp = cur; cur = nxt; nxt = tmp;
-      nrej = nnew;
-      __syncthreads();
-    }
-    if (nrej > 0 && !livelock) {              // tail: one wave, no block barriers
-      if (threadIdx.x < 64) {
-        int n = nrej;
-        int64_t p = pr;
-        int32_t t = lane < n ? cur[lane] : 0;
-        int ll = 0;
-        while (n > 0) {
-          if (++rounds > max_rounds) { ll = 1; break; }
-          int rej = 0;
-          if (lane < n) {
-            int64_t pos = p + lane;
-            if (pos >= L) pos %= L;
-            const int32_t v = rl[pos];
-            bout[t] = v;
-            rej = is_used(used, key_of(t), v) ? 1 : 0;
-          }
-          const uint64_t m = __ballot(rej);
-          if (rej) wl[__popcll(m & ((1ull << lane) - 1ull))] = t;
-          __builtin_amdgcn_wave_barrier();
-          p = (p + n) % L;
-          n = __popcll(m);
-          t = lane < n ? wl[lane] : 0;
-          __builtin_amdgcn_wave_barrier();
-        }
-        if (lane == 0) { pr_lds = p; scan_lds[1][kSampThreads / 64] = ll; }
-      }
-      __syncthreads();
-      pr = pr_lds;
-      livelock = scan_lds[1][kSampThreads / 64];
-    }
+    walk_refill(rl, L, pr, used, key_of, bout, cur, nxt, nrej, scan_lds, wl, &pr_lds,
+                livelock);
     __syncthreads();                          // LDS lists / keys reused by the next batch
   }
   if (bad_key) atomicExch(status, -2);
   if (livelock && threadIdx.x == 0) atomicExch(status, -3);
   __syncthreads();
   if (threadIdx.x == 0) pr_dev[0] = pr;
+}
+
+// ---- wide path (batches of more than kWideMin slots: a data-parallel global
+// batch of G x 512 positives walks G x 2,048 slots per step on every rank).
+// The single-block kernel above spends ~3 ns per round-0 slot in one CU, so a
+// 16k-slot batch took ~50 us. Round 0 only depends on the batch's start
+// position, so it runs over the whole chip (walk_round0_kernel: values, and a
+// 64-slot rejection mask per wave); one block then orders the rejected slots
+// from the masks and runs the refill rounds (walk_refill_kernel), which
+// publishes the next batch's start position in pr_dev. Two launches per batch,
+// stream-ordered; same walk, same values as the single-block kernel.
+constexpr int64_t kWideMin = 4096;
+constexpr int kR0Threads = 256;
+constexpr int kR0PerThread = 4;   // slots per thread (lane-strided: coalesced)
+
+__global__ __launch_bounds__(kR0Threads) void walk_round0_kernel(
+    const int32_t* __restrict__ rl, int64_t L, const int64_t* __restrict__ pr_dev,
+    const int64_t* __restrict__ bkeys, int32_t Kb, int64_t total, UsedSet used,
+    int64_t key_space, int reject, int64_t* __restrict__ bout, uint64_t* __restrict__ masks,
+    int32_t* __restrict__ status) {
+  if (status[0] == -3) return;                      // an earlier batch gave up
+  const int64_t pr = pr_dev[0] % L;
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * (kR0Threads / 64) + (threadIdx.x >> 6)) *
+                     kR0PerThread;                  // first 64-slot word of this wave
+  int32_t vals[kR0PerThread];
+  int64_t keyv[kR0PerThread];
+#pragma unroll
+  for (int j = 0; j < kR0PerThread; ++j) {
+    const int64_t t = (w0 + j) * 64 + lane;
+    int64_t pos = pr + t;
+    if (pos >= L) pos %= L;
+    vals[j] = t < total ? rl[pos] : 0;
+    int64_t key = -1;
+    if (reject && t < total) {
+      key = bkeys[(int32_t)(t % Kb)];
+      if (key < 0 || key >= key_space) key = -1;
+    }
+    keyv[j] = key;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < kR0PerThread; ++j) {
+    const int64_t t = (w0 + j) * 64 + lane;
+    int rej = 0;
+    if (t < total) {
+      bout[t] = vals[j];
+      if (reject) {
+        if (keyv[j] < 0) bad = 1;
+        else rej = is_used(used, keyv[j], vals[j]) ? 1 : 0;
+      }
+    }
+    const uint64_t m = __ballot(rej);
+    if (lane == 0 && (w0 + j) * 64 < total) masks[w0 + j] = m;
+  }
+  if (bad) atomicExch(status, -2);
+}
+
+__global__ __launch_bounds__(kSampThreads) void walk_refill_kernel(
+    const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
+    const int64_t* __restrict__ bkeys, int32_t Kb, int64_t total, UsedSet used,
+    int64_t key_space, int64_t* __restrict__ bout, const uint64_t* __restrict__ masks,
+    int32_t* __restrict__ status, int32_t* __restrict__ rejA_g, int32_t* __restrict__ rejB_g) {
+  __shared__ int scan_lds[2][kSampThreads / 64 + 1];
+  __shared__ int32_t listA[kListLds];
+  __shared__ int32_t listB[kListLds];
+  __shared__ int32_t wl[64];
+  __shared__ int64_t pr_lds;
+  if (status[0] == -3) return;
+  int64_t pr = pr_dev[0] % L;
+  // count the rejected slots (popcounts of the masks, block-reduced)
+  const int64_t n_words = (total + 63) / 64;
+  int cnt = 0;
+  for (int64_t w = threadIdx.x; w < n_words; w += kSampThreads) cnt += __popcll(masks[w]);
+  int nrej;
+  block_exclusive_scan(cnt, scan_lds[0], &nrej);
+  const bool lds_lists = nrej <= kListLds;
+  int32_t* cur = lds_lists ? listA : rejA_g;
+  int32_t* nxt = lds_lists ? listB : rejB_g;
+  // ascending list: words are taken in order, kSampThreads at a time
+  int32_t base = 0;
+  for (int64_t w0 = 0; w0 < n_words; w0 += kSampThreads) {
+    const int64_t w = w0 + threadIdx.x;
+    const uint64_t m = w < n_words ? masks[w] : 0ull;
+    int tot;
+    int excl = block_exclusive_scan(__popcll(m), scan_lds[1], &tot);
+    uint64_t mm = m;
+    while (mm) {
+      const int b = __ffsll((unsigned long long)mm) - 1;
+      cur[base + excl++] = (int32_t)(w * 64 + b);
+      mm &= mm - 1;
+    }
+    base += tot;
+  }
+  __syncthreads();
+  pr = (pr + total) % L;
+  auto key_of = [&](int64_t t) -> int64_t {
+    const int64_t key = bkeys[(int32_t)(t % Kb)];
+    return (key < 0 || key >= key_space) ? -1 : key;
+  };
+  int livelock = 0;
+  walk_refill(rl, L, pr, used, key_of, bout, cur, nxt, nrej, scan_lds, wl, &pr_lds, livelock);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pr_dev[0] = pr;
+    if (livelock) atomicExch(status, -3);
+  }
 }
 
 // bits[key, v>>5] |= 1 << (v & 31) for every used id; one wave per key.
@@ -236,7 +356,8 @@ using namespace mirec;
 
 extern "C" size_t mirec_sample_walk_workspace_size(int64_t batch_keys, int64_t num) {
   if (batch_keys <= 0 || num <= 0) return 256;
-  return (size_t)(2 * batch_keys * num) * sizeof(int32_t) + 256;
+  const int64_t total = batch_keys * num;
+  return (size_t)(2 * total) * sizeof(int32_t) + (size_t)((total + 63) / 64 + 1) * 8 + 256;
 }
 
 extern "C" size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits) {
@@ -300,8 +421,29 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
   u.bits = used_bits;
   u.nbits = n_bits;
   u.words = used_bits ? (n_bits + 31) / 32 : 0;
-  hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, (hipStream_t)stream,
-                     random_list, L, pr_dev, keys, n_keys, batch_keys, n_batches, num, u,
-                     n_key_space, reject, out, out_stride, status_dev, rejA, rejB);
+  hipStream_t st = (hipStream_t)stream;
+  if (batch_keys * num <= kWideMin) {
+    hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, st, random_list, L,
+                       pr_dev, keys, n_keys, batch_keys, n_batches, num, u, n_key_space, reject,
+                       out, out_stride, status_dev, rejA, rejB);
+    return launch_status("mirec_sample_walk");
+  }
+  // 8-byte aligned mask words after the two lists
+  uint64_t* masks = (uint64_t*)(((uintptr_t)(rejB + batch_keys * num) + 7) & ~(uintptr_t)7);
+  for (int64_t b = 0; b < n_batches; ++b) {
+    const int64_t k0 = b * batch_keys;
+    const int64_t Kb = min(batch_keys, n_keys - k0);
+    if (Kb <= 0) break;
+    const int64_t total = Kb * num;
+    const int64_t words = (total + 63) / 64;
+    const unsigned blocks =
+        (unsigned)((words + (kR0Threads / 64) * kR0PerThread - 1) / ((kR0Threads / 64) * kR0PerThread));
+    hipLaunchKernelGGL(walk_round0_kernel, dim3(blocks), dim3(kR0Threads), 0, st, random_list, L,
+                       pr_dev, keys + k0, (int32_t)Kb, total, u, n_key_space, reject,
+                       out + b * out_stride, masks, status_dev);
+    hipLaunchKernelGGL(walk_refill_kernel, dim3(1), dim3(kSampThreads), 0, st, random_list, L,
+                       pr_dev, keys + k0, (int32_t)Kb, total, u, n_key_space, out + b * out_stride,
+                       masks, status_dev, rejA, rejB);
+  }
   return launch_status("mirec_sample_walk");
 }

@@ -74,10 +74,11 @@ def test_sampler_random_vs_c_oracle(dev, n_items, n_users, K, num, bits):
 
 
 @pytest.mark.parametrize('bits', [False, True])
-def test_sampler_multi_batch_launch_equals_sequential(dev, bits):
+@pytest.mark.parametrize('B', [256, 1536])      # 1536 x 4 slots: the wide (multi-CU round 0) path
+def test_sampler_multi_batch_launch_equals_sequential(dev, bits, B):
     from recbole_amd import ops
     rng = np.random.default_rng(11)
-    n_users, n_items, B, T, nb = 500, 3000, 256, 4, 7
+    n_users, n_items, T, nb = 500, 3000, 4, 7
     u = rng.integers(0, n_users, 40000)
     i = rng.integers(1, n_items, 40000)
     ptr, cols = cpu_ref.used_csr(n_users, u, i)
@@ -111,26 +112,28 @@ def test_repeatable_sampler_no_rejection(dev):
 
 
 @pytest.mark.parametrize('bits', [False, True])
-def test_sampler_livelock_reports_status(dev, bits):
+@pytest.mark.parametrize('reps', [1, 2500])     # 2 slots (single block) / 5,000 (wide path)
+def test_sampler_livelock_reports_status(dev, bits, reps):
     from recbole_amd import ops
     rl = np.array([1, 2, 3, 4])
     ptr, cols = cpu_ref.used_csr(2, np.array([0, 0, 0, 1, 1, 1]), np.array([1, 3, 4, 2, 3, 4]))
     drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.sample_walk(drl, torch.zeros(1, dtype=torch.int64, device=dev),
-                    torch.tensor([0, 1], device=dev), 1, dup, duc, 2, True, status=status,
+                    torch.tensor([0, 1] * reps, device=dev), 1, dup, duc, 2, True, status=status,
                     **_membership(dup, duc, 2, 5, bits))
     assert int(status.item()) == -3
 
 
-def test_sampler_bad_key_status(dev):
+@pytest.mark.parametrize('reps', [1, 2500])
+def test_sampler_bad_key_status(dev, reps):
     from recbole_amd import ops
     rl = np.arange(1, 20)
     ptr, cols = cpu_ref.used_csr(3, np.array([0, 1]), np.array([1, 2]))
     drl, dup, duc = _walk_dev(rl, ptr, cols, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.sample_walk(drl, torch.zeros(1, dtype=torch.int64, device=dev),
-                    torch.tensor([0, 7], device=dev), 2, dup, duc, 3, True, status=status)
+                    torch.tensor([0, 7] * reps, device=dev), 2, dup, duc, 3, True, status=status)
     assert int(status.item()) == -2
 
 
