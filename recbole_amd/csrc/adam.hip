@@ -34,6 +34,7 @@
 // ~13k divisors of several beta2), i.e. bit-identical to IEEE division in 3
 // instead of ~11 instructions. x = +inf takes the IEEE division.
 #include "common.h"
+#include "adam_math.h"
 
 // No FMA contraction: every op rounds on its own, as in torch's op-by-op
 // _single_tensor_adam, and the streamed / deferred schedules stay bit-identical
@@ -221,6 +222,188 @@ __device__ __forceinline__ void adam_replay(V& p, V& m, V& v, int s0, int s1,
   }
 }
 
+// ---- replay of a row that fills whole waves (s0 wave-uniform); the fast-path
+// sqrt / division it uses live in adam_math.h.
+// Zero-gradient replay of steps [s0, s1) (wd == 0, 1-b1 < 0.5) for a thread whose
+// wave holds one row (s0 the same on every lane). Same per-element results as
+// adam_elem_zero applied step by step.
+//
+// The loop-carried chain of a zero-gradient step is one fma (m) and one mul (v);
+// the expensive part (sqrt, two divisions) depends on that step's m and v only,
+// and p just accumulates the increments in step order. So steps go in groups of
+// four: the m / v chain first, then the four increments side by side (four
+// independent sqrt / division chains in flight instead of one), then the four
+// additions to p in step order — the same operations and roundings as one step
+// at a time. While every element's p update provably rounds away
+// (p_update_vanishes; p is then fixed, so its exponent part is computed once)
+// a group only moves m and v. The test runs at the first step of every group
+// outside that state (as adam_replay's every 4th step); a group whose four steps
+// do not all pass goes step by step. Full steps use the fast-path sqrt /
+// division of adam_math.h.
+template <typename V>
+__device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1,
+                                                const float* __restrict__ consts,
+                                                const AdamConsts& k) {
+  constexpr int N = Lanes<V>::n;
+  constexpr int G = 4;
+  int s = __builtin_amdgcn_readfirstlane(s0);
+  if (s >= s1) return;
+  bool skipping = false;
+  float scale[N];
+  bool okp[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) { scale[i] = 0.f; okp[i] = false; }
+  const bool eps_pos = k.eps > 0.f;
+  float mc[N], vc[N], pc[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    mc[i] = Lanes<V>::at(m, i);
+    vc[i] = Lanes<V>::at(v, i);
+    pc[i] = Lanes<V>::at(p, i);
+  }
+  // vanishing test with p's exponent part precomputed (p fixed while skipping)
+  auto fixed_p_vanish = [&](float me, float ve, const StepConsts& sc, int i) {
+    const float t = (sc.kq * fabsf(me)) * scale[i];
+    return (me == 0.f && eps_pos) || (okp[i] && ve >= 0x1p-100f && t * t < 0.999f * ve);
+  };
+  auto enter_skip = [&]() {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t ex = (__float_as_uint(pc[i]) >> 23) & 0xffu;
+      scale[i] = __uint_as_float((279u - ex) << 23);
+      okp[i] = ex >= 67u && ex < 255u;
+    }
+  };
+  // full increments of one step for every element: q = RN(RN(-ss*me) / den)
+  auto incr = [&](const float* me, const float* ve, const StepConsts& sc, float* q) {
+    bool fast = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) fast = fast && sqrt_fast_ok(ve[i]);
+    float sq[N];
+    if (__all(fast)) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) sq[i] = sqrt_rn_normal(ve[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) sq[i] = sqrtf(ve[i]);
+    }
+    float num[N], den[N];
+    bool fdiv = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      den[i] = div_bc2s(sq[i], sc) + k.eps;
+      num[i] = (-sc.ss) * me[i];
+      fdiv = fdiv && div_fast_ok(num[i], den[i]);
+    }
+    if (__all(fdiv)) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) q[i] = div_rn_normal(num[i], den[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) q[i] = num[i] / den[i];
+    }
+  };
+  // one step, state machine of adam_replay (test every step while skipping,
+  // else at `test`)
+  auto one_step = [&](const float* me, const float* ve, const StepConsts& sc, bool test) {
+    bool vanish = false;
+    if (skipping) {
+      bool mine = true;
+#pragma unroll
+      for (int i = 0; i < N; ++i) mine = mine && fixed_p_vanish(me[i], ve[i], sc, i);
+      vanish = __all(mine);
+    } else if (test) {
+      bool mine = true;
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        mine = mine && p_update_vanishes(pc[i], me[i], ve[i], sc, k.eps);
+      vanish = __all(mine);
+      if (vanish) enter_skip();
+    }
+    if (!vanish) {
+      float q[N];
+      incr(me, ve, sc, q);
+#pragma unroll
+      for (int i = 0; i < N; ++i) pc[i] = pc[i] + q[i];
+    }
+    skipping = vanish;
+  };
+
+  for (; s + G <= s1; s += G) {
+    StepConsts sc[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) sc[j] = step_consts(consts, s + j);
+    float me[G][N], ve[G][N];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        me[j][i] = fmaf(-k.omb1, mc[i], mc[i]);
+        ve[j][i] = vc[i] * k.b2;
+        mc[i] = me[j][i];
+        vc[i] = ve[j][i];
+      }
+    }
+    bool group_done = false;
+    if (skipping) {
+      bool mine = true;
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+#pragma unroll
+        for (int i = 0; i < N; ++i) mine = mine && fixed_p_vanish(me[j][i], ve[j][i], sc[j], i);
+      group_done = __all(mine);                 // four skipped steps
+    } else {
+      bool mine = true;
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        mine = mine && p_update_vanishes(pc[i], me[0][i], ve[0][i], sc[0], k.eps);
+      if (!__all(mine)) {                       // four full steps, increments side by side
+        float q[G][N];
+#pragma unroll
+        for (int j = 0; j < G; ++j) incr(me[j], ve[j], sc[j], q[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+#pragma unroll
+          for (int i = 0; i < N; ++i) pc[i] = pc[i] + q[j][i];
+        group_done = true;
+      }
+    }
+    if (!group_done) {                          // a transition: step by step
+#pragma unroll
+      for (int j = 0; j < G; ++j) one_step(me[j], ve[j], sc[j], j == 0);
+    }
+  }
+  for (int j = 0; s < s1; ++s, ++j) {           // the last s1 - s < 4 steps
+    const StepConsts sc = step_consts(consts, s);
+    float me[N], ve[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      me[i] = fmaf(-k.omb1, mc[i], mc[i]);
+      ve[i] = vc[i] * k.b2;
+      mc[i] = me[i];
+      vc[i] = ve[i];
+    }
+    one_step(me, ve, sc, j == 0);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    Lanes<V>::at(m, i) = mc[i];
+    Lanes<V>::at(v, i) = vc[i];
+    Lanes<V>::at(p, i) = pc[i];
+  }
+}
+
+// Replay dispatch: whole-wave rows in the common configuration take
+// adam_replay_row, everything else the general adam_replay.
+template <typename V, bool kRowWave>
+__device__ __forceinline__ void replay(V& p, V& m, V& v, int s0, int s1,
+                                       const float* __restrict__ consts, const AdamConsts& k) {
+  if (kRowWave && k.wd == 0.f && k.lerp_small)
+    adam_replay_row(p, m, v, s0, s1, consts, k);
+  else
+    adam_replay(p, m, v, s0, s1, consts, k);
+}
+
 __device__ __forceinline__ int segment_of(const AdamTables& tabs, int64_t b) {
   int si = 0;
 #pragma unroll
@@ -326,9 +509,10 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 }
 
 // ---------------------------------------------------------------- deferred
-// Two columns per thread (float2: packed fp32 math, and a row's replay is a
-// serial chain per element, so few columns per thread keep the chain short).
-// RPB = 256 / (D/2) whole rows per block.
+// One column per thread: a row's replay is a serial chain per element and the
+// launch holds only the batch's rows (a few waves per SIMD), so its time is the
+// longest chain — one element per lane keeps each wave's chain shortest.
+// RPB = 256 / D whole rows per block (D >= 64: whole waves per row).
 //  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
 //               zero gradient, applies step s with its gradient; last = s+1.
 //  segment 2q+1 (look-ahead): row = ahead_uniq[u], rows the NEXT batch reads
@@ -341,7 +525,7 @@ template <int D>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     const AdamTables tabs, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
-  constexpr int VPR = D / 2;                        // float2 per row
+  constexpr int VPR = D;                            // one float per thread
   constexpr int RPB = kAdamThreads / VPR;           // rows per block
   static_assert(kAdamThreads % VPR == 0, "row width");
   const int si = segment_of(tabs, blockIdx.x);
@@ -358,28 +542,28 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   const bool valid = u < n;
   int64_t row = 0;
   int last = st;
-  float2 p = make_float2(0.f, 0.f), m = p, v = p, g = p;
+  float p = 0.f, m = 0.f, v = 0.f, g = 0.f;
   if (valid) {
     row = ahead ? T.ahead_uniq[u] : T.uniq[u];
     const int64_t off = row * VPR + c;
     last = T.last[row];
-    p = reinterpret_cast<const float2*>(T.p)[off];
-    m = reinterpret_cast<const float2*>(T.m)[off];
-    v = reinterpret_cast<const float2*>(T.v)[off];
-    if (!ahead) g = grouped_grad<float2>(T, u, VPR, c);
+    p = T.p[off];
+    m = T.m[off];
+    v = T.v[off];
+    if (!ahead) g = grouped_grad<float>(T, u, VPR, c);
   }
   // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop);
   // a row already complete through st (last > st: a repeated look-ahead of the
   // same step) is left as it is
-  adam_replay(p, m, v, last, st, consts, k);
+  replay<float, (VPR >= 64)>(p, m, v, last, st, consts, k);
   const bool fresh = last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
   __syncthreads();
   if (!valid || !fresh) return;
   const int64_t off = row * VPR + c;
-  reinterpret_cast<float2*>(T.p)[off] = p;
-  reinterpret_cast<float2*>(T.m)[off] = m;
-  reinterpret_cast<float2*>(T.v)[off] = v;
+  T.p[off] = p;
+  T.m[off] = m;
+  T.v[off] = v;
   if (c == 0) T.last[row] = st + 1;
 }
 
@@ -418,6 +602,39 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
       if (c == 0) T.last[r] = target;  // a row lies in one wave here (VPR <= 64)
     }
   }
+}
+
+// Flush with one row per wave (D >= 64: D/64 floats per lane), so every lane of
+// a wave replays the same steps (the float4 kernel above puts 256/D rows in a
+// wave, whose replay counts differ: the wave runs the longest of them). Rows
+// already complete exit without loading.
+template <int D>
+struct FlushVec { using T = float; };
+template <> struct FlushVec<128> { using T = float2; };
+template <> struct FlushVec<256> { using T = float4; };
+
+template <int D>
+__global__ __launch_bounds__(kAdamThreads) void adam_flush_row_kernel(
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k) {
+  using V = typename FlushVec<D>::T;
+  constexpr int RPB = kAdamThreads / 64;            // rows (waves) per block
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si];
+  const int64_t r = ((int64_t)blockIdx.x - tabs.block_start[si]) * RPB + (threadIdx.x >> 6);
+  if (r >= T.n_rows) return;
+  const int target = step_base[0] + step_off;
+  const int last = __builtin_amdgcn_readfirstlane(min(T.last[r], target));
+  if (last >= target) return;
+  const int64_t off = r * 64 + (threadIdx.x & 63);
+  V p = reinterpret_cast<const V*>(T.p)[off];
+  V m = reinterpret_cast<const V*>(T.m)[off];
+  V v = reinterpret_cast<const V*>(T.v)[off];
+  replay<V, true>(p, m, v, last, target, consts, k);
+  reinterpret_cast<V*>(T.p)[off] = p;
+  reinterpret_cast<V*>(T.m)[off] = m;
+  reinterpret_cast<V*>(T.v)[off] = v;
+  if ((threadIdx.x & 63) == 0) T.last[r] = target;
 }
 
 }  // namespace mirec
@@ -463,7 +680,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = kAdamThreads / (d / 2);
+      const int rpb = kAdamThreads / d;
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
@@ -471,7 +688,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       if (t.ahead_uniq) blocks += nb;
     } else {
       tabs.block_start[q] = blocks;
-      blocks += (t.n_rows + kAdamRows - 1) / kAdamRows;
+      const int64_t rows_per_block =
+          (sched == Sched::kFlush && d >= 64) ? kAdamThreads / 64 : kAdamRows;
+      blocks += (t.n_rows + rows_per_block - 1) / rows_per_block;
     }
   }
   (void)VPR;
@@ -495,6 +714,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     else if (sched == Sched::kDeferred)                                                      \
       hipLaunchKernelGGL(adam_deferred_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base, \
                          step_off, k);                                                       \
+    else if (DD >= 64)                                                                       \
+      hipLaunchKernelGGL(adam_flush_row_kernel<(DD >= 64 ? DD : 64)>, grd, blk, 0, st, tabs, \
+                         consts, step_base, step_off, k);                                    \
     else                                                                                     \
       hipLaunchKernelGGL(adam_flush_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
                          step_off, k);                                                       \
