@@ -509,10 +509,12 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 }
 
 // ---------------------------------------------------------------- deferred
-// One column per thread: a row's replay is a serial chain per element and the
-// launch holds only the batch's rows (a few waves per SIMD), so its time is the
-// longest chain — one element per lane keeps each wave's chain shortest.
-// RPB = 256 / D whole rows per block (D >= 64: whole waves per row).
+// V = float or float2 columns per thread. A row's replay is a serial chain per
+// element; a launch with few rows (one 512-positive batch: a few waves per SIMD)
+// takes as long as its longest chain, so one column per lane (shortest chains);
+// a launch with many rows (a data-parallel global batch) is issue-bound, so two
+// (half the per-wave overhead). The host picks by the launch's row bound.
+// RPB = 256 / (D / |V|) whole rows per block.
 //  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
 //               zero gradient, applies step s with its gradient; last = s+1.
 //  segment 2q+1 (look-ahead): row = ahead_uniq[u], rows the NEXT batch reads
@@ -521,11 +523,11 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 //               forward pass reads rows that are complete through step s.
 // `last` is read by every thread of a row before the barrier and written
 // after it (a row of D = 256 spans two waves).
-template <int D>
+template <int D, typename V>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     const AdamTables tabs, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
-  constexpr int VPR = D;                            // one float per thread
+  constexpr int VPR = D / Lanes<V>::n;              // V = float or float2 per thread
   constexpr int RPB = kAdamThreads / VPR;           // rows per block
   static_assert(kAdamThreads % VPR == 0, "row width");
   const int si = segment_of(tabs, blockIdx.x);
@@ -542,28 +544,29 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   const bool valid = u < n;
   int64_t row = 0;
   int last = st;
-  float p = 0.f, m = 0.f, v = 0.f, g = 0.f;
+  V p, m, v, g;
+  memset(&p, 0, sizeof(V)); m = p; v = p; g = p;
   if (valid) {
     row = ahead ? T.ahead_uniq[u] : T.uniq[u];
     const int64_t off = row * VPR + c;
     last = T.last[row];
-    p = T.p[off];
-    m = T.m[off];
-    v = T.v[off];
-    if (!ahead) g = grouped_grad<float>(T, u, VPR, c);
+    p = reinterpret_cast<const V*>(T.p)[off];
+    m = reinterpret_cast<const V*>(T.m)[off];
+    v = reinterpret_cast<const V*>(T.v)[off];
+    if (!ahead) g = grouped_grad<V>(T, u, VPR, c);
   }
   // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop);
   // a row already complete through st (last > st: a repeated look-ahead of the
   // same step) is left as it is
-  replay<float, (VPR >= 64)>(p, m, v, last, st, consts, k);
+  replay<V, (VPR >= 64)>(p, m, v, last, st, consts, k);
   const bool fresh = last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
   __syncthreads();
   if (!valid || !fresh) return;
   const int64_t off = row * VPR + c;
-  T.p[off] = p;
-  T.m[off] = m;
-  T.v[off] = v;
+  reinterpret_cast<V*>(T.p)[off] = p;
+  reinterpret_cast<V*>(T.m)[off] = m;
+  reinterpret_cast<V*>(T.v)[off] = v;
   if (c == 0) T.last[row] = st + 1;
 }
 
@@ -666,6 +669,15 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
   memset(&tabs, 0, sizeof(tabs));
   const bool deferred = sched == Sched::kDeferred;
   tabs.n_seg = deferred ? 2 * n_tables : n_tables;
+  // deferred: float columns per thread while the launch fits ~16 waves per SIMD
+  int dvec = 1;
+  if (deferred && n_max_uniq) {
+    int64_t waves = 0;
+    for (int q = 0; q < n_tables; ++q)
+      if (n_max_uniq[q] > 0)
+        waves += n_max_uniq[q] * (tables[q].ahead_uniq ? 2 : 1) * ((d + 63) / 64);
+    if (waves > 16 * 1024) dvec = 2;
+  }
   int64_t blocks = 0;
   for (int q = 0; q < n_tables; ++q) {
     const mirec_adam_table& t = tables[q];
@@ -680,7 +692,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = kAdamThreads / d;
+      const int rpb = kAdamThreads / (d / dvec);
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
@@ -712,8 +724,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
                          step_off, k);                                                       \
     else if (sched == Sched::kDeferred)                                                      \
-      hipLaunchKernelGGL(adam_deferred_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base, \
-                         step_off, k);                                                       \
+      hipLaunchKernelGGL((dvec == 2 ? adam_deferred_kernel<DD, float2>                       \
+                                    : adam_deferred_kernel<DD, float>),                      \
+                         grd, blk, 0, st, tabs, consts, step_base, step_off, k);             \
     else if (DD >= 64)                                                                       \
       hipLaunchKernelGGL(adam_flush_row_kernel<(DD >= 64 ? DD : 64)>, grd, blk, 0, st, tabs, \
                          consts, step_base, step_off, k);                                    \

@@ -331,7 +331,8 @@ def test_fused_adam_dense_step_matches_torch(dev):
 
 
 @pytest.mark.parametrize('d,beta1,wd', [(128, 0.9, 0.0), (32, 0.3, 0.01), (64, 0.9, 0.0)])
-def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
+@pytest.mark.parametrize('wide', [False, True])    # True: a row bound that selects float2 columns
+def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide):
     """The deferred schedule (touch + replay, flushes at irregular steps) leaves
     p, m, v bit-identical to the streamed dense Adam over every row."""
     from recbole_amd import ops
@@ -379,8 +380,8 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
                                   ahead=aheads[s][q] if s + 1 < steps else None))
             tabs = ops.adam_tables(specs)
             ops.adam_multi(tabs, d, consts, base, 0, schedule,
-                           n_max_uniq=[b[0].numel() for b in batch], beta1=beta1,
-                           weight_decay=wd)
+                           n_max_uniq=[max(b[0].numel(), 40000 if wide else 0) for b in batch],
+                           beta1=beta1, weight_decay=wd)
             base += 1
             if s in flush_at:
                 ops.adam_multi(tabs, d, consts, base, 0, 'flush', beta1=beta1, weight_decay=wd)
@@ -403,7 +404,8 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd):
 
 
 @pytest.mark.parametrize('lr', [1e-3, 3e-2])
-def test_adam_deferred_long_idle_rows_bitwise(dev, lr):
+@pytest.mark.parametrize('wide', [False, True])
+def test_adam_deferred_long_idle_rows_bitwise(dev, lr, wide):
     """Rows idle for hundreds of steps (where the deferred replay stops updating p
     once its increments provably round away) end bit-identical to the streamed
     dense Adam that updates them every step."""
@@ -432,7 +434,7 @@ def test_adam_deferred_long_idle_rows_bitwise(dev, lr):
             tabs = ops.adam_tables([dict(p=P[q], m=M[q], v=V[q], rows=keys[s][q][1].to(dev),
                                          segs=segs[s][q], last=last[q]) for q in range(2)])
             ops.adam_multi(tabs, d, consts, base, 0, schedule,
-                           n_max_uniq=[k.numel() for k, _ in keys[s]])
+                           n_max_uniq=[max(k.numel(), 40000 if wide else 0) for k, _ in keys[s]])
             base += 1
         if schedule == 'deferred':
             ops.adam_multi(tabs, d, consts, base, 0, 'flush')
