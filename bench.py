@@ -92,8 +92,27 @@ def pmc_bytes(substr):
     data = json.load(open(files[-1]))
     for k, v in data.items():
         if substr in k:
-            return v['hbm_bytes_per_launch'], os.path.basename(files[-1])
+            return v.get('hbm_bytes_per_launch'), os.path.basename(files[-1])
     return None, None
+
+
+def pmc_valu_insts(substr):
+    """(VALU, transcendental f32) wave-instructions per launch of the kernel whose
+    name contains `substr` (SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32 pass of
+    tools/prof_pmc.sh), or (None, None)."""
+    path = os.path.join(ROOT, 'profiles', 'r01_pmc.json')
+    if not os.path.exists(path):
+        return None, None
+    for k, v in json.load(open(path)).items():
+        if substr in k and 'sq_insts_valu_per_launch' in v:
+            return v['sq_insts_valu_per_launch'], v.get('sq_insts_valu_trans_f32_per_launch', 0.0)
+    return None, None
+
+
+# VALU issue model (MI355X_MICROARCH.md, per-instruction cycle constants): a wave64
+# f32 VALU instruction takes 2 cycles of its SIMD at full rate, a transcendental
+# (v_sqrt / v_rcp) 8; 1,024 SIMDs at 2.4 GHz.
+SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
 ADAM_FLOPS = 13      # IEEE fp32 ops per element per Adam step in torch's formula (see DESIGN.md)
@@ -125,11 +144,14 @@ def roofline(step, events, uniq, d, M):
            'achieved': round(bpr_bytes / t_bpr / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
            'frac': round(bpr_bytes / t_bpr / 1e9 / HBM_PEAK_GBS, 4),
            'bytes_per_launch': bpr_bytes, 'avg_launch_us': kernels_us['bpr']}
-    t_adam = sum(per.get('adam', [])) + sum(per.get('flush', []))
+    # K5 kernel time: touched updates + look-ahead catch-ups (side stream, beside K3) + flush
+    t_adam = sum(per.get('adam', [])) + sum(per.get('ahead', [])) + sum(per.get('flush', []))
     flops = (step.nU + step.nI) * d * M * ADAM_FLOPS
     tf = flops / t_adam / 1e12
-    name = ('K5 deferred dense Adam: adam_deferred_kernel<%d> x %d + adam_flush_kernel<%d> x %d'
-            % (d, len(per.get('adam', [])), d, len(per.get('flush', []))))
+    flush_k = 'adam_flush_row_kernel' if d >= 64 else 'adam_flush_kernel'
+    name = ('K5 deferred dense Adam: adam_deferred_kernel<%d, float> x %d + %s<%d> x %d'
+            % (d, len(per.get('adam', [])) + len(per.get('ahead', [])), flush_k, d,
+               len(per.get('flush', []))))
     if step.adam_mode == 'streamed':
         name = f'K5 adam_multi_kernel<{d}> x {len(per.get("adam", []))} (streamed dense Adam)'
     adam = {'kernel': name, 'bound': 'valu', 'achieved': round(tf, 2),
@@ -138,10 +160,23 @@ def roofline(step, events, uniq, d, M):
             'window_kernel_us': round(t_adam * 1e6, 1),
             'us_per_step': round(t_adam * 1e6 / M, 2),
             'flops_formula': '(n_users + n_items) * d * steps * 13'}
-    nd, nf = len(per.get('adam', [])), len(per.get('flush', []))
+    nd, nf = len(per.get('adam', [])) + len(per.get('ahead', [])), len(per.get('flush', []))
     if step.adam_mode == 'deferred':
-        bd, src = pmc_bytes(f'adam_deferred_kernel<{d}>')
-        bf, _ = pmc_bytes(f'adam_flush_kernel<{d}>')
+        bd, src = pmc_bytes(f'adam_deferred_kernel<{d},')
+        bf, _ = pmc_bytes(f'{flush_k}<{d}>')
+        vd, td = pmc_valu_insts(f'adam_deferred_kernel<{d},')
+        vf, tf_ = pmc_valu_insts(f'{flush_k}<{d}>')
+        if vd is not None and vf is not None:
+            insts = nd * vd + nf * vf
+            trans = nd * td + nf * tf_
+            t_issue = ((insts - trans) * 2 + trans * 8) / SIMDS / CLOCK_HZ
+            adam.update({'valu_insts_per_window': int(insts),
+                         'valu_insts_per_element_step': round(
+                             insts * 64 / ((step.nU + step.nI) * d * M), 2),
+                         'valu_issue_bound_us': round(t_issue * 1e6, 1),
+                         'valu_issue_frac': round(t_issue / t_adam, 4),
+                         'valu_issue_model': 'PMC SQ_INSTS_VALU x 2 cyc (+6 per '
+                                             'SQ_INSTS_VALU_TRANS_F32) / 1024 SIMDs / 2.4 GHz'})
         if bd is not None and bf is not None:
             adam.update({'traffic': int(nd * bd + nf * bf), 'traffic_unit': 'HBM bytes per window',
                          'traffic_source': src,

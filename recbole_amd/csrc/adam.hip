@@ -222,6 +222,39 @@ __device__ __forceinline__ void adam_replay(V& p, V& m, V& v, int s0, int s1,
   }
 }
 
+// Increments q = RN(RN(-ss*me) / den), den = RN(RN(sqrt(ve) / bc2s) + eps), of G
+// steps x N elements. The fast path is computed for all G*N first and one wave
+// vote on its range conditions decides (a branch per step would serialise the
+// steps' chains); the library path recomputes everything.
+template <int G, int N>
+__device__ __forceinline__ void incr_steps(const float (*me)[N], const float (*ve)[N],
+                                           const StepConsts* sc, const AdamConsts& k,
+                                           float (*q)[N]) {
+  float num[G][N], den[G][N];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < G; ++j)
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      ok = ok && sqrt_fast_ok(ve[j][i]);
+      den[j][i] = div_bc2s(sqrt_rn_normal(ve[j][i]), sc[j]) + k.eps;
+      num[j][i] = (-sc[j].ss) * me[j][i];
+      ok = ok && div_fast_ok(num[j][i], den[j][i]);
+    }
+  if (__all(ok)) {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+      for (int i = 0; i < N; ++i) q[j][i] = div_rn_normal(num[j][i], den[j][i]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        q[j][i] = num[j][i] / (div_bc2s(sqrtf(ve[j][i]), sc[j]) + k.eps);
+  }
+}
+
 // ---- replay of a row that fills whole waves (s0 wave-uniform); the fast-path
 // sqrt / division it uses live in adam_math.h.
 // Zero-gradient replay of steps [s0, s1) (wd == 0, 1-b1 < 0.5) for a thread whose
@@ -276,32 +309,9 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
   };
   // full increments of one step for every element: q = RN(RN(-ss*me) / den)
   auto incr = [&](const float* me, const float* ve, const StepConsts& sc, float* q) {
-    bool fast = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) fast = fast && sqrt_fast_ok(ve[i]);
-    float sq[N];
-    if (__all(fast)) {
-#pragma unroll
-      for (int i = 0; i < N; ++i) sq[i] = sqrt_rn_normal(ve[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < N; ++i) sq[i] = sqrtf(ve[i]);
-    }
-    float num[N], den[N];
-    bool fdiv = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      den[i] = div_bc2s(sq[i], sc) + k.eps;
-      num[i] = (-sc.ss) * me[i];
-      fdiv = fdiv && div_fast_ok(num[i], den[i]);
-    }
-    if (__all(fdiv)) {
-#pragma unroll
-      for (int i = 0; i < N; ++i) q[i] = div_rn_normal(num[i], den[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < N; ++i) q[i] = num[i] / den[i];
-    }
+    incr_steps<1, N>(reinterpret_cast<const float(*)[N]>(me),
+                     reinterpret_cast<const float(*)[N]>(ve), &sc, k,
+                     reinterpret_cast<float(*)[N]>(q));
   };
   // one step, state machine of adam_replay (test every step while skipping,
   // else at `test`)
@@ -329,6 +339,8 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
     skipping = vanish;
   };
 
+  // (loading the next group's step constants under this group's arithmetic was
+  // measured slower: the scalar-load wait covers both groups' loads)
   for (; s + G <= s1; s += G) {
     StepConsts sc[G];
 #pragma unroll
@@ -359,8 +371,7 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
         mine = mine && p_update_vanishes(pc[i], me[0][i], ve[0][i], sc[0], k.eps);
       if (!__all(mine)) {                       // four full steps, increments side by side
         float q[G][N];
-#pragma unroll
-        for (int j = 0; j < G; ++j) incr(me[j], ve[j], sc[j], q[j]);
+        incr_steps<G, N>(me, ve, sc, k, q);
 #pragma unroll
         for (int j = 0; j < G; ++j)
 #pragma unroll
@@ -723,7 +734,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     if (sched == Sched::kStreamed)                                                           \
       hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
                          step_off, k);                                                       \
-    else if (sched == Sched::kDeferred)                                                      \
+    else if (deferred)                                                                       \
       hipLaunchKernelGGL((dvec == 2 ? adam_deferred_kernel<DD, float2>                       \
                                     : adam_deferred_kernel<DD, float>),                      \
                          grd, blk, 0, st, tabs, consts, step_base, step_off, k);             \

@@ -16,5 +16,10 @@ echo fetch-ok
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
   python bench.py $ARGS --no-eval > $OUT/write.log 2>&1 || { echo "write rc=$?"; exit 3; }
 echo write-ok
+# VALU issue view of the VALU-bound K5 kernels (SQ block: 4 of its 8 slots)
+timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU \
+  SQ_WAVE_CYCLES --output-format csv -d $OUT/valu -o run -- \
+  python bench.py $ARGS --no-eval > $OUT/valu.log 2>&1 || { echo "valu rc=$?"; exit 3; }
+echo valu-ok
 fi
 find $OUT -name "*.csv" | head -20

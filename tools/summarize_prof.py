@@ -39,6 +39,18 @@ def main(tag='r01', src='gpurun_out/prof', dst='profiles'):
         out[k] = {'launches': max(len(f), len(w)), 'fetch_kb': round(fkb, 1),
                   'write_kb': round(wkb, 1),
                   'hbm_bytes_per_launch': round((2 * fkb + wkb) * 1024)}
+    valu = glob.glob(os.path.join(src, 'valu', '*counter_collection.csv'))
+    if valu:                                    # per-launch means of each SQ counter
+        agg = collections.defaultdict(lambda: collections.defaultdict(float))
+        disp = collections.defaultdict(set)
+        for r in csv.DictReader(open(valu[0])):
+            agg[r['Kernel_Name']][r['Counter_Name']] += float(r['Counter_Value'])
+            disp[r['Kernel_Name']].add(r['Dispatch_Id'])
+        for k, cs in agg.items():
+            n = max(len(disp[k]), 1)
+            out.setdefault(k, {}).update(
+                {'valu_launches': n, **{c.lower() + '_per_launch': round(v / n, 1)
+                                        for c, v in cs.items()}})
     json.dump(out, open(os.path.join(dst, f'{tag}_pmc.json'), 'w'), indent=1)
     for line in open(os.path.join(src, 'trace.log')):
         if line.startswith('{"metric"'):
