@@ -534,13 +534,18 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 //               forward pass reads rows that are complete through step s.
 // `last` is read by every thread of a row before the barrier and written
 // after it (a row of D = 256 spans two waves).
+// Block of the deferred kernel: one row when a row fills whole waves, else one
+// wave of rows. Small blocks: the launch's rows differ widely in replay length,
+// and a CU takes a new block only when a whole block's waves are free.
+__host__ __device__ constexpr int deferred_block(int vpr) { return vpr > 64 ? vpr : 64; }
+
 template <int D, typename V>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
     const AdamTables tabs, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
   constexpr int VPR = D / Lanes<V>::n;              // V = float or float2 per thread
-  constexpr int RPB = kAdamThreads / VPR;           // rows per block
-  static_assert(kAdamThreads % VPR == 0, "row width");
+  constexpr int RPB = deferred_block(VPR) / VPR;    // rows per block
+  static_assert(deferred_block(VPR) % VPR == 0, "row width");
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si >> 1];
   const bool ahead = si & 1;
@@ -627,12 +632,17 @@ struct FlushVec { using T = float; };
 template <> struct FlushVec<128> { using T = float2; };
 template <> struct FlushVec<256> { using T = float4; };
 
+#ifndef MIREC_FLUSH_THREADS
+#define MIREC_FLUSH_THREADS 64
+#endif
+constexpr int kFlushRowThreads = MIREC_FLUSH_THREADS;
+
 template <int D>
-__global__ __launch_bounds__(kAdamThreads) void adam_flush_row_kernel(
+__global__ __launch_bounds__(kFlushRowThreads) void adam_flush_row_kernel(
     const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
     int step_off, AdamConsts k) {
   using V = typename FlushVec<D>::T;
-  constexpr int RPB = kAdamThreads / 64;            // rows (waves) per block
+  constexpr int RPB = kFlushRowThreads / 64;        // rows (waves) per block
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si];
   const int64_t r = ((int64_t)blockIdx.x - tabs.block_start[si]) * RPB + (threadIdx.x >> 6);
@@ -703,7 +713,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = kAdamThreads / (d / dvec);
+      const int rpb = deferred_block(d / dvec) / (d / dvec);
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
@@ -712,7 +722,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     } else {
       tabs.block_start[q] = blocks;
       const int64_t rows_per_block =
-          (sched == Sched::kFlush && d >= 64) ? kAdamThreads / 64 : kAdamRows;
+          (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64 : kAdamRows;
       blocks += (t.n_rows + rows_per_block - 1) / rows_per_block;
     }
   }
@@ -737,9 +747,11 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     else if (deferred)                                                                       \
       hipLaunchKernelGGL((dvec == 2 ? adam_deferred_kernel<DD, float2>                       \
                                     : adam_deferred_kernel<DD, float>),                      \
-                         grd, blk, 0, st, tabs, consts, step_base, step_off, k);             \
+                         grd, dim3(deferred_block(DD / dvec)), 0, st, tabs, consts,          \
+                         step_base, step_off, k);                                            \
     else if (DD >= 64)                                                                       \
-      hipLaunchKernelGGL(adam_flush_row_kernel<(DD >= 64 ? DD : 64)>, grd, blk, 0, st, tabs, \
+      hipLaunchKernelGGL(adam_flush_row_kernel<(DD >= 64 ? DD : 64)>, grd,                   \
+                         dim3(kFlushRowThreads), 0, st, tabs,                                \
                          consts, step_base, step_off, k);                                    \
     else                                                                                     \
       hipLaunchKernelGGL(adam_flush_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
