@@ -58,7 +58,7 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
 
 
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
-                   dist=None):
+                   dist=None, chunk=None):
     from recbole_amd.config import Config
     from recbole_amd.data import data_preparation
     from recbole_amd.data.dataset import Dataset
@@ -78,7 +78,8 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
     return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train,
-                                                              adam_mode=adam_mode, dist=dist)
+                                                              adam_mode=adam_mode, dist=dist,
+                                                              chunk=chunk)
 
 
 def pmc_bytes(substr):
@@ -251,6 +252,8 @@ def main():
     ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
     # diagnostic: rows per step (default 2,048 = 512 positives x 4 negatives, C2)
     ap.add_argument('--batch-rows', type=int, default=2048)
+    # diagnostic: steps per captured chunk (= deferred-Adam flush period), default 64
+    ap.add_argument('--chunk', type=int, default=None)
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -267,7 +270,7 @@ def main():
     d, neg = 128, 4
     t_setup = time.time()
     config, train, test, model, opt, step = build_workload(
-        dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode,
+        dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
         dist=tdist.group.WORLD if dist else None)
     setup_s = time.time() - t_setup
     nb = step.begin_epoch()
