@@ -14,8 +14,9 @@ resident in HBM before the timed region.
 
 Prints ONE JSON line (rank 0). With --gpus N>1 (torchrun, one rank per GPU) the
 step is data parallel: each optimizer step consumes a global batch of N x 512
-positives, rank g computes K3 on its 512, one RCCL all-gather over xGMI exchanges
-the contribution rows, and every rank applies the same dense Adam to its replica of
+positives, rank g computes K3's forward on its 512, one RCCL all-gather over xGMI
+exchanges the per-row loss coefficients (10 KB per rank), every rank rebuilds the
+global batch's gradient rows, and applies the same dense Adam to its replica of
 the tables — bit-identical to one GPU running the global batch (weak scaling: the
 per-GPU batch is fixed; value = global positives / max-over-ranks time).
 """
@@ -330,7 +331,7 @@ def main():
                                'dense Adam',
                    'global_batch': step.Bg, 'per_gpu_batch': step.B, 'train_interactions': int(
                        train.dataset.inter_num), 'parallelism': 'single' if world == 1
-                   else f'dp{world} (replicated tables, RCCL all-gather of contribution rows)',
+                   else f'dp{world} (replicated tables, RCCL all-gather of per-row loss coefficients)',
                    'exchange_graph': bool(step.use_graph)},
         'roofline': roof,
         'roofline_bpr': roof_bpr,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 4
+#define MIREC_ABI_VERSION 5
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -111,6 +111,29 @@ int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t 
                           const int64_t* neg, int64_t B, int32_t times,
                           float gamma, float grad_scale,
                           float* loss_k, float* pos_score, float* neg_score,
+                          float* gU, float* gI, void* stream);
+
+/* K3 forward only, for the data-parallel step: the same per-row computation as
+ * mirec_bpr_fwd_bwd_f32 (loss_k as there) plus coef[times*B], coef[r] = dloss/dx_r
+ * of row r = j*B + k — the ONLY per-row quantity the backward needs besides the
+ * rows themselves. Ranks exchange these (4 B per row instead of a d-float row). */
+int mirec_bpr_fwd_coef_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                           int32_t d, const int64_t* user, const int64_t* pos,
+                           const int64_t* neg, int64_t B, int32_t times,
+                           float gamma, float grad_scale, float* loss_k, float* coef,
+                           void* stream);
+
+/* The gradient rows gU / gI of mirec_bpr_fwd_bwd_f32 for a (global) batch of B
+ * positives rebuilt from the rows and the coefficients, bit-identical to what
+ * mirec_bpr_fwd_bwd_f32 writes for the same batch on one GPU. Coefficient of row
+ * (j, k): coef[(k / coef_block) * coef_stride + j * coef_block + k % coef_block]
+ * (coef_block = positives per rank, coef_stride >= times * coef_block: the rank
+ * blocks of an all-gathered exchange buffer; one block of stride times*B is the
+ * single-rank layout). Replaces the backward half of the same reference path. */
+int mirec_bpr_contrib_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                          int32_t d, const int64_t* user, const int64_t* pos,
+                          const int64_t* neg, int64_t B, int32_t times,
+                          const float* coef, int64_t coef_block, int64_t coef_stride,
                           float* gU, float* gI, void* stream);
 
 /* score[r] = <EU[u[r]], EI[i[r]]>  — BPR.predict (bpr.py:85-89), used by the

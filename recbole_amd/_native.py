@@ -63,6 +63,10 @@ SIGNATURES = {
     "mirec_gather_rows_i32idx": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
                                       c_int32, c_float, c_float, _P, _P, _P, _P, _P, _P]),
+    "mirec_bpr_fwd_coef_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
+                                       c_int32, c_float, c_float, _P, _P, _P]),
+    "mirec_bpr_contrib_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, c_int64,
+                                      c_int32, _P, c_int64, c_int64, _P, _P, _P]),
     "mirec_dot_rows_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, c_int64, _P, _P]),
     "mirec_sum_f32": (c_int, [_P, c_int64, _P, _P]),
     "mirec_segment_sort_workspace_size": (c_size_t, [c_int64, c_int64]),
@@ -112,7 +116,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class NativeError(RuntimeError):

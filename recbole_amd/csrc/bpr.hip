@@ -62,6 +62,25 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return ((a.x * b.x + a.y * b.y) + a.z * b.z) + a.w * b.w;
 }
 
+// Gradient contributions of one (positive, negative) row from its coefficient
+// dx = d loss / d (pos_score - neg_score): du += dx*p - dx*n, dp += dx*u,
+// dn = -dx*u, every product and sum rounded on its own. Shared by K3 and the
+// data-parallel rebuild (bpr_contrib_kernel), so both produce the same bits.
+__device__ __forceinline__ void pair_contrib(float4& gu, float4& gp, float4& gn, float dx,
+                                             const float4& u, const float4& p,
+                                             const float4& n) {
+#pragma clang fp contract(off)
+  gu.x += dx * p.x - dx * n.x;
+  gu.y += dx * p.y - dx * n.y;
+  gu.z += dx * p.z - dx * n.z;
+  gu.w += dx * p.w - dx * n.w;
+  gp.x += dx * u.x;
+  gp.y += dx * u.y;
+  gp.z += dx * u.z;
+  gp.w += dx * u.w;
+  gn = make_float4(-dx * u.x, -dx * u.y, -dx * u.z, -dx * u.w);
+}
+
 // D/4 lanes per positive (one float4 of every row per lane: 16-B loads, a 512-B
 // row of D = 128 is one half-wave access), 64/(D/4) positives per wave. The
 // negatives are gathered NB at a time with all their loads issued before the
@@ -73,7 +92,7 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     const int64_t* __restrict__ user, const int64_t* __restrict__ pos,
     const int64_t* __restrict__ neg, int64_t B, int times, float gamma, float grad_scale,
     float* __restrict__ loss_k, float* __restrict__ pos_score, float* __restrict__ neg_score,
-    float* __restrict__ gU, float* __restrict__ gI) {
+    float* __restrict__ gU, float* __restrict__ gI, float* __restrict__ coef) {
   constexpr int LPR = D / 4;
   constexpr int GPW = 64 / LPR;
   constexpr int NB = 4;
@@ -124,19 +143,14 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
         lsum += -logf(gs);
         const float gg = ng / gs;
         const float dx = (gg * (1.f - s)) * s;
-        gu.x += dx * p.x - dx * n[q].x;
-        gu.y += dx * p.y - dx * n[q].y;
-        gu.z += dx * p.z - dx * n[q].z;
-        gu.w += dx * p.w - dx * n[q].w;
-        gp.x += dx * u.x;
-        gp.y += dx * u.y;
-        gp.z += dx * u.z;
-        gp.w += dx * u.w;
+        float4 gn;
+        pair_contrib(gu, gp, gn, dx, u, p, n[q]);
         const int64_t r = (int64_t)j * B + k;
-        if (gI)
-          reinterpret_cast<float4*>(gI + (B + r) * D)[l] =
-              make_float4(-dx * u.x, -dx * u.y, -dx * u.z, -dx * u.w);
-        if (neg_score && l == 0) neg_score[r] = sn[q];
+        if (gI) reinterpret_cast<float4*>(gI + (B + r) * D)[l] = gn;
+        if (l == 0) {
+          if (neg_score) neg_score[r] = sn[q];
+          if (coef) coef[r] = dx;
+        }
       }
     }
   }
@@ -146,6 +160,58 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     if (loss_k) loss_k[k] = lsum;
     if (pos_score) pos_score[k] = sp;
   }
+}
+
+// Data-parallel rebuild of K3's gradient rows for a GLOBAL batch from the
+// exchanged coefficients: same lane layout, same row loads, same pair_contrib
+// sequence (negatives in order), so the rows are bit-identical to K3's on one
+// GPU. Coefficient of row (j, k): coef[(k / Bl) * stride + j * Bl + k % Bl] (the
+// per-rank blocks of the exchange buffer; Bl = positives per rank).
+template <int D>
+__global__ __launch_bounds__(256) void bpr_contrib_kernel(
+    const float* __restrict__ EU, int64_t nU, const float* __restrict__ EI, int64_t nI,
+    const int64_t* __restrict__ user, const int64_t* __restrict__ pos,
+    const int64_t* __restrict__ neg, int64_t B, int times, const float* __restrict__ coef,
+    int64_t Bl, int64_t stride, float* __restrict__ gU, float* __restrict__ gI) {
+  constexpr int LPR = D / 4;
+  constexpr int GPW = 64 / LPR;
+  constexpr int NB = 4;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR;
+  const int l = lane - g * LPR;
+  const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
+  if (k >= B) return;
+  int64_t uid = user[k], pid = pos[k];
+  uid = uid < 0 ? 0 : (uid >= nU ? nU - 1 : uid);
+  pid = pid < 0 ? 0 : (pid >= nI ? nI - 1 : pid);
+  const float4 u = reinterpret_cast<const float4*>(EU + uid * D)[l];
+  const float4 p = reinterpret_cast<const float4*>(EI + pid * D)[l];
+  const float* __restrict__ ck = coef + (k / Bl) * stride + (k % Bl);
+  float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gp = gu;
+  for (int j0 = 0; j0 < times; j0 += NB) {
+    float4 n[NB];
+    float dx[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int j = j0 + q;
+      int64_t id = j < times ? neg[(int64_t)j * B + k] : 0;
+      id = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
+      n[q] = j < times ? reinterpret_cast<const float4*>(EI + id * D)[l]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      dx[q] = j < times ? ck[(int64_t)j * Bl] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int j = j0 + q;
+      if (j < times) {
+        float4 gn;
+        pair_contrib(gu, gp, gn, dx[q], u, p, n[q]);
+        reinterpret_cast<float4*>(gI + (B + (int64_t)j * B + k) * D)[l] = gn;
+      }
+    }
+  }
+  reinterpret_cast<float4*>(gU + k * D)[l] = gu;
+  reinterpret_cast<float4*>(gI + k * D)[l] = gp;
 }
 
 // score[r] = <EU[u[r]], EI[i[r]]> — BPR.predict (bpr.py:85-89) and the
@@ -202,15 +268,17 @@ extern "C" int mirec_dot_rows_f32(const float* EU, int64_t nU, const float* EI, 
   return launch_status("mirec_dot_rows_f32");
 }
 
-extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
-                                     int32_t d, const int64_t* user, const int64_t* pos,
-                                     const int64_t* neg, int64_t B, int32_t times, float gamma,
-                                     float grad_scale, float* loss_k, float* pos_score,
-                                     float* neg_score, float* gU, float* gI, void* stream) {
+namespace {
+
+int launch_bpr(const float* EU, int64_t nU, const float* EI, int64_t nI, int32_t d,
+               const int64_t* user, const int64_t* pos, const int64_t* neg, int64_t B,
+               int32_t times, float gamma, float grad_scale, float* loss_k, float* pos_score,
+               float* neg_score, float* gU, float* gI, float* coef, void* stream,
+               const char* what) {
   if (B == 0) return 0;
   if (!EU || !EI || !user || !pos || (times > 0 && !neg) || B < 0 || times < 0 || nU <= 0 ||
       nI <= 0) {
-    set_error("mirec_bpr_fwd_bwd_f32: bad arguments");
+    set_error("%s: bad arguments", what);
     return -1;
   }
   const dim3 blk(256);
@@ -220,7 +288,8 @@ extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* E
     hipLaunchKernelGGL(bpr_fwd_bwd_kernel<DD>,                                                \
                        dim3((unsigned)((B + 4 * (256 / DD) - 1) / (4 * (256 / DD)))), blk, 0, \
                        st, EU, nU, EI, nI, user, pos,                                         \
-                       neg, B, times, gamma, grad_scale, loss_k, pos_score, neg_score, gU, gI); \
+                       neg, B, times, gamma, grad_scale, loss_k, pos_score, neg_score, gU, gI, \
+                       coef);                                                                 \
     break;
   switch (d) {
     MIREC_BPR_CASE(32)
@@ -228,9 +297,66 @@ extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* E
     MIREC_BPR_CASE(128)
     MIREC_BPR_CASE(256)
     default:
-      set_error("mirec_bpr_fwd_bwd_f32: embedding_size %d not in {32,64,128,256}", d);
+      set_error("%s: embedding_size %d not in {32,64,128,256}", what, d);
       return -1;
   }
 #undef MIREC_BPR_CASE
-  return launch_status("mirec_bpr_fwd_bwd_f32");
+  return launch_status(what);
+}
+
+}  // namespace
+
+extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                                     int32_t d, const int64_t* user, const int64_t* pos,
+                                     const int64_t* neg, int64_t B, int32_t times, float gamma,
+                                     float grad_scale, float* loss_k, float* pos_score,
+                                     float* neg_score, float* gU, float* gI, void* stream) {
+  return launch_bpr(EU, nU, EI, nI, d, user, pos, neg, B, times, gamma, grad_scale, loss_k,
+                    pos_score, neg_score, gU, gI, nullptr, stream, "mirec_bpr_fwd_bwd_f32");
+}
+
+extern "C" int mirec_bpr_fwd_coef_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                                      int32_t d, const int64_t* user, const int64_t* pos,
+                                      const int64_t* neg, int64_t B, int32_t times, float gamma,
+                                      float grad_scale, float* loss_k, float* coef,
+                                      void* stream) {
+  if (B > 0 && times > 0 && !coef) {
+    set_error("mirec_bpr_fwd_coef_f32: coef is required");
+    return -1;
+  }
+  return launch_bpr(EU, nU, EI, nI, d, user, pos, neg, B, times, gamma, grad_scale, loss_k,
+                    nullptr, nullptr, nullptr, nullptr, coef, stream, "mirec_bpr_fwd_coef_f32");
+}
+
+extern "C" int mirec_bpr_contrib_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
+                                     int32_t d, const int64_t* user, const int64_t* pos,
+                                     const int64_t* neg, int64_t B, int32_t times,
+                                     const float* coef, int64_t coef_block,
+                                     int64_t coef_stride, float* gU, float* gI, void* stream) {
+  if (B == 0) return 0;
+  if (!EU || !EI || !user || !pos || (times > 0 && (!neg || !coef)) || !gU || !gI || B < 0 ||
+      times < 0 || nU <= 0 || nI <= 0 || coef_block <= 0 || coef_stride < times * coef_block) {
+    set_error("mirec_bpr_contrib_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 blk(256);
+#define MIREC_CONTRIB_CASE(DD)                                                                \
+  case DD:                                                                                    \
+    hipLaunchKernelGGL(bpr_contrib_kernel<DD>,                                                \
+                       dim3((unsigned)((B + 4 * (256 / DD) - 1) / (4 * (256 / DD)))), blk, 0, \
+                       st, EU, nU, EI, nI, user, pos, neg, B, times, coef, coef_block,        \
+                       coef_stride, gU, gI);                                                  \
+    break;
+  switch (d) {
+    MIREC_CONTRIB_CASE(32)
+    MIREC_CONTRIB_CASE(64)
+    MIREC_CONTRIB_CASE(128)
+    MIREC_CONTRIB_CASE(256)
+    default:
+      set_error("mirec_bpr_contrib_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_CONTRIB_CASE
+  return launch_status("mirec_bpr_contrib_f32");
 }

@@ -156,6 +156,38 @@ def bpr_fwd_bwd(EU, EI, user, pos, neg, times: int, gamma: float = 1e-10,
     return o
 
 
+def bpr_fwd_coef(EU, EI, user, pos, neg, times: int, grad_scale: float, gamma: float = 1e-10):
+    """K3 forward only: (loss_k [B], coef [times*B]) with coef[r] = d loss / d x_r
+    (the data-parallel step's exchanged quantity)."""
+    B = user.numel()
+    for n_, t_ in (("user", user), ("pos", pos), ("neg", neg)):
+        _dev(t_, torch.int64, n_)
+    loss_k = torch.empty(B, dtype=torch.float32, device=EU.device)
+    coef = torch.empty(max(B * times, 1), dtype=torch.float32, device=EU.device)
+    rc = lib().mirec_bpr_fwd_coef_f32(ptr(EU), EU.shape[0], ptr(EI), EI.shape[0], EU.shape[1],
+                                      ptr(user), ptr(pos), ptr(neg), B, times, gamma,
+                                      grad_scale, ptr(loss_k), ptr(coef), stream_handle())
+    check(rc, "mirec_bpr_fwd_coef_f32")
+    return loss_k, coef[:B * times]
+
+
+def bpr_contrib(EU, EI, user, pos, neg, times: int, coef, coef_block: int | None = None,
+                coef_stride: int | None = None):
+    """Gradient rows (gU [B,d], gI [(1+times)B,d]) of a batch rebuilt from its
+    coefficients (mirec_bpr_contrib_f32); default: the single-rank layout."""
+    B, d = user.numel(), EU.shape[1]
+    _dev(coef, torch.float32, "coef")
+    block = B if coef_block is None else coef_block
+    stride = times * block if coef_stride is None else coef_stride
+    gU = torch.empty(B, d, dtype=torch.float32, device=EU.device)
+    gI = torch.empty((1 + times) * B, d, dtype=torch.float32, device=EU.device)
+    rc = lib().mirec_bpr_contrib_f32(ptr(EU), EU.shape[0], ptr(EI), EI.shape[0], d, ptr(user),
+                                     ptr(pos), ptr(neg), B, times, ptr(coef), block, stride,
+                                     ptr(gU), ptr(gI), stream_handle())
+    check(rc, "mirec_bpr_contrib_f32")
+    return gU, gI
+
+
 def dot_rows(EU, EI, u, i, out=None):
     """score[r] = <EU[u[r]], EI[i[r]]> (BPR.predict, bpr.py:85-89)."""
     _dev(EU, torch.float32, "EU")

@@ -9,7 +9,8 @@ data side (depends only on ids; runs AHEAD on a side stream, CHUNK batches per l
                                            straight into per-batch [pos | neg] key rows
   K2 segment sort  (embedding backward)   rows grouped by table row, one workgroup/batch
 model side (main stream, per batch)
-  K3 fused BPR     (bpr.py:74-83)         loss rows + per-row gradients
+  K3 fused BPR     (bpr.py:74-83)         loss rows + per-row gradients (G > 1: forward +
+                                           coefficient exchange + rebuild of the rows)
   K5 dense Adam    (optim.Adam.step)      both tables in one launch, grouped gradients
                                            summed on the fly; schedule 'deferred' (default)
                                            or 'streamed', bit-identical (see adam.hip)
@@ -88,12 +89,14 @@ class FusedBPRTrainStep(object):
 
     Data parallel over G ranks (`dist` = a torch.distributed process group, or None
     for one GPU): one optimizer step consumes a GLOBAL batch of G*B positives, rank g
-    runs K3 on positives [g*B, (g+1)*B) of it, one all-gather (RCCL over xGMI)
-    exchanges the packed contribution rows (trainer/exchange.py), and every rank
-    applies the same dense Adam to its replica of the tables. The walk and the K2
-    grouping of the global batch are computed on every rank (cheap, on the prep
-    stream), so each rank's result is bit-identical to ONE GPU running the global
-    batch. A ragged last batch is computed whole on every rank (no exchange)."""
+    runs K3's forward on positives [g*B, (g+1)*B) of it (losses + one coefficient per
+    row), one all-gather (RCCL over xGMI) exchanges those (trainer/exchange.py: 4 B per
+    row instead of a d-float gradient row), and every rank rebuilds the global batch's
+    gradient rows with the same arithmetic as K3 and applies the same Adam step. The
+    sampler walk and the grouping of the global batch are computed on every rank
+    (cheap, on the prep stream), so each rank's result is bit-identical to ONE GPU
+    running the global batch (tables and Adam state are replicas: 288 GB per GPU).
+    A ragged last batch is computed whole on every rank (no exchange)."""
 
     CHUNK = 64
 
@@ -127,10 +130,10 @@ class FusedBPRTrainStep(object):
         self.d = d
         dev = self.device
         self.layout = ExchangeLayout(G, B, T, d)
-        # packed exchange rows [G, R, d]; with G = 1 (or a ragged global batch) the
-        # same memory holds [user rows | item rows] of the whole batch
-        self.xbuf = torch.empty(max(G * self.layout.R, self.Bg * (2 + T)) * d,
-                                dtype=torch.float32, device=dev)
+        # gradient rows of the (global) batch: [user rows | item rows]
+        self.xbuf = torch.empty(self.Bg * (2 + T) * d, dtype=torch.float32, device=dev)
+        # data parallel: per-rank [losses | coefficients] blocks, all-gathered per step
+        self.xchg = torch.empty(G * self.layout.W, dtype=torch.float32, device=dev)
         self.loss_k = torch.empty(self.C * self.Bg, dtype=torch.float32, device=dev)
         deferred = adam_mode == 'deferred'
         self.slots = [_Slot(self.C, B, T, G, dev, deferred) for _ in range(2)]
@@ -193,9 +196,6 @@ class FusedBPRTrainStep(object):
                 slot.lu[:nb * B].view(nb, B).copy_(lay.local_users(users, g))
                 slot.li[:nb * (1 + T) * B].view(nb, 1 + T, B).copy_(
                     lay.local_items(slot.item_keys[:nb * KI], g))
-                up, ip = slot.u_perm[:nb * Bc], slot.i_perm[:nb * KI]
-                up.copy_(lay.user_rows(up))
-                ip.copy_(lay.item_rows(ip))
             if self.adam_mode == 'deferred':
                 ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
                 ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
@@ -240,28 +240,40 @@ class FusedBPRTrainStep(object):
         sharded = self._sharded(Bc)
         x0 = self.xbuf.data_ptr()
         loss_p = self.loss_k.data_ptr() + 4 * c * self.Bg
+        user_g = slot.user_keys.data_ptr() + 8 * c * Bc      # the (global) batch
+        keys_g = slot.item_keys.data_ptr() + 8 * c * KI
+        gU, gI = x0, x0 + 4 * Bc * d
+        rowsU, rowsI = gU, gI
         if sharded:
+            # K3 forward on the local slice -> [losses | coefficients] of this rank's
+            # block; all-gather; every rank rebuilds the global batch's gradient rows
             lay, B = self.layout, self.B
             user_p = slot.lu.data_ptr() + 8 * c * B
             keys_p = slot.li.data_ptr() + 8 * c * (1 + T) * B
-            mine = x0 + 4 * self.rank * lay.R * d
-            n_pos, gU, gI = B, mine, mine + 4 * lay.item0 * d
-            bpr_loss = mine + 4 * lay.loss0 * d
-            rowsU = rowsI = x0
-        else:
-            user_p = slot.user_keys.data_ptr() + 8 * c * Bc
-            keys_p = slot.item_keys.data_ptr() + 8 * c * KI
-            n_pos, gU, gI, bpr_loss = Bc, x0, x0 + 4 * Bc * d, loss_p
-            rowsU, rowsI = gU, gI
+            mine = self.xchg.data_ptr() + 4 * self.rank * lay.W
 
-        def bpr():
-            check(L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
-                                          self.nI, d, user_p, keys_p, keys_p + 8 * n_pos,
-                                          n_pos, T, 1e-10, self._grad_scale(Bc), bpr_loss,
-                                          None, None, gU, gI, st), 'mirec_bpr_fwd_bwd_f32')
-        self._record('bpr', stream, bpr)
-        if sharded:
+            def bpr():
+                check(L.mirec_bpr_fwd_coef_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
+                                               self.nI, d, user_p, keys_p, keys_p + 8 * B, B, T,
+                                               1e-10, self._grad_scale(Bc), mine,
+                                               mine + 4 * lay.coef0, st),
+                      'mirec_bpr_fwd_coef_f32')
+            self._record('bpr', stream, bpr)
             self._record('exchange', stream, lambda: self._exchange(c))
+
+            def contrib():
+                check(L.mirec_bpr_contrib_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
+                                              self.nI, d, user_g, keys_g, keys_g + 8 * Bc, Bc, T,
+                                              self.xchg.data_ptr() + 4 * lay.coef0, B, lay.W,
+                                              gU, gI, st), 'mirec_bpr_contrib_f32')
+            self._record('contrib', stream, contrib)
+        else:
+            def bpr():
+                check(L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
+                                              self.nI, d, user_g, keys_g, keys_g + 8 * Bc, Bc,
+                                              T, 1e-10, self._grad_scale(Bc), loss_p, None,
+                                              None, gU, gI, st), 'mirec_bpr_fwd_bwd_f32')
+            self._record('bpr', stream, bpr)
         t = self._tables
         t[0].rows, t[1].rows = rowsU, rowsI
         t[0].perm = slot.u_perm.data_ptr() + 4 * c * Bc
@@ -295,18 +307,18 @@ class FusedBPRTrainStep(object):
             self.kernel_uniq.append(torch.stack([slot.u_nu[c], slot.i_nu[c]]))
 
     def _exchange(self, c):
-        """All-gather the packed contribution rows of every rank (RCCL over xGMI),
-        then lay the G*B losses out in global positive order for chunk_finish."""
+        """All-gather every rank's [losses | coefficients] block (RCCL over xGMI: 10 KB
+        per rank at C2), then lay the G*B losses out in global positive order for
+        chunk_finish."""
         import torch.distributed as tdist
         lay = self.layout
-        full = self.xbuf[:self.G * lay.R * self.d]
-        parts = list(full.view(self.G, -1).unbind(0))
+        parts = list(self.xchg.view(self.G, lay.W).unbind(0))
         if self._backend == 'nccl':            # RCCL: in place, one collective
-            tdist.all_gather_into_tensor(full, parts[self.rank], group=self.group)
+            tdist.all_gather_into_tensor(self.xchg, parts[self.rank], group=self.group)
         else:                                  # gloo (CPU-staged; tests): list form
             tdist.all_gather(parts, parts[self.rank].clone(), group=self.group)
         self.loss_k[c * self.Bg:(c + 1) * self.Bg].view(self.G, self.B).copy_(
-            lay.gathered_losses(full.view(self.G, lay.R, self.d)))
+            lay.gathered_losses(self.xchg))
 
     def _finish(self, c0, n_steps, Bc, stream):
         """Losses of batches c0..c0+n_steps of the slot -> loss_hist; step_idx += n."""

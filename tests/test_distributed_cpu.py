@@ -1,16 +1,17 @@
 """The data-parallel exchange protocol on CPU (gloo, world size 2).
 
-Each rank computes the per-contribution gradient rows of ITS slice of a global
-BPR batch (torch-CPU autograd with the global-batch mean, the oracle's model),
-packs them in the trainer/exchange.py layout, all-gathers, and sums every table
-row's contributions through the GLOBAL batch's grouping remapped to packed rows.
-The result must equal — bit for bit — the same grouped sums of one process that
-computed the whole global batch; this is what makes the fused GPU step with G
-ranks bit-identical to one GPU running the global batch."""
+Each rank computes, for ITS slice of a global BPR batch, the per-row coefficients
+coef_r = d loss / d (pos_score - neg_score) (torch-CPU autograd with the global-batch
+mean, the oracle's model) and the per-positive losses, packs them in the
+trainer/exchange.py layout, all-gathers, and rebuilds the gradient rows of the
+GLOBAL batch from the rows and the gathered coefficients (the arithmetic of
+mirec_bpr_contrib_f32), then sums every table row's contributions through the
+global batch's grouping. The result must equal — bit for bit — the same grouped
+sums of one process that computed the whole global batch; this is what makes the
+fused GPU step with G ranks bit-identical to one GPU running the global batch."""
 import os
 
 import numpy as np
-import pytest
 import torch
 import torch.distributed as tdist
 import torch.multiprocessing as mp
@@ -29,26 +30,42 @@ def _batch():
     return EU, EI, users, items
 
 
-def _contrib_rows(EU, EI, users, pos, neg, R_total):
-    """d loss / d (gathered rows) of the reference's BPR (bpr.py:74-83, loss.py:48)
-    for positives users[k], pos[k], neg[j*n + k]; mean over the GLOBAL R_total rows."""
+def _coef(EU, EI, users, pos, neg, R_total):
+    """Per-row d loss / d x and per-positive losses of the reference's BPR
+    (bpr.py:74-83, loss.py:48) for rows (users[k], pos[k], neg[j*n + k]), mean over
+    the GLOBAL R_total rows."""
     n = users.numel()
-    u = EU[users].clone().requires_grad_()
-    p = EI[pos].clone().requires_grad_()
-    q = EI[neg].clone().requires_grad_()
+    u, p, q = EU[users], EI[pos], EI[neg]
     ur, pr = u.repeat(T, 1), p.repeat(T, 1)
-    x = (ur * pr).sum(-1) - (ur * q).sum(-1)
-    loss = -torch.log(1e-10 + torch.sigmoid(x)).sum() / R_total
-    loss.backward()
-    return u.grad, torch.cat([p.grad, q.grad]).view(1 + T, n, D)
+    x = ((ur * pr).sum(-1) - (ur * q).sum(-1)).detach().requires_grad_()
+    per_row = -torch.log(1e-10 + torch.sigmoid(x))
+    (per_row.sum() / R_total).backward()
+    return x.grad.view(T, n), per_row.detach().view(T, n).sum(0)
 
 
-def _grouped(rows, keys, perm_rows, n_rows):
+def _rows(EU, EI, users, pos, neg, coef):
+    """Gradient rows from the coefficients, in the order of mirec_bpr_contrib_f32:
+    du = sum_j (c*p - c*n_j), dp = sum_j c*u, dn_j = -c*u."""
+    n = users.numel()
+    u, p = EU[users], EI[pos]
+    q = EI[neg].view(T, n, D)
+    gu = torch.zeros(n, D)
+    gp = torch.zeros(n, D)
+    gn = torch.empty(T, n, D)
+    for j in range(T):
+        c = coef[j].unsqueeze(1)
+        gu = gu + (c * p - c * q[j])
+        gp = gp + c * u
+        gn[j] = -c * u
+    return gu, torch.cat([gp.unsqueeze(0), gn]).view(1 + T, n, D)
+
+
+def _grouped(rows, keys, n_rows):
     """Row sums in the order of a stable sort of `keys` (K2's grouping)."""
     order = np.argsort(keys.numpy(), kind='stable')
     out = torch.zeros(n_rows, D)
     for c in order:
-        out[keys[c]] += rows[perm_rows[c]]
+        out[keys[c]] += rows[c]
     return out
 
 
@@ -59,35 +76,39 @@ def _worker(rank, port, q):
     lay = ExchangeLayout(G, B, T, D)
     lu = lay.local_users(users, rank).reshape(-1)
     li = lay.local_items(items, rank).reshape(1 + T, B)
-    gU, gI = _contrib_rows(EU, EI, lu, li[0], li[1:].reshape(-1), G * B * T)
-    xbuf = torch.zeros(G, lay.R, D)
-    xbuf[rank, :B] = gU
-    xbuf[rank, lay.item0:lay.loss0] = gI.reshape(-1, D)
-    parts = list(xbuf.unbind(0))
+    coef, loss = _coef(EU, EI, lu, li[0], li[1:].reshape(-1), G * B * T)
+    buf = torch.zeros(G, lay.W)
+    buf[rank, :B] = loss
+    buf[rank, lay.coef0:] = coef.reshape(-1)
+    parts = list(buf.unbind(0))
     tdist.all_gather(parts, parts[rank].clone())
-    flat = xbuf.view(-1, D)
-    cu = torch.arange(G * B, dtype=torch.int32)
-    ci = torch.arange((1 + T) * G * B, dtype=torch.int32)
-    sumU = _grouped(flat, users, lay.user_rows(cu).long(), NU)
-    sumI = _grouped(flat, items, lay.item_rows(ci).long(), NI)
-    q.put((rank, sumU, sumI))
+    cg = lay.coef_global(buf).view(T, G * B)
+    gU, gI = _rows(EU, EI, users, items[:G * B], items[G * B:], cg)
+    sumU = _grouped(gU, users, NU)
+    sumI = _grouped(gI.reshape(-1, D), items, NI)
+    q.put((rank, sumU, sumI, lay.gathered_losses(buf).reshape(-1).clone()))
     tdist.destroy_process_group()
 
 
-def test_exchange_layout_remaps_are_bijections():
+def test_exchange_layout_blocks():
     lay = ExchangeLayout(3, 5, 2, 4)
-    u = lay.user_rows(torch.arange(15)).tolist()
-    i = lay.item_rows(torch.arange(45)).tolist()
-    assert len(set(u) | set(i)) == 60
-    assert all(0 <= r < 3 * lay.R for r in u + i)
-    assert all(lay.loss0 > r % lay.R for r in u + i)       # never the loss rows
+    buf = torch.arange(3 * lay.W, dtype=torch.float32)
+    assert lay.gathered_losses(buf).reshape(-1).tolist() == \
+        [g * lay.W + k for g in range(3) for k in range(5)]
+    cg = lay.coef_global(buf).view(2, 15)
+    # global row (j, g*B + k) <- rank g's local coefficient j*B + k
+    for j in range(2):
+        for g in range(3):
+            for k in range(5):
+                assert cg[j, g * 5 + k] == g * lay.W + lay.coef0 + j * 5 + k
 
 
 def test_two_rank_exchange_equals_global_batch():
     EU, EI, users, items = _batch()
-    gU, gI = _contrib_rows(EU, EI, users, items[:G * B], items[G * B:], G * B * T)
-    refU = _grouped(gU, users, torch.arange(G * B), NU)
-    refI = _grouped(gI.reshape(-1, D), items, torch.arange((1 + T) * G * B), NI)
+    coef, loss = _coef(EU, EI, users, items[:G * B], items[G * B:], G * B * T)
+    gU, gI = _rows(EU, EI, users, items[:G * B], items[G * B:], coef)
+    refU = _grouped(gU, users, NU)
+    refI = _grouped(gI.reshape(-1, D), items, NI)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = 29500 + os.getpid() % 1000
@@ -98,6 +119,7 @@ def test_two_rank_exchange_equals_global_batch():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, sumU, sumI in got:
+    for rank, sumU, sumI, losses in got:
         assert torch.equal(sumU, refU), rank
         assert torch.equal(sumI, refI), rank
+        assert torch.equal(losses, loss), rank

@@ -249,6 +249,37 @@ def test_bpr_fwd_bwd_vs_torch_autograd(dev, d, times, B):
     torch.testing.assert_close(dEI.cpu(), m.item_embedding.weight.grad, rtol=RTOL, atol=ATOL)
 
 
+@pytest.mark.parametrize('d,times', [(32, 1), (128, 4), (256, 7)])
+def test_bpr_coef_exchange_rebuild_bitwise(dev, d, times):
+    """Data-parallel K3: per-rank forward (losses + coefficients) on slices of a
+    global batch, the coefficient blocks concatenated as the all-gather leaves them,
+    and the rebuild of the global batch's gradient rows must equal — bit for bit —
+    the fused K3 on the global batch (losses too)."""
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(d + times)
+    G, B, nU, nI = 4, 37, 50, 90
+    EU = (torch.randn(nU, d, generator=g) * 0.1).to(dev)
+    EI = (torch.randn(nI, d, generator=g) * 0.1).to(dev)
+    users = torch.randint(0, nU, (G * B,), generator=g).to(dev)
+    items = torch.randint(0, nI, ((1 + times) * G * B,), generator=g).to(dev)
+    gs = 1.0 / (G * B * times)
+    ref = ops.bpr_fwd_bwd(EU, EI, users, items[:G * B], items[G * B:], times, grad_scale=gs)
+    W = (1 + times) * B
+    buf = torch.empty(G, W, device=dev)
+    it = items.view(1 + times, G, B)
+    for r in range(G):
+        lu = users.view(G, B)[r].contiguous()
+        li = it[:, r, :].contiguous()
+        loss, coef = ops.bpr_fwd_coef(EU, EI, lu, li[0].contiguous(),
+                                      li[1:].reshape(-1).contiguous(), times, gs)
+        buf[r, :B] = loss
+        buf[r, B:] = coef
+    gU, gI = ops.bpr_contrib(EU, EI, users, items[:G * B].contiguous(),
+                             items[G * B:].contiguous(), times, buf.view(-1)[B:], B, W)
+    assert torch.equal(gU, ref['gU']) and torch.equal(gI, ref['gI'])
+    assert torch.equal(buf[:, :B].reshape(-1), ref['loss_k'])
+
+
 def test_bpr_extreme_scores_no_nan(dev):
     from recbole_amd import ops
     d = 64
