@@ -661,6 +661,35 @@ __global__ __launch_bounds__(kFlushRowThreads) void adam_flush_row_kernel(
   if ((threadIdx.x & 63) == 0) T.last[r] = target;
 }
 
+// Flush of a width-1 table (DeepFM's first-order [V, 1] weights): one row per
+// lane; the rows of a wave lag by different step counts, so the general replay
+// (wave-uniform step loop from the wave's smallest count, lanes active from their
+// own) applies.
+__global__ __launch_bounds__(kAdamThreads) void adam_flush_scalar_kernel(
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k) {
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si];
+  const int64_t r = ((int64_t)blockIdx.x - tabs.block_start[si]) * kAdamThreads + threadIdx.x;
+  const int target = step_base[0] + step_off;
+  const bool valid = r < T.n_rows;
+  const int last = valid ? min(T.last[r], target) : target;
+  if (__all(last >= target)) return;
+  float p = 0.f, m = 0.f, v = 0.f;
+  if (last < target) {
+    p = T.p[r];
+    m = T.m[r];
+    v = T.v[r];
+  }
+  adam_replay(p, m, v, last, target, consts, k);
+  if (last < target) {
+    T.p[r] = p;
+    T.m[r] = m;
+    T.v[r] = v;
+    T.last[r] = target;
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -681,8 +710,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     set_error("%s: step constants must be 16-byte aligned", what);
     return -1;
   }
-  if (d != 4 && d != 16 && d != 32 && d != 64 && d != 128 && d != 256) {
-    set_error("%s: row width %d not in {4,16,32,64,128,256}", what, d);
+  if (d != 4 && d != 16 && d != 32 && d != 64 && d != 128 && d != 256 &&
+      !(d == 1 && sched != Sched::kStreamed)) {
+    set_error("%s: row width %d not in {4,16,32,64,128,256} (1: deferred / flush)", what, d);
     return -1;
   }
   const int VPR = d / 4;
@@ -692,7 +722,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
   tabs.n_seg = deferred ? 2 * n_tables : n_tables;
   // deferred: float columns per thread while the launch fits ~16 waves per SIMD
   int dvec = 1;
-  if (deferred && n_max_uniq) {
+  if (deferred && n_max_uniq && d >= 4) {
     int64_t waves = 0;
     for (int q = 0; q < n_tables; ++q)
       if (n_max_uniq[q] > 0)
@@ -721,8 +751,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       if (t.ahead_uniq) blocks += nb;
     } else {
       tabs.block_start[q] = blocks;
-      const int64_t rows_per_block =
-          (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64 : kAdamRows;
+      const int64_t rows_per_block = d == 1 ? kAdamThreads
+                                     : (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64
+                                                                           : kAdamRows;
       blocks += (t.n_rows + rows_per_block - 1) / rows_per_block;
     }
   }
@@ -758,6 +789,14 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                          step_off, k);                                                       \
     break;
   switch (d) {
+    case 1:
+      if (deferred)
+        hipLaunchKernelGGL((adam_deferred_kernel<1, float>), grd, dim3(deferred_block(1)), 0, st,
+                           tabs, consts, step_base, step_off, k);
+      else
+        hipLaunchKernelGGL(adam_flush_scalar_kernel, grd, blk, 0, st, tabs, consts, step_base,
+                           step_off, k);
+      break;
     MIREC_ADAM_SCHED(4)
     MIREC_ADAM_SCHED(16)
     MIREC_ADAM_SCHED(32)

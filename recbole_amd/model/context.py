@@ -155,11 +155,16 @@ class _CtxFMFn(torch.autograd.Function):
                 torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
                 + off.unsqueeze(1))
             ctx.segs = h.catch_up(T, keys)
+            h1 = getattr(T1, '_mirec_deferred', None)
+            if h1 is not None:                # the first-order [V, 1] table, same rows
+                h1.catch_up(T1, keys, ctx.segs)
         else:
             ctx.segs = None
+            h1 = None
         concat, y_fm, _ = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
         ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
         ctx.deferred_T = T if h is not None else None
+        ctx.deferred_T1 = T1 if h1 is not None else None
         ctx.save_for_backward(concat, keys)
         return concat, y_fm
 
@@ -193,7 +198,10 @@ class _CtxFMFn(torch.autograd.Function):
                 ctx.deferred_T._mirec_deferred.stash(ctx.deferred_T, grads['T'], keys, segs)
             else:
                 dT = ops.segment_scatter_add(grads['T'], segs, torch.zeros_like(T))
-            dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))
+            if ctx.deferred_T1 is not None:
+                ctx.deferred_T1._mirec_deferred.stash(ctx.deferred_T1, grads['T1'], keys, segs)
+            else:
+                dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))
         if nf:
             dEf = torch.empty_like(tables['Ef'])
             check(lib().mirec_colsum_f32(ptr(grads['Ef']), B, nf * d, ptr(dEf), stream_handle()),

@@ -55,5 +55,9 @@ class DeepFM(ContextRecommender):
 
     def deferred_tables(self):
         """Tables the trainer may run on the deferred K5 schedule (only rows a
-        batch reads are touched; the first-order [V, 1] table stays dense)."""
-        return [self.token_embedding_table.embedding.weight] if self.token_field_names else []
+        batch reads are touched): the token table [V, d] and the first-order
+        token weights [V, 1], read by the same rows."""
+        if not self.token_field_names:
+            return []
+        return [self.token_embedding_table.embedding.weight,
+                self.first_order_linear.token_embedding_table.embedding.weight]

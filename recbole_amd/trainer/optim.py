@@ -175,7 +175,7 @@ class FusedAdam(torch.optim.Optimizer):
     # lag and are completed by flush() (window end, epoch end, state_dict()). The
     # result is bit-identical to the dense Adam the reference runs over every row.
     def enable_deferred(self, params, window: int = 256):
-        """Run the deferred schedule for these 2-D parameters (width 4..256)."""
+        """Run the deferred schedule for these 2-D parameters (width 1, 4..256)."""
         params = list(params)
         if not params:
             return
@@ -186,7 +186,7 @@ class FusedAdam(torch.optim.Optimizer):
             self._dummy_i32 = torch.zeros(2, dtype=torch.int32, device=dev)
             self._dummy_f32 = torch.zeros(4, dtype=torch.float32, device=dev)
         for p in params:
-            if p.dim() != 2 or p.shape[1] not in (4, 16, 32, 64, 128, 256) or not p.is_cuda:
+            if p.dim() != 2 or p.shape[1] not in (1, 4, 16, 32, 64, 128, 256) or not p.is_cuda:
                 continue
             self._ensure_state(p)
             self._deferred[p] = {'last': torch.zeros(p.shape[0], dtype=torch.int32,
@@ -210,10 +210,12 @@ class FusedAdam(torch.optim.Optimizer):
         spec.update(kw)
         return ops.adam_tables([spec])
 
-    def catch_up(self, p, keys):
+    def catch_up(self, p, keys, segs=None):
         """Make the rows `keys` (int64, any order / duplicates) current before a
-        forward pass reads them; returns their K2 grouping."""
-        segs = ops.segment_sort(keys.contiguous(), p.shape[0])
+        forward pass reads them; returns their K2 grouping (`segs`: the grouping
+        when the caller already has it, e.g. another table read by the same keys)."""
+        if segs is None:
+            segs = ops.segment_sort(keys.contiguous(), p.shape[0])
         ds = self._dstate(p)
         r = self.n_steps - ds['t0']
         if r > 0:
