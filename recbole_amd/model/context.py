@@ -29,6 +29,16 @@ class FieldLayout:
         self.float_names = list(float_names)
         self.token_offsets = [int(x) for x in token_offsets] if len(token_names) else []
         self.n_fields = len(self.token_names) + len(self.seq_names) + len(self.float_names)
+        self._dev_offsets = {}
+
+    def offsets_on(self, device):
+        """token_offsets as an int64 device tensor (uploaded once per device: a
+        pageable host-to-device copy per step would stall the stream)."""
+        t = self._dev_offsets.get(device)
+        if t is None:
+            t = torch.as_tensor(self.token_offsets, dtype=torch.int64, device=device)
+            self._dev_offsets[device] = t
+        return t
 
 
 def _col(interaction, name, dtype):
@@ -150,7 +160,7 @@ class _CtxFMFn(torch.autograd.Function):
         keys = torch.empty(len(layout.token_names) * B, dtype=torch.int64, device=bias.device)
         h = getattr(T, '_mirec_deferred', None) if T is not None else None
         if h is not None:                     # deferred Adam: complete the rows read
-            off = torch.as_tensor(layout.token_offsets, dtype=torch.int64, device=bias.device)
+            off = layout.offsets_on(bias.device)
             keys.view(len(layout.token_names), B).copy_(
                 torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
                 + off.unsqueeze(1))
