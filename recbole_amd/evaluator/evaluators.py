@@ -8,7 +8,8 @@ import numpy as np
 import torch
 from torch.nn.utils.rnn import pad_sequence
 
-from recbole_amd.evaluator.metrics import metrics_dict, topk_metric_rows
+from recbole_amd.evaluator.metrics import (metrics_dict, pattern_codes, topk_metric_rows,
+                                           uses_patterns)
 
 topk_metrics = {m.lower(): m for m in ['Hit', 'Recall', 'MRR', 'Precision', 'NDCG', 'MAP']}
 loss_metrics = {m.lower(): m for m in ['AUC', 'RMSE', 'MAE', 'LOGLOSS']}
@@ -74,8 +75,12 @@ class TopKEvaluator(BaseEvaluator):
         """Metric reduction from the [n_users, max(topk)] positive matrix
         (evaluators.py:78-141)."""
         out = {}
-        vals = np.stack([topk_metric_rows(m.lower(), pos_idx, pos_len_list) for m in self.metrics],
-                        axis=0).mean(axis=1)
+        # one pattern-code pass for all metrics; each metric's mean over users is
+        # the same ordered reduction as the stacked [metrics, users, K] mean
+        # (axis 0 of a [users, K] matrix), without the stacked copy
+        codes = pattern_codes(pos_idx) if uses_patterns(pos_idx) else None
+        vals = [topk_metric_rows(m.lower(), pos_idx, pos_len_list, codes).mean(axis=0)
+                for m in self.metrics]
         for m, v in zip(self.metrics, vals):
             for k in self.topk:
                 out[f'{m}@{k}'] = round(v[k - 1], self.precision)

@@ -124,16 +124,28 @@ def _all_patterns(K):
     return ((codes[:, None] >> np.arange(K)) & 1).astype(bool)
 
 
-def topk_metric_rows(name, pos_index, pos_len):
+def uses_patterns(pos_index):
+    K, n = pos_index.shape[1], pos_index.shape[0]
+    return K <= _PATTERN_MAX_K and n >= (1 << K) * 4
+
+
+def pattern_codes(pos_index):
+    """Row codes sum_k hit[k] << k of a [n, K] hit matrix (the pattern-table index)."""
+    K = pos_index.shape[1]
+    return np.asarray(pos_index, dtype=np.int64) @ (np.int64(1) << np.arange(K, dtype=np.int64))
+
+
+def topk_metric_rows(name, pos_index, pos_len, codes=None):
     """metrics_dict[name](pos_index, pos_len) through the pattern table when
-    max(topk) is small; identical values either way."""
+    max(topk) is small; identical values either way. `codes`: pattern_codes of
+    pos_index when the caller evaluates several metrics of the same matrix."""
     fn = metrics_dict[name]
     K = pos_index.shape[1]
-    n = pos_index.shape[0]
-    if K > _PATTERN_MAX_K or n < (1 << K) * 4:
+    if not uses_patterns(pos_index):
         return fn(pos_index, pos_len)
     pos_len = np.asarray(pos_len)
-    codes = np.asarray(pos_index, dtype=np.int64) @ (np.int64(1) << np.arange(K, dtype=np.int64))
+    if codes is None:
+        codes = pattern_codes(pos_index)
     pats = _all_patterns(K)
     if name == 'recall':
         # cumsum of hits / pos_len: the same integer cumsum and the same division
