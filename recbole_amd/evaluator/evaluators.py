@@ -79,8 +79,17 @@ class TopKEvaluator(BaseEvaluator):
         # the same ordered reduction as the stacked [metrics, users, K] mean
         # (axis 0 of a [users, K] matrix), without the stacked copy
         codes = pattern_codes(pos_idx) if uses_patterns(pos_idx) else None
-        vals = [topk_metric_rows(m.lower(), pos_idx, pos_len_list, codes).mean(axis=0)
-                for m in self.metrics]
+
+        def one(m):
+            return topk_metric_rows(m.lower(), pos_idx, pos_len_list, codes).mean(axis=0)
+        if len(self.metrics) > 1 and pos_idx.shape[0] >= 1 << 16:
+            # 10^5+ users: the metrics are independent numpy passes (GIL released in
+            # the gathers / ufuncs), one thread each — the same values
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(min(len(self.metrics), 8)) as ex:
+                vals = list(ex.map(one, self.metrics))
+        else:
+            vals = [one(m) for m in self.metrics]
         for m, v in zip(self.metrics, vals):
             for k in self.topk:
                 out[f'{m}@{k}'] = round(v[k - 1], self.precision)
