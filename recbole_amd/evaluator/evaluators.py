@@ -95,6 +95,32 @@ class TopKEvaluator(BaseEvaluator):
                 out[f'{m}@{k}'] = round(v[k - 1], self.precision)
         return out
 
+    def evaluate_pos_idx_chunks(self, chunks, n_users):
+        """evaluate_pos_idx over (pos_idx, pos_len) row blocks arriving in user order
+        (the fused evaluator hands over each K6 launch's block while the next runs).
+        Each metric keeps a running [1, K] sum continued block by block — the same
+        sequential over-users reduction as the mean of the whole matrix (numpy's
+        axis-0 reduce of a [users, K] block, K >= 2), so the values are identical."""
+        from concurrent.futures import ThreadPoolExecutor
+        acc = {m: None for m in self.metrics}
+
+        def one(m, pos_idx, pos_len, codes):
+            rows = topk_metric_rows(m.lower(), pos_idx, pos_len, codes)
+            a = acc[m]
+            if a is not None:
+                rows = np.concatenate([a, rows])
+            acc[m] = np.add.reduce(rows, axis=0, keepdims=True)
+        with ThreadPoolExecutor(min(len(self.metrics), 8)) as ex:
+            for pos_idx, pos_len in chunks:
+                codes = pattern_codes(pos_idx) if uses_patterns(pos_idx) else None
+                list(ex.map(lambda m: one(m, pos_idx, pos_len, codes), self.metrics))
+        out = {}
+        for m in self.metrics:
+            v = acc[m][0] / n_users
+            for k in self.topk:
+                out[f'{m}@{k}'] = round(v[k - 1], self.precision)
+        return out
+
 
 class LossEvaluator(BaseEvaluator):
 

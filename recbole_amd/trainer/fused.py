@@ -487,7 +487,8 @@ class FusedBPRTrainStep(object):
         return self.end_epoch()
 
 
-def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, dp=None):
+def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, dp=None,
+                         round_users=None):
     """Trainer.evaluate for a FULL loader (trainer.py:355-412) on K6: scores,
     pad/history mask, top-K and positive flags in one kernel per user batch; only
     the [n_users, K] positive matrix returns to the host for the metric
@@ -501,6 +502,10 @@ def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, d
     n = uids.numel()
     lo, hi, blk = dp.user_block(n) if dp is not None else (0, n, n)
     flags = torch.empty(max(hi - lo, 0), K, dtype=torch.uint8, device=dev)
+    rnd = round_users or _fullsort_round_users(dev, EI.shape[1])
+    if dp is None and n > rnd and user_batch >= n and round_users != 0:
+        return _fullsort_overlapped(model, eval_data, topk_evaluator, uids, hist_ptr, hist_cols,
+                                    pos_ptr, pos_cols, EI, K, flags, rnd)
     for s in range(lo, hi, user_batch):
         e = min(hi, s + user_batch)
         Uq = model.fused_user_vectors(uids[s:e]).contiguous()
@@ -511,6 +516,48 @@ def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, d
         flags = dp.gather_rows(flags, n, blk)
     pos_idx = flags.cpu().numpy().astype(bool)
     return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
+
+
+def _fullsort_round_users(dev, d):
+    """Users of one full round of K6 workgroups (128 users each; two resident per
+    CU for d <= 128, one for d = 256): launches of this size fill the chip."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return 128 * cus * (2 if d <= 128 else 1)
+
+
+def _fullsort_overlapped(model, eval_data, topk_evaluator, uids, hist_ptr, hist_cols, pos_ptr,
+                         pos_cols, EI, K, flags, chunk):
+    """fused_full_sort_eval in round-sized K6 launches: each launch's flags go to the
+    host on a copy stream and its metric rows are reduced while the next launches
+    run (TopKEvaluator.evaluate_pos_idx_chunks: the same values as one block)."""
+    dev = flags.device
+    n = uids.numel()
+    host = torch.empty(flags.shape, dtype=torch.uint8, pin_memory=True)
+    copy_stream = torch.cuda.Stream(device=dev)
+    done = []
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        Uq = model.fused_user_vectors(uids[s:e]).contiguous()
+        ops.fullsort_topk(Uq, EI, K, hist_ptr=hist_ptr[s:e + 1], hist_cols=hist_cols,
+                          pos_ptr=pos_ptr[s:e + 1], pos_cols=pos_cols,
+                          out={'pos_flags': flags[s:e]})
+        ready = torch.cuda.Event()
+        ready.record()
+        with torch.cuda.stream(copy_stream):
+            copy_stream.wait_event(ready)
+            host[s:e].copy_(flags[s:e], non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record(copy_stream)
+        done.append((s, e, copied, Uq))
+    pl = np.asarray(eval_data.get_pos_len_list())
+
+    def blocks():
+        for s, e, copied, _ in done:
+            copied.synchronize()
+            yield host[s:e].numpy().astype(bool), pl[s:e]
+    out = topk_evaluator.evaluate_pos_idx_chunks(blocks(), n)
+    torch.cuda.current_stream(dev).wait_stream(copy_stream)
+    return out
 
 
 def fused_seq_full_sort_eval(model, eval_data, topk_evaluator):

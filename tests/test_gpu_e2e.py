@@ -145,6 +145,21 @@ def test_fused_full_sort_eval_matches_generic(tmp_path):
         assert fused[k] == pytest.approx(generic[k], abs=2e-4), k
 
 
+def test_fused_full_sort_eval_overlapped_identical(tmp_path):
+    """Round-sized K6 launches with the host metric reduction of each launch's block
+    overlapping the next (the path C2's 138 K users take) give exactly the metrics
+    of one launch and one block (round_users=0 disables the split)."""
+    from recbole_amd.evaluator import TopKEvaluator
+    from recbole_amd.trainer import Trainer
+    from recbole_amd.trainer.fused import fused_full_sort_eval
+    config, train, valid, test, model = _pipeline(tmp_path, epochs=1)
+    Trainer(config, model)._train_epoch(train, 0)
+    ev = TopKEvaluator(config, ['recall', 'mrr', 'ndcg', 'hit', 'precision', 'map'])
+    one = fused_full_sort_eval(model, test, ev, round_users=0)
+    for r in (128, 300, 4096):
+        assert fused_full_sort_eval(model, test, ev, round_users=r) == one, r
+
+
 def test_run_recbole_end_to_end(tmp_path):
     from recbole_amd.quick_start import run_recbole
     root = _write_dataset(str(tmp_path), 'synth')
