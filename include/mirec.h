@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 5
+#define MIREC_ABI_VERSION 6
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -313,6 +313,19 @@ int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float* EI, int64_
                             const int64_t* pos_ptr, const int32_t* pos_cols, int32_t K,
                             float* top_scores, int32_t* top_ids, uint8_t* pos_flags,
                             void* stream);
+
+/* mirec_fullsort_topk_f32 with the item range split over n_split workgroups per user
+ * block (partial top-K lists in the workspace, then a per-user merge by (score desc,
+ * id asc) — the same total order, so the same outputs). For launches too small to
+ * fill the chip (the last user block of an evaluation). Same reference code as
+ * mirec_fullsort_topk_f32. */
+size_t mirec_fullsort_topk_split_workspace_size(int64_t nq, int32_t K, int32_t n_split);
+int mirec_fullsort_topk_split_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,
+                                  int32_t d, const int64_t* hist_ptr, const int32_t* hist_cols,
+                                  const int64_t* pos_ptr, const int32_t* pos_cols, int32_t K,
+                                  int32_t n_split, void* ws, size_t ws_bytes,
+                                  float* top_scores, int32_t* top_ids, uint8_t* pos_flags,
+                                  void* stream);
 
 /* Plain score matrix S[q, i] = <Uq[q], EI[i]> (FP32 MFMA) for the
  * full_sort_predict API contract (flat [nq*I] scores, bpr.py:91-96). */

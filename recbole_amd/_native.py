@@ -95,6 +95,10 @@ SIGNATURES = {
     "mirec_chunk_finish": (c_int, [_P, c_int64, c_int64, c_int32, c_float, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
                                         c_int32, _P, _P, _P, _P]),
+    "mirec_fullsort_topk_split_workspace_size": (ctypes.c_size_t, [c_int64, c_int32, c_int32]),
+    "mirec_fullsort_topk_split_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,
+                                              c_int32, c_int32, _P, ctypes.c_size_t, _P, _P, _P,
+                                              _P]),
     "mirec_score_matrix_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P]),
     "mirec_spmm_csr_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
                                    _P, _P, c_int64, _P, ctypes.POINTER(RowsRef),
@@ -116,7 +120,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class NativeError(RuntimeError):

@@ -117,10 +117,15 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     const int64_t* __restrict__ hist_ptr, const int32_t* __restrict__ hist_cols,
     const int64_t* __restrict__ pos_ptr, const int32_t* __restrict__ pos_cols, int K,
     float* __restrict__ top_scores, int32_t* __restrict__ top_ids,
-    uint8_t* __restrict__ pos_flags) {
+    uint8_t* __restrict__ pos_flags, int64_t span) {
   constexpr int LDR = D + 2;
   constexpr int V4 = D / 4;
   constexpr int NPF = (32 * V4 + kFsThreads - 1) / kFsThreads;   // float4 per thread per tile
+  // item split (gridDim.y > 1): this workgroup sweeps items [ilo, ihi) and writes its
+  // partial lists (merged by fullsort_merge_kernel); span is a multiple of 32
+  const bool split = gridDim.y > 1;
+  const int64_t ilo = (int64_t)blockIdx.y * span;
+  const int64_t ihi = min(I, ilo + span);
   __shared__ __attribute__((aligned(16))) float tile[2][32 * LDR];
   __shared__ uint32_t hmask[2][128];   // history bits of the WG's 128 users over one tile
   const int lane = threadIdx.x & 63;
@@ -148,6 +153,7 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
   if (threadIdx.x < 128 && qu < nq && hist_ptr) {
     hcur = hist_ptr[qu];
     hend = hist_ptr[qu + 1];
+    while (hcur < hend && hist_cols[hcur] < ilo) ++hcur;   // sorted: skip items before the split
     if (hcur < hend) hnext = hist_cols[hcur];
   }
   auto build_mask = [&](int64_t base, uint32_t* dst) {
@@ -188,15 +194,15 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     }
   };
 
-  const int64_t ntile = (I + 31) / 32;
-  load_tile(0);
+  const int64_t ntile = (ihi - ilo + 31) / 32;
+  load_tile(ilo);
   store_tile(tile[0]);
-  build_mask(0, hmask[0]);
+  build_mask(ilo, hmask[0]);
   __syncthreads();
   int cur = 0;
   const int ul = w * 32 + j;   // this lane's user within the workgroup
   for (int64_t t = 0; t < ntile; ++t) {
-    const int64_t base = t * 32;
+    const int64_t base = ilo + t * 32;
     const bool more = t + 1 < ntile;
     if (more) load_tile(base + 32);          // global loads in flight under the MFMAs
     floatx16 acc;
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t item = base + row;
-      const bool valid = qv & (item < I) & (item != 0) & !((hm >> row) & 1u);
+      const bool valid = qv & (item < ihi) & (item != 0) & !((hm >> row) & 1u);
       ok |= (valid ? 1u : 0u) << r;
       best = fmaxf(best, valid ? acc[r] : -INFINITY);
     }
@@ -260,7 +266,17 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     const int oi = __shfl(ti[t], j + 32, 64);
     if (h == 0) topk_merge_insert<KC>(ts, ti, os, oi);
   }
-  if (h == 0 && qv) {
+  if (h == 0 && qv && split) {             // partial lists of this item range
+#pragma unroll
+    for (int t = 0; t < KC; ++t) {
+      if (t < K) {
+        const int64_t o = ((int64_t)blockIdx.y * nq + q) * K + t;
+        top_scores[o] = ts[t];
+        top_ids[o] = ti[t];
+      }
+    }
+  }
+  if (h == 0 && qv && !split) {
     const int64_t p0 = pos_ptr ? pos_ptr[q] : 0;
     const int64_t p1 = pos_ptr ? pos_ptr[q + 1] : 0;
 #pragma unroll
@@ -272,6 +288,38 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
         if (pos_flags)
           pos_flags[o] = (ti[t] >= 0 && sorted_contains(pos_cols, p0, p1, ti[t])) ? 1 : 0;
       }
+    }
+  }
+}
+
+// Merge of the item-split partial lists: per user, the K best of the S lists by
+// (score desc, id asc) — the same total order as one sweep, so the same top-K.
+template <int KC>
+__global__ __launch_bounds__(256) void fullsort_merge_kernel(
+    int64_t nq, int S, int K, const float* __restrict__ ps, const int32_t* __restrict__ pi,
+    const int64_t* __restrict__ pos_ptr, const int32_t* __restrict__ pos_cols,
+    float* __restrict__ top_scores, int32_t* __restrict__ top_ids,
+    uint8_t* __restrict__ pos_flags) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  float ts[KC];
+  int ti[KC];
+#pragma unroll
+  for (int t = 0; t < KC; ++t) { ts[t] = -INFINITY; ti[t] = -1; }
+  for (int s = 0; s < S; ++s)
+    for (int t = 0; t < K; ++t) {
+      const int64_t o = ((int64_t)s * nq + q) * K + t;
+      topk_merge_insert<KC>(ts, ti, ps[o], pi[o]);
+    }
+  const int64_t p0 = pos_ptr ? pos_ptr[q] : 0;
+  const int64_t p1 = pos_ptr ? pos_ptr[q + 1] : 0;
+#pragma unroll
+  for (int t = 0; t < KC; ++t) {
+    if (t < K) {
+      const int64_t o = q * K + t;
+      if (top_scores) top_scores[o] = ts[t];
+      if (top_ids) top_ids[o] = ti[t];
+      if (pos_flags) pos_flags[o] = (ti[t] >= 0 && sorted_contains(pos_cols, p0, p1, ti[t])) ? 1 : 0;
     }
   }
 }
@@ -343,7 +391,7 @@ extern "C" int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float*
 #define MIREC_FS(DD, KK)                                                                      \
   hipLaunchKernelGGL((fullsort_topk_kernel<DD, KK>), grd, dim3(kFsThreads), 0, st, Uq, nq, EI, \
                      I, hist_ptr, hist_cols, pos_ptr, pos_cols, K, top_scores, top_ids,        \
-                     pos_flags)
+                     pos_flags, (int64_t)((I + 31) / 32 * 32))
 #define MIREC_FS_D(DD)                                 \
   case DD:                                             \
     if (K <= 10) MIREC_FS(DD, 10);                     \
@@ -363,6 +411,65 @@ extern "C" int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float*
 #undef MIREC_FS_D
 #undef MIREC_FS
   return launch_status("mirec_fullsort_topk_f32");
+}
+
+extern "C" size_t mirec_fullsort_topk_split_workspace_size(int64_t nq, int32_t K,
+                                                          int32_t n_split) {
+  if (nq <= 0 || K <= 0 || n_split <= 0) return 256;
+  return (size_t)n_split * (size_t)nq * (size_t)K * (sizeof(float) + sizeof(int32_t)) + 256;
+}
+
+extern "C" int mirec_fullsort_topk_split_f32(const float* Uq, int64_t nq, const float* EI,
+                                             int64_t I, int32_t d, const int64_t* hist_ptr,
+                                             const int32_t* hist_cols, const int64_t* pos_ptr,
+                                             const int32_t* pos_cols, int32_t K, int32_t n_split,
+                                             void* ws, size_t ws_bytes, float* top_scores,
+                                             int32_t* top_ids, uint8_t* pos_flags, void* stream) {
+  if (nq == 0) return 0;
+  if (!Uq || !EI || nq < 0 || I <= 0 || K < 1 || K > 50 || n_split < 1 || n_split > 64 ||
+      (hist_ptr && !hist_cols) || (pos_ptr && !pos_cols) || (pos_flags && !pos_ptr)) {
+    set_error("mirec_fullsort_topk_split_f32: bad arguments");
+    return -1;
+  }
+  if (I > INT32_MAX) {
+    set_error("mirec_fullsort_topk_split_f32: item count exceeds int32");
+    return -1;
+  }
+  const size_t need = mirec_fullsort_topk_split_workspace_size(nq, K, n_split);
+  if (!ws || ws_bytes < need) {
+    set_error("mirec_fullsort_topk_split_f32: workspace %zu < %zu", ws_bytes, need);
+    return -1;
+  }
+  float* ps = (float*)ws;
+  int32_t* pi = (int32_t*)(ps + (size_t)n_split * nq * K);
+  const int64_t tiles = (I + 31) / 32;
+  const int64_t span = (tiles + n_split - 1) / n_split * 32;
+  const int S = (int)((I + span - 1) / span);
+  const dim3 grd((unsigned)((nq + 127) / 128), (unsigned)S);
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_FSS(DD, KK)                                                                     \
+  hipLaunchKernelGGL((fullsort_topk_kernel<DD, KK>), grd, dim3(kFsThreads), 0, st, Uq, nq, EI, \
+                     I, hist_ptr, hist_cols, nullptr, nullptr, K, ps, pi, nullptr, span);      \
+  hipLaunchKernelGGL((fullsort_merge_kernel<KK>), dim3((unsigned)((nq + 255) / 256)), dim3(256), \
+                     0, st, nq, S, K, ps, pi, pos_ptr, pos_cols, top_scores, top_ids, pos_flags)
+#define MIREC_FSS_D(DD)                                \
+  case DD:                                             \
+    if (K <= 10) { MIREC_FSS(DD, 10); }                \
+    else if (K <= 20) { MIREC_FSS(DD, 20); }           \
+    else { MIREC_FSS(DD, 50); }                        \
+    break;
+  switch (d) {
+    MIREC_FSS_D(32)
+    MIREC_FSS_D(64)
+    MIREC_FSS_D(128)
+    MIREC_FSS_D(256)
+    default:
+      set_error("mirec_fullsort_topk_split_f32: embedding_size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_FSS_D
+#undef MIREC_FSS
+  return launch_status("mirec_fullsort_topk_split_f32");
 }
 
 extern "C" int mirec_score_matrix_f32(const float* Uq, int64_t nq, const float* EI, int64_t I,

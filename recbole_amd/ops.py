@@ -416,7 +416,7 @@ def step_finish(loss_k, denom: float, loss_hist, step_idx):
 
 # ---------------------------------------------------------------- K6 full sort
 def fullsort_topk(Uq, EI, K: int, hist_ptr=None, hist_cols=None, pos_ptr=None, pos_cols=None,
-                  out: dict | None = None) -> dict:
+                  out: dict | None = None, n_split: int = 1) -> dict:
     _dev(Uq, torch.float32, "Uq")
     _dev(EI, torch.float32, "EI")
     nq, d = Uq.shape
@@ -432,6 +432,16 @@ def fullsort_topk(Uq, EI, K: int, hist_ptr=None, hist_cols=None, pos_ptr=None, p
     o.setdefault("ids", torch.empty(nq, K, dtype=torch.int32, device=dev))
     if pos_ptr is not None:
         o.setdefault("pos_flags", torch.empty(nq, K, dtype=torch.uint8, device=dev))
+    if n_split > 1:                      # item range split over n_split workgroups + merge
+        wsz = lib().mirec_fullsort_topk_split_workspace_size(nq, K, n_split)
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        rc = lib().mirec_fullsort_topk_split_f32(
+            ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr), ptr(hist_cols), ptr(pos_ptr),
+            ptr(pos_cols), K, n_split, ptr(ws), wsz, ptr(o["scores"]), ptr(o["ids"]),
+            ptr(o.get("pos_flags")), stream_handle())
+        check(rc, "mirec_fullsort_topk_split_f32")
+        o["_ws"] = ws
+        return o
     rc = lib().mirec_fullsort_topk_f32(ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr),
                                        ptr(hist_cols), ptr(pos_ptr), ptr(pos_cols), K,
                                        ptr(o["scores"]), ptr(o["ids"]), ptr(o.get("pos_flags")),

@@ -538,9 +538,13 @@ def _fullsort_overlapped(model, eval_data, topk_evaluator, uids, hist_ptr, hist_
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         Uq = model.fused_user_vectors(uids[s:e]).contiguous()
+        # a launch far below a round (the last one) splits the item range instead,
+        # so it does not take a full round's time for a few workgroups
+        wgs, full = -(-(e - s) // 128), chunk // 128
+        split = min(16, full // wgs) if 2 * wgs <= full else 1
         ops.fullsort_topk(Uq, EI, K, hist_ptr=hist_ptr[s:e + 1], hist_cols=hist_cols,
                           pos_ptr=pos_ptr[s:e + 1], pos_cols=pos_cols,
-                          out={'pos_flags': flags[s:e]})
+                          out={'pos_flags': flags[s:e]}, n_split=split)
         ready = torch.cuda.Event()
         ready.record()
         with torch.cuda.stream(copy_stream):

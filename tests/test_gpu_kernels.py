@@ -594,6 +594,33 @@ def test_fullsort_topk_vs_oracle(dev, nq, I, d, K):
                 o['scores'].cpu().numpy())
 
 
+@pytest.mark.parametrize('n_split', [1, 2, 3, 8])
+def test_fullsort_item_split_identical(dev, n_split):
+    """K6 with the item range split over workgroups + the per-user merge returns
+    the same scores, ids and positive flags as one sweep (history masked, ties)."""
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(n_split)
+    nq, I, d, K = 300, 1000, 64, 10
+    Uq = torch.randn(nq, d, generator=g).to(dev)
+    EI = torch.randn(I, d, generator=g).round().to(dev)       # many tied scores
+    EI[500:520] = EI[10:30]                                     # exact duplicates
+    hp, hc, pp, pc = [0], [], [0], []
+    for q in range(nq):
+        h = sorted(set(torch.randint(1, I, (q % 37,), generator=g).tolist()))
+        hc += h
+        hp.append(len(hc))
+        p = sorted(set(torch.randint(1, I, (3,), generator=g).tolist()) - set(h))
+        pc += p
+        pp.append(len(pc))
+    T64 = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)
+    T32 = lambda a: torch.tensor(a if a else [0], dtype=torch.int32, device=dev)
+    args = dict(hist_ptr=T64(hp), hist_cols=T32(hc), pos_ptr=T64(pp), pos_cols=T32(pc))
+    ref = ops.fullsort_topk(Uq, EI, K, **args)
+    got = ops.fullsort_topk(Uq, EI, K, n_split=n_split, **args)
+    for key in ('scores', 'ids', 'pos_flags'):
+        assert torch.equal(got[key], ref[key]), key
+
+
 def test_fullsort_fewer_items_than_k(dev):
     from recbole_amd import ops
     rng = np.random.default_rng(1)
