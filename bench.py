@@ -226,28 +226,67 @@ def gather_throughput(step, d, neg, B=65536, reps=20):
             'launch_us': round(t * 1e6, 1), 'positives_per_s': round(B / t, 1)}
 
 
-def cpu_baseline(train, step_obj, d, neg, steps):
+def _cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(train, step_obj, d, neg, steps, warmup=20, runs=3):
+    """SURVEY.md §8d protocol: the oracle's faithful CPU restatement of the
+    reference step, `warmup` untimed steps then `steps` timed steps, median of
+    `runs` runs, torch threads = the host's cores (capped at 16: the box's share)."""
     from oracle import cpu_baseline as cb
     users = train.dataset.inter_feat['user_id'].cpu().numpy()
     items = train.dataset.inter_feat['item_id'].cpu().numpy()
     ptr, cols = train.sampler.used_csr['train']
     threads = min(16, os.cpu_count() or 1)
-    pps, dt, used = cb.time_bpr_steps(users, items, ptr, cols, train.sampler.random_list,
-                                      step_obj.nU, step_obj.nI, d, step_obj.B, neg, steps=steps,
-                                      warmup=2, threads=threads)
-    return {'value': round(pps, 1), 'unit': 'positives/s', 'cores': used, 'kind': 'port',
-            'sample': f'{steps} C2 steps ({steps * step_obj.B} positives x {neg} negatives) of '
-                      f'the oracle restatement: Python rejection sampler + torch-CPU '
-                      f'nn.Embedding/BPRLoss/dense Adam, {dt:.1f} s'}
+    vals, dts = [], []
+    for r in range(runs):
+        pps, dt, used = cb.time_bpr_steps(users, items, ptr, cols, train.sampler.random_list,
+                                          step_obj.nU, step_obj.nI, d, step_obj.B, neg,
+                                          steps=steps, warmup=warmup, threads=threads, seed=r)
+        vals.append(pps)
+        dts.append(dt)
+    return {'value': round(float(np.median(vals)), 1), 'unit': 'positives/s', 'cores': used,
+            'kind': 'port', 'runs': [round(v, 1) for v in vals],
+            'nproc': os.cpu_count(), 'cpu_model': _cpu_model(),
+            'torch_threads': used,
+            'sample': f'median of {runs} runs of {warmup} warm-up + {steps} timed C2 steps '
+                      f'({steps * step_obj.B} positives x {neg} negatives per run) of the oracle '
+                      f'restatement: Python rejection sampler + torch-CPU nn.Embedding/BPRLoss/'
+                      f'dense Adam; {sum(dts):.1f} s timed in all'}
+
+
+def _spawn_ranks(n):
+    """`--gpus N` without a torchrun environment: start N ranks (one process per
+    GPU) with torch.distributed.run and exit with its status. This parent never
+    touches the GPU (no exec after GPU init on this pool)."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(('127.0.0.1', 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    # defaults are whole chunks (FusedBPRTrainStep.CHUNK = 64 steps per HIP graph)
+    # timed steps / warm-up steps (any values: the timed region always holds the
+    # sampler walk + grouping of every timed step, see below)
     ap.add_argument('--steps', type=int, default=256)
     ap.add_argument('--warmup', type=int, default=64)
-    ap.add_argument('--cpu-steps', type=int, default=20)
+    ap.add_argument('--cpu-steps', type=int, default=200)
+    ap.add_argument('--cpu-warmup', type=int, default=20)
+    ap.add_argument('--cpu-runs', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-eval', action='store_true')
     ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
@@ -257,9 +296,13 @@ def main():
     ap.add_argument('--chunk', type=int, default=None)
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -274,9 +317,16 @@ def main():
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
         dist=tdist.group.WORLD if dist else None)
     setup_s = time.time() - t_setup
-    nb = step.begin_epoch()
     K, W = args.steps, args.warmup
-    M = step.C - (W + K) % step.C          # measurement window: up to the next chunk end
+    if K < 1 or W < 0:
+        raise SystemExit('--steps must be >= 1 and --warmup >= 0')
+    # Chunks (one sampler-walk + grouping launch each, C steps) are cut at W, W+K and
+    # W+K+C, and the preparation of the chunk at W and of every later chunk is held
+    # until the timed region has started: the timed region holds the K4 walk and the
+    # K2 grouping of every timed step (the first timed chunk's serially, the rest on
+    # the prep stream beside the model side, as in steady state).
+    M = step.C                                 # per-kernel measurement window after it
+    nb = step.begin_epoch(cuts=(W, W + K, W + K + M), hold_prep_from=W)
     if W + K + M > nb:
         raise SystemExit(f'steps+warmup exceed one epoch ({nb} batches)')
     step.run_batches(0, W)
@@ -284,9 +334,15 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
+    marks = os.environ.get('BENCH_MARKERS') == '1'   # trace markers (tools/check_timed_window.py)
     t0 = time.perf_counter()
+    if marks:
+        torch.cuda._sleep(1)
+    step.release_prep()
     step.run_batches(W, W + K)
     step.sync_params()          # deferred schedule: every row complete inside the timed region
+    if marks:
+        torch.cuda._sleep(1)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -319,6 +375,8 @@ def main():
         'n_gpus': world,
         'steps': K,
         'warmup': W,
+        'timed_region': 'K steps incl. the sampler walk + grouping of every timed step '
+                        '(chunk prep held until t0) and the closing deferred-Adam flush',
         'ms_per_step': round(elapsed / K * 1e3, 4),
         'higher_is_better': True,
         'scaling': 'weak',
@@ -356,7 +414,8 @@ def main():
     if rank == 0 and not args.no_eval:
         result['gather_throughput'] = gather_throughput(step, d, neg)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline(train, step, d, neg, args.cpu_steps)
+        result['cpu_baseline'] = cpu_baseline(train, step, d, neg, args.cpu_steps,
+                                              args.cpu_warmup, args.cpu_runs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

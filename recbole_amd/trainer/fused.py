@@ -81,7 +81,7 @@ class _Slot(object):
         self.free = torch.cuda.Event()
         self.free_recorded = False
         self.chunk = None            # (first global batch, n batches, global batch size)
-        self.graph = None            # HIP graph of a full chunk's model-side steps
+        self.graphs = {}             # n batches -> HIP graph of that chunk's model-side steps
 
 
 class FusedBPRTrainStep(object):
@@ -146,6 +146,8 @@ class FusedBPRTrainStep(object):
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
         self.kernel_events = None   # list -> (name, start, end) HIP events (bench.py)
         self.kernel_uniq = []       # per eager step: [touched users, touched items]
+        self._plan, self._plan_starts = [], None
+        self._current = True        # no step enqueued since the last flush
         self.opt._ensure_state(self.pU)
         self.opt._ensure_state(self.pI)
         self._tables = (AdamTable * 2)()
@@ -158,11 +160,16 @@ class FusedBPRTrainStep(object):
         self._fill_tables()
 
     # ------------------------------------------------------------------ data side
-    def _chunks(self):
-        """(first global batch, batches, global batch size) per chunk."""
+    def _chunks(self, cuts=()):
+        """(first global batch, batches, global batch size) per chunk: chunks of at
+        most C full batches, starting at 0 and at every batch index in `cuts`, then
+        the ragged last batch on its own."""
         n = self._users.numel()
         full = n // self.Bg
-        out = [(b0, min(self.C, full - b0), self.Bg) for b0 in range(0, full, self.C)]
+        bounds = sorted({0, full} | {int(c) for c in cuts if 0 < int(c) < full})
+        out = []
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            out.extend((b0, min(self.C, hi - b0), self.Bg) for b0 in range(lo, hi, self.C))
         if n % self.Bg:
             out.append((full, 1, n % self.Bg))
         return out
@@ -347,24 +354,34 @@ class FusedBPRTrainStep(object):
             self._gs = float(np.float32(1.0) / np.float32(R))
         return self._gs
 
-    def _graph_for(self, slot):
-        if slot.graph is None:
+    def _graph_for(self, slot, nb):
+        """HIP graph of the model-side steps of an nb-batch chunk in `slot`
+        (captured once per (slot, nb); capture synchronizes, so begin_epoch
+        captures every size its plan uses before any batch runs)."""
+        g = slot.graphs.get(nb)
+        if g is None:
             g = torch.cuda.CUDAGraph()
             cap = torch.cuda.Stream(device=self.device)
             cap.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=cap):
-                for c in range(self.C):
-                    self._step(slot, c, self.Bg, cap, c, c + 1 < self.C)
-                self._finish(0, self.C, self.Bg, cap)
+                for c in range(nb):
+                    self._step(slot, c, self.Bg, cap, c, c + 1 < nb)
+                self._finish(0, nb, self.Bg, cap)
                 self._flush(cap)
             torch.cuda.current_stream(self.device).wait_stream(cap)
-            slot.graph = g
-        return slot.graph
+            slot.graphs[nb] = g
+        return g
 
     # ------------------------------------------------------------------ epoch API
-    def begin_epoch(self):
+    def begin_epoch(self, cuts=(), hold_prep_from=None):
         """Shuffle (reference order of RNG use), stage the epoch's Adam constants,
-        and start preparing the first chunks; returns the number of (global) batches."""
+        and start preparing the first chunks; returns the number of (global) batches.
+
+        cuts: batch indices at which a chunk must start (bench.py cuts at the
+        warm-up / timed / measurement boundaries). hold_prep_from: batch index
+        whose chunk (and every later one) is not prepared until release_prep() —
+        so a timed region that starts there contains its own chunks' sampler walk
+        and grouping."""
         data = self.data
         if data.shuffle:
             data._shuffle()                     # randperm (CPU RNG) + device reorder
@@ -379,33 +396,28 @@ class FusedBPRTrainStep(object):
             self.consts = torch.zeros(table.size, dtype=torch.float32, device=self.device)
             self.loss_hist = torch.zeros(max(nb, 1), dtype=torch.float32, device=self.device)
             for s in self.slots:
-                s.graph = None
+                s.graphs = {}
         ptrs = [(t.p, t.m, t.v) for t in self._tables]
         self._fill_tables()                    # optimizer state may have been reloaded
         if ptrs != [(t.p, t.m, t.v) for t in self._tables]:
             for s in self.slots:
-                s.graph = None
+                s.graphs = {}
         self.consts[:table.size].copy_(torch.from_numpy(table))
         self.loss_hist.zero_()
         self.step_idx.zero_()
         if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
             self.lastU.zero_()
             self.lastI.zero_()
-        if self.use_graph and nb >= self.C:
-            try:
-                for s in self.slots:            # capture up front: capture synchronizes
-                    self._graph_for(s)
-            except RuntimeError:
-                if self.G == 1:
-                    raise
-                # collectives that cannot be captured: replay the steps eagerly
-                torch.cuda.synchronize(self.device)
-                self.use_graph = False
-                for s in self.slots:
-                    s.graph = None
+        self._plan, self._plan_starts = self._chunks(cuts), None
+        if self.use_graph:                      # capture up front: capture synchronizes
+            sizes = sorted({n for _, n, Bc in self._plan if Bc == self.Bg})
+            for s in self.slots:
+                for n in sizes:
+                    self._graph_for(s, n)
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
-        self._plan = self._chunks()
         self._next_chunk = 0
+        self._prep_limit = (len(self._plan) if hold_prep_from is None
+                            else self._chunk_of(hold_prep_from))
         self._cur = None                       # chunk index being consumed
         for s in self.slots:
             s.free_recorded = False
@@ -413,9 +425,14 @@ class FusedBPRTrainStep(object):
         self._issue_prep()
         return nb
 
+    def release_prep(self):
+        """Let the chunks held by begin_epoch(hold_prep_from=...) be prepared; the
+        first is issued when run_batches enters it."""
+        self._prep_limit = len(self._plan)
+
     def _issue_prep(self):
         k = self._next_chunk
-        if k >= len(self._plan):
+        if k >= min(len(self._plan), self._prep_limit):
             return
         self._prepare(self.slots[k % 2], self._plan[k])
         self._next_chunk += 1
@@ -427,15 +444,20 @@ class FusedBPRTrainStep(object):
             prev = self.slots[self._cur % 2]
             prev.free.record(stream)
             prev.free_recorded = True
-        while self._next_chunk <= k + 1 and self._next_chunk < len(self._plan):
+        while self._next_chunk <= k + 1 and self._next_chunk < min(len(self._plan),
+                                                                     self._prep_limit):
             self._issue_prep()
+        if self._next_chunk <= k:
+            raise RuntimeError(f'chunk {k} is held (begin_epoch(hold_prep_from=...)): '
+                               'call release_prep() first')
         stream.wait_event(self.slots[k % 2].ready)
         self._cur = k
 
     def run_batches(self, b_start, b_end):
         """Enqueue global batches [b_start, b_end) in order (no host sync). Whole
-        chunks replay their captured graph; partial chunks launch eagerly, one step
-        and one loss bookkeeping launch at a time, flushing when a chunk completes."""
+        chunks replay their captured graph; a chunk entered mid-way (or timed with
+        per-kernel events) launches eagerly, one step and one loss bookkeeping launch
+        at a time, flushing when the chunk completes."""
         stream = torch.cuda.current_stream(self.device)
         b = b_start
         while b < b_end:
@@ -444,29 +466,36 @@ class FusedBPRTrainStep(object):
             self._enter_chunk(k, stream)
             slot = self.slots[k % 2]
             c0, c1 = b - b0, min(nb, b_end - b0)
-            if (self.use_graph and c0 == 0 and c1 == nb == self.C and Bc == self.Bg
-                    and self.kernel_events is None):
-                self._graph_for(slot).replay()
+            if (self.use_graph and c0 == 0 and c1 == nb and Bc == self.Bg
+                    and self.kernel_events is None and nb in slot.graphs):
+                slot.graphs[nb].replay()             # ends with the chunk's flush
+                self._current = True
             else:
                 for c in range(c0, c1):
                     self._step(slot, c, Bc, stream, 0, c + 1 < nb)
                     self._finish(c, 1, Bc, stream)
+                self._current = False
                 if c1 == nb:
                     self._flush(stream)
+                    self._current = True
             b = b0 + c1
 
     def launch_batch(self, b):
         self.run_batches(b, b + 1)
 
     def _chunk_of(self, b):
-        full = self._users.numel() // self.Bg
-        if b >= full:
-            return len(self._plan) - 1
-        return b // self.C
+        """Index of the plan chunk holding global batch b."""
+        starts = self._plan_starts
+        if starts is None or len(starts) != len(self._plan):
+            starts = self._plan_starts = np.array([c[0] for c in self._plan], dtype=np.int64)
+        return max(int(np.searchsorted(starts, b, side='right')) - 1, 0)
 
     def sync_params(self):
-        """Make the parameters current (deferred schedule: flush every row)."""
-        self._flush(torch.cuda.current_stream(self.device))
+        """Make the parameters current (deferred schedule: flush every row, unless
+        the last enqueued work was a chunk's closing flush)."""
+        if not self._current:
+            self._flush(torch.cuda.current_stream(self.device))
+            self._current = True
 
     def end_epoch(self, n_done=None):
         """Complete the parameters, account the optimizer steps and read the

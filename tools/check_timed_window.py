@@ -1,0 +1,40 @@
+"""Which kernels ran inside bench.py's timed region, from a rocprofv3 kernel trace
+of `BENCH_MARKERS=1 python bench.py ...` (two 1-cycle spin kernels mark t0 and the
+end of the timed region; they are the first two spin kernels of the run).
+
+usage: python tools/check_timed_window.py <dir with *kernel_trace.csv> [out.json]
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main(src, out=None):
+    path = glob.glob(f'{src}/**/*kernel_trace.csv', recursive=True)[0]
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
+    marks = [r for r in rows if 'spin' in r['Kernel_Name'] or 'sleep' in r['Kernel_Name']]
+    if len(marks) < 2:
+        raise SystemExit('no markers in trace (run bench.py with BENCH_MARKERS=1)')
+    t0, t1 = int(marks[0]['Start_Timestamp']), int(marks[1]['End_Timestamp'])
+    inside = collections.Counter()
+    before = collections.Counter()
+    for r in rows:
+        name = r['Kernel_Name'].split('(')[0]
+        s = int(r['Start_Timestamp'])
+        if t0 <= s <= t1:
+            inside[name] += 1
+        elif s < t0:
+            before[name] += 1
+    res = {'trace': path, 'timed_window_us': (t1 - t0) / 1e3,
+           'kernels_inside': dict(inside.most_common()),
+           'walk_launches_inside': sum(v for k, v in inside.items() if 'walk' in k),
+           'sort_launches_inside': sum(v for k, v in inside.items() if 'sort' in k)}
+    print(json.dumps(res, indent=1))
+    if out:
+        json.dump(res, open(out, 'w'), indent=1)
+
+
+if __name__ == '__main__':
+    main(*sys.argv[1:])
