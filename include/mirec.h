@@ -65,6 +65,21 @@ int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t* pr_dev,
                       int64_t* out, int64_t out_stride, int32_t* status_dev,
                       void* ws, size_t ws_bytes, void* stream);
 
+/* Successive sample_by_key_ids calls of DIFFERENT sizes in one launch (the
+ * evaluation loaders' one call per user, general_dataloader.py:210-221 ->
+ * sampler.py:246-265): call s uses keys[seg_ptr[s] .. seg_ptr[s+1]) and writes
+ * its K_s*num values (layout j*K_s + k) at out + seg_ptr[s]*num; the walk
+ * continues from call to call. seg_ptr: device int64 [n_seg+1]; K_s <=
+ * max_seg_keys; workspace = mirec_sample_walk_workspace_size(max_seg_keys, num).
+ * Same status codes as mirec_sample_walk. */
+int mirec_sample_walk_segments(const int32_t* random_list, int64_t L, int64_t* pr_dev,
+                               const int64_t* keys, const int64_t* seg_ptr, int64_t n_seg,
+                               int64_t max_seg_keys, int64_t num,
+                               const int64_t* used_ptr, const int32_t* used_cols,
+                               const uint32_t* used_bits, int64_t n_bits,
+                               int64_t n_key_space, int reject, int64_t* out,
+                               int32_t* status_dev, void* ws, size_t ws_bytes, void* stream);
+
 /* Used-id bitmap of a CSR (sampler.py:206-227 used_ids as bits):
  * bits[k * ceil(n_bits/32) + v/32] bit v%32 set iff v in used[k], v < n_bits. */
 size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits);

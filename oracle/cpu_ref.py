@@ -179,6 +179,132 @@ def c_sample_walk(random_list, pr: int, keys, num: int, used_ptr, used_cols, key
 
 
 # --------------------------------------------------------------------------
+# Dataset pipeline  (recbole/data/dataset/dataset.py, data/utils.py:59-112)
+# --------------------------------------------------------------------------
+def read_atomic_tokens(path, field):
+    """The token column `field` of an atomic file as strings, file order
+    (dataset.py:342-408: header `name:type`, tab separated)."""
+    with open(path, encoding='utf-8') as f:
+        header = f.readline().rstrip('\n').split('\t')
+        col = [h.split(':')[0] for h in header].index(field)
+        return [line.rstrip('\n').split('\t')[col] for line in f if line.strip()]
+
+
+def factorize(tokens):
+    """pd.factorize order (dataset.py:908-928): ids 1.. by first appearance, 0 = [PAD]."""
+    tok = np.asarray(tokens)
+    uniq, first, inv = np.unique(tok, return_index=True, return_inverse=True)
+    rank = np.empty(len(uniq), dtype=np.int64)
+    rank[np.argsort(first, kind='stable')] = np.arange(len(uniq))
+    return rank[inv] + 1, len(uniq) + 1
+
+
+def load_ml100k(data_dir):
+    """ml-100k as the reference's Dataset builds it for BPR
+    (properties/dataset/ml-100k.yaml): .inter + the item file's item_id;
+    filter_inter_by_user_or_item drops interactions whose item is not in the item
+    file (dataset.py:_filter_inter_by_user_or_item); no user file is loaded; then
+    remap (dataset.py:844-928): users over the inter column, items over
+    [inter column, item-file column] concatenated. Returns
+    (user ids, item ids, n_users, n_items), file order."""
+    inter = os.path.join(data_dir, 'ml-100k.inter')
+    u_tok = read_atomic_tokens(inter, 'user_id')
+    i_tok = read_atomic_tokens(inter, 'item_id')
+    item_tok = read_atomic_tokens(os.path.join(data_dir, 'ml-100k.item'), 'item_id')
+    known = set(item_tok)
+    keep = [k for k, t in enumerate(i_tok) if t in known]
+    u_tok = [u_tok[k] for k in keep]
+    i_tok = [i_tok[k] for k in keep]
+    users, n_users = factorize(u_tok)
+    items_all, n_items = factorize(i_tok + item_tok)
+    return users, items_all[:len(i_tok)], n_users, n_items
+
+
+def calcu_split_ids(tot, ratios):
+    """Dataset._calcu_split_ids (dataset.py:1258-1279): all parts but the first
+    rounded down, a non-empty part of < 1 row bumped to 1 while the first part has
+    more than one row."""
+    cnt = [int(r * tot) for r in ratios]
+    cnt[0] = tot - sum(cnt[1:])
+    for k in range(1, len(ratios)):
+        if cnt[0] <= 1:
+            break
+        if 0 < ratios[-k] * tot < 1:
+            cnt[-k] += 1
+            cnt[0] -= 1
+    return np.cumsum(cnt)[:-1]
+
+
+def ro_rs_split(users, ratios=(0.8, 0.1, 0.1)):
+    """Dataset.build for eval_setting RO_RS (dataset.py:1377-1413): one
+    torch.randperm over all rows (Interaction.shuffle, interaction.py:272-276; the
+    FIRST torch CPU draw after init_seed), then split_by_ratio grouped by user
+    (dataset.py:1281-1315): groups in first-appearance order of the shuffled table,
+    each group's rows in table order cut by calcu_split_ids. Returns the row index
+    (into the UNshuffled arrays) of each part, in part order."""
+    users = np.asarray(users)
+    n = len(users)
+    perm = torch.randperm(n).numpy()
+    ku = users[perm]
+    tot_r = sum(ratios)
+    ratios = [r / tot_r for r in ratios]
+    order = np.argsort(ku, kind='stable')                 # rows of each user in table order
+    su = ku[order]
+    starts = np.flatnonzero(np.r_[True, su[1:] != su[:-1]]) if n else np.zeros(0, np.int64)
+    sizes = np.diff(np.r_[starts, n])
+    rank = np.arange(n) - np.repeat(starts, sizes)         # position within its user group
+    first = order[starts]                                  # first table row of each group
+    group_pos = np.empty(len(starts), dtype=np.int64)
+    group_pos[np.argsort(first, kind='stable')] = np.arange(len(starts))
+    cuts = {t: calcu_split_ids(t, ratios) for t in np.unique(sizes)}
+    cut = np.stack([cuts[t] for t in sizes]) if len(sizes) else np.zeros((0, len(ratios) - 1))
+    part = (rank[:, None] >= np.repeat(cut, sizes, axis=0)).sum(1)
+    gp = np.repeat(group_pos, sizes)
+    out = []
+    for k in range(len(ratios)):
+        sel = np.flatnonzero(part == k)
+        sel = sel[np.lexsort((rank[sel], gp[sel]))]        # group order, then table order
+        out.append(perm[order[sel]])
+    return out
+
+
+def bpr_replay(model, train_users, train_items, random_list, used_ptr, used_cols, n_users,
+               B, T, n_steps, lr=1e-3, on_step=None):
+    """Trainer.fit's epochs for BPR with a uniform Sampler, from the current torch /
+    numpy RNG state: per epoch one torch.randperm of the train table
+    (GeneralNegSampleDataLoader._shuffle -> Interaction.shuffle), batches of B
+    positives (general_dataloader.py:194-197), the walk + rejection
+    (sampler.py:103-154, C restatement) continuing across batches and epochs,
+    pairwise rows (:235-241), BPR + BPRLoss + optim.Adam on torch CPU
+    (trainer.py:157-174). Stops after n_steps optimizer steps. Returns (per-step
+    losses, per-step negatives, final walk pointer)."""
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    users = torch.as_tensor(np.asarray(train_users, dtype=np.int64))
+    items = torch.as_tensor(np.asarray(train_items, dtype=np.int64))
+    pr, losses, negs, done = 0, [], [], 0
+    while done < n_steps:
+        perm = torch.randperm(len(users))              # in place: epochs compose
+        users, items = users[perm], items[perm]
+        for s in range(0, len(users), B):
+            if done == n_steps:
+                break
+            ub, ib = users[s:s + B], items[s:s + B]
+            neg, pr = c_sample_walk(random_list, pr, ub.numpy(), T, used_ptr, used_cols,
+                                    n_users, True)
+            ur, pr_, nr = pairwise_rows(ub, ib, torch.as_tensor(neg), T)
+            opt.zero_grad()
+            loss = model.calculate_loss(ur, pr_, nr)
+            losses.append(loss.item())
+            loss.backward()
+            opt.step()
+            negs.append(neg)
+            done += 1
+            if on_step is not None:
+                on_step(done, model)
+    return losses, negs, pr
+
+
+# --------------------------------------------------------------------------
 # BPR model + loss + Adam step, torch CPU fp32 (the reference's own ops)
 # --------------------------------------------------------------------------
 class BPRCPU(torch.nn.Module):
@@ -227,6 +353,57 @@ def bpr_train_steps(model: BPRCPU, batches, lr=1e-3, weight_decay=0.0):
         loss.backward()
         opt.step()
     return losses, opt
+
+
+def general_sampled_eval(user_emb, item_emb, uid_list, uid2start, uid2items_num, items_by_user,
+                         step, random_list, pr, used_ptr, used_cols, n_users, N, K, full=True):
+    """Trainer.evaluate over a GeneralNegSampleDataLoader in evaluation for BPR
+    (point-wise uni-N, whole users per batch), as written:
+      per batch of `step` users (general_dataloader.py:210-221): per user, its rows
+      (dataset sorted by user), sample_by_user_ids([u]*n_u, N) (the walk + rejection,
+      C restatement), rows repeated 1+N times with the negatives after the positives
+      (_neg_sample_by_point_wise_sampling :243-251); users concatenated;
+      BPR.predict = sum(u * i) (bpr.py:85-89) on torch CPU;
+      TopKEvaluator.collect (evaluators.py:53-76): get_score_matrix —
+      full_sort_collect's view(n_users_in_batch, -1) when 'full' is in
+      eval_setting (abstract_evaluator.py:77-95; this fork's uni1000 validation
+      keeps 'full'), else sample_collect's -inf padding — then flip + topk(K);
+      TopKEvaluator.evaluate: pos_idx = topk_idx >= shape - pos_len.
+    Returns (per-batch list of (items, scores, score matrix after flip, topk idx),
+    pos_idx [n_users, K], final walk pointer)."""
+    batches = []
+    pos_rows = []
+    for b0 in range(0, len(uid_list), step):
+        ul = uid_list[b0:b0 + step]
+        users, items, lens = [], [], []
+        for u in ul:
+            n = int(uid2items_num[u])
+            s0 = int(uid2start[u])
+            pos = np.asarray(items_by_user[s0:s0 + n], dtype=np.int64)
+            neg, pr = c_sample_walk(random_list, pr, np.full(n, u, dtype=np.int64), N,
+                                    used_ptr, used_cols, n_users, True)
+            items.append(np.concatenate([pos, neg]))
+            users.append(np.full(n * (1 + N), u, dtype=np.int64))
+            lens.append(n * (1 + N))
+        it = torch.as_tensor(np.concatenate(items))
+        us = torch.as_tensor(np.concatenate(users))
+        scores = torch.mul(user_emb[us], item_emb[it]).sum(dim=1)
+        if full:
+            mat = scores.view(len(ul), -1)
+        else:
+            mat = torch.nn.utils.rnn.pad_sequence(torch.split(scores, lens), batch_first=True,
+                                                  padding_value=-np.inf)
+            if mat.shape[1] < K:
+                m2 = torch.full((mat.shape[0], K), -np.inf)
+                m2[:, :mat.shape[1]] = mat
+                mat = m2
+        mat = torch.flip(mat, dims=[-1])
+        _, idx = torch.topk(mat, K, dim=-1)
+        pos_len = np.asarray([uid2items_num[u] for u in ul])
+        pos_rows.append(idx.numpy() >= (mat.shape[1] - pos_len).reshape(-1, 1))
+        batches.append((it.numpy(), scores, mat, idx))
+    pos_idx = np.concatenate(pos_rows) if pos_rows else np.zeros((0, K), dtype=bool)
+    return batches, pos_idx, pr
 
 
 # --------------------------------------------------------------------------

@@ -56,6 +56,9 @@ SIGNATURES = {
     "mirec_sample_walk": (c_int, [_P, c_int64, _P, _P, c_int64, c_int64, c_int64, c_int64,
                                   _P, _P, _P, c_int64, c_int64, c_int, _P, c_int64, _P, _P,
                                   c_size_t, _P]),
+    "mirec_sample_walk_segments": (c_int, [_P, c_int64, _P, _P, _P, c_int64, c_int64, c_int64,
+                                           _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
+                                           c_size_t, _P]),
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
     "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),

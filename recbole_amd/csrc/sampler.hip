@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
     int64_t num, UsedSet used, int64_t key_space, int reject, int64_t* __restrict__ out,
     int64_t out_stride, int32_t* __restrict__ status, int32_t* __restrict__ rejA_g,
-    int32_t* __restrict__ rejB_g) {
+    int32_t* __restrict__ rejB_g, const int64_t* __restrict__ seg_ptr) {
   __shared__ int scan_lds[2][kSampThreads / 64 + 1];
   __shared__ int32_t listA[kListLds];
   __shared__ int32_t listB[kListLds];
@@ -154,12 +154,15 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
   int livelock = 0;
 
   for (int64_t b = 0; b < n_batches && !livelock; ++b) {
-    const int64_t k0 = b * batch_keys;
-    const int64_t Kb = min(batch_keys, n_keys - k0);
+    // batch b = one sample_by_key_ids call: fixed-size batches, or the segments
+    // [seg_ptr[b], seg_ptr[b+1]) of the key list (output packed at k0 * num)
+    const int64_t k0 = seg_ptr ? seg_ptr[b] : b * batch_keys;
+    const int64_t Kb = seg_ptr ? seg_ptr[b + 1] - k0 : min(batch_keys, n_keys - k0);
+    if (seg_ptr && Kb == 0) continue;
     if (Kb <= 0) break;
     const int64_t total = Kb * num;
     const int64_t* __restrict__ bkeys = keys + k0;
-    int64_t* __restrict__ bout = out + b * out_stride;
+    int64_t* __restrict__ bout = out + (seg_ptr ? k0 * num : b * out_stride);
     const bool lds_lists = total <= kListLds;
     int32_t* cur = lds_lists ? listA : rejA_g;
     int32_t* nxt = lds_lists ? listB : rejB_g;
@@ -425,7 +428,7 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
   if (batch_keys * num <= kWideMin) {
     hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, st, random_list, L,
                        pr_dev, keys, n_keys, batch_keys, n_batches, num, u, n_key_space, reject,
-                       out, out_stride, status_dev, rejA, rejB);
+                       out, out_stride, status_dev, rejA, rejB, (const int64_t*)nullptr);
     return launch_status("mirec_sample_walk");
   }
   // 8-byte aligned mask words after the two lists
@@ -446,4 +449,56 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
                        masks, status_dev, rejA, rejB);
   }
   return launch_status("mirec_sample_walk");
+}
+
+// Many consecutive sample_by_key_ids calls of different sizes in one launch: call
+// s samples `num` values for keys[seg_ptr[s] .. seg_ptr[s+1]) (its values packed
+// at out + seg_ptr[s] * num, layout j * K_s + k), in call order — the walk pointer
+// continues from call to call exactly as the reference's successive calls do
+// (GeneralNegSampleDataLoader._next_batch_data in evaluation: one call per user,
+// general_dataloader.py:210-221). seg_ptr is a DEVICE int64 [n_seg + 1];
+// max_seg_keys bounds K_s (workspace = mirec_sample_walk_workspace_size(max_seg_keys, num)).
+extern "C" int mirec_sample_walk_segments(const int32_t* random_list, int64_t L, int64_t* pr_dev,
+                                          const int64_t* keys, const int64_t* seg_ptr,
+                                          int64_t n_seg, int64_t max_seg_keys, int64_t num,
+                                          const int64_t* used_ptr, const int32_t* used_cols,
+                                          const uint32_t* used_bits, int64_t n_bits,
+                                          int64_t n_key_space, int reject, int64_t* out,
+                                          int32_t* status_dev, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  if (L <= 0 || !random_list || !pr_dev || !out || !status_dev || !seg_ptr || n_seg < 0 ||
+      num < 0 || max_seg_keys < 0 || (n_seg > 0 && !keys)) {
+    set_error("mirec_sample_walk_segments: bad arguments (L=%lld)", (long long)L);
+    return -1;
+  }
+  if (n_seg == 0 || num == 0 || max_seg_keys == 0) return 0;
+  if (reject && ((!used_ptr || !used_cols) && !used_bits)) {
+    set_error("mirec_sample_walk_segments: reject=1 needs the used-id CSR or bitmap");
+    return -1;
+  }
+  if (used_bits && n_bits <= 0) {
+    set_error("mirec_sample_walk_segments: bitmap needs n_bits > 0");
+    return -1;
+  }
+  if (max_seg_keys * num > INT32_MAX) {
+    set_error("mirec_sample_walk_segments: max_seg_keys*num exceeds int32");
+    return -1;
+  }
+  const size_t need = mirec_sample_walk_workspace_size(max_seg_keys, num);
+  if (!ws || ws_bytes < need) {
+    set_error("mirec_sample_walk_segments: workspace %zu < %zu", ws_bytes, need);
+    return -1;
+  }
+  int32_t* rejA = (int32_t*)ws;
+  int32_t* rejB = rejA + max_seg_keys * num;
+  UsedSet u;
+  u.ptr = used_ptr;
+  u.cols = used_cols;
+  u.bits = used_bits;
+  u.nbits = n_bits;
+  u.words = used_bits ? (n_bits + 31) / 32 : 0;
+  hipLaunchKernelGGL(sample_walk_kernel, dim3(1), dim3(kSampThreads), 0, (hipStream_t)stream,
+                     random_list, L, pr_dev, keys, (int64_t)0, max_seg_keys, n_seg, num, u,
+                     n_key_space, reject, out, (int64_t)0, status_dev, rejA, rejB, seg_ptr);
+  return launch_status("mirec_sample_walk_segments");
 }

@@ -100,7 +100,9 @@ class TopKEvaluator(BaseEvaluator):
         (the fused evaluator hands over each K6 launch's block while the next runs).
         Each metric keeps a running [1, K] sum continued block by block — the same
         sequential over-users reduction as the mean of the whole matrix (numpy's
-        axis-0 reduce of a [users, K] block, K >= 2), so the values are identical."""
+        axis-0 reduce of a [users, K] block) for K >= 2, so the values are identical;
+        with K = 1 numpy reduces the [users, 1] matrix pairwise instead, so callers
+        take this path only for max(topk) >= 2."""
         from concurrent.futures import ThreadPoolExecutor
         acc = {m: None for m in self.metrics}
 
@@ -114,6 +116,9 @@ class TopKEvaluator(BaseEvaluator):
             for pos_idx, pos_len in chunks:
                 codes = pattern_codes(pos_idx) if uses_patterns(pos_idx) else None
                 list(ex.map(lambda m: one(m, pos_idx, pos_len, codes), self.metrics))
+        if n_users == 0 or any(acc[m] is None for m in self.metrics):
+            return self.evaluate_pos_idx(np.zeros((0, max(self.topk)), dtype=bool),
+                                         np.zeros(0, dtype=np.int64))
         out = {}
         for m in self.metrics:
             v = acc[m][0] / n_users

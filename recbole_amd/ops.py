@@ -68,6 +68,39 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
     return out
 
 
+def sample_walk_segments(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Tensor,
+                         seg_ptr: torch.Tensor, max_seg_keys: int, num: int,
+                         used_ptr: torch.Tensor | None, used_cols: torch.Tensor | None,
+                         n_key_space: int, reject: bool, used_bits: torch.Tensor | None = None,
+                         n_bits: int = 0, status: torch.Tensor | None = None) -> torch.Tensor:
+    """Successive sample_by_key_ids calls, call s over keys[seg_ptr[s]:seg_ptr[s+1]]
+    (device int64 seg_ptr), in one launch; values of call s at seg_ptr[s]*num."""
+    _dev(random_list, torch.int32, "random_list")
+    _dev(pr_dev, torch.int64, "pr_dev")
+    _dev(keys, torch.int64, "keys")
+    _dev(seg_ptr, torch.int64, "seg_ptr")
+    out = torch.empty(keys.numel() * num, dtype=torch.int64, device=keys.device)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=keys.device)
+    bits = reject and used_bits is not None
+    if reject and not bits:
+        _dev(used_ptr, torch.int64, "used_ptr")
+        _dev(used_cols, torch.int32, "used_cols")
+    if bits:
+        _dev(used_bits, torch.int32, "used_bits")
+    ws = torch.empty(lib().mirec_sample_walk_workspace_size(max(max_seg_keys, 1), max(num, 1)),
+                     dtype=torch.uint8, device=keys.device)
+    rc = lib().mirec_sample_walk_segments(
+        ptr(random_list), random_list.numel(), ptr(pr_dev), ptr(keys), ptr(seg_ptr),
+        seg_ptr.numel() - 1, max_seg_keys, num,
+        ptr(used_ptr) if reject and not bits else None,
+        ptr(used_cols) if reject and not bits else None,
+        ptr(used_bits) if bits else None, n_bits if bits else 0, n_key_space,
+        1 if reject else 0, ptr(out), ptr(status), ptr(ws), ws.numel(), stream_handle())
+    check(rc, "mirec_sample_walk_segments")
+    return out
+
+
 def used_bitmap(used_ptr: torch.Tensor, used_cols: torch.Tensor, n_keys: int,
                 n_bits: int) -> torch.Tensor:
     """Per-key used-id bitmap [n_keys, ceil(n_bits/32)] (int32 words) of a CSR."""

@@ -151,6 +151,19 @@ class AbstractSampler(object):
                                n_batches=n_batches, out=out, status=self._status, ws=ws,
                                out_stride=out_stride, used_bits=bits, n_bits=n_bits)
 
+    def launch_segments(self, keys_dev, seg_ptr_dev, max_seg_keys, num):
+        """Successive sample_by_key_ids calls (call s over keys_dev[seg_ptr[s]:
+        seg_ptr[s+1]]) in ONE launch, the walk continuing from call to call; call
+        s's values at [seg_ptr[s]*num, seg_ptr[s+1]*num) in the j*K_s + k layout."""
+        if self._rl_dev is None:
+            self.to_device(keys_dev.device)
+        up, uc = self._used_dev()
+        bits, n_bits = self._used_bits()
+        return ops.sample_walk_segments(self._rl_dev, self._pr_dev, keys_dev, seg_ptr_dev,
+                                        int(max_seg_keys), int(num), up, uc, self.n_users,
+                                        up is not None, used_bits=bits, n_bits=n_bits,
+                                        status=self._status)
+
     def sample_by_user_ids(self, user_ids, num):
         """sampler.py:246-265: empty input returns None (the reference's IndexError
         path); ids outside [0, n_users) raise ValueError."""

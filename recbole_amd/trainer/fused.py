@@ -532,7 +532,7 @@ def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, d
     lo, hi, blk = dp.user_block(n) if dp is not None else (0, n, n)
     flags = torch.empty(max(hi - lo, 0), K, dtype=torch.uint8, device=dev)
     rnd = round_users or _fullsort_round_users(dev, EI.shape[1])
-    if dp is None and n > rnd and user_batch >= n and round_users != 0:
+    if dp is None and n > rnd and user_batch >= n and round_users != 0 and K >= 2:
         return _fullsort_overlapped(model, eval_data, topk_evaluator, uids, hist_ptr, hist_cols,
                                     pos_ptr, pos_cols, EI, K, flags, rnd)
     for s in range(lo, hi, user_batch):
@@ -655,3 +655,67 @@ def fused_seq_sampled_eval(model, eval_data, topk_evaluator):
     rank = torch.cat(ranks) if ranks else torch.zeros(0, dtype=torch.int32, device=dev)
     pos_idx = (rank.unsqueeze(1) == torch.arange(K, device=dev).unsqueeze(0)).cpu().numpy()
     return topk_evaluator.evaluate_pos_idx(pos_idx, eval_data.get_pos_len_list())
+
+
+def fused_general_sampled_eval(model, eval_data, evaluator):
+    """Trainer.evaluate for a GeneralNegSampleDataLoader in evaluation (uni-N /
+    pop-N, point-wise, one batch = whole users: this fork's uni1000 validation,
+    data/utils.py:86-88) with every batch built on the device.
+
+    The reference builds each batch on the host (general_dataloader.py:210-221):
+    per user, slice its rows, sample_by_user_ids(uids, N) (one sampler call per
+    user), repeat them 1+N times with the negatives written after the positives
+    (_neg_sample_by_point_wise_sampling, :243-251), join every user/item feature
+    (unused by the general models' predict), concatenate the users, then
+    predict + evaluator.collect (trainer.py:384-409). Here one K4 launch walks the
+    batch's per-user calls in order (mirec_sample_walk_segments: the same walk,
+    the same values, the pointer advanced exactly as the calls would), the
+    [pos | negs] layout is assembled with two device scatters, and the model's
+    own predict and the evaluator's collect run on the same layout — so the
+    collected matrices are the ones the reference sequence produces on this
+    device, without the per-user host loop and the feature joins."""
+    sampler = eval_data.sampler
+    dev = model.fused_item_table().device
+    sampler.to_device(dev)
+    ds = eval_data.dataset
+    uid_f, iid_f = eval_data.uid_field, eval_data.iid_field
+    items_all = ds.inter_feat[iid_f].to(dev)
+    N = int(eval_data.neg_sample_by)
+    times = eval_data.times
+    test_bs = eval_data.config['eval_batch_size']
+    out = []
+    for start in range(0, eval_data.pr_end, eval_data.step):
+        ul = eval_data.uid_list[start:start + eval_data.step]
+        n_u = eval_data.uid2items_num[ul].astype(np.int64)
+        s_u = eval_data.uid2start[ul].astype(np.int64)
+        P = int(n_u.sum())
+        if P == 0:
+            continue
+        seg = np.r_[0, np.cumsum(n_u)]
+        # positive rows of the batch's users, user after user (dataset sorted by user)
+        rows = np.repeat(s_u - seg[:-1], n_u) + np.arange(P)
+        keys = torch.as_tensor(np.repeat(ul, n_u), dtype=torch.int64).to(dev)
+        negs = sampler.launch_segments(keys, torch.as_tensor(seg).to(dev), int(n_u.max()), N)
+        # block of user b: [its n_b positives | its n_b * N negatives], blocks in order
+        blk = np.repeat(seg[:-1] * times, n_u)                  # block start per positive
+        within = np.arange(P) - np.repeat(seg[:-1], n_u)        # positive's index in its block
+        pos_at = torch.as_tensor(blk + within).to(dev)
+        neg_blk = np.repeat(seg[:-1] * times + n_u, n_u * N)    # negatives' region start
+        neg_at = torch.as_tensor(neg_blk + np.arange(P * N) - np.repeat(seg[:-1] * N, n_u * N))
+        items = torch.empty(P * times, dtype=torch.int64, device=dev)
+        items[pos_at] = items_all[torch.as_tensor(rows).to(dev)]
+        items[neg_at.to(dev)] = negs
+        users = torch.as_tensor(np.repeat(ul, n_u * times), dtype=torch.int64).to(dev)
+        from recbole_amd.data.interaction import Interaction
+        inter = Interaction({uid_f: users, iid_f: items})
+        inter.set_additional_info(list(n_u), list(n_u * times))
+        bs = inter.length
+        if bs <= test_bs:
+            scores = model.predict(inter)
+        else:                                   # trainer.py _spilt_predict
+            scores = torch.cat([model.predict(Interaction({uid_f: users[i:i + test_bs],
+                                                           iid_f: items[i:i + test_bs]}))
+                                for i in range(0, bs, test_bs)])
+        out.append(evaluator.collect(inter, scores))
+    sampler.check_status()
+    return evaluator.evaluate(out, eval_data)

@@ -35,7 +35,8 @@ from recbole_amd.evaluator import ProxyEvaluator
 from recbole_amd.data.dataloader.sequential_dataloader import SequentialNegSampleDataLoader
 from recbole_amd.sampler import RepeatableSampler
 from recbole_amd.trainer.fused import (FusedBPRTrainStep, fused_full_sort_eval,
-                                       fused_seq_full_sort_eval, fused_seq_sampled_eval)
+                                       fused_general_sampled_eval, fused_seq_full_sort_eval,
+                                       fused_seq_sampled_eval)
 from recbole_amd.trainer.dist import DataParallelStep, active_group
 from recbole_amd.trainer.optim import FusedAdam
 from recbole_amd.utils import (DataLoaderType, InputType, calculate_valid_score, dict2str,
@@ -330,6 +331,12 @@ class Trainer(AbstractTrainer):
                 and topk is not None and len(self.evaluator.evaluators) == 1
                 and self.model.fused_item_table().is_cuda):
             return fused_seq_sampled_eval(self.model, eval_data, topk)
+        if (isinstance(eval_data, GeneralNegSampleDataLoader) and eval_data.user_inter_in_one_batch
+                and eval_data.dl_format == InputType.POINTWISE
+                and self.config['fused_eval'] is not False
+                and hasattr(self.model, 'fused_user_vectors')
+                and self.model.fused_item_table().is_cuda):
+            return fused_general_sampled_eval(self.model, eval_data, self.evaluator)
         if eval_data.dl_type == DataLoaderType.FULL:
             if self.item_tensor is None:
                 self.item_tensor = eval_data.get_item_feature().to(self.device).repeat(eval_data.step)

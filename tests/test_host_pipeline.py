@@ -80,14 +80,12 @@ def test_train_batch_order_without_shuffle():
             pr += bs
 
 
-@pytest.mark.skipif(not os.path.isdir('/root/reference/dataset/ml-100k'),
-                    reason='bundled ml-100k only exists in the build container')
 def test_ml100k_split_sizes():
     from recbole_amd.config import Config
     from recbole_amd.data import create_dataset, data_preparation
     from recbole_amd.utils import init_seed
     config = Config(model='BPR', dataset='ml-100k',
-                    config_dict={'data_path': '/root/reference/dataset/', 'use_gpu': False})
+                    config_dict={'data_path': os.path.join(ROOT, 'dataset'), 'use_gpu': False})
     init_seed(config['seed'], config['reproducibility'])
     ds = create_dataset(config)
     assert (ds.user_num, ds.item_num, ds.inter_num) == (944, 1682, 99991)
