@@ -59,12 +59,12 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
 
 
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
-                   dist=None, chunk=None):
+                   dist=None, chunk=None, sharded=False):
     from recbole_amd.config import Config
     from recbole_amd.data import data_preparation
     from recbole_amd.data.dataset import Dataset
     from recbole_amd.model.general_recommender import BPR
-    from recbole_amd.trainer.fused import FusedBPRTrainStep
+    from recbole_amd.trainer.fused import FusedBPRTrainStep, ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     from recbole_amd.utils import init_seed
     config = Config(model='BPR', dataset='synthetic-ml20m', config_dict={
@@ -78,9 +78,9 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     train, valid, test = data_preparation(config, ds)
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
-    return config, train, test, model, opt, FusedBPRTrainStep(model, opt, train,
-                                                              adam_mode=adam_mode, dist=dist,
-                                                              chunk=chunk)
+    cls = ShardedBPRTrainStep if sharded else FusedBPRTrainStep
+    return config, train, test, model, opt, cls(model, opt, train, adam_mode=adam_mode,
+                                                dist=dist, chunk=chunk)
 
 
 def pmc_bytes(substr):
@@ -148,7 +148,8 @@ def roofline(step, events, uniq, d, M):
            'bytes_per_launch': bpr_bytes, 'avg_launch_us': kernels_us['bpr']}
     # K5 kernel time: touched updates + look-ahead catch-ups (side stream, beside K3) + flush
     t_adam = sum(per.get('adam', [])) + sum(per.get('ahead', [])) + sum(per.get('flush', []))
-    flops = (step.nU + step.nI) * d * M * ADAM_FLOPS
+    rows = getattr(step, 'SU', step.nU) + getattr(step, 'SI', step.nI)   # this rank's table rows
+    flops = rows * d * M * ADAM_FLOPS
     tf = flops / t_adam / 1e12
     flush_k = 'adam_flush_row_kernel' if d >= 64 else 'adam_flush_kernel'
     name = ('K5 deferred dense Adam: adam_deferred_kernel<%d, float> x %d + %s<%d> x %d'
@@ -161,7 +162,7 @@ def roofline(step, events, uniq, d, M):
             'traffic': None, 'flops_per_window': flops, 'window_steps': M,
             'window_kernel_us': round(t_adam * 1e6, 1),
             'us_per_step': round(t_adam * 1e6 / M, 2),
-            'flops_formula': '(n_users + n_items) * d * steps * 13'}
+            'flops_formula': '(table rows on this rank) * d * steps * 13'}
     nd, nf = len(per.get('adam', [])) + len(per.get('ahead', [])), len(per.get('flush', []))
     if step.adam_mode == 'deferred':
         bd, src = pmc_bytes(f'adam_deferred_kernel<{d},')
@@ -174,7 +175,7 @@ def roofline(step, events, uniq, d, M):
             t_issue = ((insts - trans) * 2 + trans * 8) / SIMDS / CLOCK_HZ
             adam.update({'valu_insts_per_window': int(insts),
                          'valu_insts_per_element_step': round(
-                             insts * 64 / ((step.nU + step.nI) * d * M), 2),
+                             insts * 64 / (rows * d * M), 2),
                          'valu_issue_bound_us': round(t_issue * 1e6, 1),
                          'valu_issue_frac': round(t_issue / t_adam, 4),
                          'valu_issue_model': 'PMC SQ_INSTS_VALU x 2 cyc (+6 per '
@@ -294,6 +295,9 @@ def main():
     ap.add_argument('--batch-rows', type=int, default=2048)
     # diagnostic: steps per captured chunk (= deferred-Adam flush period), default 64
     ap.add_argument('--chunk', type=int, default=None)
+    # multi-GPU table layout: row-sharded (default) or replicated;
+    # 'sharded' with --gpus 1 runs the sharded protocol on one rank (diagnostic)
+    ap.add_argument('--dp-mode', default=None, choices=['sharded', 'replicated'])
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -303,7 +307,9 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
-    dist = world > 1
+    # a process group also at one rank when asked for the sharded protocol under
+    # torchrun (exercises the RCCL path on a 1-GPU box)
+    dist = world > 1 or (args.dp_mode == 'sharded' and 'WORLD_SIZE' in os.environ)
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -313,9 +319,12 @@ def main():
 
     d, neg = 128, 4
     t_setup = time.time()
+    dp_mode = args.dp_mode or ('sharded' if dist else 'single')
+    if dp_mode == 'replicated' and not dist:
+        dp_mode = 'single'
     config, train, test, model, opt, step = build_workload(
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
-        dist=tdist.group.WORLD if dist else None)
+        dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded')
     setup_s = time.time() - t_setup
     K, W = args.steps, args.warmup
     if K < 1 or W < 0:
@@ -348,6 +357,7 @@ def main():
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    local_elapsed = elapsed
     if dist:
         t = torch.tensor([elapsed], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -367,6 +377,13 @@ def main():
     losses = step.end_epoch(W + K + M)
     assert all(np.isfinite(losses)), 'non-finite loss'
     roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M)
+    mine = {'rank': rank, 'timed_s': round(local_elapsed, 6), 'kernels_us': kernels_us,
+            'k5_us_per_step': roof['us_per_step'],
+            'table_rows': int(getattr(step, 'SU', step.nU) + getattr(step, 'SI', step.nI))}
+    per_rank = [mine]
+    if dist:
+        per_rank = [None] * world
+        tdist.all_gather_object(per_rank, mine)
     positives = K * step.Bg                    # global batch = world x 512 positives
     result = {
         'metric': 'train positives/sec (+neg) per node',
@@ -388,12 +405,18 @@ def main():
                                '4 uniform negatives, 512 positives (2,048 rows) per step, '
                                'dense Adam',
                    'global_batch': step.Bg, 'per_gpu_batch': step.B, 'train_interactions': int(
-                       train.dataset.inter_num), 'parallelism': 'single' if world == 1
-                   else f'dp{world} (replicated tables, RCCL all-gather of per-row loss coefficients)',
+                       train.dataset.inter_num), 'parallelism': {
+                           'single': 'single',
+                           'sharded': f'dp{world} x row-sharded tables (cyclic ownership; 2 RCCL '
+                                      f'all-to-alls of rows per step, cap {getattr(step, "cap", 0)} '
+                                      f'rows per rank pair)',
+                           'replicated': f'dp{world} (replicated tables, RCCL all-gather of '
+                                         f'per-row loss coefficients)'}[dp_mode],
                    'exchange_graph': bool(step.use_graph)},
         'roofline': roof,
         'roofline_bpr': roof_bpr,
         'kernels_us': kernels_us,
+        'ranks': per_rank,
         'adam_mode': step.adam_mode,
         'setup_s': round(setup_s, 1),
     }
@@ -419,6 +442,8 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
+        step.close()             # captured collectives go before destroy_process_group
+        del step
         tdist.destroy_process_group()
 
 

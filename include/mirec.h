@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 6
+#define MIREC_ABI_VERSION 7
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -498,6 +498,49 @@ int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table, int
                               int32_t d, const int64_t* pos, const int64_t* neg, int64_t B,
                               int32_t n_neg, float grad_scale, float* loss, float* g_seq,
                               float* g_items, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Row-sharded tables over G ranks (replaces the single-process
+ * nn.Embedding tables of bpr.py:40-41 + the dense optim.Adam state of
+ * trainer.py:109-130 by G shards). Ownership: row id on rank id % G, local row
+ * id / G; S = rows per shard. Global slots of a batch of Bc positives (the
+ * pairwise layout, general_dataloader.py:235-241): user slot t = k, item slot
+ * t = Bc + j*Bc + k; slot t belongs to slice g = k / B (rank g's positives).
+ * Message (g, o) = the slots of slice g whose row rank o owns, ascending t; a
+ * slot's place in it is idx(t) < cap (else status -4).
+ * ------------------------------------------------------------------------- */
+/* keys[i] = (ids[i] % G) * S + ids[i] / G: owner-major sort keys for K2. */
+int mirec_shard_keys(const int64_t* ids, int64_t n, int32_t G, int64_t S, int64_t* keys,
+                     void* stream);
+/* Exchange plans of n_batches batches (users [nb, Bc], items [nb, (1+T)*Bc], original
+ * ids) for rank `rank`:
+ *   fwd_rows[nb, G*cap]  owner side: message (g, rank) entry idx = the slot's local
+ *                        row (user shard: row >= 0; item shard: -(row+1)); padding 0
+ *   map2[nb, Bc + (1+T)*Bc]  owner side: slot t of a row it owns -> g*cap + idx(t)
+ *   pos[nb, (2+T)*B]     requester side (slice = rank): local slot ls (users k',
+ *                        items n + j*n + k', n = this slice's positives) -> o*cap + idx
+ *   bwd_src[nb, G*cap]   requester side: message (rank, o) entry idx -> local slot ls;
+ *                        padding 0. */
+int mirec_shard_plan(const int64_t* users, const int64_t* items, int64_t n_batches, int64_t Bc,
+                     int64_t B, int32_t T, int32_t G, int32_t rank, int64_t cap,
+                     int64_t* fwd_rows, int32_t* map2, int64_t* pos, int32_t* bwd_src,
+                     int32_t* status, void* stream);
+/* Rank `rank`'s slice of the K2 grouping of each batch (uniq keyed by
+ * mirec_shard_keys, sorted; per-batch strides per_batch / per_batch + 1): the key
+ * range [rank*S, (rank+1)*S) -> own_uniq (local rows), own_seg (its segment
+ * offsets, n+1 entries), own_n; perm2[p] = map2[map_off + perm[p]] for the
+ * positions p of those segments (the contribution's place in the backward receive
+ * buffer); the same range of the look-ahead list (ahead may be NULL). */
+int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq,
+                    const int32_t* perm, int64_t per_batch, int64_t n_batches,
+                    const int32_t* ahead, const int32_t* n_ahead, const int32_t* map2,
+                    int64_t map_stride, int64_t map_off, int64_t S, int32_t rank,
+                    int32_t* own_uniq, int32_t* own_seg, int32_t* own_n, int32_t* perm2,
+                    int32_t* own_ahead, int32_t* own_nah, void* stream);
+/* out[i] = idx[i] >= 0 ? U[idx[i]] : I[-idx[i]-1] (rows of d floats; d in
+ * {32,64,128,256}): an owner's forward message from its two shards. */
+int mirec_shard_gather_f32(const float* U, const float* I, int32_t d, const int64_t* idx,
+                           int64_t n, float* out, void* stream);
 
 #ifdef __cplusplus
 }

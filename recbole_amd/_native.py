@@ -60,6 +60,12 @@ SIGNATURES = {
                                            _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
                                            c_size_t, _P]),
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
+    "mirec_shard_keys": (c_int, [_P, c_int64, c_int32, c_int64, _P, _P]),
+    "mirec_shard_plan": (c_int, [_P, _P, c_int64, c_int64, c_int64, c_int32, c_int32, c_int32,
+                                 c_int64, _P, _P, _P, _P, _P, _P]),
+    "mirec_shard_own": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P, c_int64, c_int64,
+                                c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P]),
+    "mirec_shard_gather_f32": (c_int, [_P, _P, c_int32, _P, c_int64, _P, _P]),
     "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
     "mirec_window_gather": (c_int, [_P, c_int32, _P, _P, c_int64, c_int32, _P, _P]),
@@ -123,7 +129,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class NativeError(RuntimeError):

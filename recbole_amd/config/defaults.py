@@ -20,7 +20,7 @@ OVERALL = dict(
     metric_decimal_place=4,
     # MI355X build extensions
     n_gpus=None, fused_train=True, fused_eval=True, train_graph=True, profile=False,
-    adam_mode='deferred',
+    adam_mode='deferred', shard_tables=True,
 )
 
 SAMPLE = dict(

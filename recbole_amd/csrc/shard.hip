@@ -1,0 +1,271 @@
+// Row-sharded embedding tables over G ranks: the index plans of
+// the two per-step row exchanges and the owner's slice of the global grouping.
+//
+// Ownership is cyclic — row `id` lives on rank id % G at local row id / G — so the
+// Zipf head rows of a table spread over every rank. Every rank walks the sampler
+// and groups the GLOBAL batch itself (replicated, cheap, on the prep stream), so
+// each rank knows, without any exchange, which rows every other rank needs:
+//
+//   global slots of a batch of Bc positives (the reference's pairwise layout,
+//   general_dataloader.py:235-241):   user slot t = k,  item slot t = Bc + j*Bc + k
+//   (k < Bc positive, j = 0 the positive item, j >= 1 the negatives);
+//   slice of a slot: g = k / B (rank g computes positives [g*B, g*B + n_g));
+//   message (g, o): the slots of slice g whose row rank o owns, ascending t; a slot's
+//   index in it is idx(t); every message is padded to `cap` rows.
+//
+// Forward: owner o sends rows -> rank g receives them at o*cap + idx(t) (one
+// all-to-all of equal blocks). Rank g runs K3 on its slice reading rows at those
+// positions, writes the slice's per-slot gradient rows, and sends each back in the
+// same (g, o) message position (the second all-to-all). The owner finds
+// contribution t of its rows at g*cap + idx(t), so K5 sums every owned row's
+// contributions in the GLOBAL grouping order — the same sums, the same Adam step,
+// the same bits as one GPU running the global batch.
+//
+// The K2 grouping sorts owner-major keys key(id) = (id % G) * S + id / G (S = rows per
+// shard), so rank r's rows are the contiguous key range [r*S, (r+1)*S) of every
+// sorted list and its slice of the grouping is a sub-range found by binary search.
+#include "common.h"
+
+namespace mirec {
+
+constexpr int kPlanThreads = 256;
+constexpr int kMaxRanks = 64;
+
+__global__ void shard_keys_kernel(const int64_t* __restrict__ ids, int64_t n, int32_t G,
+                                  int64_t S, int64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  keys[i] = (id % G) * S + id / G;
+}
+
+// One workgroup per (batch c, slice g). Scans slice g's slots in ascending t and
+// numbers them per owner; writes what rank r needs as owner and as requester.
+__global__ __launch_bounds__(kPlanThreads) void shard_plan_kernel(
+    const int64_t* __restrict__ users, const int64_t* __restrict__ items, int64_t Bc,
+    int64_t B, int32_t T, int32_t G, int32_t r, int64_t cap, int64_t* __restrict__ fwd_rows,
+    int32_t* __restrict__ map2, int64_t* __restrict__ pos, int32_t* __restrict__ bwd_src,
+    int32_t* __restrict__ status) {
+  __shared__ int wave_cnt[kMaxRanks][kPlanThreads / 64];
+  __shared__ int run[kMaxRanks];
+  const int64_t c = blockIdx.x / G;
+  const int g = blockIdx.x % G;
+  const int64_t KI = (1 + (int64_t)T) * Bc;
+  const int64_t* __restrict__ u_c = users + c * Bc;
+  const int64_t* __restrict__ i_c = items + c * KI;
+  const int64_t k0 = (int64_t)g * B;
+  const int64_t n_g = max((int64_t)0, min(B, Bc - k0));
+  const int64_t n_slots = (2 + (int64_t)T) * n_g;
+  const int64_t M = (int64_t)G * cap;
+  int64_t* __restrict__ fr = fwd_rows + c * M;
+  int32_t* __restrict__ m2 = map2 + c * (Bc + KI);
+  int64_t* __restrict__ ps = pos + c * (2 + (int64_t)T) * B;
+  int32_t* __restrict__ bs = bwd_src + c * M;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int o = threadIdx.x; o < G; o += kPlanThreads) run[o] = 0;
+  __syncthreads();
+  int overflow = 0;
+  for (int64_t base = 0; base < n_slots; base += kPlanThreads) {
+    const int64_t s = base + threadIdx.x;       // slot of the slice: users, then items j-major
+    const bool act = s < n_slots;
+    int64_t t = 0, id = 0, ls = s;
+    bool is_user = false;
+    if (act) {
+      if (s < n_g) {
+        is_user = true;
+        t = k0 + s;
+        id = u_c[t];
+      } else {
+        const int64_t q = s - n_g;
+        const int64_t j = q / n_g, kk = q % n_g;
+        t = Bc + j * Bc + k0 + kk;
+        id = i_c[j * Bc + k0 + kk];
+      }
+    }
+    const int o = act ? (int)(id % G) : -1;
+    // per-owner ranks of this tile's slots: ballots, then the waves before this one
+    int pre = 0;
+    for (int q = 0; q < G; ++q) {
+      const uint64_t m = __ballot(o == q);
+      if (q == o) pre = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wave_cnt[q][wid] = __popcll(m);
+    }
+    __syncthreads();
+    int64_t idx = 0;
+    if (act) {
+      int before = run[o];
+      for (int w = 0; w < wid; ++w) before += wave_cnt[o][w];
+      idx = before + pre;
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {
+      int tot = 0;
+      for (int w = 0; w < kPlanThreads / 64; ++w) tot += wave_cnt[threadIdx.x][w];
+      run[threadIdx.x] += tot;
+    }
+    if (act) {
+      if (idx >= cap) {
+        overflow = 1;
+      } else {
+        const int64_t local = id / G;
+        if (o == r) {                                   // owner side: rows to send to g
+          fr[(int64_t)g * cap + idx] = is_user ? local : -(local + 1);
+          m2[t] = (int32_t)((int64_t)g * cap + idx);
+        }
+        if (g == r) {                                   // requester side: where my slot's row lands
+          ps[ls] = (int64_t)o * cap + idx;
+          bs[(int64_t)o * cap + idx] = (int32_t)ls;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // padding of the messages this workgroup owns (harmless rows: user row 0 / slot 0)
+  for (int q = 0; q < G; ++q) {
+    const int64_t cnt = min((int64_t)run[q], cap);
+    if (q == r)
+      for (int64_t i = cnt + threadIdx.x; i < cap; i += kPlanThreads) fr[(int64_t)g * cap + i] = 0;
+    if (g == r)
+      for (int64_t i = cnt + threadIdx.x; i < cap; i += kPlanThreads) bs[(int64_t)q * cap + i] = 0;
+  }
+  if (overflow) atomicExch(status, -4);
+}
+
+__device__ __forceinline__ int32_t lower_bound_i32(const int32_t* __restrict__ a, int32_t n,
+                                                   int64_t key) {
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if ((int64_t)a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// One workgroup per batch: rank r's sub-range [lo, hi) of the sorted (keyed) uniq
+// list -> local row ids, its segment offsets, and the contributions of those
+// segments remapped to their positions in the backward receive buffer; the same
+// for the look-ahead list.
+__global__ __launch_bounds__(kPlanThreads) void shard_own_kernel(
+    const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ n_uniq, const int32_t* __restrict__ perm, int64_t per_batch,
+    const int32_t* __restrict__ ahead, const int32_t* __restrict__ n_ahead,
+    const int32_t* __restrict__ map2, int64_t map_stride, int64_t map_off, int64_t S, int32_t r,
+    int32_t* __restrict__ own_uniq, int32_t* __restrict__ own_seg, int32_t* __restrict__ own_n,
+    int32_t* __restrict__ perm2, int32_t* __restrict__ own_ahead, int32_t* __restrict__ own_nah) {
+  const int64_t c = blockIdx.x;
+  const int32_t* __restrict__ uq = uniq + c * per_batch;
+  const int32_t* __restrict__ sg = seg + c * (per_batch + 1);
+  const int32_t* __restrict__ pm = perm + c * per_batch;
+  const int32_t* __restrict__ m2 = map2 + c * map_stride + map_off;
+  const int64_t kb = (int64_t)r * S, ke = kb + S;
+  const int32_t n = n_uniq[c];
+  const int32_t lo = lower_bound_i32(uq, n, kb), hi = lower_bound_i32(uq, n, ke);
+  int32_t* __restrict__ ou = own_uniq + c * per_batch;
+  int32_t* __restrict__ os = own_seg + c * (per_batch + 1);
+  int32_t* __restrict__ p2 = perm2 + c * per_batch;
+  for (int32_t j = lo + threadIdx.x; j < hi; j += kPlanThreads) ou[j - lo] = (int32_t)(uq[j] - kb);
+  for (int32_t j = lo + threadIdx.x; j <= hi; j += kPlanThreads) os[j - lo] = sg[j];
+  for (int32_t p = sg[lo] + threadIdx.x; p < sg[hi]; p += kPlanThreads) p2[p] = m2[pm[p]];
+  if (threadIdx.x == 0) own_n[c] = hi - lo;
+  if (ahead) {
+    const int32_t* __restrict__ ah = ahead + c * per_batch;
+    const int32_t na = n_ahead[c];
+    const int32_t alo = lower_bound_i32(ah, na, kb), ahi = lower_bound_i32(ah, na, ke);
+    int32_t* __restrict__ oa = own_ahead + c * per_batch;
+    for (int32_t j = alo + threadIdx.x; j < ahi; j += kPlanThreads) oa[j - alo] = (int32_t)(ah[j] - kb);
+    if (threadIdx.x == 0) own_nah[c] = ahi - alo;
+  }
+}
+
+// out[i, :] = idx[i] >= 0 ? U[idx[i], :] : I[-idx[i] - 1, :]  (d/4 lanes per row,
+// 16-B vectors): the forward message of an owner, rows of its two shards.
+template <int D>
+__global__ __launch_bounds__(256) void shard_gather_kernel(const float* __restrict__ U,
+                                                           const float* __restrict__ I,
+                                                           const int64_t* __restrict__ idx,
+                                                           int64_t n, float* __restrict__ out) {
+  constexpr int LPR = D / 4;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  if (row >= n) return;
+  const int64_t s = idx[row];
+  const float4* src = reinterpret_cast<const float4*>(s >= 0 ? U + s * D : I + (-s - 1) * D);
+  reinterpret_cast<float4*>(out + row * D)[c] = src[c];
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_shard_keys(const int64_t* ids, int64_t n, int32_t G, int64_t S,
+                                int64_t* keys, void* stream) {
+  if (n < 0 || G < 1 || S < 1 || (n > 0 && (!ids || !keys))) {
+    set_error("mirec_shard_keys: bad arguments");
+    return -1;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(shard_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ids, n, G, S, keys);
+  return launch_status("mirec_shard_keys");
+}
+
+extern "C" int mirec_shard_plan(const int64_t* users, const int64_t* items, int64_t n_batches,
+                                int64_t Bc, int64_t B, int32_t T, int32_t G, int32_t rank,
+                                int64_t cap, int64_t* fwd_rows, int32_t* map2, int64_t* pos,
+                                int32_t* bwd_src, int32_t* status, void* stream) {
+  if (n_batches < 0 || Bc < 0 || B < 1 || T < 0 || G < 1 || G > kMaxRanks || rank < 0 ||
+      rank >= G || cap < 1 || (Bc > (int64_t)G * B) || !users || !items || !fwd_rows ||
+      !map2 || !pos || !bwd_src || !status) {
+    set_error("mirec_shard_plan: bad arguments (G=%d rank=%d Bc=%lld B=%lld)", G, rank,
+              (long long)Bc, (long long)B);
+    return -1;
+  }
+  if (n_batches == 0 || Bc == 0) return 0;
+  hipLaunchKernelGGL(shard_plan_kernel, dim3((unsigned)(n_batches * G)), dim3(kPlanThreads), 0,
+                     (hipStream_t)stream, users, items, Bc, B, T, G, rank, cap, fwd_rows, map2,
+                     pos, bwd_src, status);
+  return launch_status("mirec_shard_plan");
+}
+
+extern "C" int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq,
+                               const int32_t* perm, int64_t per_batch, int64_t n_batches,
+                               const int32_t* ahead, const int32_t* n_ahead, const int32_t* map2,
+                               int64_t map_stride, int64_t map_off, int64_t S, int32_t rank,
+                               int32_t* own_uniq, int32_t* own_seg, int32_t* own_n,
+                               int32_t* perm2, int32_t* own_ahead, int32_t* own_nah,
+                               void* stream) {
+  if (!uniq || !seg || !n_uniq || !perm || !map2 || !own_uniq || !own_seg || !own_n ||
+      !perm2 || per_batch < 1 || n_batches < 0 || S < 1 || rank < 0 ||
+      (ahead && (!n_ahead || !own_ahead || !own_nah))) {
+    set_error("mirec_shard_own: bad arguments");
+    return -1;
+  }
+  if (n_batches == 0) return 0;
+  hipLaunchKernelGGL(shard_own_kernel, dim3((unsigned)n_batches), dim3(kPlanThreads), 0,
+                     (hipStream_t)stream, uniq, seg, n_uniq, perm, per_batch, ahead, n_ahead, map2,
+                     map_stride, map_off, S, rank, own_uniq, own_seg, own_n, perm2, own_ahead,
+                     own_nah);
+  return launch_status("mirec_shard_own");
+}
+
+extern "C" int mirec_shard_gather_f32(const float* U, const float* I, int32_t d,
+                                      const int64_t* idx, int64_t n, float* out, void* stream) {
+  if (n < 0 || !U || !I || !out || (n > 0 && !idx)) {
+    set_error("mirec_shard_gather_f32: bad arguments");
+    return -1;
+  }
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned blocks = (unsigned)((n * (d / 4) + 255) / 256);
+  switch (d) {
+    case 32: hipLaunchKernelGGL(shard_gather_kernel<32>, dim3(blocks), dim3(256), 0, st, U, I, idx, n, out); break;
+    case 64: hipLaunchKernelGGL(shard_gather_kernel<64>, dim3(blocks), dim3(256), 0, st, U, I, idx, n, out); break;
+    case 128: hipLaunchKernelGGL(shard_gather_kernel<128>, dim3(blocks), dim3(256), 0, st, U, I, idx, n, out); break;
+    case 256: hipLaunchKernelGGL(shard_gather_kernel<256>, dim3(blocks), dim3(256), 0, st, U, I, idx, n, out); break;
+    default:
+      set_error("mirec_shard_gather_f32: d must be 32, 64, 128 or 256 (got %d)", d);
+      return -1;
+  }
+  return launch_status("mirec_shard_gather_f32");
+}

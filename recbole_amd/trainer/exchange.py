@@ -51,3 +51,78 @@ class ExchangeLayout(object):
         order j*G*B + g*B + k' (a copy; the kernels index the rank blocks directly)."""
         c = buf.view(self.G, self.W)[:, self.coef0:].reshape(self.G, self.T, self.B)
         return c.permute(1, 0, 2).reshape(-1)
+
+
+class ShardLayout(object):
+    """Specification (torch, any device) of the row-sharded exchange plans that
+    csrc/shard.hip computes on the device (include/mirec.h, "Row-sharded tables"):
+    cyclic ownership (row id on rank id % G, local row id // G), owner-major K2 keys,
+    per-(slice, owner) messages of `cap` rows in ascending global slot order.
+    Used by the tests to pin the kernels bit for bit and to run the protocol on
+    gloo CPU ranks."""
+
+    def __init__(self, G: int, B: int, T: int, nU: int, nI: int, cap: int):
+        self.G, self.B, self.T, self.cap = G, B, T, cap
+        self.SU, self.SI = -(-nU // G), -(-nI // G)
+
+    def keys(self, ids: torch.Tensor, S: int) -> torch.Tensor:
+        return (ids % self.G) * S + ids // self.G
+
+    def slots(self, users: torch.Tensor, items: torch.Tensor):
+        """Global slots of one batch: (t, row id, is_user, slice, local slot index in
+        its slice) — users t = k, items t = Bc + j*Bc + k."""
+        Bc, T, B = users.numel(), self.T, self.B
+        k = torch.arange(Bc)
+        j = torch.arange(1 + T).repeat_interleave(Bc)
+        kk = torch.arange(Bc).repeat(1 + T)
+        t = torch.cat([k, Bc + j * Bc + kk])
+        ids = torch.cat([users.cpu(), items.cpu()])
+        is_user = torch.cat([torch.ones(Bc, dtype=torch.bool), torch.zeros((1 + T) * Bc,
+                                                                          dtype=torch.bool)])
+        kall = torch.cat([k, kk])
+        g = kall // B
+        n_g = torch.clamp(Bc - g * B, 0, B)
+        jall = torch.cat([torch.zeros(Bc, dtype=torch.long), j])
+        ls = torch.where(is_user, kall - g * B, n_g + jall * n_g + (kall - g * B))
+        return t, ids, is_user, g, ls
+
+    def plan(self, users: torch.Tensor, items: torch.Tensor, rank: int):
+        """(fwd_rows [G*cap], map2 [Bc + (1+T)Bc] (-1 where not owned), pos
+        [(2+T)*B] (-1 beyond the slice), bwd_src [G*cap], overflow) of one batch."""
+        G, cap, T, B = self.G, self.cap, self.T, self.B
+        t, ids, is_user, g, ls = self.slots(users, items)
+        o = ids % G
+        order = torch.argsort(t)
+        t, ids, is_user, g, ls, o = (x[order] for x in (t, ids, is_user, g, ls, o))
+        idx = torch.zeros_like(t)
+        cnt = {}
+        for q in range(len(t)):                     # ascending t within each (g, o)
+            key = (int(g[q]), int(o[q]))
+            idx[q] = cnt.get(key, 0)
+            cnt[key] = idx[q] + 1
+        over = bool((idx >= cap).any())
+        fwd = torch.zeros(G * cap, dtype=torch.int64)
+        bwd = torch.zeros(G * cap, dtype=torch.int32)
+        Bc = users.numel()
+        map2 = torch.full((Bc + (1 + T) * Bc,), -1, dtype=torch.int32)
+        pos = torch.full(((2 + T) * B,), -1, dtype=torch.int64)
+        ok = idx < cap
+        local = ids // G
+        mine = ok & (o == rank)
+        fwd[(g * cap + idx)[mine]] = torch.where(is_user, local, -(local + 1))[mine]
+        map2[t[mine]] = (g * cap + idx)[mine].to(torch.int32)
+        req = ok & (g == rank)
+        pos[ls[req]] = (o * cap + idx)[req]
+        bwd[(o * cap + idx)[req]] = ls[req].to(torch.int32)
+        return fwd, map2, pos, bwd, over
+
+    def own(self, uniq: torch.Tensor, seg: torch.Tensor, perm: torch.Tensor,
+            map2: torch.Tensor, map_off: int, S: int, rank: int):
+        """Rank `rank`'s slice of one batch's sorted keyed uniq list: (local rows,
+        segment offsets, {p: perm2[p]} for the positions of those segments)."""
+        lo = int(torch.searchsorted(uniq, torch.tensor(rank * S, dtype=uniq.dtype)))
+        hi = int(torch.searchsorted(uniq, torch.tensor((rank + 1) * S, dtype=uniq.dtype)))
+        own = uniq[lo:hi] - rank * S
+        oseg = seg[lo:hi + 1]
+        p = torch.arange(int(seg[lo]), int(seg[hi]))
+        return own, oseg, p, map2[map_off + perm[p]]

@@ -515,6 +515,273 @@ class FusedBPRTrainStep(object):
         self.run_batches(0, nb)
         return self.end_epoch()
 
+    def close(self):
+        """Drop the captured chunk graphs (they hold collectives of the process
+        group: release them before torch.distributed.destroy_process_group)."""
+        torch.cuda.synchronize(self.device)
+        for s in self.slots:
+            s.graphs = {}
+        torch.cuda.synchronize(self.device)
+
+
+class ShardedBPRTrainStep(FusedBPRTrainStep):
+    """The fused pairwise step with ROW-SHARDED tables over G ranks:
+    rank r owns rows id % G == r of both tables (parameters, Adam m / v and the
+    deferred step counts) as a [S, d] shard, S = ceil(n / G).
+
+    Per optimizer step over a global batch of G*B positives (csrc/shard.hip):
+      prep (replicated on every rank, prep stream): walk + K2 grouping of the global
+        batch over owner-major keys, the exchange plans and this rank's slice of the
+        grouping (mirec_shard_plan / mirec_shard_own);
+      forward exchange: each owner gathers the rows every slice needs from its shards
+        (mirec_shard_gather_f32) and one all-to-all (RCCL over xGMI; equal blocks of
+        `cap` rows per rank pair) delivers them;
+      K3 on this rank's slice of positives, reading rows from the receive buffer;
+      backward exchange: the slice's per-slot gradient rows go back to the owners
+        in the same message positions (second all-to-all);
+      K5 (deferred) on the owned rows only, summing each row's contributions in the
+        global grouping order — the result is bit-identical to one GPU running the
+        global batch;
+      per chunk: one all-gather of the per-positive losses for the loss history.
+    The dominant optimizer work (touched rows + flush) is 1/G per rank. The model's
+    full parameter tensors are written back from the shards at end_epoch() (one
+    all-gather of p, m, v per epoch) for evaluation and checkpoints, and re-read
+    into the shards at begin_epoch(). With dist=None it runs the same protocol on
+    one rank (G = 1; the all-to-alls are copies)."""
+
+    CAP_SLACK = 1.25
+
+    def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
+                 adam_mode='deferred', dist=None, cap=None):
+        if adam_mode != 'deferred':
+            raise ValueError('the row-sharded step runs the deferred Adam schedule')
+        super().__init__(model, optimizer, train_data, chunk=chunk, use_graph=use_graph,
+                         adam_mode=adam_mode, dist=dist)
+        G, B, T, d, dev = self.G, self.B, self.times, self.d, self.device
+        self.SU, self.SI = -(-self.nU // G), -(-self.nI // G)
+        # rows per (slice, owner) message: the slice's (2+T)*B slots spread over G
+        # owners (cyclic ownership); overflow is detected (status -4), never silent
+        self.cap = int(cap or min((2 + T) * B,
+                                  math.ceil(self.CAP_SLACK * (2 + T) * B / G) + 64))
+        M = G * self.cap
+        self.shU = [torch.zeros(self.SU, d, device=dev) for _ in range(3)]   # p, m, v
+        self.shI = [torch.zeros(self.SI, d, device=dev) for _ in range(3)]
+        self.lastU = torch.zeros(self.SU, dtype=torch.int32, device=dev)
+        self.lastI = torch.zeros(self.SI, dtype=torch.int32, device=dev)
+        solo = dist is None                  # one rank, no process group: no collectives
+        self.sendF = torch.empty(M, d, device=dev)
+        self.recvF = self.sendF if solo else torch.empty(M, d, device=dev)
+        self.xloc = torch.empty((2 + T) * B, d, device=dev)
+        self.sendB = torch.empty(M, d, device=dev)
+        self.recvB = self.sendB if solo else torch.empty(M, d, device=dev)
+        self.loss_g = torch.empty(G * self.C * B, dtype=torch.float32, device=dev)
+        self.loss_mine = torch.zeros(self.C * B, dtype=torch.float32, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        Bg, KI = self.Bg, (1 + T) * self.Bg
+        C = self.C
+        for sl in self.slots:
+            sl.u_keyed = torch.empty(C * Bg, dtype=torch.int64, device=dev)
+            sl.i_keyed = torch.empty(C * KI, dtype=torch.int64, device=dev)
+            sl.fwd_rows = torch.empty(C * M, dtype=torch.int64, device=dev)
+            sl.map2 = torch.empty(C * (Bg + KI), dtype=torch.int32, device=dev)
+            sl.pos = torch.empty(C * (2 + T) * B, dtype=torch.int64, device=dev)
+            sl.bwd_src = torch.empty(C * M, dtype=torch.int32, device=dev)
+            for tag, per in (('u', Bg), ('i', KI)):
+                setattr(sl, f'own_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
+                setattr(sl, f'own_{tag}_seg', torch.empty(C * (per + 1), dtype=torch.int32,
+                                                          device=dev))
+                setattr(sl, f'own_{tag}_n', torch.zeros(C, dtype=torch.int32, device=dev))
+                setattr(sl, f'perm2_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
+                setattr(sl, f'own_{tag}_ah', torch.empty(C * per, dtype=torch.int32, device=dev))
+                setattr(sl, f'own_{tag}_nah', torch.zeros(C, dtype=torch.int32, device=dev))
+        self._n_max = (ctypes.c_int64 * 2)(min(Bg, self.SU), min(KI, self.SI))
+        self._fill_tables()
+
+    # ------------------------------------------------------------ shards <-> full tensors
+    def _owned_ids(self, n, S):
+        ids = torch.arange(S, device=self.device, dtype=torch.int64) * self.G + self.rank
+        return ids[ids < n]
+
+    def _load_shards(self):
+        """Owned rows of the model's full p and the optimizer's m, v -> the shards."""
+        full = [(self.pU, self.opt.state[self.pU]), (self.pI, self.opt.state[self.pI])]
+        for (p, st), sh, n, S in zip(full, (self.shU, self.shI), (self.nU, self.nI),
+                                     (self.SU, self.SI)):
+            ids = self._owned_ids(n, S)
+            for dst, src in zip(sh, (p.data, st['exp_avg'], st['exp_avg_sq'])):
+                dst[:ids.numel()].copy_(src[ids])
+
+    def _store_shards(self):
+        """All shards -> the full p, m, v on every rank (one all-gather each)."""
+        full = [(self.pU, self.opt.state[self.pU]), (self.pI, self.opt.state[self.pI])]
+        for (p, st), sh, n, S in zip(full, (self.shU, self.shI), (self.nU, self.nI),
+                                     (self.SU, self.SI)):
+            for src, dst in zip(sh, (p.data, st['exp_avg'], st['exp_avg_sq'])):
+                g = self._all_gather(src)                       # [G*S, d], owner-major
+                dst.copy_(g.view(self.G, S, self.d).transpose(0, 1).reshape(-1, self.d)[:n])
+
+    def _all_gather(self, x):
+        if self.group is None:
+            return x
+        import torch.distributed as tdist
+        out = torch.empty((self.G,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        if self._backend == 'nccl':
+            tdist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        else:
+            parts = list(out.unbind(0))
+            tdist.all_gather(parts, x.contiguous(), group=self.group)
+        return out.view((-1,) + tuple(x.shape[1:]))
+
+    def _all_to_all(self, recv, send):
+        if self.group is None:
+            return                                              # recv is send
+        import torch.distributed as tdist
+        if self._backend == 'nccl':
+            tdist.all_to_all_single(recv, send, group=self.group)
+        else:                                                   # gloo: host-staged
+            r = torch.empty(recv.shape, dtype=recv.dtype)
+            tdist.all_to_all_single(r, send.cpu(), group=self.group)
+            recv.copy_(r)
+
+    # ------------------------------------------------------------ data side
+    def _prepare(self, slot, chunk):
+        b0, nb, Bc = chunk
+        T, G, r = self.times, self.G, self.rank
+        KI = (1 + T) * Bc
+        L = lib()
+        if slot.free_recorded:
+            self.prep_stream.wait_event(slot.free)
+        with torch.cuda.stream(self.prep_stream):
+            st = self.prep_stream.cuda_stream
+            s0 = b0 * self.Bg
+            users = slot.user_keys[:nb * Bc]
+            users.copy_(self._users[s0:s0 + nb * Bc])
+            keys = slot.item_keys[:nb * KI].view(nb, 1 + T, Bc)
+            keys[:, 0, :].copy_(self._items[s0:s0 + nb * Bc].view(nb, Bc))
+            neg = slot.item_keys[Bc:nb * KI]
+            self.data.sampler.launch_batches(users, Bc, nb, T, neg, out_stride=KI,
+                                             ws=self.samp_ws)
+            items = slot.item_keys[:nb * KI]
+            check(L.mirec_shard_keys(users.data_ptr(), nb * Bc, G, self.SU,
+                                     slot.u_keyed.data_ptr(), st), 'mirec_shard_keys')
+            check(L.mirec_shard_keys(items.data_ptr(), nb * KI, G, self.SI,
+                                     slot.i_keyed.data_ptr(), st), 'mirec_shard_keys')
+            self.sort_ws = ops.segment_sort_batched(slot.u_keyed[:nb * Bc], Bc, G * self.SU,
+                                                    slot.u_perm, slot.u_uniq, slot.u_seg,
+                                                    slot.u_nu, ws=self.sort_ws)
+            self.sort_ws = ops.segment_sort_batched(slot.i_keyed[:nb * KI], KI, G * self.SI,
+                                                    slot.i_perm, slot.i_uniq, slot.i_seg,
+                                                    slot.i_nu, ws=self.sort_ws)
+            ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
+            ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
+            check(L.mirec_shard_plan(users.data_ptr(), items.data_ptr(), nb, Bc, self.B, T, G, r,
+                                     self.cap, slot.fwd_rows.data_ptr(), slot.map2.data_ptr(),
+                                     slot.pos.data_ptr(), slot.bwd_src.data_ptr(),
+                                     self.status.data_ptr(), st), 'mirec_shard_plan')
+            for tag, per, off, S in (('u', Bc, 0, self.SU), ('i', KI, Bc, self.SI)):
+                g_ = lambda n: getattr(slot, n).data_ptr()
+                check(L.mirec_shard_own(g_(f'{tag}_uniq'), g_(f'{tag}_seg'), g_(f'{tag}_nu'),
+                                        g_(f'{tag}_perm'), per, nb, g_(f'{tag}_ahead'),
+                                        g_(f'{tag}_nah'), slot.map2.data_ptr(), Bc + KI, off,
+                                        S, r, g_(f'own_{tag}'), g_(f'own_{tag}_seg'),
+                                        g_(f'own_{tag}_n'), g_(f'perm2_{tag}'),
+                                        g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), st),
+                      'mirec_shard_own')
+            slot.ready.record(self.prep_stream)
+        slot.chunk = chunk
+
+    # ------------------------------------------------------------ model side
+    def _fill_tables(self):
+        if not hasattr(self, 'shU'):
+            return super()._fill_tables()
+        t = self._tables
+        for q, (sh, last, S) in enumerate(((self.shU, self.lastU, self.SU),
+                                           (self.shI, self.lastI, self.SI))):
+            t[q].p, t[q].m, t[q].v = (x.data_ptr() for x in sh)
+            t[q].n_rows = S
+            t[q].last = last.data_ptr()
+            t[q].dense_grad = None
+            t[q].rows = self.recvB.data_ptr()
+
+    def _n_local(self, Bc):
+        return max(0, min(self.B, Bc - self.rank * self.B))
+
+    def _step(self, slot, c, Bc, stream, step_off, ahead):
+        T, d, G, B, M = self.times, self.d, self.G, self.B, self.G * self.cap
+        KI = (1 + T) * Bc
+        L = lib()
+        st = stream.cuda_stream
+        n = self._n_local(Bc)
+
+        def fwd_gather():
+            check(L.mirec_shard_gather_f32(self.shU[0].data_ptr(), self.shI[0].data_ptr(), d,
+                                           slot.fwd_rows.data_ptr() + 8 * c * M, M,
+                                           self.sendF.data_ptr(), st), 'mirec_shard_gather_f32')
+        self._record('gather', stream, fwd_gather)
+        self._record('exchange', stream, lambda: self._all_to_all(self.recvF, self.sendF))
+        loss_p = self.loss_mine.data_ptr() + 4 * c * B
+        pos_p = slot.pos.data_ptr() + 8 * c * (2 + T) * B
+        x0 = self.xloc.data_ptr()
+
+        def bpr():
+            if n == 0:
+                return
+            check(L.mirec_bpr_fwd_bwd_f32(self.recvF.data_ptr(), M, self.recvF.data_ptr(), M, d,
+                                          pos_p, pos_p + 8 * n, pos_p + 16 * n, n, T, 1e-10,
+                                          self._grad_scale(Bc), loss_p, None, None, x0,
+                                          x0 + 4 * n * d, st), 'mirec_bpr_fwd_bwd_f32')
+        self._record('bpr', stream, bpr)
+
+        def bwd_gather():
+            check(L.mirec_gather_rows_i32idx(self.xloc.data_ptr(), self.xloc.shape[0], 4 * d,
+                                             slot.bwd_src.data_ptr() + 4 * c * M, M,
+                                             self.sendB.data_ptr(), st), 'mirec_gather_rows_i32idx')
+        self._record('gather_bwd', stream, bwd_gather)
+        self._record('exchange_bwd', stream, lambda: self._all_to_all(self.recvB, self.sendB))
+        t = self._tables
+        for q, (tag, per) in enumerate((('u', Bc), ('i', KI))):
+            t[q].perm = getattr(slot, f'perm2_{tag}').data_ptr() + 4 * c * per
+            t[q].uniq = getattr(slot, f'own_{tag}').data_ptr() + 4 * c * per
+            t[q].seg = getattr(slot, f'own_{tag}_seg').data_ptr() + 4 * c * (per + 1)
+            t[q].n_uniq = getattr(slot, f'own_{tag}_n').data_ptr() + 4 * c
+            if ahead:
+                t[q].ahead_uniq = getattr(slot, f'own_{tag}_ah').data_ptr() + 4 * c * per
+                t[q].ahead_n_uniq = getattr(slot, f'own_{tag}_nah').data_ptr() + 4 * c
+            else:
+                t[q].ahead_uniq = t[q].ahead_n_uniq = None
+
+        def adam():
+            check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
+                                            self.step_idx.data_ptr(), step_off,
+                                            *self._adam_args, st), 'mirec_adam_deferred_f32')
+        self._record('adam', stream, adam)
+        if self.kernel_events is not None:
+            self.kernel_uniq.append(torch.stack([slot.own_u_n[c], slot.own_i_n[c]]))
+
+    def _finish(self, c0, n_steps, Bc, stream):
+        """Losses of this rank's slices of steps c0..c0+n_steps -> all ranks (one
+        all-gather), laid out in global positive order, then chunk_finish."""
+        B, G = self.B, self.G
+        mine = self.loss_mine[c0 * B:(c0 + n_steps) * B]
+        gathered = self._all_gather(mine).view(G, n_steps, B)
+        self.loss_k.view(self.C, self.Bg)[c0:c0 + n_steps].view(n_steps, G, B).copy_(
+            gathered.transpose(0, 1))
+        super()._finish(c0, n_steps, Bc, stream)
+
+    # ------------------------------------------------------------ epoch API
+    def begin_epoch(self, cuts=(), hold_prep_from=None):
+        self.status.zero_()
+        self._load_shards()
+        return super().begin_epoch(cuts=cuts, hold_prep_from=hold_prep_from)
+
+    def end_epoch(self, n_done=None):
+        losses = super().end_epoch(n_done)
+        if int(self.status.item()) == -4:
+            raise RuntimeError(f'row exchange overflow: a (slice, owner) message exceeded '
+                               f'cap={self.cap} rows; construct with a larger cap')
+        self._store_shards()
+        return losses
+
 
 def fused_full_sort_eval(model, eval_data, topk_evaluator, user_batch=1 << 20, dp=None,
                          round_users=None):

@@ -34,7 +34,8 @@ from recbole_amd.data.dataloader.general_dataloader import GeneralNegSampleDataL
 from recbole_amd.evaluator import ProxyEvaluator
 from recbole_amd.data.dataloader.sequential_dataloader import SequentialNegSampleDataLoader
 from recbole_amd.sampler import RepeatableSampler
-from recbole_amd.trainer.fused import (FusedBPRTrainStep, fused_full_sort_eval,
+from recbole_amd.trainer.fused import (FusedBPRTrainStep, ShardedBPRTrainStep,
+                                       fused_full_sort_eval,
                                        fused_general_sampled_eval, fused_seq_full_sort_eval,
                                        fused_seq_sampled_eval)
 from recbole_amd.trainer.dist import DataParallelStep, active_group
@@ -139,10 +140,14 @@ class Trainer(AbstractTrainer):
         self.model.train()
         if loss_func is None and self._fused_applicable(train_data):
             if self._fused_step is None or self._fused_step.data is not train_data:
-                self._fused_step = FusedBPRTrainStep(
+                mode = self.config['adam_mode'] or 'deferred'
+                # data parallel: row-sharded tables unless
+                # shard_tables: False asks for replicas
+                cls = (ShardedBPRTrainStep if self._dp is not None and mode == 'deferred'
+                       and self.config['shard_tables'] is not False else FusedBPRTrainStep)
+                self._fused_step = cls(
                     self.model, self.optimizer, train_data,
-                    use_graph=self.config['train_graph'] is not False,
-                    adam_mode=self.config['adam_mode'] or 'deferred',
+                    use_graph=self.config['train_graph'] is not False, adam_mode=mode,
                     dist=self._dp.group if self._dp is not None else None)
             losses = self._fused_step.run_epoch()
             total = None

@@ -1,0 +1,214 @@
+"""Row-sharded tables (csrc/shard.hip, trainer/fused.py ShardedBPRTrainStep) on
+the GPU:
+  * the exchange plans and the owner's slice of the grouping, bit for bit against
+    the specification (trainer/exchange.py ShardLayout) for G = 1, 2, 3, 8, every
+    rank, full and ragged batches, and the overflow status;
+  * the sharded step on one rank (G = 1, no process group) bit-identical to the
+    single-GPU fused step (weights, Adam state, losses; graph and eager);
+  * 2 ranks (gloo, both on cuda:0) bit-identical to ONE process running the global
+    batch (ragged last batch, partial chunks);
+  * the RCCL code path (a 1-rank nccl group: all-to-all + all-gather inside the
+    captured chunk graphs) equal to the single-GPU step."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+from recbole_amd.trainer.exchange import ShardLayout
+
+pytestmark = pytest.mark.gpu
+
+EPOCHS, CHUNK = 2, 4
+
+
+@pytest.mark.parametrize('G,Bc', [(1, 48), (2, 96), (3, 144), (3, 100), (8, 384), (8, 170)])
+def test_shard_plan_and_own_match_spec(dev, G, Bc):
+    from recbole_amd import ops
+    from recbole_amd._native import check, lib
+    B, T, nU, nI = 48, 4, 301, 523
+    cap = min((2 + T) * B, -(-5 * (2 + T) * B // (4 * G)) + 64)
+    lay = ShardLayout(G, B, T, nU, nI, cap)
+    g = torch.Generator().manual_seed(G * 1000 + Bc)
+    users = torch.randint(0, nU, (Bc,), generator=g)
+    items = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
+    items[:Bc // 3] = 5                                        # a hot item
+    ud, idv = users.to(dev), items.to(dev)
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    keyed = {}
+    for tag, ids, S in (('u', ud, lay.SU), ('i', idv, lay.SI)):
+        k = torch.empty_like(ids)
+        check(L.mirec_shard_keys(ids.data_ptr(), ids.numel(), G, S, k.data_ptr(), st), 'keys')
+        assert torch.equal(k.cpu(), lay.keys(ids.cpu(), S))
+        n = ids.numel()
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        uniq = torch.empty(n, dtype=torch.int32, device=dev)
+        seg = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        nu = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.segment_sort_batched(k, n, G * S, perm, uniq, seg, nu)
+        keyed[tag] = (perm, uniq, seg, nu, S)
+    M = G * cap
+    KI = (1 + T) * Bc
+    for r in range(G):
+        fwd = torch.empty(M, dtype=torch.int64, device=dev)
+        map2 = torch.full((Bc + KI,), -7, dtype=torch.int32, device=dev)
+        pos = torch.full(((2 + T) * B,), -1, dtype=torch.int64, device=dev)
+        bwd = torch.empty(M, dtype=torch.int32, device=dev)
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        check(L.mirec_shard_plan(ud.data_ptr(), idv.data_ptr(), 1, Bc, B, T, G, r, cap,
+                                 fwd.data_ptr(), map2.data_ptr(), pos.data_ptr(), bwd.data_ptr(),
+                                 status.data_ptr(), st), 'plan')
+        efwd, emap, epos, ebwd, over = lay.plan(users, items, r)
+        assert not over and int(status.item()) == 0
+        assert torch.equal(fwd.cpu(), efwd)
+        assert torch.equal(bwd.cpu(), ebwd)
+        n_r = max(0, min(B, Bc - r * B))
+        assert torch.equal(pos.cpu()[:(2 + T) * n_r], epos[:(2 + T) * n_r])
+        owned = emap >= 0
+        assert torch.equal(map2.cpu()[owned], emap[owned])
+        for tag, off in (('u', 0), ('i', Bc)):
+            perm, uniq, seg, nu, S = keyed[tag]
+            n = perm.numel()
+            own = torch.empty(n, dtype=torch.int32, device=dev)
+            oseg = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            on = torch.zeros(1, dtype=torch.int32, device=dev)
+            p2 = torch.full((n,), -9, dtype=torch.int32, device=dev)
+            check(L.mirec_shard_own(uniq.data_ptr(), seg.data_ptr(), nu.data_ptr(),
+                                    perm.data_ptr(), n, 1, None, None, map2.data_ptr(), Bc + KI,
+                                    off, S, r, own.data_ptr(), oseg.data_ptr(), on.data_ptr(),
+                                    p2.data_ptr(), None, None, st), 'own')
+            nn = int(nu.item())
+            e_own, e_seg, e_p, e_p2 = lay.own(uniq.cpu()[:nn], seg.cpu()[:nn + 1], perm.cpu(),
+                                             map2.cpu(), off, S, r)
+            k = int(on.item())
+            assert k == e_own.numel()
+            assert torch.equal(own.cpu()[:k], e_own)
+            assert torch.equal(oseg.cpu()[:k + 1], e_seg)
+            assert torch.equal(p2.cpu()[e_p], e_p2)
+    if G > 1:                                                  # a too-small cap is reported
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        bufs = [torch.empty(G * 2, dtype=torch.int64, device=dev),
+                torch.empty(Bc + KI, dtype=torch.int32, device=dev),
+                torch.empty((2 + T) * B, dtype=torch.int64, device=dev),
+                torch.empty(G * 2, dtype=torch.int32, device=dev)]
+        check(L.mirec_shard_plan(ud.data_ptr(), idv.data_ptr(), 1, Bc, B, T, G, 0, 2,
+                                 *[b.data_ptr() for b in bufs], status.data_ptr(), st), 'plan')
+        assert int(status.item()) == -4
+
+
+def _pipeline(root, batch_rows):
+    import pathlib
+    from test_gpu_e2e import _pipeline as pipe
+    return pipe(pathlib.Path(root), train_batch_size=batch_rows, epochs=EPOCHS)
+
+
+def _train(step):
+    losses = []
+    for _ in range(EPOCHS):
+        nb = step.begin_epoch()
+        step.run_batches(0, min(5, nb))
+        step.run_batches(min(5, nb), nb)
+        losses += step.end_epoch()
+    st = [step.opt.state[p][k].cpu() for p in (step.pU, step.pI)
+          for k in ('exp_avg', 'exp_avg_sq')]
+    return [step.pU.detach().cpu(), step.pI.detach().cpu()] + st, losses
+
+
+@pytest.mark.parametrize('graph', [True, False])
+def test_sharded_solo_equals_fused(tmp_path, graph):
+    from recbole_amd.trainer.fused import FusedBPRTrainStep, ShardedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    out = []
+    for cls in (FusedBPRTrainStep, ShardedBPRTrainStep):
+        config, train, valid, test, model = _pipeline(str(tmp_path), 512)
+        opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+        out.append(_train(cls(model, opt, train, chunk=CHUNK, use_graph=graph)))
+    (ta, la), (tb, lb) = out
+    assert la == lb
+    for a, b in zip(ta, tb):
+        assert torch.equal(a, b)
+
+
+def _worker(rank, port, root, q):
+    import torch.distributed as tdist
+    from recbole_amd.trainer.fused import ShardedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    tdist.init_process_group('gloo', rank=rank, world_size=2)
+    try:
+        torch.cuda.set_device(0)
+        config, train, valid, test, model = _pipeline(root, 256)
+        opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+        step = ShardedBPRTrainStep(model, opt, train, chunk=CHUNK, dist=tdist.group.WORLD)
+        tensors, losses = _train(step)
+        q.put((rank, step.Bg, step.SU, [t.numpy() for t in tensors], losses))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path):
+    from recbole_amd.trainer.fused import FusedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    root = str(tmp_path)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29800 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=600) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    config, train, valid, test, model = _pipeline(root, 512)
+    opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+    step = FusedBPRTrainStep(model, opt, train, chunk=CHUNK)
+    assert train.dataset.inter_num % step.B != 0            # a ragged last batch
+    ref_t, ref_l = _train(step)
+    for rank, Bg, SU, tensors, losses in got:
+        assert Bg == step.B and SU == -(-step.nU // 2)
+        assert losses == ref_l, rank
+        for a, b in zip(ref_t, tensors):
+            assert np.array_equal(a.numpy(), b), (rank, np.abs(a.numpy() - b).max())
+
+
+NCCL_SCRIPT = r'''
+import os, sys, pathlib, torch, torch.distributed as tdist
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], 'tests'))
+os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=sys.argv[3], RANK='0', WORLD_SIZE='1')
+torch.cuda.set_device(0)
+tdist.init_process_group('nccl', device_id=torch.device('cuda', 0))
+from test_gpu_e2e import _pipeline
+from recbole_amd.trainer.fused import FusedBPRTrainStep, ShardedBPRTrainStep
+from recbole_amd.trainer.optim import FusedAdam
+res = []
+for cls, dist in ((FusedBPRTrainStep, None), (ShardedBPRTrainStep, tdist.group.WORLD)):
+    config, train, valid, test, model = _pipeline(pathlib.Path(sys.argv[2]), epochs=2)
+    opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+    step = cls(model, opt, train, chunk=4, dist=dist)
+    assert step.use_graph
+    losses = []
+    for _ in range(2):
+        losses += step.run_epoch()
+    res.append((losses, step.pU.detach().cpu(), step.pI.detach().cpu()))
+    step.close()                 # captured collectives go before destroy_process_group
+    del step
+assert res[0][0] == res[1][0]
+assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+tdist.destroy_process_group()
+print('NCCL_OK')
+'''
+
+
+def test_sharded_rccl_path_one_rank(tmp_path):
+    script = tmp_path / 'nccl_one_rank.py'
+    script.write_text(NCCL_SCRIPT)
+    port = str(29900 + os.getpid() % 50)
+    out = subprocess.run([sys.executable, str(script), ROOT, str(tmp_path), port],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and 'NCCL_OK' in out.stdout, out.stderr[-3000:]

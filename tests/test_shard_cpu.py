@@ -1,0 +1,137 @@
+"""The row-sharded exchange protocol on CPU (gloo, world size 2 and 3), with the
+specification of the plans (trainer/exchange.py ShardLayout) and torch ops in
+place of the kernels:
+
+each rank holds the rows id % G == rank of both tables; for one global BPR batch it
+  1. gathers, per (slice, owner) message, the rows other slices need from its
+     shards; one all-to-all;
+  2. runs the reference's BPR loss (bpr.py:74-83, loss.py:48; torch-CPU autograd,
+     mean over the GLOBAL batch) on ITS slice, reading rows from the receive buffer;
+  3. sends every slot's gradient row back to its owner in the same message position;
+     one all-to-all;
+  4. sums, for every row it owns, the contributions in the global grouping order
+     (ascending contribution index) via the perm2 map of ShardLayout.own.
+The owned rows' sums must equal — bit for bit — the grouped sums of one process
+running the whole global batch, and the union over ranks must cover every touched
+row exactly once."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+from recbole_amd.trainer.exchange import ShardLayout
+
+B, T, D, NU, NI = 5, 3, 8, 13, 19
+
+
+def _global_batch(G):
+    g = torch.Generator().manual_seed(11 + G)
+    EU = torch.randn(NU, D, generator=g)
+    EI = torch.randn(NI, D, generator=g)
+    Bc = G * B - (1 if G > 2 else 0)                         # ragged for G = 3
+    users = torch.randint(0, 6, (Bc,), generator=g)
+    items = torch.randint(1, 9, ((1 + T) * Bc,), generator=g)
+    return EU, EI, users, items
+
+
+def _slot_grads(EU, EI, users, items, R_total):
+    """Gradient rows of every slot of (users, items) in the global slot order
+    [users | items j-major], from autograd of the reference's loss."""
+    n = users.numel()
+    u = EU[users].clone().requires_grad_()
+    it = EI[items].clone().requires_grad_()
+    p, q = it[:n], it[n:].view(T, n, D)
+    x = (u * p).sum(-1).repeat(T) - (u.repeat(T, 1) * q.reshape(T * n, D)).sum(-1)
+    (-torch.log(1e-10 + torch.sigmoid(x))).sum().div(R_total).backward()
+    return u.grad, it.grad
+
+
+def _grouped(ids, grads):
+    """Per touched row: its contributions summed in ascending contribution order."""
+    out = {}
+    for k in range(ids.numel()):
+        r = int(ids[k])
+        out[r] = grads[k].clone() if r not in out else out[r] + grads[k]
+    return out
+
+
+def _worker(rank, G, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    tdist.init_process_group('gloo', rank=rank, world_size=G)
+    try:
+        EU, EI, users, items = _global_batch(G)
+        Bc = users.numel()
+        cap = (2 + T) * B
+        lay = ShardLayout(G, B, T, NU, NI, cap)
+        shU = torch.stack([EU[l * G + rank] if l * G + rank < NU else torch.zeros(D)
+                           for l in range(lay.SU)])
+        shI = torch.stack([EI[l * G + rank] if l * G + rank < NI else torch.zeros(D)
+                           for l in range(lay.SI)])
+        fwd, map2, pos, bwd, over = lay.plan(users, items, rank)
+        assert not over
+        send = torch.stack([shU[i] if i >= 0 else shI[-i - 1] for i in fwd.tolist()])
+        recv = torch.empty_like(send)
+        tdist.all_to_all_single(recv, send)
+        n = max(0, min(B, Bc - rank * B))
+        R_total = Bc * T
+        if n:
+            rows = recv[pos[:(2 + T) * n]]
+            u = rows[:n].clone().requires_grad_()
+            it = rows[n:].clone().requires_grad_()
+            p, qn = it[:n], it[n:].view(T, n, D)
+            x = (u * p).sum(-1).repeat(T) - (u.repeat(T, 1) * qn.reshape(T * n, D)).sum(-1)
+            (-torch.log(1e-10 + torch.sigmoid(x))).sum().div(R_total).backward()
+            xloc = torch.cat([u.grad, it.grad])
+        else:
+            xloc = torch.zeros(1, D)
+        sendB = xloc[bwd.long()]
+        recvB = torch.empty_like(sendB)
+        tdist.all_to_all_single(recvB, sendB)
+        owned = {}
+        for tag, ids, S, off in (('u', users, lay.SU, 0), ('i', items, lay.SI, Bc)):
+            keys = lay.keys(ids, S)
+            perm = torch.argsort(keys, stable=True).to(torch.int32)
+            sk = keys[perm.long()]
+            uniq, counts = torch.unique_consecutive(sk, return_counts=True)
+            seg = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(counts, 0)])
+            own, oseg, pp, p2 = lay.own(uniq, seg, perm.long(), map2.long(), off, S, rank)
+            where = dict(zip(pp.tolist(), p2.tolist()))
+            for j in range(own.numel()):
+                acc = None
+                for p_ in range(int(oseg[j]), int(oseg[j + 1])):
+                    row = recvB[where[p_]]
+                    acc = row.clone() if acc is None else acc + row
+                owned[(tag, int(own[j]) * G + rank)] = acc.numpy()
+        q.put((rank, owned))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize('G', [2, 3])
+def test_sharded_protocol_equals_one_process(G):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29600 + G * 10 + os.getpid() % 50
+    procs = [ctx.Process(target=_worker, args=(r, G, port, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(G)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    EU, EI, users, items = _global_batch(G)
+    gu, gi = _slot_grads(EU, EI, users, items, users.numel() * T)
+    ref = {('u', r): v for r, v in _grouped(users, gu).items()}
+    ref.update({('i', r): v for r, v in _grouped(items, gi).items()})
+    merged = {}
+    for rank, owned in got:
+        for k, v in owned.items():
+            assert k not in merged                          # every row on one owner
+            assert k[1] % G == rank
+            merged[k] = v
+    assert merged.keys() == ref.keys()
+    for k in ref:
+        assert np.array_equal(merged[k], ref[k].numpy()), k
