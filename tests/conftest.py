@@ -10,6 +10,15 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 
 
+def free_port():
+    """A TCP port the OS reports free on 127.0.0.1 (rendezvous of multi-rank tests;
+    pid-derived ports collided with sockets left in TIME_WAIT by earlier tests)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
 

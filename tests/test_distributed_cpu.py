@@ -13,6 +13,7 @@ import os
 
 import numpy as np
 import torch
+from conftest import free_port
 import torch.distributed as tdist
 import torch.multiprocessing as mp
 
@@ -111,7 +112,7 @@ def test_two_rank_exchange_equals_global_batch():
     refI = _grouped(gI.reshape(-1, D), items, NI)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(G)]
     for p in procs:
         p.start()

@@ -8,6 +8,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from conftest import free_port
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
@@ -56,7 +57,7 @@ def test_two_ranks_equal_one_gpu_global_batch(tmp_path):
     root = str(tmp_path)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29700 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, port, root, q)) for r in range(2)]
     for p in procs:
         p.start()

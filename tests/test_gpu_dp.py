@@ -10,6 +10,7 @@ import pathlib
 import numpy as np
 import pytest
 import torch
+from conftest import free_port
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
@@ -97,7 +98,7 @@ def test_two_ranks_match_one_process(tmp_path, name):
     assert not dp
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29800 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, port, name, str(tmp_path / f'r{r}'), q))
              for r in range(2)]
     for p in procs:

@@ -18,7 +18,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import ROOT
+from conftest import ROOT, free_port
 from recbole_amd.trainer.exchange import ShardLayout
 
 pytestmark = pytest.mark.gpu
@@ -157,7 +157,7 @@ def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path):
     root = str(tmp_path)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29800 + os.getpid() % 1000
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, port, root, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -208,7 +208,7 @@ print('NCCL_OK')
 def test_sharded_rccl_path_one_rank(tmp_path):
     script = tmp_path / 'nccl_one_rank.py'
     script.write_text(NCCL_SCRIPT)
-    port = str(29900 + os.getpid() % 50)
+    port = str(free_port())
     out = subprocess.run([sys.executable, str(script), ROOT, str(tmp_path), port],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and 'NCCL_OK' in out.stdout, out.stderr[-3000:]

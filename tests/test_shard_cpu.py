@@ -19,6 +19,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from conftest import free_port
 import torch.distributed as tdist
 import torch.multiprocessing as mp
 
@@ -114,7 +115,7 @@ def _worker(rank, G, port, q):
 def test_sharded_protocol_equals_one_process(G):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29600 + G * 10 + os.getpid() % 50
+    port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, G, port, q)) for r in range(G)]
     for p in procs:
         p.start()

@@ -31,7 +31,14 @@ def main(src, out=None):
            'kernels_inside': dict(inside.most_common()),
            'walk_launches_inside': sum(v for k, v in inside.items() if 'walk' in k),
            'sort_launches_inside': sum(v for k, v in inside.items() if 'sort' in k)}
-    print(json.dumps(res, indent=1))
+    # launch timeline inside the window: offset from t0, duration, queue
+    res['timeline'] = [
+        '%9.1f %8.1f q%s %s' % ((int(r['Start_Timestamp']) - t0) / 1e3,
+                               (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3,
+                               r.get('Queue_Id', '?'), r['Kernel_Name'].split('(')[0][-60:])
+        for r in rows if t0 <= int(r['Start_Timestamp']) <= t1]
+    print(json.dumps({k: v for k, v in res.items() if k != 'timeline'}, indent=1))
+    print('\n'.join(res['timeline']))
     if out:
         json.dump(res, open(out, 'w'), indent=1)
 
