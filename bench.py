@@ -347,7 +347,7 @@ def main():
     t0 = time.perf_counter()
     if marks:
         torch.cuda._sleep(1)
-    step.release_prep()
+    step.release_prep(upto=W + K)              # the timed steps' chunks only
     step.run_batches(W, W + K)
     step.sync_params()          # deferred schedule: every row complete inside the timed region
     if marks:
@@ -368,6 +368,7 @@ def main():
     # events bracket kernel time only (not host enqueue gaps).
     # spin long enough (~2.4k cycles/us) to cover the host's enqueue of the whole
     # window (~5 eager launches per step), so the events bracket kernel time only
+    step.release_prep()
     torch.cuda._sleep(int(2.4e3 * 400 * M))
     step.kernel_events, step.kernel_uniq = [], []
     step.run_batches(W + K, W + K + M)

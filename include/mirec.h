@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 7
+#define MIREC_ABI_VERSION 8
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -281,7 +281,13 @@ int mirec_adam_multi_f32(const mirec_adam_table* tables, int32_t n_tables, int32
  * A row with last[r] > s (already complete through s) is left unchanged.
  * n_max_uniq[q] (host array) bounds table q's n_uniq and ahead count (grid
  * size). dense_grad must be NULL. Rows never touched lag until
- * mirec_adam_flush_f32. */
+ * mirec_adam_flush_f32.
+ * last[r] == MIREC_ADAM_ZERO_STATE marks a row whose m and v are all +0 (the
+ * caller sets it, only with weight_decay == 0): every zero-gradient step is then
+ * the identity on p, m and v, bit for bit, so the row is current at any step —
+ * look-ahead and flush leave it untouched; its first gradient step applies
+ * directly (no replay) and ends the mark (last[r] = s + 1). */
+#define MIREC_ADAM_ZERO_STATE 0x7fffffff
 int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n_tables,
                             const int64_t* n_max_uniq, int32_t d,
                             const float* step_consts_dev, const int32_t* step_base_dev,
@@ -305,9 +311,13 @@ int mirec_step_finish(const float* loss_k, int64_t n, float denom, float* loss_h
 
 /* The same for n_steps consecutive steps whose losses sit at
  * loss_k[c*stride .. c*stride+n): loss_hist[step_base + c] (same reduction
- * order as mirec_step_finish), then step_base_dev[0] += n_steps. */
+ * order as mirec_step_finish), then step_base_dev[0] += n_steps. One workgroup
+ * per step; ticket_dev is one device int32, zero before the call and zero
+ * again after it (it orders the last workgroup's counter update after every
+ * workgroup has read the counter). */
 int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride, int32_t n_steps,
-                       float denom, float* loss_hist, int32_t* step_base_dev, void* stream);
+                       float denom, float* loss_hist, int32_t* step_base_dev,
+                       int32_t* ticket_dev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K6  Full-sort scorer + mask + top-K + positive flags, fused (no [n,I] matrix).

@@ -46,6 +46,12 @@ namespace mirec {
 constexpr int kAdamThreads = 256;
 constexpr int kAdamRows = 64;  // table rows per block (streamed / flush)
 constexpr int kMaxTables = 4;
+// last[row] mark of the deferred schedule (MIREC_ADAM_ZERO_STATE in mirec.h): the
+// row's m and v are all +0 and weight_decay is 0, so every zero-gradient step is
+// the identity (m' = fma(-(1-b1), +0, +0) = +0, v' = +0 * b2 = +0, p' = p + (-0)
+// = p, bit for bit). Such a row is current at any step: a flush or a look-ahead
+// leaves it untouched (no load, no store); its first real step starts from it.
+constexpr int kZeroState = MIREC_ADAM_ZERO_STATE;
 
 struct AdamConsts {
   float omb1, omb1m1, b2, omb2, eps, wd;
@@ -222,25 +228,40 @@ __device__ __forceinline__ void adam_replay(V& p, V& m, V& v, int s0, int s1,
   }
 }
 
+// x / bc2_sqrt as div_bc2s for a finite x (the fast path: x = sqrt(v), v <= FLT_MAX).
+__device__ __forceinline__ float div_bc2s_finite(float x, const StepConsts& sc) {
+  const float q = x * sc.rbc;
+  return fmaf(fmaf(-q, sc.bc2s, x), sc.rbc, q);
+}
+
 // Increments q = RN(RN(-ss*me) / den), den = RN(RN(sqrt(ve) / bc2s) + eps), of G
-// steps x N elements. The fast path is computed for all G*N first and one wave
-// vote on its range conditions decides (a branch per step would serialise the
-// steps' chains); the library path recomputes everything.
+// consecutive zero-gradient steps x N elements. The fast path is computed for all
+// G*N first and one wave vote on its range conditions decides (a branch per step
+// would serialise the steps' chains); the library path recomputes everything.
+// The range conditions are tested at the group's first and last step only: over
+// consecutive zero-gradient steps ve (= RN(ve * b2)), |me| (= RN(me * (1-b1)),
+// lerp_small), step_size (host table, non-increasing: FusedAdam.step_constants
+// checks it) and so |num| and den (bc2s non-decreasing) never increase, and every
+// operation involved is monotone, so the bounds at the two ends hold for the
+// steps between them.
 template <int G, int N>
 __device__ __forceinline__ void incr_steps(const float (*me)[N], const float (*ve)[N],
                                            const StepConsts* sc, const AdamConsts& k,
                                            float (*q)[N]) {
   float num[G][N], den[G][N];
-  bool ok = true;
 #pragma unroll
   for (int j = 0; j < G; ++j)
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      ok = ok && sqrt_fast_ok(ve[j][i]);
-      den[j][i] = div_bc2s(sqrt_rn_normal(ve[j][i]), sc[j]) + k.eps;
+      den[j][i] = div_bc2s_finite(sqrt_rn_normal(ve[j][i]), sc[j]) + k.eps;
       num[j][i] = (-sc[j].ss) * me[j][i];
-      ok = ok && div_fast_ok(num[j][i], den[j][i]);
     }
+  int ok = 1;                                   // int: no short-circuit branches
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    ok &= (int)(ve[0][i] <= 0x1.fffffep127f) & (int)(ve[G - 1][i] >= 0x1p-96f) &
+          (int)(fabsf(num[0][i]) <= 0x1p40f) & (int)(fabsf(num[G - 1][i]) >= 0x1p-60f) &
+          (int)(den[0][i] <= 0x1p40f) & (int)(den[G - 1][i] >= 0x1p-40f);
   if (__all(ok)) {
 #pragma unroll
     for (int j = 0; j < G; ++j)
@@ -560,22 +581,28 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   const bool valid = u < n;
   int64_t row = 0;
   int last = st;
+  bool idle = !valid;   // nothing to load or store: outside the list, or a look-ahead
+                        // row in the zero state (already current for every step)
   V p, m, v, g;
   memset(&p, 0, sizeof(V)); m = p; v = p; g = p;
   if (valid) {
     row = ahead ? T.ahead_uniq[u] : T.uniq[u];
     const int64_t off = row * VPR + c;
-    last = T.last[row];
-    p = reinterpret_cast<const V*>(T.p)[off];
-    m = reinterpret_cast<const V*>(T.m)[off];
-    v = reinterpret_cast<const V*>(T.v)[off];
-    if (!ahead) g = grouped_grad<V>(T, u, VPR, c);
+    const int raw = T.last[row];
+    last = raw == kZeroState ? st : raw;
+    idle = ahead && raw == kZeroState;
+    if (!idle) {
+      p = reinterpret_cast<const V*>(T.p)[off];
+      m = reinterpret_cast<const V*>(T.m)[off];
+      v = reinterpret_cast<const V*>(T.v)[off];
+      if (!ahead) g = grouped_grad<V>(T, u, VPR, c);
+    }
   }
   // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop);
   // a row already complete through st (last > st: a repeated look-ahead of the
   // same step) is left as it is
-  replay<V, (VPR >= 64)>(p, m, v, last, st, consts, k);
-  const bool fresh = last <= st;
+  replay<V, (VPR >= 64)>(p, m, v, idle ? st : last, st, consts, k);
+  const bool fresh = !idle && last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
   __syncthreads();
   if (!valid || !fresh) return;

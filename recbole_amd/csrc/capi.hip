@@ -74,31 +74,39 @@ extern "C" int mirec_step_finish(const float* loss_k, int64_t n, float denom, fl
 
 // Per-chunk version: n_steps losses at loss_k[c*stride .. +n), each reduced in
 // exactly step_finish's order, written to loss_hist[step_base + c]; then
-// step_base += n_steps (one launch per chunk instead of one per step).
+// step_base += n_steps. One workgroup per step (the reductions run side by
+// side); the workgroup that takes the last ticket — every workgroup has read
+// step_base before taking one — advances the counter and resets the ticket.
 __global__ __launch_bounds__(1024) void chunk_finish_kernel(const float* __restrict__ loss_k,
                                                             int64_t n, int64_t stride,
                                                             int32_t n_steps, float denom,
                                                             float* __restrict__ loss_hist,
-                                                            int32_t* __restrict__ step_base) {
+                                                            int32_t* __restrict__ step_base,
+                                                            int32_t* __restrict__ ticket) {
   __shared__ float lds[1024];
-  const int32_t st = step_base[0];
-  for (int c = 0; c < n_steps; ++c) {
-    float s = block_fixed_sum(loss_k + (int64_t)c * stride, n, lds);
-    if (threadIdx.x == 0 && loss_hist) loss_hist[st + c] = s / denom;
-    __syncthreads();  // lds reused by the next reduction
+  const int c = blockIdx.x;
+  float s = block_fixed_sum(loss_k + (int64_t)c * stride, n, lds);
+  if (threadIdx.x == 0) {
+    const int32_t st = __hip_atomic_load(step_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (loss_hist) loss_hist[st + c] = s / denom;
+    const int32_t t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == n_steps - 1) {
+      __hip_atomic_store(step_base, st + n_steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  if (threadIdx.x == 0) step_base[0] = st + n_steps;
 }
 
 extern "C" int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride,
                                   int32_t n_steps, float denom, float* loss_hist,
-                                  int32_t* step_base_dev, void* stream) {
-  if (!step_base_dev || n < 0 || n_steps < 0 || stride < n || (n > 0 && n_steps > 0 && !loss_k)) {
+                                  int32_t* step_base_dev, int32_t* ticket_dev, void* stream) {
+  if (!step_base_dev || !ticket_dev || n < 0 || n_steps < 0 || stride < n ||
+      (n > 0 && n_steps > 0 && !loss_k)) {
     set_error("mirec_chunk_finish: bad arguments");
     return -1;
   }
   if (n_steps == 0) return 0;
-  hipLaunchKernelGGL(chunk_finish_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, loss_k, n,
-                     stride, n_steps, denom, loss_hist, step_base_dev);
+  hipLaunchKernelGGL(chunk_finish_kernel, dim3(n_steps), dim3(1024), 0, (hipStream_t)stream,
+                     loss_k, n, stride, n_steps, denom, loss_hist, step_base_dev, ticket_dev);
   return launch_status("mirec_chunk_finish");
 }

@@ -381,6 +381,29 @@ def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None =
     check(rc, "mirec_adam_sparse_grad_f32")
 
 
+ADAM_ZERO_STATE = 0x7fffffff   # MIREC_ADAM_ZERO_STATE (include/mirec.h)
+
+
+def zero_state_marks(m, v, last, weight_decay=0.0):
+    """Set the deferred schedule's step counts for a new window in place:
+    last[r] = ADAM_ZERO_STATE where row r's m and v are all +0 (a fixed point of
+    the zero-gradient Adam step when weight_decay == 0: flushes and look-aheads
+    skip it), else 0."""
+    if weight_decay != 0:
+        last.zero_()
+        return last
+    zs = (m.view(torch.int32) == 0).all(1) & (v.view(torch.int32) == 0).all(1)
+    last.copy_(torch.where(zs, ADAM_ZERO_STATE, 0).to(torch.int32))
+    return last
+
+
+def reset_marks(last):
+    """Window start for counts that already carry zero-state marks: every count
+    that is not a mark restarts at 0 (marks stay: those rows are still +0)."""
+    last.masked_fill_(last != ADAM_ZERO_STATE, 0)
+    return last
+
+
 def adam_tables(specs):
     """ctypes array of mirec_adam_table from dicts with keys p, m, v (2-D float32
     tables of one width) and optional rows + segs (grouped gradient), dense_grad,
@@ -431,11 +454,24 @@ def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
     check(rc, f"adam_multi[{schedule}]")
 
 
+_TICKETS = {}
+
+
+def finish_ticket(device):
+    """Per-device zeroed int32 of mirec_chunk_finish (left zero by every launch)."""
+    key = str(device)
+    t = _TICKETS.get(key)
+    if t is None:
+        t = _TICKETS[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return t
+
+
 def chunk_finish(loss_k, n: int, stride: int, n_steps: int, denom: float, loss_hist, step_base):
     _dev(loss_k, torch.float32, "loss_k")
     _dev(step_base, torch.int32, "step_base")
     rc = lib().mirec_chunk_finish(ptr(loss_k), n, stride, n_steps, float(denom), ptr(loss_hist),
-                                  ptr(step_base), stream_handle())
+                                  ptr(step_base), ptr(finish_ticket(loss_k.device)),
+                                  stream_handle())
     check(rc, "mirec_chunk_finish")
 
 

@@ -144,6 +144,7 @@ class FusedBPRTrainStep(object):
         self.loss_hist = torch.zeros(1, dtype=torch.float32, device=dev)
         self.consts = torch.zeros(4, dtype=torch.float32, device=dev)
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # mirec_chunk_finish
         self.kernel_events = None   # list -> (name, start, end) HIP events (bench.py)
         self.kernel_uniq = []       # per eager step: [touched users, touched items]
         self._plan, self._plan_starts = [], None
@@ -224,6 +225,12 @@ class FusedBPRTrainStep(object):
             t[0].last, t[1].last = self.lastU.data_ptr(), self.lastI.data_ptr()
         else:
             t[0].last = t[1].last = None
+
+    def _adam_state(self):
+        """(m, v, deferred step counts) of each table."""
+        stU, stI = self.opt.state[self.pU], self.opt.state[self.pI]
+        return [(stU['exp_avg'], stU['exp_avg_sq'], self.lastU),
+                (stI['exp_avg'], stI['exp_avg_sq'], self.lastI)]
 
     def _record(self, name, stream, fn):
         ev = self.kernel_events
@@ -332,7 +339,7 @@ class FusedBPRTrainStep(object):
         rc = lib().mirec_chunk_finish(self.loss_k.data_ptr() + 4 * c0 * self.Bg, Bc, self.Bg,
                                       n_steps, float(Bc * self.times),
                                       self.loss_hist.data_ptr(), self.step_idx.data_ptr(),
-                                      stream.cuda_stream)
+                                      self.ticket.data_ptr(), stream.cuda_stream)
         check(rc, 'mirec_chunk_finish')
 
     def _flush(self, stream):
@@ -406,8 +413,8 @@ class FusedBPRTrainStep(object):
         self.loss_hist.zero_()
         self.step_idx.zero_()
         if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
-            self.lastU.zero_()
-            self.lastI.zero_()
+            for m, v, last in self._adam_state():   # zero-state rows: marked (adam.hip)
+                ops.zero_state_marks(m, v, last, self._adam_args[3])
         self._plan, self._plan_starts = self._chunks(cuts), None
         if self.use_graph:                      # capture up front: capture synchronizes
             sizes = sorted({n for _, n, Bc in self._plan if Bc == self.Bg})
@@ -425,10 +432,13 @@ class FusedBPRTrainStep(object):
         self._issue_prep()
         return nb
 
-    def release_prep(self):
+    def release_prep(self, upto=None):
         """Let the chunks held by begin_epoch(hold_prep_from=...) be prepared; the
-        first is issued when run_batches enters it."""
-        self._prep_limit = len(self._plan)
+        first is issued when run_batches enters it. upto: prepare only the chunks
+        that start before global batch `upto` (a later call releases the rest), so a
+        timed region does not also run the sampler walk of the batches after it."""
+        self._prep_limit = (len(self._plan) if upto is None
+                            else self._chunk_of(max(int(upto) - 1, 0)) + 1)
 
     def _issue_prep(self):
         k = self._next_chunk
@@ -702,6 +712,9 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             t[q].last = last.data_ptr()
             t[q].dense_grad = None
             t[q].rows = self.recvB.data_ptr()
+
+    def _adam_state(self):
+        return [(self.shU[1], self.shU[2], self.lastU), (self.shI[1], self.shI[2], self.lastI)]
 
     def _n_local(self, Bc):
         return max(0, min(self.B, Bc - self.rank * self.B))

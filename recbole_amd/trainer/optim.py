@@ -77,6 +77,11 @@ class FusedAdam(torch.optim.Optimizer):
                              np.nextafter(kq32, np.float32(np.inf)), kq32)
         if count and not (out[:, 1] > 0).all():
             raise ValueError(f'beta2={b2} too close to 1: sqrt(1 - beta2^t) rounds to 0 in fp32')
+        # the K5 replay tests its fast-path ranges at the ends of step groups only
+        # (adam.hip incr_steps): |step_size| must not increase, bc2_sqrt not decrease
+        if count > 1 and not ((np.diff(np.abs(out[:, 0])) <= 0).all()
+                              and (np.diff(out[:, 1]) >= 0).all()):
+            raise ValueError('Adam step constants are not monotone (beta1/beta2 outside [0, 1))')
         return out
 
     def prepare_window(self, n_steps_ahead: int, device):
@@ -191,7 +196,8 @@ class FusedAdam(torch.optim.Optimizer):
             self._ensure_state(p)
             self._deferred[p] = {'last': torch.zeros(p.shape[0], dtype=torch.int32,
                                                      device=p.device),
-                                 'window': window, 't0': None, 'consts': None, 'stash': []}
+                                 'window': window, 't0': None, 'consts': None, 'stash': [],
+                                 'marked': False}
             p._mirec_deferred = self
 
     def _dstate(self, p):
@@ -201,7 +207,13 @@ class FusedAdam(torch.optim.Optimizer):
             ds['consts'] = torch.as_tensor(
                 self.step_constants(self.n_steps + 1, ds['window']).reshape(-1),
                 device=p.device)
-            ds['last'].zero_()
+            if ds['marked']:                  # marks kept: those rows are still +0
+                ops.reset_marks(ds['last'])
+            else:                             # rows whose m, v are +0 (adam.hip kZeroState)
+                st = self.state[p]
+                ops.zero_state_marks(st['exp_avg'], st['exp_avg_sq'], ds['last'],
+                                     self._group_args()['weight_decay'])
+                ds['marked'] = True
         return ds
 
     def _dtable(self, p, ds, **kw):
@@ -331,6 +343,7 @@ class FusedAdam(torch.optim.Optimizer):
         for ds in getattr(self, '_deferred', {}).values():
             ds['t0'] = None                   # loaded rows are complete: new window
             ds['stash'] = []
+            ds['marked'] = False              # zero-state marks recomputed from the state
         params = self._params()
         for g, sg in zip(self.param_groups, state_dict['param_groups']):
             for key, v in sg.items():

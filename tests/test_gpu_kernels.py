@@ -363,9 +363,13 @@ def test_fused_adam_dense_step_matches_torch(dev):
 
 @pytest.mark.parametrize('d,beta1,wd', [(128, 0.9, 0.0), (32, 0.3, 0.01), (64, 0.9, 0.0)])
 @pytest.mark.parametrize('wide', [False, True])    # True: a row bound that selects float2 columns
-def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide):
+@pytest.mark.parametrize('marks', [False, True])   # True: zero-state marks (MIREC_ADAM_ZERO_STATE)
+def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide, marks):
     """The deferred schedule (touch + replay, flushes at irregular steps) leaves
-    p, m, v bit-identical to the streamed dense Adam over every row."""
+    p, m, v bit-identical to the streamed dense Adam over every row. With marks,
+    half the rows start from a nonzero (m, v) and the rest from +0 marked as a
+    zero-gradient fixed point (skipped by look-aheads and flushes until their
+    first gradient step)."""
     from recbole_amd import ops
     from recbole_amd.trainer.optim import FusedAdam
     g = torch.Generator().manual_seed(d)
@@ -397,11 +401,23 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide):
         aheads.append(row)
     snaps = []
 
+    m0 = [torch.zeros(n, d) for n in sizes]
+    v0 = [torch.zeros(n, d) for n in sizes]
+    if marks:                        # rows 0, 2, 4, ... carry optimizer state
+        for q, n in enumerate(sizes):
+            m0[q][::2] = torch.randn(len(range(0, n, 2)), d, generator=g) * 1e-3
+            v0[q][::2] = torch.rand(len(range(0, n, 2)), d, generator=g) * 1e-6
+
     def run(schedule, flush_at=(), check_ahead=False):
         P = [x.clone().to(dev) for x in init]
-        M = [torch.zeros_like(x) for x in P]
-        V = [torch.zeros_like(x) for x in P]
+        M = [x.clone().to(dev) for x in m0]
+        V = [x.clone().to(dev) for x in v0]
         last = [torch.zeros(x.shape[0], dtype=torch.int32, device=dev) for x in P]
+        if marks and schedule == 'deferred':
+            for q in range(2):
+                ops.zero_state_marks(M[q], V[q], last[q], wd)
+                if wd == 0:
+                    assert int((last[q] == ops.ADAM_ZERO_STATE).sum()) == sizes[q] // 2
         base = torch.zeros(1, dtype=torch.int32, device=dev)
         for s, batch in enumerate(batches):
             specs = []
@@ -424,7 +440,9 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide):
                     assert torch.equal(P[q].cpu()[k], snaps[s][q][k]), (s, q)
         if schedule == 'deferred':
             ops.adam_multi(tabs, d, consts, base, 0, 'flush', beta1=beta1, weight_decay=wd)
-            assert all(bool((x == steps).all()) for x in last)
+            assert all(bool(((x == steps) | (x == ops.ADAM_ZERO_STATE)).all()) for x in last)
+            if marks and wd == 0:    # some rows were never touched: still marked
+                assert any(bool((x == ops.ADAM_ZERO_STATE).any()) for x in last)
         return [t.cpu() for t in P + M + V]
 
     ref = run('streamed')
