@@ -22,6 +22,24 @@
 
 namespace mirec {
 
+// Phase profile of the single-block walk (build variant -DMIREC_WALK_PROF, see
+// tools/probe_walk.py): thread 0 accumulates shader-clock deltas per phase.
+#ifdef MIREC_WALK_PROF
+__device__ unsigned long long g_walk_prof[16];
+#define WALK_MARK(slot, t0)                                                          \
+  do {                                                                               \
+    if (threadIdx.x == 0) {                                                          \
+      const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                   \
+      atomicAdd(&g_walk_prof[slot], t1_ - (t0));                                     \
+      (t0) = t1_;                                                                    \
+    }                                                                                \
+  } while (0)
+#define WALK_COUNT(slot, n) do { if (threadIdx.x == 0) atomicAdd(&g_walk_prof[slot], (unsigned long long)(n)); } while (0)
+#else
+#define WALK_MARK(slot, t0) do {} while (0)
+#define WALK_COUNT(slot, n) do {} while (0)
+#endif
+
 constexpr int kSampThreads = 1024;
 constexpr int kPer = 4;          // round-0 slots per lane per pass
 constexpr int kListLds = 4096;   // pending-slot lists in LDS up to this many slots
@@ -81,6 +99,7 @@ __device__ __forceinline__ void walk_refill(const int32_t* __restrict__ rl, int6
   int sel = 0;
   while (nrej > 64) {                       // wide rounds: whole block
     if (++rounds > max_rounds) { livelock = 1; break; }
+    WALK_COUNT(9, 1);
     int32_t nnew = 0;
     for (int32_t base = 0; base < nrej; base += kSampThreads) {
       const int32_t i = base + threadIdx.x;
@@ -105,6 +124,7 @@ __device__ __forceinline__ void walk_refill(const int32_t* __restrict__ rl, int6
     nrej = nnew;
     __syncthreads();
   }
+  WALK_COUNT(10, nrej);
   if (nrej > 0 && !livelock) {              // tail: one wave, no block barriers
     if (threadIdx.x < 64) {
       int n = nrej;
@@ -113,6 +133,7 @@ __device__ __forceinline__ void walk_refill(const int32_t* __restrict__ rl, int6
       int ll = 0;
       while (n > 0) {
         if (++rounds > max_rounds) { ll = 1; break; }
+        WALK_COUNT(11, 1);
         int rej = 0;
         if (lane < n) {
           int64_t pos = p + lane;
@@ -153,6 +174,9 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
   int bad_key = 0;
   int livelock = 0;
 
+#ifdef MIREC_WALK_PROF
+  unsigned long long tp = __builtin_amdgcn_s_memtime();
+#endif
   for (int64_t b = 0; b < n_batches && !livelock; ++b) {
     // batch b = one sample_by_key_ids call: fixed-size batches, or the segments
     // [seg_ptr[b], seg_ptr[b+1]) of the key list (output packed at k0 * num)
@@ -182,6 +206,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
       return (key < 0 || key >= key_space) ? -1 : key;
     };
 
+    WALK_MARK(0, tp);                         // batch setup + keys to LDS
     // ---- round 0: fill every slot, collect rejected slots in ascending order
     int32_t nrej = 0;
     for (int64_t base = 0; base < total; base += (int64_t)kSampThreads * kPer) {
@@ -219,10 +244,13 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     }
     pr = (pr + total) % L;
     __syncthreads();
+    WALK_MARK(1, tp);                         // round 0 incl. its scan
+    WALK_COUNT(8, nrej);
 
     walk_refill(rl, L, pr, used, key_of, bout, cur, nxt, nrej, scan_lds, wl, &pr_lds,
                 livelock);
     __syncthreads();                          // LDS lists / keys reused by the next batch
+    WALK_MARK(2, tp);                         // refill rounds
   }
   if (bad_key) atomicExch(status, -2);
   if (livelock && threadIdx.x == 0) atomicExch(status, -3);
@@ -329,7 +357,8 @@ __global__ __launch_bounds__(kSampThreads) void walk_refill_kernel(
     return (key < 0 || key >= key_space) ? -1 : key;
   };
   int livelock = 0;
-  walk_refill(rl, L, pr, used, key_of, bout, cur, nxt, nrej, scan_lds, wl, &pr_lds, livelock);
+  walk_refill(rl, L, pr, used, key_of, bout, cur, nxt, nrej, scan_lds, wl, &pr_lds,
+              livelock);
   __syncthreads();
   if (threadIdx.x == 0) {
     pr_dev[0] = pr;
@@ -356,6 +385,18 @@ __global__ __launch_bounds__(256) void used_bitmap_kernel(const int64_t* __restr
 }  // namespace mirec
 
 using namespace mirec;
+
+#ifdef MIREC_WALK_PROF
+extern "C" int mirec_walk_prof(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_walk_prof), sizeof(unsigned long long) * 16) !=
+      hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_walk_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" size_t mirec_sample_walk_workspace_size(int64_t batch_keys, int64_t num) {
   if (batch_keys <= 0 || num <= 0) return 256;
