@@ -348,7 +348,9 @@ def main():
     if marks:
         torch.cuda._sleep(1)
     step.release_prep(upto=W + K)              # the timed steps' chunks only
+    eager0 = step.n_eager_steps
     step.run_batches(W, W + K)
+    eager_timed = step.n_eager_steps - eager0
     step.sync_params()          # deferred schedule: every row complete inside the timed region
     if marks:
         torch.cuda._sleep(1)
@@ -413,7 +415,9 @@ def main():
                                       f'rows per rank pair)',
                            'replicated': f'dp{world} (replicated tables, RCCL all-gather of '
                                          f'per-row loss coefficients)'}[dp_mode],
-                   'exchange_graph': bool(step.use_graph)},
+                   'exchange_graph': bool(step.use_graph),
+                   'chunk_plan_timed': [n for b0, n, _ in step._plan if W <= b0 < W + K],
+                   'eager_steps_timed': eager_timed},
         'roofline': roof,
         'roofline_bpr': roof_bpr,
         'kernels_us': kernels_us,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 8
+#define MIREC_ABI_VERSION 9
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -190,6 +190,32 @@ int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
  * n_out[n_batches-1] = 0. */
 int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t stride,
                           int64_t n_batches, int32_t* out, int32_t* n_out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Chunk preparation of the fused pairwise train step (the data side of
+ * Trainer._train_epoch, trainer.py:157-174, for n_batches consecutive batches of
+ * the shuffled train table: GeneralNegSampleDataLoader._next_batch_data +
+ * _neg_sampling, general_dataloader.py:181-251) in ONE call, stream-ordered:
+ *   keys     user_keys[b*Bc + k] = users[s0 + b*Bc + k];
+ *            item_keys[b*(1+T)*Bc + k] = items[s0 + b*Bc + k]   (row 0: positives)
+ *   K4 walk  negatives of each batch into item_keys rows 1..T (mirec_sample_walk)
+ *   K2       groupings of the user keys and of the [pos | neg] item keys per batch
+ *            (mirec_segment_sort_batched, key spaces n_users / n_items)
+ *   ahead    look-ahead lists (mirec_uniq_ahead_diff), when u_ahead != NULL
+ * Every pointer is a device pointer except the struct itself (host). sort_ws:
+ * mirec_segment_sort_workspace_size(n_batches*(1+T)*Bc, n_items) bytes. */
+typedef struct mirec_chunk_prep {
+  const int64_t* users;  const int64_t* items;  int64_t s0;
+  int64_t n_batches, Bc, T;
+  int64_t* user_keys;    int64_t* item_keys;
+  const int32_t* random_list; int64_t L; int64_t* pr_dev;
+  const int64_t* used_ptr; const int32_t* used_cols; const uint32_t* used_bits; int64_t n_bits;
+  int64_t n_users, n_items; int32_t reject; int32_t* status;
+  void* walk_ws; size_t walk_ws_bytes; void* sort_ws; size_t sort_ws_bytes;
+  int32_t *u_perm, *u_uniq, *u_seg, *u_nu, *i_perm, *i_uniq, *i_seg, *i_nu;
+  int32_t *u_ahead, *u_nah, *i_ahead, *i_nah;
+} mirec_chunk_prep;
+int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
 
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of

@@ -48,6 +48,21 @@ class AdamTable(ctypes.Structure):
                 ('last', _P), ('ahead_uniq', _P), ('ahead_n_uniq', _P)]
 
 
+class ChunkPrep(ctypes.Structure):
+    """struct mirec_chunk_prep (include/mirec.h)."""
+    _fields_ = [('users', _P), ('items', _P), ('s0', c_int64),
+                ('n_batches', c_int64), ('Bc', c_int64), ('T', c_int64),
+                ('user_keys', _P), ('item_keys', _P),
+                ('random_list', _P), ('L', c_int64), ('pr_dev', _P),
+                ('used_ptr', _P), ('used_cols', _P), ('used_bits', _P), ('n_bits', c_int64),
+                ('n_users', c_int64), ('n_items', c_int64), ('reject', c_int32), ('status', _P),
+                ('walk_ws', _P), ('walk_ws_bytes', c_size_t), ('sort_ws', _P),
+                ('sort_ws_bytes', c_size_t),
+                ('u_perm', _P), ('u_uniq', _P), ('u_seg', _P), ('u_nu', _P),
+                ('i_perm', _P), ('i_uniq', _P), ('i_seg', _P), ('i_nu', _P),
+                ('u_ahead', _P), ('u_nah', _P), ('i_ahead', _P), ('i_nah', _P)]
+
+
 # Every symbol include/mirec.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "mirec_abi_version": (c_int, []),
@@ -83,6 +98,7 @@ SIGNATURES = {
     "mirec_segment_sort_batched": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
+    "mirec_prepare_chunk": (c_int, [_P, _P]),
     "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,
                                          _P]),
     "mirec_segment_scatter_add_workspace_size": (c_size_t, [c_int64, c_int32]),
@@ -129,7 +145,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class NativeError(RuntimeError):

@@ -577,6 +577,9 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   // that orders every thread's read of `last` before the row's write sits at
   // the end, so no thread leaves early.
   const int n = ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
+  // the grid is sized for the host's bound on the lists: blocks past the actual
+  // count leave at once (block-uniform: no thread reaches the barrier below)
+  if ((int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) >= n) return;
   const int st = step_base[0] + step_off;
   const bool valid = u < n;
   int64_t row = 0;

@@ -110,3 +110,4 @@ extern "C" int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride
                      loss_k, n, stride, n_steps, denom, loss_hist, step_base_dev, ticket_dev);
   return launch_status("mirec_chunk_finish");
 }
+

@@ -6,6 +6,7 @@
 // instruction; consecutive lanes walk one row, so each row is read as whole
 // 64-B segments.
 #include "common.h"
+#include <algorithm>
 
 namespace mirec {
 
@@ -118,4 +119,52 @@ extern "C" int mirec_window_gather(const void* col, int32_t elem_bytes, const in
     hipLaunchKernelGGL(window_gather_kernel<int32_t>, dim3((unsigned)g), dim3(256), 0, st,
                        (const int32_t*)col, start, len, n, L, (int32_t*)out);
   return launch_status("mirec_window_gather");
+}
+
+// ---- chunk preparation (include/mirec.h mirec_chunk_prep)
+namespace mirec {
+
+int sort_chunk_pair(const int64_t* ukeys, int64_t nU_keys, int64_t Bu, int64_t u_space,
+                    int32_t* u_perm, int32_t* u_uniq, int32_t* u_seg, int32_t* u_nu,
+                    const int64_t* ikeys, int64_t nI_keys, int64_t Bi, int64_t i_space,
+                    int32_t* i_perm, int32_t* i_uniq, int32_t* i_seg, int32_t* i_nu,
+                    int64_t n_batches, int32_t* u_ahead, int32_t* u_nah, int32_t* i_ahead,
+                    int32_t* i_nah, void* ws, size_t ws_bytes, hipStream_t st);
+
+__global__ __launch_bounds__(256) void chunk_keys_kernel(const int64_t* __restrict__ users,
+                                                         const int64_t* __restrict__ items,
+                                                         int64_t s0, int64_t n, int64_t Bc,
+                                                         int64_t KI, int64_t* __restrict__ ukeys,
+                                                         int64_t* __restrict__ ikeys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    ukeys[i] = users[s0 + i];
+    ikeys[(i / Bc) * KI + i % Bc] = items[s0 + i];
+  }
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {
+  if (!p || !p->users || !p->items || !p->user_keys || !p->item_keys || p->n_batches <= 0 ||
+      p->Bc <= 0 || p->T <= 0 || p->s0 < 0) {
+    mirec::set_error("mirec_prepare_chunk: bad arguments");
+    return -1;
+  }
+  const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(mirec::chunk_keys_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     p->users, p->items, p->s0, n, p->Bc, KI, p->user_keys, p->item_keys);
+  int rc = mirec::launch_status("mirec_prepare_chunk: keys");
+  if (rc) return rc;
+  rc = mirec_sample_walk(p->random_list, p->L, p->pr_dev, p->user_keys, n, p->Bc, p->n_batches,
+                         p->T, p->used_ptr, p->used_cols, p->used_bits, p->n_bits, p->n_users,
+                         p->reject, p->item_keys + p->Bc, KI, p->status, p->walk_ws,
+                         p->walk_ws_bytes, stream);
+  if (rc) return rc;
+  return mirec::sort_chunk_pair(p->user_keys, n, p->Bc, p->n_users, p->u_perm, p->u_uniq,
+                                p->u_seg, p->u_nu, p->item_keys, p->n_batches * KI, KI,
+                                p->n_items, p->i_perm, p->i_uniq, p->i_seg, p->i_nu,
+                                p->n_batches, p->u_ahead, p->u_nah, p->i_ahead, p->i_nah,
+                                p->sort_ws, p->sort_ws_bytes, (hipStream_t)stream);
 }

@@ -209,6 +209,61 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     WALK_MARK(0, tp);                         // batch setup + keys to LDS
     // ---- round 0: fill every slot, collect rejected slots in ascending order
     int32_t nrej = 0;
+    if (Kb <= kSampThreads && num <= 4 && lds_keys) {
+      // one thread per key k: its slots t = j*Kb + k (j < num) — positions of one j
+      // are consecutive over the threads (coalesced), the key is read once and its
+      // membership rows are hit num times; ascending t = (j, k) order comes from one
+      // block scan of the num per-j flags packed as 16-bit fields
+      const int k = threadIdx.x;
+      const bool has = k < Kb;
+      const int64_t key = has && reject ? key_lds[k] : 0;
+      int32_t v4[4];
+      int64_t pos = pr + k;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (pos >= L) pos %= L;
+        v4[j] = (has && j < num) ? rl[pos] : 0;
+        pos += Kb;
+      }
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (has && j < num) {
+          bout[(int64_t)j * Kb + k] = v4[j];
+          if (reject) {
+            if (key < 0) bad_key = 1;
+            else if (is_used(used, key, v4[j])) packed |= 1ull << (16 * j);
+          }
+        }
+      }
+      // exclusive scan of the packed per-j counts (each field < 2^16: Kb <= 1024)
+      const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+      uint64_t incl = packed;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      __shared__ uint64_t wsum[kSampThreads / 64];
+      if (lane == 63) wsum[wid] = incl;
+      __syncthreads();
+      uint64_t before = 0, tot = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        const uint64_t c = wsum[w];
+        before += w < wid ? c : 0;
+        tot += c;
+      }
+      const uint64_t excl = before + incl - packed;
+      int base_j = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cj = (int)((tot >> (16 * j)) & 0xffff);
+        if ((packed >> (16 * j)) & 1ull)
+          cur[base_j + (int)((excl >> (16 * j)) & 0xffff)] = (int32_t)((int64_t)j * Kb + k);
+        base_j += cj;
+      }
+      nrej = base_j;
+    } else
     for (int64_t base = 0; base < total; base += (int64_t)kSampThreads * kPer) {
       const int64_t t0 = base + (int64_t)threadIdx.x * kPer;
       int32_t vals[kPer];

@@ -21,7 +21,7 @@ constexpr int kSortThreads = 1024;
 constexpr int kLdsMax = 8192;
 constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
 
-__device__ __forceinline__ int nbits_for(int64_t key_space) {
+__host__ __device__ __forceinline__ int nbits_for(int64_t key_space) {
   int b = 0;
   while (b < 31 && ((int64_t)1 << b) < key_space) ++b;
   return b;
@@ -57,13 +57,21 @@ __device__ void emit_segments(KeyPtr skey, int n, int32_t* __restrict__ uniq,
 
 // One workgroup per batch: batch b sorts keys[b*batch_n, min((b+1)*batch_n, n_total))
 // and writes perm/uniq at b*batch_n, seg at b*(batch_n+1), n_uniq[b].
-__global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
+struct SortLds {
+  int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
+  int scan[kSortThreads / 64 + 1];
+  uint64_t wtot[kSortThreads / 64][4];   // per-wave packed digit counts
+};
+
+__device__ __forceinline__ void segsort_lds_batch(
     const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n, int nbits,
     int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
-    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all) {
-  __shared__ int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
-  __shared__ int scan_lds[kSortThreads / 64 + 1];
-  const int64_t b = blockIdx.x;
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all, int64_t b, SortLds& L) {
+  int32_t* kA = L.kA;
+  int32_t* vA = L.vA;
+  int32_t* kB = L.kB;
+  int32_t* vB = L.vB;
+  int* scan_lds = L.scan;
   const int n = (int)min((int64_t)batch_n, n_total - b * batch_n);
   const int64_t* __restrict__ keys = keys_all + b * batch_n;
   int32_t* __restrict__ perm = perm_all + b * batch_n;
@@ -79,19 +87,71 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
   const int ipt = (n + kSortThreads - 1) / kSortThreads;
   const int lo = threadIdx.x * ipt;
   const int hi = min(n, lo + ipt);
-  for (int bit = 0; bit < nbits; ++bit) {
-    int z = 0;
-    for (int i = lo; i < hi; ++i) z += ((ks[i] >> bit) & 1) ? 0 : 1;
-    int Z;
-    const int ez = block_exclusive_scan(z, scan_lds, &Z);
-    int zb = ez;  // zeros before element i
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  // Stable LSD passes of 4-bit digits (a blocked arrangement: thread t owns
+  // positions [lo, hi)). Per-digit counts travel packed, four 16-bit fields per
+  // 64-bit word (n <= 8192 < 2^16: no carries), so one wave scan of four words
+  // and one barrier give every thread its per-digit exclusive prefix; the
+  // destination of an item is (items of smaller digits) + (items of its digit
+  // before it) — the same permutation as the 1-bit splits, in a quarter of the
+  // passes.
+  for (int shift = 0; shift < nbits; shift += 4) {
+    uint64_t c[4] = {0ull, 0ull, 0ull, 0ull};
+    for (int i = lo; i < hi; ++i) {
+      const int d = (ks[i] >> shift) & 15;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) c[w] += (d >> 2) == w ? 1ull << (16 * (d & 3)) : 0ull;
+    }
+    uint64_t inc[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) inc[w] = c[w];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint64_t y = __shfl_up(inc[w], off, 64);
+        if (lane >= off) inc[w] += y;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) L.wtot[wid][w] = inc[w];
+    }
+    __syncthreads();
+    uint64_t ex[4], tot[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { ex[w] = inc[w] - c[w]; tot[w] = 0ull; }
+    for (int v = 0; v < nw; ++v) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint64_t x = L.wtot[v][w];
+        ex[w] += v < wid ? x : 0ull;
+        tot[w] += x;
+      }
+    }
+    auto fsum = [](uint64_t x) {     // sum of the four 16-bit fields
+      return (int)((x & 0xffff) + ((x >> 16) & 0xffff) + ((x >> 32) & 0xffff) + (x >> 48));
+    };
     for (int i = lo; i < hi; ++i) {
       const int32_t kv = ks[i];
-      const int one = (kv >> bit) & 1;
-      const int dst = one ? (Z + (i - zb)) : zb;
+      const int d = (kv >> shift) & 15;
+      const int w = d >> 2, f = 16 * (d & 3);
+      int base = 0;
+      uint64_t e = 0ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        base += q < w ? fsum(tot[q]) : 0;
+        if (q == w) {
+          base += fsum(tot[q] & ((1ull << f) - 1ull));
+          e = ex[q];
+          ex[q] += 1ull << f;
+        }
+      }
+      const int dst = base + (int)((e >> f) & 0xffff);
       kd[dst] = kv;
       vd[dst] = vs[i];
-      zb += 1 - one;
     }
     __syncthreads();
     int32_t* t;
@@ -100,6 +160,31 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
   }
   for (int i = threadIdx.x; i < n; i += kSortThreads) perm[i] = vs[i];
   emit_segments(ks, n, uniq, seg, n_uniq, scan_lds);
+}
+
+__global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
+    const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n, int nbits,
+    int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all) {
+  __shared__ SortLds L;
+  segsort_lds_batch(keys_all, n_total, batch_n, nbits, perm_all, uniq_all, seg_all, n_uniq_all,
+                    blockIdx.x, L);
+}
+
+// Two batched sorts in one launch (the user and the item keys of a chunk):
+// workgroups [0, nbA) sort table A's batches, the rest table B's.
+struct SortJob {
+  const int64_t* keys; int64_t n_total; int batch_n; int nbits;
+  int32_t *perm, *uniq, *seg, *n_uniq;
+};
+
+__global__ __launch_bounds__(kSortThreads) void segsort_lds2_kernel(SortJob A, SortJob B,
+                                                                    int64_t nbA) {
+  __shared__ SortLds L;
+  const bool a = (int64_t)blockIdx.x < nbA;
+  const SortJob& J = a ? A : B;
+  segsort_lds_batch(J.keys, J.n_total, J.batch_n, J.nbits, J.perm, J.uniq, J.seg, J.n_uniq,
+                    a ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nbA, L);
 }
 
 // Same algorithm, global ping-pong buffers, processed in chunks of
@@ -657,12 +742,10 @@ namespace mirec {
 
 constexpr int kDiffLds = 8192;
 
-__global__ __launch_bounds__(kSortThreads) void uniq_ahead_diff_kernel(
+__device__ __forceinline__ void uniq_ahead_diff_batch(
     const int32_t* __restrict__ uniq, const int32_t* __restrict__ n_uniq, int64_t stride,
-    int64_t n_batches, int32_t* __restrict__ out, int32_t* __restrict__ n_out) {
-  __shared__ int32_t a_lds[kDiffLds];
-  __shared__ int scan_lds[kSortThreads / 64 + 1];
-  const int64_t b = blockIdx.x;
+    int64_t n_batches, int32_t* __restrict__ out, int32_t* __restrict__ n_out, int64_t b,
+    int32_t* a_lds, int* scan_lds) {
   if (b + 1 >= n_batches) {                 // last batch of the chunk: nothing ahead
     if (threadIdx.x == 0) n_out[b] = 0;
     return;
@@ -695,6 +778,29 @@ __global__ __launch_bounds__(kSortThreads) void uniq_ahead_diff_kernel(
   if (threadIdx.x == 0) n_out[b] = base;
 }
 
+__global__ __launch_bounds__(kSortThreads) void uniq_ahead_diff_kernel(
+    const int32_t* __restrict__ uniq, const int32_t* __restrict__ n_uniq, int64_t stride,
+    int64_t n_batches, int32_t* __restrict__ out, int32_t* __restrict__ n_out) {
+  __shared__ int32_t a_lds[kDiffLds];
+  __shared__ int scan_lds[kSortThreads / 64 + 1];
+  uniq_ahead_diff_batch(uniq, n_uniq, stride, n_batches, out, n_out, blockIdx.x, a_lds, scan_lds);
+}
+
+struct DiffJob {
+  const int32_t* uniq; const int32_t* n_uniq; int64_t stride; int32_t* out; int32_t* n_out;
+};
+
+// Both tables' look-ahead lists in one launch: workgroups [0, nb) table A, the rest B.
+__global__ __launch_bounds__(kSortThreads) void uniq_ahead_diff2_kernel(DiffJob A, DiffJob B,
+                                                                        int64_t nb) {
+  __shared__ int32_t a_lds[kDiffLds];
+  __shared__ int scan_lds[kSortThreads / 64 + 1];
+  const bool a = (int64_t)blockIdx.x < nb;
+  const DiffJob& J = a ? A : B;
+  uniq_ahead_diff_batch(J.uniq, J.n_uniq, J.stride, nb, J.out, J.n_out,
+                        a ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nb, a_lds, scan_lds);
+}
+
 }  // namespace mirec
 
 extern "C" int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq, int64_t stride,
@@ -710,3 +816,38 @@ extern "C" int mirec_uniq_ahead_diff(const int32_t* uniq, const int32_t* n_uniq,
                      n_batches, out, n_out);
   return mirec::launch_status("mirec_uniq_ahead_diff");
 }
+
+// ---- both tables of a chunk (mirec_prepare_chunk, gather.hip): one sort launch
+// and one look-ahead launch when both fit the LDS path, else the separate calls.
+namespace mirec {
+int sort_chunk_pair(const int64_t* ukeys, int64_t nU_keys, int64_t Bu, int64_t u_space,
+                    int32_t* u_perm, int32_t* u_uniq, int32_t* u_seg, int32_t* u_nu,
+                    const int64_t* ikeys, int64_t nI_keys, int64_t Bi, int64_t i_space,
+                    int32_t* i_perm, int32_t* i_uniq, int32_t* i_seg, int32_t* i_nu,
+                    int64_t n_batches, int32_t* u_ahead, int32_t* u_nah, int32_t* i_ahead,
+                    int32_t* i_nah, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (Bu <= kLdsMax && Bi <= kLdsMax && u_space <= INT32_MAX && i_space <= INT32_MAX &&
+      nU_keys == n_batches * Bu && nI_keys == n_batches * Bi && n_batches > 0) {
+    SortJob A = {ukeys, nU_keys, (int)Bu, nbits_for(u_space), u_perm, u_uniq, u_seg, u_nu};
+    SortJob B = {ikeys, nI_keys, (int)Bi, nbits_for(i_space), i_perm, i_uniq, i_seg, i_nu};
+    hipLaunchKernelGGL(segsort_lds2_kernel, dim3((unsigned)(2 * n_batches)), dim3(kSortThreads),
+                       0, st, A, B, n_batches);
+    int rc = launch_status("mirec_prepare_chunk: sort");
+    if (rc || !u_ahead) return rc;
+    DiffJob DA = {u_uniq, u_nu, Bu, u_ahead, u_nah};
+    DiffJob DB = {i_uniq, i_nu, Bi, i_ahead, i_nah};
+    hipLaunchKernelGGL(uniq_ahead_diff2_kernel, dim3((unsigned)(2 * n_batches)),
+                       dim3(kSortThreads), 0, st, DA, DB, n_batches);
+    return launch_status("mirec_prepare_chunk: look-ahead");
+  }
+  int rc = mirec_segment_sort_batched(ukeys, nU_keys, Bu, u_space, u_perm, u_uniq, u_seg, u_nu,
+                                      ws, ws_bytes, st);
+  if (rc) return rc;
+  rc = mirec_segment_sort_batched(ikeys, nI_keys, Bi, i_space, i_perm, i_uniq, i_seg, i_nu, ws,
+                                  ws_bytes, st);
+  if (rc || !u_ahead) return rc;
+  rc = mirec_uniq_ahead_diff(u_uniq, u_nu, Bu, n_batches, u_ahead, u_nah, st);
+  if (rc) return rc;
+  return mirec_uniq_ahead_diff(i_uniq, i_nu, Bi, n_batches, i_ahead, i_nah, st);
+}
+}  // namespace mirec

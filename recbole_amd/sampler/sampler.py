@@ -151,6 +151,16 @@ class AbstractSampler(object):
                                n_batches=n_batches, out=out, status=self._status, ws=ws,
                                out_stride=out_stride, used_bits=bits, n_bits=n_bits)
 
+    def walk_args(self, device):
+        """Device operands of the walk for the native chunk preparation
+        (mirec_prepare_chunk): (random_list, pr, used_ptr, used_cols, used_bits,
+        n_bits, reject, status)."""
+        if self._rl_dev is None:
+            self.to_device(device)
+        up, uc = self._used_dev()
+        bits, n_bits = self._used_bits()
+        return self._rl_dev, self._pr_dev, up, uc, bits, n_bits, up is not None, self._status
+
     def launch_segments(self, keys_dev, seg_ptr_dev, max_seg_keys, num):
         """Successive sample_by_key_ids calls (call s over keys_dev[seg_ptr[s]:
         seg_ptr[s+1]]) in ONE launch, the walk continuing from call to call; call

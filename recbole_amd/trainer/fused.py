@@ -52,6 +52,52 @@ from recbole_amd.trainer.exchange import ExchangeLayout
 ADAM_MODES = ('deferred', 'streamed')
 
 
+_PREP_STREAMS = {}
+
+
+def _prep_stream_for(dev):
+    """A side stream whose hardware queue is not the current stream's.
+
+    HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 by
+    default) round-robin; a side stream that lands on the main stream's queue
+    runs in order with it, so the chunk preparation would run behind the model
+    steps instead of beside them. Probe: hold the current stream busy with a
+    spin kernel and see whether an event on the candidate completes meanwhile
+    (a dedicated high-priority or CU-masked queue avoids the sharing too, but
+    measured 4-8x slower kernels on both queues: the extra queue oversubscribes
+    the hardware queue slots). Falls back to the first candidate."""
+    key = str(dev)
+    st = _PREP_STREAMS.get(key)
+    if st is not None:
+        return st
+    import time
+    main = torch.cuda.current_stream(dev)
+    first = None
+    for _ in range(8):
+        cand = torch.cuda.Stream(device=dev)
+        first = first or cand
+        torch.cuda.synchronize(dev)
+        with torch.cuda.stream(main):
+            torch.cuda._sleep(int(2.4e3 * 3000))          # ~3 ms of spinning on main
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(cand):
+            torch.cuda._sleep(1)
+            ev.record(cand)
+        t0 = time.perf_counter()
+        free = False
+        while time.perf_counter() - t0 < 1.5e-3:
+            if ev.query():
+                free = True
+                break
+        torch.cuda.synchronize(dev)
+        if free:
+            st = cand
+            break
+    st = st or first
+    _PREP_STREAMS[key] = st
+    return st
+
+
 class _Slot(object):
     """Buffers of one chunk of prepared batches (global-batch keys and groupings;
     for G > 1 also this rank's local key slices)."""
@@ -81,7 +127,7 @@ class _Slot(object):
         self.free = torch.cuda.Event()
         self.free_recorded = False
         self.chunk = None            # (first global batch, n batches, global batch size)
-        self.graphs = {}             # n batches -> HIP graph of that chunk's model-side steps
+        self.graphs = {}             # (n batches, entry, flush) -> HIP graph of the model side
 
 
 class FusedBPRTrainStep(object):
@@ -99,6 +145,8 @@ class FusedBPRTrainStep(object):
     A ragged last batch is computed whole on every rank (no exchange)."""
 
     CHUNK = 64
+    SLOTS = 3                     # chunk buffers in flight (walk, grouping, model)
+    RAMP = (4, 8, 16, 32)         # chunk sizes after a (re)start of the prep pipeline
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None):
@@ -136,11 +184,14 @@ class FusedBPRTrainStep(object):
         self.xchg = torch.empty(G * self.layout.W, dtype=torch.float32, device=dev)
         self.loss_k = torch.empty(self.C * self.Bg, dtype=torch.float32, device=dev)
         deferred = adam_mode == 'deferred'
-        self.slots = [_Slot(self.C, B, T, G, dev, deferred) for _ in range(2)]
+        self.slots = [_Slot(self.C, B, T, G, dev, deferred) for _ in range(self.SLOTS)]
         self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(self.Bg, T),
                                    dtype=torch.uint8, device=dev)
         self.sort_ws = None
-        self.prep_stream = torch.cuda.Stream(device=dev)
+        # keys, K4 walk, K2 grouping: on a side stream that does not share the
+        # main stream's hardware queue (_prep_stream_for)
+        self.prep_stream = _prep_stream_for(dev)
+        self.zero_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
         self.loss_hist = torch.zeros(1, dtype=torch.float32, device=dev)
         self.consts = torch.zeros(4, dtype=torch.float32, device=dev)
         self.step_idx = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -149,6 +200,7 @@ class FusedBPRTrainStep(object):
         self.kernel_uniq = []       # per eager step: [touched users, touched items]
         self._plan, self._plan_starts = [], None
         self._current = True        # no step enqueued since the last flush
+        self.n_eager_steps = 0      # steps launched outside a captured chunk graph
         self.opt._ensure_state(self.pU)
         self.opt._ensure_state(self.pI)
         self._tables = (AdamTable * 2)()
@@ -161,19 +213,46 @@ class FusedBPRTrainStep(object):
         self._fill_tables()
 
     # ------------------------------------------------------------------ data side
-    def _chunks(self, cuts=()):
+    def _chunks(self, cuts=(), ramps=(0,)):
         """(first global batch, batches, global batch size) per chunk: chunks of at
         most C full batches, starting at 0 and at every batch index in `cuts`, then
-        the ragged last batch on its own."""
+        the ragged last batch on its own. From each batch index in `ramps` (where
+        the prep pipeline starts empty) up to the next cut, the chunk sizes ramp up
+        (RAMP, then C): the first steps wait for a 4-batch walk, not a C-batch one,
+        and each next walk runs beside the previous chunk's steps."""
         n = self._users.numel()
         full = n // self.Bg
         bounds = sorted({0, full} | {int(c) for c in cuts if 0 < int(c) < full})
+        ramp_at = {int(r) for r in ramps}
         out = []
         for lo, hi in zip(bounds[:-1], bounds[1:]):
-            out.extend((b0, min(self.C, hi - b0), self.Bg) for b0 in range(lo, hi, self.C))
+            ri = 0 if lo in ramp_at else len(self.RAMP)
+            b0 = lo
+            while b0 < hi:
+                size = self.RAMP[ri] if ri < len(self.RAMP) else self.C
+                ri += 1
+                nb = min(size, self.C, hi - b0)
+                out.append((b0, nb, self.Bg))
+                b0 += nb
         if n % self.Bg:
             out.append((full, 1, n % self.Bg))
         return out
+
+    def _chunk_flags(self, plan):
+        """(entry, flush) per chunk of the deferred schedule: a chunk flushes every
+        row at its end once C or more steps have run since the last flush (and
+        before a ragged batch / the end); a chunk after one that did not flush
+        starts with an entry catch-up of the rows its first batch reads."""
+        flags, since = [], 0
+        for i, (_, nb, Bc) in enumerate(plan):
+            entry = since > 0
+            since += nb
+            nxt_full = i + 1 < len(plan) and plan[i + 1][2] == self.Bg
+            flush = since >= self.C or not nxt_full
+            if flush:
+                since = 0
+            flags.append((entry, flush))
+        return flags
 
     def _sharded(self, Bc):
         return self.G > 1 and Bc == self.Bg
@@ -184,6 +263,17 @@ class FusedBPRTrainStep(object):
         KI = (1 + T) * Bc
         if slot.free_recorded:
             self.prep_stream.wait_event(slot.free)
+        if not self._sharded(Bc):
+            # keys, K4 walk, K2 groupings and look-ahead lists: one native call
+            # (mirec_prepare_chunk) on the prep stream
+            cp = self._chunk_prep(slot)
+            cp.users, cp.items = self._users.data_ptr(), self._items.data_ptr()
+            cp.s0, cp.n_batches, cp.Bc = b0 * self.Bg, nb, Bc
+            check(lib().mirec_prepare_chunk(ctypes.byref(cp), self.prep_stream.cuda_stream),
+                  'mirec_prepare_chunk')
+            slot.ready.record(self.prep_stream)
+            slot.chunk = chunk
+            return
         with torch.cuda.stream(self.prep_stream):
             s0 = b0 * self.Bg
             users = slot.user_keys[:nb * Bc]
@@ -199,16 +289,48 @@ class FusedBPRTrainStep(object):
             self.sort_ws = ops.segment_sort_batched(slot.item_keys[:nb * KI], KI, self.nI,
                                                     slot.i_perm, slot.i_uniq, slot.i_seg,
                                                     slot.i_nu, ws=self.sort_ws)
-            if self._sharded(Bc):
-                lay, g, B = self.layout, self.rank, self.B
-                slot.lu[:nb * B].view(nb, B).copy_(lay.local_users(users, g))
-                slot.li[:nb * (1 + T) * B].view(nb, 1 + T, B).copy_(
-                    lay.local_items(slot.item_keys[:nb * KI], g))
+            lay, g, B = self.layout, self.rank, self.B
+            slot.lu[:nb * B].view(nb, B).copy_(lay.local_users(users, g))
+            slot.li[:nb * (1 + T) * B].view(nb, 1 + T, B).copy_(
+                lay.local_items(slot.item_keys[:nb * KI], g))
             if self.adam_mode == 'deferred':
                 ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
                 ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
+
+    def _chunk_prep(self, slot):
+        """The slot's mirec_chunk_prep descriptor (pointers fixed per slot)."""
+        cp = getattr(slot, 'prep', None)
+        if cp is not None:
+            return cp
+        from recbole_amd._native import ChunkPrep
+        dev = self.device
+        with torch.cuda.stream(self.prep_stream):   # a first call builds the used-id bitmap:
+            walk = self.data.sampler.walk_args(dev)   # stream-ordered before the walk reads it
+        rl, pr, up, uc, bits, n_bits, reject, status = walk
+        T = self.times
+        nsort = lib().mirec_segment_sort_workspace_size(self.C * (1 + T) * self.Bg, self.nI)
+        if self.sort_ws is None or self.sort_ws.numel() < nsort:
+            self.sort_ws = torch.empty(nsort, dtype=torch.uint8, device=dev)
+        p = lambda x: x.data_ptr() if x is not None else None
+        cp = ChunkPrep()
+        cp.T = T
+        cp.user_keys, cp.item_keys = slot.user_keys.data_ptr(), slot.item_keys.data_ptr()
+        cp.random_list, cp.L, cp.pr_dev = rl.data_ptr(), rl.numel(), pr.data_ptr()
+        cp.used_ptr, cp.used_cols = (p(up), p(uc)) if bits is None else (None, None)
+        cp.used_bits, cp.n_bits = p(bits), n_bits if bits is not None else 0
+        cp.n_users, cp.n_items, cp.reject, cp.status = self.nU, self.nI, int(reject), p(status)
+        cp.walk_ws, cp.walk_ws_bytes = self.samp_ws.data_ptr(), self.samp_ws.numel()
+        cp.sort_ws, cp.sort_ws_bytes = self.sort_ws.data_ptr(), self.sort_ws.numel()
+        for tag in ('u', 'i'):
+            for f in ('perm', 'uniq', 'seg', 'nu'):
+                setattr(cp, f'{tag}_{f}', getattr(slot, f'{tag}_{f}').data_ptr())
+            if self.adam_mode == 'deferred':
+                setattr(cp, f'{tag}_ahead', getattr(slot, f'{tag}_ahead').data_ptr())
+                setattr(cp, f'{tag}_nah', getattr(slot, f'{tag}_nah').data_ptr())
+        slot.prep = cp
+        return cp
 
     # ------------------------------------------------------------------ model side
     def _fill_tables(self):
@@ -353,6 +475,31 @@ class FusedBPRTrainStep(object):
                                              stream.cuda_stream), 'mirec_adam_flush_f32')
         self._record('flush', stream, flush)
 
+    def _entry_lists(self, slot):
+        """(row list, device count) per table: the rows batch 0 of `slot` reads."""
+        return [(slot.u_uniq, slot.u_nu), (slot.i_uniq, slot.i_nu)]
+
+    def _entry(self, slot, stream):
+        """Deferred schedule, chunk entered without a flush before it: bring the
+        rows its first batch reads through the previous step (a look-ahead launch
+        at step step_idx - 1: K5 with no touched rows)."""
+        if self.adam_mode != 'deferred':
+            return
+        t = (AdamTable * 2)()                   # own descriptors: self._tables keeps its rows
+        ctypes.memmove(t, self._tables, ctypes.sizeof(t))
+        for q, (uniq, n) in enumerate(self._entry_lists(slot)):
+            t[q].rows = self.xbuf.data_ptr()            # unused: no touched rows
+            t[q].perm = t[q].uniq = t[q].seg = uniq.data_ptr()
+            t[q].n_uniq = self.zero_i32.data_ptr()
+            t[q].ahead_uniq = uniq.data_ptr()
+            t[q].ahead_n_uniq = n.data_ptr()
+
+        def entry():
+            check(lib().mirec_adam_deferred_f32(t, 2, self._n_max, self.d, self.consts.data_ptr(),
+                                                self.step_idx.data_ptr(), -1, *self._adam_args,
+                                                stream.cuda_stream), 'mirec_adam_deferred_f32')
+        self._record('ahead', stream, entry)
+
     def _grad_scale(self, Bc):
         """1 / (rows of the GLOBAL batch): the reference's .mean() over the batch."""
         R = Bc * self.times
@@ -361,22 +508,27 @@ class FusedBPRTrainStep(object):
             self._gs = float(np.float32(1.0) / np.float32(R))
         return self._gs
 
-    def _graph_for(self, slot, nb):
-        """HIP graph of the model-side steps of an nb-batch chunk in `slot`
-        (captured once per (slot, nb); capture synchronizes, so begin_epoch
-        captures every size its plan uses before any batch runs)."""
-        g = slot.graphs.get(nb)
+    def _graph_for(self, slot, nb, entry, flush):
+        """HIP graph of the model-side steps of an nb-batch chunk in `slot`, with
+        the entry catch-up and / or the closing flush (captured once per (slot, nb,
+        entry, flush); capture synchronizes, so begin_epoch captures every variant
+        its plan uses before any batch runs)."""
+        key = (nb, entry, flush)
+        g = slot.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             cap = torch.cuda.Stream(device=self.device)
             cap.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=cap):
+                if entry:
+                    self._entry(slot, cap)
                 for c in range(nb):
                     self._step(slot, c, self.Bg, cap, c, c + 1 < nb)
                 self._finish(0, nb, self.Bg, cap)
-                self._flush(cap)
+                if flush:
+                    self._flush(cap)
             torch.cuda.current_stream(self.device).wait_stream(cap)
-            slot.graphs[nb] = g
+            slot.graphs[key] = g
         return g
 
     # ------------------------------------------------------------------ epoch API
@@ -415,12 +567,15 @@ class FusedBPRTrainStep(object):
         if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
             for m, v, last in self._adam_state():   # zero-state rows: marked (adam.hip)
                 ops.zero_state_marks(m, v, last, self._adam_args[3])
-        self._plan, self._plan_starts = self._chunks(cuts), None
+        ramps = (0,) if hold_prep_from is None else (0, int(hold_prep_from))
+        self._plan, self._plan_starts = self._chunks(cuts, ramps), None
+        self._flags = self._chunk_flags(self._plan)
         if self.use_graph:                      # capture up front: capture synchronizes
-            sizes = sorted({n for _, n, Bc in self._plan if Bc == self.Bg})
-            for s in self.slots:
-                for n in sizes:
-                    self._graph_for(s, n)
+            S = len(self.slots)
+            variants = sorted({(k % S, n, e, f) for k, ((_, n, Bc), (e, f)) in
+                               enumerate(zip(self._plan, self._flags)) if Bc == self.Bg})
+            for k, n, e, f in variants:
+                self._graph_for(self.slots[k], n, e, f)
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
         self._next_chunk = 0
         self._prep_limit = (len(self._plan) if hold_prep_from is None
@@ -428,8 +583,8 @@ class FusedBPRTrainStep(object):
         self._cur = None                       # chunk index being consumed
         for s in self.slots:
             s.free_recorded = False
-        self._issue_prep()
-        self._issue_prep()
+        for _ in range(len(self.slots)):
+            self._issue_prep()
         return nb
 
     def release_prep(self, upto=None):
@@ -444,51 +599,66 @@ class FusedBPRTrainStep(object):
         k = self._next_chunk
         if k >= min(len(self._plan), self._prep_limit):
             return
-        self._prepare(self.slots[k % 2], self._plan[k])
+        self._prepare(self.slots[k % len(self.slots)], self._plan[k])
         self._next_chunk += 1
 
     def _enter_chunk(self, k, stream):
         if self._cur == k:
             return
+        S = len(self.slots)
         if self._cur is not None:              # previous chunk fully enqueued
-            prev = self.slots[self._cur % 2]
+            prev = self.slots[self._cur % S]
             prev.free.record(stream)
             prev.free_recorded = True
-        while self._next_chunk <= k + 1 and self._next_chunk < min(len(self._plan),
-                                                                     self._prep_limit):
+        while self._next_chunk <= k and self._next_chunk < min(len(self._plan),
+                                                               self._prep_limit):
             self._issue_prep()
         if self._next_chunk <= k:
             raise RuntimeError(f'chunk {k} is held (begin_epoch(hold_prep_from=...)): '
                                'call release_prep() first')
-        stream.wait_event(self.slots[k % 2].ready)
+        stream.wait_event(self.slots[k % S].ready)
         self._cur = k
 
     def run_batches(self, b_start, b_end):
         """Enqueue global batches [b_start, b_end) in order (no host sync). Whole
         chunks replay their captured graph; a chunk entered mid-way (or timed with
         per-kernel events) launches eagerly, one step and one loss bookkeeping launch
-        at a time, flushing when the chunk completes."""
+        at a time. A chunk starts with the entry catch-up and ends with the flush
+        when its plan flags say so (_chunk_flags)."""
         stream = torch.cuda.current_stream(self.device)
         b = b_start
         while b < b_end:
             k = self._chunk_of(b)
             b0, nb, Bc = self._plan[k]
+            entry, flush = self._flags[k]
             self._enter_chunk(k, stream)
-            slot = self.slots[k % 2]
+            slot = self.slots[k % len(self.slots)]
             c0, c1 = b - b0, min(nb, b_end - b0)
+            key = (nb, entry, flush)
             if (self.use_graph and c0 == 0 and c1 == nb and Bc == self.Bg
-                    and self.kernel_events is None and nb in slot.graphs):
-                slot.graphs[nb].replay()             # ends with the chunk's flush
-                self._current = True
+                    and self.kernel_events is None and key in slot.graphs):
+                slot.graphs[key].replay()
+                self._current = flush
             else:
+                self.n_eager_steps += c1 - c0
+                if c0 == 0 and entry:
+                    self._entry(slot, stream)
                 for c in range(c0, c1):
                     self._step(slot, c, Bc, stream, 0, c + 1 < nb)
                     self._finish(c, 1, Bc, stream)
                 self._current = False
-                if c1 == nb:
+                if c1 == nb and flush:
                     self._flush(stream)
                     self._current = True
-            b = b0 + c1
+            self._top_up_prep(k)       # after the chunk's launch: the host enqueues the
+            b = b0 + c1                # model side first, the walks of later chunks behind it
+
+    def _top_up_prep(self, k):
+        """Prepare chunks up to k + SLOTS - 1 (their slots are free once the chunks
+        before them have run)."""
+        lim = min(len(self._plan), self._prep_limit, k + len(self.slots))
+        while self._next_chunk < lim:
+            self._issue_prep()
 
     def launch_batch(self, b):
         self.run_batches(b, b + 1)
@@ -715,6 +885,9 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
 
     def _adam_state(self):
         return [(self.shU[1], self.shU[2], self.lastU), (self.shI[1], self.shI[2], self.lastI)]
+
+    def _entry_lists(self, slot):
+        return [(slot.own_u, slot.own_u_n), (slot.own_i, slot.own_i_n)]
 
     def _n_local(self, Bc):
         return max(0, min(self.B, Bc - self.rank * self.B))

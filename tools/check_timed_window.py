@@ -14,10 +14,14 @@ import sys
 def main(src, out=None):
     path = glob.glob(f'{src}/**/*kernel_trace.csv', recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
-    marks = [r for r in rows if 'spin' in r['Kernel_Name'] or 'sleep' in r['Kernel_Name']]
+    # the markers are 1-cycle spins (longer spins: the prep-stream probe, the
+    # measurement window's launch cover)
+    marks = [r for r in rows if ('spin' in r['Kernel_Name'] or 'sleep' in r['Kernel_Name'])
+             and int(r['End_Timestamp']) - int(r['Start_Timestamp']) < 20000]
     if len(marks) < 2:
         raise SystemExit('no markers in trace (run bench.py with BENCH_MARKERS=1)')
-    t0, t1 = int(marks[0]['Start_Timestamp']), int(marks[1]['End_Timestamp'])
+    # the last two: the prep-stream probe's short spins come before the timed region
+    t0, t1 = int(marks[-2]['Start_Timestamp']), int(marks[-1]['End_Timestamp'])
     inside = collections.Counter()
     before = collections.Counter()
     for r in rows:
