@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 9
+#define MIREC_ABI_VERSION 10
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -327,6 +327,15 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
                          const float* step_consts_dev, const int32_t* step_base_dev,
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
+
+/* Self-test of the K5 replay's fast correctly rounded sqrt and division
+ * (csrc/adam_math.h) against sqrtf / IEEE division, bitwise, on this GPU:
+ * every sqrt_stride-th float of [2^-96, FLT_MAX] plus the floats near each power
+ * of two, and n_div pseudo-random pairs of the fast division range. out4_dev
+ * (device) receives {sqrt mismatches, sqrt tested, div mismatches, div tested}.
+ * (tools/check_adam_math.hip is the exhaustive / 2^34-pair version.) */
+int mirec_selftest_adam_math(uint64_t sqrt_stride, uint64_t n_div, uint64_t seed,
+                             unsigned long long* out4_dev, void* stream);
 
 /* End-of-step bookkeeping of Trainer._train_epoch (trainer.py:161-169):
  * loss_hist[step] = (sum of loss_k[0..n), fixed order) / denom, then

@@ -153,7 +153,14 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
   if (threadIdx.x < 128 && qu < nq && hist_ptr) {
     hcur = hist_ptr[qu];
     hend = hist_ptr[qu + 1];
-    while (hcur < hend && hist_cols[hcur] < ilo) ++hcur;   // sorted: skip items before the split
+    if (ilo > 0) {                          // sorted: lower_bound of the split's first item
+      int64_t a = hcur, b = hend;
+      while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if (hist_cols[mid] < ilo) a = mid + 1; else b = mid;
+      }
+      hcur = a;
+    }
     if (hcur < hend) hnext = hist_cols[hcur];
   }
   auto build_mask = [&](int64_t base, uint32_t* dst) {

@@ -444,6 +444,26 @@ class Dataset(object):
                     feat[field] = np.split(lst, sp)
 
     # ------------------------------------------------------------------ API
+    def token2id(self, field, tokens):
+        """External token(s) -> internal id(s) (reference dataset.py:1040-1058):
+        ValueError for an unknown token, TypeError for another input type."""
+        if isinstance(tokens, str):
+            if tokens in self.field2token_id[field]:
+                return self.field2token_id[field][tokens]
+            raise ValueError(f'token [{tokens}] is not existed in {field}')
+        if isinstance(tokens, (list, np.ndarray)):
+            return np.array([self.token2id(field, t) for t in tokens])
+        raise TypeError(f'The type of tokens [{tokens}] is not supported')
+
+    def id2token(self, field, ids):
+        """Internal id(s) -> external token(s) (reference dataset.py:1082-1098)."""
+        try:
+            return self.field2id_token[field][ids]
+        except IndexError:
+            if isinstance(ids, list):
+                raise ValueError(f'[{ids}] is not a one-dimensional list.')
+            raise ValueError(f'[{ids}] is not a valid ids.')
+
     def num(self, field):
         if field not in self.field2type:
             raise ValueError(f'Field [{field}] not defined in dataset.')

@@ -196,9 +196,10 @@ class Trainer(AbstractTrainer):
 
     def _save_checkpoint(self, epoch):
         self._sync_params()
+        cfg = (dict(self.config.final_config_dict) if hasattr(self.config, 'final_config_dict')
+               else dict(self.config))
         state = {
-            'config': dict(self.config.final_config_dict) if hasattr(self.config, 'final_config_dict')
-            else self.config,
+            'config': _plain_config(cfg),
             'epoch': epoch,
             'cur_step': self.cur_step,
             'best_valid_score': self.best_valid_score,
@@ -208,7 +209,7 @@ class Trainer(AbstractTrainer):
         torch.save(state, self.saved_model_file)
 
     def resume_checkpoint(self, resume_file):
-        checkpoint = torch.load(str(resume_file), weights_only=False)
+        checkpoint = _load_checkpoint(resume_file)
         self.start_epoch = checkpoint['epoch'] + 1
         self.cur_step = checkpoint['cur_step']
         self.best_valid_score = checkpoint['best_valid_score']
@@ -313,7 +314,7 @@ class Trainer(AbstractTrainer):
             return
         if load_best_model:
             checkpoint_file = model_file or self.saved_model_file
-            checkpoint = torch.load(checkpoint_file, weights_only=False)
+            checkpoint = _load_checkpoint(checkpoint_file)
             self.model.load_state_dict(checkpoint['state_dict'])
             self.logger.info(f'Loading model structure and parameters from {checkpoint_file}')
         self._sync_params()
@@ -368,3 +369,27 @@ class Trainer(AbstractTrainer):
             r = self.model.predict(cur.to(self.device))
             out.append(r.unsqueeze(0) if r.dim() == 0 else r)
         return torch.cat(out, dim=0)
+
+
+def _plain_config(cfg):
+    """The config as plain Python values (enums by name, devices and other objects
+    as strings): checkpoints then load with torch.load(weights_only=True)."""
+    import enum
+
+    def plain(v):
+        if isinstance(v, enum.Enum):
+            return v.name
+        if isinstance(v, (str, int, float, bool)) or v is None:
+            return v
+        if isinstance(v, (list, tuple)):
+            return [plain(x) for x in v]
+        if isinstance(v, dict):
+            return {str(k): plain(x) for k, x in v.items()}
+        return str(v)
+    return {str(k): plain(v) for k, v in cfg.items()}
+
+
+def _load_checkpoint(path):
+    """torch.load without unpickling arbitrary objects (tensors, plain containers
+    and numbers only), so a user-supplied .pth cannot run code on load."""
+    return torch.load(str(path), map_location='cpu', weights_only=True)

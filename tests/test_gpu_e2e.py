@@ -177,7 +177,7 @@ def test_checkpoint_roundtrip(tmp_path):
     tr = Trainer(config, model)
     tr._train_epoch(train, 0)
     tr._save_checkpoint(0)
-    sd = torch.load(tr.saved_model_file, weights_only=False)
+    sd = torch.load(tr.saved_model_file, weights_only=True)   # plain checkpoint: no unpickling
     assert set(sd['state_dict']) == {'user_embedding.weight', 'item_embedding.weight'}
     assert set(sd['optimizer']['state'][0]) == {'step', 'exp_avg', 'exp_avg_sq'}
     config2, train2, _, _, model2 = _pipeline(tmp_path, epochs=1)

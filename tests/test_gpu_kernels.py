@@ -612,19 +612,23 @@ def test_fullsort_topk_vs_oracle(dev, nq, I, d, K):
                 o['scores'].cpu().numpy())
 
 
-@pytest.mark.parametrize('n_split', [1, 2, 3, 8])
-def test_fullsort_item_split_identical(dev, n_split):
+@pytest.mark.parametrize('n_split,d,K', [(1, 64, 10), (2, 64, 10), (3, 64, 10), (8, 64, 10),
+                                          (8, 32, 20), (3, 256, 50), (8, 256, 20)])
+def test_fullsort_item_split_identical(dev, n_split, d, K):
     """K6 with the item range split over workgroups + the per-user merge returns
-    the same scores, ids and positive flags as one sweep (history masked, ties)."""
+    the same scores, ids and positive flags as one sweep (history masked, ties),
+    for the K = 20 / 50 merges, d = 32 / 256, and users whose history spans several
+    split ranges (the split's history cursor starts by a binary search)."""
     from recbole_amd import ops
-    g = torch.Generator().manual_seed(n_split)
-    nq, I, d, K = 300, 1000, 64, 10
+    g = torch.Generator().manual_seed(n_split * 1000 + d + K)
+    nq, I = 300, 1000
     Uq = torch.randn(nq, d, generator=g).to(dev)
     EI = torch.randn(I, d, generator=g).round().to(dev)       # many tied scores
     EI[500:520] = EI[10:30]                                     # exact duplicates
     hp, hc, pp, pc = [0], [], [0], []
     for q in range(nq):
-        h = sorted(set(torch.randint(1, I, (q % 37,), generator=g).tolist()))
+        n_h = 400 if q % 10 == 0 else q % 37                    # some longer than a split span
+        h = sorted(set(torch.randint(1, I, (n_h,), generator=g).tolist()))
         hc += h
         hp.append(len(hc))
         p = sorted(set(torch.randint(1, I, (3,), generator=g).tolist()) - set(h))
@@ -694,3 +698,18 @@ def test_large_segment_sort_and_hot_row_scatter(dev, n, key_space, d):
         0, torch.as_tensor(keys), rows.double())
     got = ops.segment_scatter_add(rows.to(dev), segs, torch.zeros(n_rows, d, device=dev))
     torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-4, atol=2e-3)
+
+
+def test_adam_fast_math_selftest(dev):
+    """The K5 replay's fast sqrt / division (csrc/adam_math.h) equal sqrtf and IEEE
+    division bit for bit on this GPU: every 64th float of the fast sqrt range plus
+    the floats around each power of two, and 2^26 random division pairs of the fast
+    range (tools/check_adam_math.hip runs the exhaustive / 2^34-pair version)."""
+    from recbole_amd._native import check, lib
+    out = torch.zeros(4, dtype=torch.int64, device=dev)
+    check(lib().mirec_selftest_adam_math(64, 1 << 26, 2024, out.data_ptr(),
+                                         torch.cuda.current_stream(dev).cuda_stream),
+          'mirec_selftest_adam_math')
+    sq_bad, sq_n, dv_bad, dv_n = out.cpu().tolist()
+    assert sq_n > 2 ** 24 and dv_n > 2 ** 24
+    assert sq_bad == 0 and dv_bad == 0, (sq_bad, dv_bad)
