@@ -102,13 +102,14 @@ def pmc_valu_insts(substr):
     """(VALU, transcendental f32) wave-instructions per launch of the kernel whose
     name contains `substr` (SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32 pass of
     tools/prof_pmc.sh), or (None, None)."""
-    path = os.path.join(ROOT, 'profiles', 'r01_pmc.json')
-    if not os.path.exists(path):
-        return None, None
-    for k, v in json.load(open(path)).items():
-        if substr in k and 'sq_insts_valu_per_launch' in v:
-            return v['sq_insts_valu_per_launch'], v.get('sq_insts_valu_trans_f32_per_launch', 0.0)
-    return None, None
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))[::-1]:
+        for k, v in json.load(open(path)).items():
+            if substr in k and 'sq_insts_valu_per_launch' in v:
+                return (v['sq_insts_valu_per_launch'],
+                        v.get('sq_insts_valu_trans_f32_per_launch', 0.0),
+                        v.get('valu_busy_frac'), os.path.basename(path))
+    return None, None, None, None
 
 
 # VALU issue model (MI355X_MICROARCH.md, per-instruction cycle constants): a wave64
@@ -167,8 +168,13 @@ def roofline(step, events, uniq, d, M):
     if step.adam_mode == 'deferred':
         bd, src = pmc_bytes(f'adam_deferred_kernel<{d},')
         bf, _ = pmc_bytes(f'{flush_k}<{d}>')
-        vd, td = pmc_valu_insts(f'adam_deferred_kernel<{d},')
-        vf, tf_ = pmc_valu_insts(f'{flush_k}<{d}>')
+        vd, td, bd_busy, vsrc = pmc_valu_insts(f'adam_deferred_kernel<{d},')
+        vf, tf_, bf_busy, _ = pmc_valu_insts(f'{flush_k}<{d}>')
+        if bd_busy is not None and bf_busy is not None:
+            # measured VALU pipe occupancy of the two K5 kernels (PMC pass, tools/
+            # prof_pmc.sh: 4 * SQ_ACTIVE_INST_VALU / (SIMDs * clock * duration))
+            adam.update({'valu_busy_frac_deferred': bd_busy, 'valu_busy_frac_flush': bf_busy,
+                         'valu_source': vsrc})
         if vd is not None and vf is not None:
             insts = nd * vd + nf * vf
             trans = nd * td + nf * tf_

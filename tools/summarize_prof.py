@@ -42,15 +42,26 @@ def main(tag='r01', src='gpurun_out/prof', dst='profiles'):
     valu = glob.glob(os.path.join(src, 'valu', '*counter_collection.csv'))
     if valu:                                    # per-launch means of each SQ counter
         agg = collections.defaultdict(lambda: collections.defaultdict(float))
-        disp = collections.defaultdict(set)
+        disp = collections.defaultdict(dict)
         for r in csv.DictReader(open(valu[0])):
             agg[r['Kernel_Name']][r['Counter_Name']] += float(r['Counter_Value'])
-            disp[r['Kernel_Name']].add(r['Dispatch_Id'])
+            if 'Start_Timestamp' in r:
+                disp[r['Kernel_Name']][r['Dispatch_Id']] = (
+                    int(r['End_Timestamp']) - int(r['Start_Timestamp']))
         for k, cs in agg.items():
             n = max(len(disp[k]), 1)
-            out.setdefault(k, {}).update(
-                {'valu_launches': n, **{c.lower() + '_per_launch': round(v / n, 1)
-                                        for c, v in cs.items()}})
+            rec = {'valu_launches': n, **{c.lower() + '_per_launch': round(v / n, 1)
+                                          for c, v in cs.items()}}
+            # VALU pipe occupancy: SQ_ACTIVE_INST_VALU counts quad-cycles summed over
+            # the waves; one SIMD issues one VALU instruction at a time, so
+            # 4 * ACTIVE_INST_VALU / (SIMDs * clock * duration) is the fraction of the
+            # chip's VALU issue time the kernel kept busy (1,024 SIMDs, 2.4 GHz)
+            dur = sum(disp[k].values())
+            if dur and 'SQ_ACTIVE_INST_VALU' in cs:
+                rec['valu_busy_frac'] = round(4 * cs['SQ_ACTIVE_INST_VALU'] /
+                                              (1024 * 2.4 * dur), 4)
+                rec['pmc_duration_ns_per_launch'] = round(dur / n, 1)
+            out.setdefault(k, {}).update(rec)
     json.dump(out, open(os.path.join(dst, f'{tag}_pmc.json'), 'w'), indent=1)
     for line in open(os.path.join(src, 'trace.log')):
         if line.startswith('{"metric"'):
