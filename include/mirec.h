@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 10
+#define MIREC_ABI_VERSION 11
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -327,6 +327,12 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
                          const float* step_consts_dev, const int32_t* step_base_dev,
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
+
+/* Copy n_bytes (a multiple of 4, at most a few KiB: e.g. the mirec_ctx_field
+ * descriptors of a batch) from host memory to dst_dev through kernel arguments:
+ * stream-ordered, and recorded BY VALUE when the stream is being captured into a
+ * graph (a host-to-device memcpy node would re-read the host buffer at replay). */
+int mirec_write_bytes(void* dst_dev, const void* src_host, size_t n_bytes, void* stream);
 
 /* Self-test of the K5 replay's fast correctly rounded sqrt and division
  * (csrc/adam_math.h) against sqrtf / IEEE division, bitwise, on this GPU:

@@ -99,6 +99,7 @@ SIGNATURES = {
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
     "mirec_prepare_chunk": (c_int, [_P, _P]),
+    "mirec_write_bytes": (c_int, [_P, _P, c_size_t, _P]),
     "mirec_selftest_adam_math": (c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P, _P]),
     "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,
                                          _P]),
@@ -146,7 +147,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class NativeError(RuntimeError):

@@ -1,6 +1,7 @@
 // Error state, version and the small reduction kernels of the trainer loop.
 #include <stdarg.h>
 #include "common.h"
+#include <algorithm>
 
 namespace mirec {
 
@@ -111,3 +112,32 @@ extern "C" int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride
   return launch_status("mirec_chunk_finish");
 }
 
+
+// ---- small host -> device writes that a graph capture records by value
+namespace mirec {
+constexpr int kPayloadWords = 768;     // 3 KiB of kernel arguments per launch
+struct Payload { uint32_t w[kPayloadWords]; };
+
+__global__ __launch_bounds__(256) void write_bytes_kernel(uint32_t* __restrict__ dst, Payload p,
+                                                          int n_words) {
+  for (int i = threadIdx.x; i < n_words; i += blockDim.x) dst[i] = p.w[i];
+}
+}  // namespace mirec
+
+extern "C" int mirec_write_bytes(void* dst_dev, const void* src_host, size_t n_bytes,
+                                 void* stream) {
+  if ((n_bytes && (!dst_dev || !src_host)) || (n_bytes & 3) || ((uintptr_t)dst_dev & 3)) {
+    set_error("mirec_write_bytes: bad arguments (n_bytes %zu)", n_bytes);
+    return -1;
+  }
+  const uint32_t* src = (const uint32_t*)src_host;
+  uint32_t* dst = (uint32_t*)dst_dev;
+  for (size_t off = 0; off < n_bytes / 4; off += kPayloadWords) {
+    const int n = (int)std::min<size_t>(kPayloadWords, n_bytes / 4 - off);
+    Payload p;
+    memcpy(p.w, src + off, (size_t)n * 4);
+    hipLaunchKernelGGL(write_bytes_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, dst + off,
+                       p, n);
+  }
+  return launch_status("mirec_write_bytes");
+}

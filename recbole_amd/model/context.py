@@ -94,39 +94,16 @@ def build_fields(layout, interaction, tables, grads=None):
     return arr, keep
 
 
-class _Staging(object):
-    """Ring of pinned host slots for the per-batch field descriptors: the copy to
-    the device is asynchronous; a slot is reused only after its copy completed."""
-
-    def __init__(self, n=8, nbytes=1 << 14):
-        self.n, self.nbytes, self.k = n, nbytes, 0
-        self.host = [None] * n
-        self.events = [None] * n
-
-    def upload(self, arr, device):
-        raw = bytes(arr)
-        if len(raw) > self.nbytes or not torch.cuda.is_available():
-            return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
-        i = self.k
-        self.k = (self.k + 1) % self.n
-        if self.host[i] is None:
-            self.host[i] = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
-        if self.events[i] is not None:
-            self.events[i].synchronize()
-        h = self.host[i][:len(raw)]
-        h.numpy()[:] = np.frombuffer(raw, dtype=np.uint8)
-        out = h.to(device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[i] = ev
-        return out
-
-
-_STAGING = _Staging()
-
-
 def _upload(arr, device):
-    return _STAGING.upload(arr, device)
+    """The batch's field descriptors to the device through kernel arguments
+    (mirec_write_bytes): stream-ordered with no host staging buffer to recycle, and
+    recorded by value when the step is being captured into a graph."""
+    raw = bytes(arr)
+    n = (len(raw) + 3) // 4 * 4
+    out = torch.empty(max(n, 4), dtype=torch.uint8, device=device)
+    buf = ctypes.create_string_buffer(raw, n)
+    check(lib().mirec_write_bytes(ptr(out), buf, n, stream_handle()), 'mirec_write_bytes')
+    return out
 
 
 def ctx_fm_forward(layout, interaction, tables, B, d, bias, keys=None):

@@ -16,6 +16,10 @@ from recbole_amd.model.layers import BaseFactorizationMachine, MLPLayers
 
 class DeepFM(ContextRecommender):
 
+    # the training step has no host synchronisation or host-side branching on device
+    # values: the trainer may capture it in a HIP graph (trainer/graph_step.py)
+    graph_step_safe = True
+
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
         self.mlp_hidden_size = config['mlp_hidden_size']

@@ -120,13 +120,63 @@ class FusedAdam(torch.optim.Optimizer):
         params = [p for p in self._params() if p.grad is not None and p not in deferred]
         for p in deferred:
             self._deferred_step(p)
-        if not params:
-            if deferred:
-                self.n_steps += 1
-            return loss
-        self._dense_step(params)
-        self.n_steps += 1
+        if params:
+            self._dense_step(params)
+        if params or deferred:
+            if self._g is not None:
+                self._g['step'].add_(1)       # the device step counter of graph mode
+            self.n_steps += 1
         return loss
+
+    # ------------------------------------------------------------------ graph mode
+    # A training step whose kernels take no host-side step index, so the whole step
+    # (forward, backward, optimizer) can be captured in a HIP graph and replayed:
+    # every parameter — dense and deferred — reads its Adam constants from ONE
+    # window table indexed by a device counter that the step itself advances. The
+    # host only rolls the window over between steps (graph_window()), flushing the
+    # deferred tables exactly where the eager schedule would.
+    _g = None
+
+    def graph_mode(self, device, window: int = 256):
+        self.flush()
+        for ds in getattr(self, '_deferred', {}).values():
+            ds['t0'] = None
+            ds['window'] = window
+        self._g = {'W': window, 't0': None,
+                   'consts': torch.zeros(window * 4, dtype=torch.float32, device=device),
+                   'step': torch.zeros(1, dtype=torch.int32, device=device)}
+        self._graph_open_window()
+
+    def _graph_open_window(self):
+        g = self._g
+        g['t0'] = self.n_steps
+        g['consts'].copy_(torch.as_tensor(self.step_constants(self.n_steps + 1, g['W'])
+                                          .reshape(-1)))
+        g['step'].zero_()
+        for p in getattr(self, '_deferred', {}):
+            ds = self._deferred[p]
+            ds['t0'], ds['consts'] = self.n_steps, g['consts']
+            if ds['marked']:
+                ops.reset_marks(ds['last'])
+            else:
+                st = self.state[p]
+                ops.zero_state_marks(st['exp_avg'], st['exp_avg_sq'], ds['last'],
+                                     self._group_args()['weight_decay'])
+                ds['marked'] = True
+
+    def graph_window(self):
+        """Before a graph-mode step: when the window is full, complete every deferred
+        row and start the next window (host side, outside any captured graph)."""
+        g = self._g
+        if g is not None and self.n_steps - g['t0'] >= g['W']:
+            self.flush()
+            self._graph_open_window()
+
+    def _sref(self, r, off=0):
+        """(step base tensor, offset) of step index r + off of the current window."""
+        if self._g is not None:
+            return self._g['step'], off
+        return self._zero_i32 if hasattr(self, '_zero_i32') else self._dwin['zero'], r + off
 
     def _dense_step(self, params, window=256):
         """One Adam step of parameters with dense gradients: the step constants come
@@ -135,8 +185,13 @@ class FusedAdam(torch.optim.Optimizer):
         rest, the flat kernel for numel % 4 != 0) — few launches and no per-step
         host-to-device copy."""
         dev = params[0].device
-        w = getattr(self, '_dwin', None)
-        if (w is None or w['dev'] != dev or not 0 <= self.n_steps - w['t0'] < w['W']):
+        if self._g is not None:               # graph mode: the shared window, device index
+            w = {'consts': self._g['consts'], 'zero': self._g['step'], 't0': self.n_steps,
+                 'idx': self._g['step']}
+        else:
+            w = getattr(self, '_dwin', None)
+        if self._g is None and (w is None or w['dev'] != dev or
+                                not 0 <= self.n_steps - w['t0'] < w['W']):
             w = self._dwin = {
                 'dev': dev, 't0': self.n_steps, 'W': window,
                 'consts': torch.as_tensor(
@@ -164,7 +219,8 @@ class FusedAdam(torch.optim.Optimizer):
                                schedule='streamed', **self._group_args())
         for p, st, g in flat:
             ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], w['consts'],
-                          w['idx'][r:r + 1], dense_grad=g, **self._group_args())
+                          w['idx'] if self._g is not None else w['idx'][r:r + 1], dense_grad=g,
+                          **self._group_args())
 
     def advance(self, n: int):
         self.n_steps += n
@@ -230,13 +286,14 @@ class FusedAdam(torch.optim.Optimizer):
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])
         ds = self._dstate(p)
         r = self.n_steps - ds['t0']
-        if r > 0:
+        if r > 0 or self._g is not None:      # (graph mode at r = 0: a no-op launch)
             class _Z:
                 perm = uniq = seg = self._dummy_i32
                 n_uniq = self._zero_i32
             tab = self._dtable(p, ds, rows=self._dummy_f32, segs=_Z,
                                ahead=(segs.uniq, segs.n_uniq))
-            ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, r - 1,
+            base, off = self._sref(r, -1)
+            ops.adam_multi(tab, p.shape[1], ds['consts'], base, off,
                            schedule='deferred', n_max_uniq=[keys.numel()],
                            **self._group_args())
         return segs
@@ -246,11 +303,14 @@ class FusedAdam(torch.optim.Optimizer):
         (segs: their K2 grouping when the caller already has it)."""
         self._deferred[p]['stash'].append((rows, keys, segs))
 
-    def _flush_table(self, p, ds, target):
-        if ds['t0'] is None or target <= 0:
+    def _flush_table(self, p, ds, target, device_step=False):
+        """Every row of p through step index `target` of the window (device_step:
+        through the graph-mode device counter instead)."""
+        if ds['t0'] is None or (target <= 0 and not device_step):
             return
         tab = self._dtable(p, ds)
-        ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, target,
+        base, off = (self._g['step'], 0) if device_step else (self._zero_i32, target)
+        ops.adam_multi(tab, p.shape[1], ds['consts'], base, off,
                        schedule='flush', **self._group_args())
 
     def flush(self):
@@ -302,20 +362,25 @@ class FusedAdam(torch.optim.Optimizer):
         r = self.n_steps - ds['t0']
         if stash:
             rows, segs, n_keys = self._combine_stash(p, stash)
+        graph = self._g is not None
         if p.grad is not None:                # a dense contribution too: stream every row
-            self._flush_table(p, ds, r)
+            self._flush_table(p, ds, r, device_step=graph)
             st = self.state[p]
             kw = {'rows': rows.contiguous(), 'segs': segs} if stash else {}
             ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], ds['consts'],
-                          self._zero_i32 + r, dense_grad=p.grad.contiguous(),
-                          **kw, **self._group_args())
-            ds['last'].fill_(r + 1)
+                          self._g['step'] if graph else self._zero_i32 + r,
+                          dense_grad=p.grad.contiguous(), **kw, **self._group_args())
+            if graph:
+                ds['last'].copy_((self._g['step'] + 1).expand_as(ds['last']))
+            else:
+                ds['last'].fill_(r + 1)
         else:
             tab = self._dtable(p, ds, rows=rows.contiguous(), segs=segs)
-            ops.adam_multi(tab, p.shape[1], ds['consts'], self._zero_i32, r,
+            base, off = self._sref(r, 0)
+            ops.adam_multi(tab, p.shape[1], ds['consts'], base, off,
                            schedule='deferred', n_max_uniq=[n_keys],
                            **self._group_args())
-        if r + 1 >= ds['window']:             # window full: complete every row
+        if not graph and r + 1 >= ds['window']:   # window full: complete every row
             self._flush_table(p, ds, r + 1)
             ds['t0'] = None
 
@@ -357,3 +422,5 @@ class FusedAdam(torch.optim.Optimizer):
             mine['exp_avg_sq'].copy_(st['exp_avg_sq'].to(p.device))
             steps = int(float(st['step']))
         self.n_steps = steps
+        if self._g is not None:               # graph mode: a new window at the loaded step
+            self._graph_open_window()

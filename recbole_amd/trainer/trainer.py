@@ -156,6 +156,8 @@ class Trainer(AbstractTrainer):
                 if np.isnan(v):
                     raise ValueError('Training loss is nan')
             return total
+        if loss_func is None and self._graph_step_applicable():
+            return self._train_epoch_graphed(train_data)
         loss_func = loss_func or self.model.calculate_loss
         total_loss = None
         dp = self._dp
@@ -185,6 +187,36 @@ class Trainer(AbstractTrainer):
             self.optimizer.step()
         self._sync_params()
         return total_loss
+
+    def _graph_step_applicable(self):
+        """The captured generic step (trainer/graph_step.py): FusedAdam, one process,
+        no gradient clipping, and a model whose training step is capture-safe."""
+        return (self.config['train_graph'] is not False and isinstance(self.optimizer, FusedAdam)
+                and self._dp is None and not self.clip_grad_norm
+                and getattr(self.model, 'graph_step_safe', False)
+                and next(self.model.parameters()).is_cuda)
+
+    def _train_epoch_graphed(self, train_data):
+        """_train_epoch with each full batch replayed from one captured HIP graph of
+        the whole step. Per-batch losses are summed on the device in float64 (the
+        reference's Python-float sum, same order) and read once per epoch; the NaN
+        check is per epoch (the reference checks every batch)."""
+        from recbole_amd.trainer.graph_step import GraphedTrainStep
+        gs = getattr(self, '_graph_step', None)
+        if gs is None or gs.model is not self.model or gs.opt is not self.optimizer:
+            gs = self._graph_step = GraphedTrainStep(self.model, self.optimizer)
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        n = 0
+        for interaction in train_data:
+            total.add_(gs.step(interaction.to(self.device)))
+            n += 1
+        self._sync_params()
+        if n == 0:
+            return None
+        v = float(total.item())
+        if np.isnan(v):
+            raise ValueError('Training loss is nan')
+        return v
 
     def _valid_epoch(self, valid_data, show_progress=False):
         valid_result = self.evaluate(valid_data, load_best_model=False, show_progress=show_progress)

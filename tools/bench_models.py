@@ -37,6 +37,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # fp32 MFMA / vector peak
 CPU_BASELINE = True
 ADAM_MODE = 'deferred'
+GRAPH_STEP = True
 
 
 class StubDataset:
@@ -133,10 +134,17 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
     if ADAM_MODE == 'deferred':
         opt.enable_deferred(model.deferred_tables())
     it = [0]
+    gs = None
+    if GRAPH_STEP:                 # the Trainer's captured step (trainer/graph_step.py)
+        from recbole_amd.trainer.graph_step import GraphedTrainStep
+        gs = GraphedTrainStep(model, opt)
 
     def step():
         b = batches[it[0] % n_batches]
         it[0] += 1
+        if gs is not None:
+            gs.step(b)
+            return
         opt.zero_grad()
         loss = model.calculate_loss(b)
         loss.backward()
@@ -173,7 +181,7 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                          f'optim.Adam over every table), {dt:.1f} s'}
     return {
         'cpu_baseline': cpu,
-        'adam_mode': ADAM_MODE,
+        'adam_mode': ADAM_MODE, 'graph_step': bool(GRAPH_STEP),
         'config': 'C4', 'metric': 'train samples/s', 'value': round(B / t, 1),
         'unit': 'samples/s', 'ms_per_step': round(t * 1e3, 3), 'batch': B, 'steps': steps,
         'workload': f'DeepFM Criteo-shape: 13 float + 26 token fields, vocab {V:,} '
@@ -385,9 +393,11 @@ def main():
     ap.add_argument('--out', default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
+    ap.add_argument('--eager-step', action='store_true', help='C4 without the captured step')
     args = ap.parse_args()
-    global CPU_BASELINE, ADAM_MODE
+    global CPU_BASELINE, ADAM_MODE, GRAPH_STEP
     CPU_BASELINE = not args.no_cpu_baseline
+    GRAPH_STEP = not args.eager_step
     ADAM_MODE = args.adam_mode
     dev = torch.device('cuda', 0)
     res = []
