@@ -59,7 +59,7 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
 
 
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
-                   dist=None, chunk=None, sharded=False):
+                   dist=None, chunk=None, sharded=False, alias=False):
     from recbole_amd.config import Config
     from recbole_amd.data import data_preparation
     from recbole_amd.data.dataset import Dataset
@@ -70,7 +70,7 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     config = Config(model='BPR', dataset='synthetic-ml20m', config_dict={
         'data_path': ROOT, 'embedding_size': d, 'training_neg_sample_num': neg,
         'train_batch_size': batch_rows, 'eval_setting': 'RO_RS,full', 'use_gpu': True,
-        'state': 'ERROR'})
+        'state': 'ERROR', 'neg_sampling_alias': alias})
     config['device'] = dev
     init_seed(config['seed'], config['reproducibility'])
     u, i, nU, nI = make_c2(seed)
@@ -304,6 +304,9 @@ def main():
     # multi-GPU table layout: row-sharded (default) or replicated;
     # 'sharded' with --gpus 1 runs the sharded protocol on one rank (diagnostic)
     ap.add_argument('--dp-mode', default=None, choices=['sharded', 'replicated'])
+    # negative sampler: the bit-exact walk (default, the headline) or the alias-table
+    # fast mode (labelled NON-PARITY: i.i.d. draws of the same distribution)
+    ap.add_argument('--sampler', default='walk', choices=['walk', 'alias'])
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -330,7 +333,8 @@ def main():
         dp_mode = 'single'
     config, train, test, model, opt, step = build_workload(
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
-        dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded')
+        dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded',
+        alias=args.sampler == 'alias')
     setup_s = time.time() - t_setup
     K, W = args.steps, args.warmup
     if K < 1 or W < 0:
@@ -422,6 +426,8 @@ def main():
                            'replicated': f'dp{world} (replicated tables, RCCL all-gather of '
                                          f'per-row loss coefficients)'}[dp_mode],
                    'exchange_graph': bool(step.use_graph),
+                   'sampler': ('walk (bit-exact)' if args.sampler == 'walk' else
+                               'alias table (NON-PARITY fast mode)'),
                    'chunk_plan_timed': [n for b0, n, _ in step._plan if W <= b0 < W + K],
                    'eager_steps_timed': eager_timed},
         'roofline': roof,

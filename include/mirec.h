@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 11
+#define MIREC_ABI_VERSION 12
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -79,6 +79,30 @@ int mirec_sample_walk_segments(const int32_t* random_list, int64_t L, int64_t* p
                                const uint32_t* used_bits, int64_t n_bits,
                                int64_t n_key_space, int reject, int64_t* out,
                                int32_t* status_dev, void* ws, size_t ws_bytes, void* stream);
+
+/* Alias-table FAST MODE (labelled non-parity; north_star (c)): i.i.d. draws from
+ * the same distribution the walk follows — p(v) proportional to counts[v], i.e.
+ * the number of times v appears in random_list (uniform: 1 for ids 1..n-1;
+ * popularity: item frequency, sampler.py:197-201) — with the same rejection of
+ * used ids, but NOT the reference's value sequence. Replaces random_num's
+ * cyclic walk (sampler.py:82-101) when Sampler.enable_alias() was called.
+ *
+ * mirec_alias_build (HOST pointers, host-side setup): Vose's alias method in
+ * exact integer arithmetic over n columns; thr[c] in units of 2^-32.
+ * mirec_sample_alias: draw id = counter + g for the g-th value of the call
+ * (batches in order, slot j*Kb + k inside batch b, values at out + b*out_stride
+ * like mirec_sample_walk); random bits = splitmix64(seed ^ splitmix64(id*4096 +
+ * attempt)); a used value is redrawn with attempt+1 (status -3 after 4096
+ * attempts, -2 for a key outside [0, n_key_space)). The caller advances counter
+ * by n_keys*num per call. Deterministic for a given (seed, counter). */
+int mirec_alias_build(const int64_t* counts, int64_t n, uint32_t* thr, int32_t* alias);
+int mirec_sample_alias(const uint32_t* thr, const int32_t* alias, int64_t n_cols,
+                       uint64_t seed, uint64_t counter, const int64_t* keys,
+                       int64_t n_keys, int64_t batch_keys, int64_t num,
+                       const int64_t* used_ptr, const int32_t* used_cols,
+                       const uint32_t* used_bits, int64_t n_bits, int64_t n_key_space,
+                       int reject, int64_t* out, int64_t out_stride,
+                       int32_t* status_dev, void* stream);
 
 /* Used-id bitmap of a CSR (sampler.py:206-227 used_ids as bits):
  * bits[k * ceil(n_bits/32) + v/32] bit v%32 set iff v in used[k], v < n_bits. */
@@ -214,6 +238,9 @@ typedef struct mirec_chunk_prep {
   void* walk_ws; size_t walk_ws_bytes; void* sort_ws; size_t sort_ws_bytes;
   int32_t *u_perm, *u_uniq, *u_seg, *u_nu, *i_perm, *i_uniq, *i_seg, *i_nu;
   int32_t *u_ahead, *u_nah, *i_ahead, *i_nah;
+  /* alias fast mode (alias_thr != NULL): mirec_sample_alias replaces the walk */
+  const uint32_t* alias_thr; const int32_t* alias_idx; int64_t n_alias;
+  uint64_t alias_seed, alias_counter;
 } mirec_chunk_prep;
 int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
 

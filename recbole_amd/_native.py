@@ -60,7 +60,9 @@ class ChunkPrep(ctypes.Structure):
                 ('sort_ws_bytes', c_size_t),
                 ('u_perm', _P), ('u_uniq', _P), ('u_seg', _P), ('u_nu', _P),
                 ('i_perm', _P), ('i_uniq', _P), ('i_seg', _P), ('i_nu', _P),
-                ('u_ahead', _P), ('u_nah', _P), ('i_ahead', _P), ('i_nah', _P)]
+                ('u_ahead', _P), ('u_nah', _P), ('i_ahead', _P), ('i_nah', _P),
+                ('alias_thr', _P), ('alias_idx', _P), ('n_alias', c_int64),
+                ('alias_seed', ctypes.c_uint64), ('alias_counter', ctypes.c_uint64)]
 
 
 # Every symbol include/mirec.h declares: name -> (restype, argtypes)
@@ -75,6 +77,10 @@ SIGNATURES = {
                                            _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
                                            c_size_t, _P]),
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
+    "mirec_alias_build": (c_int, [_P, c_int64, _P, _P]),
+    "mirec_sample_alias": (c_int, [_P, _P, c_int64, ctypes.c_uint64, ctypes.c_uint64, _P, c_int64,
+                                   c_int64, c_int64, _P, _P, _P, c_int64, c_int64, c_int, _P,
+                                   c_int64, _P, _P]),
     "mirec_shard_keys": (c_int, [_P, c_int64, c_int32, c_int64, _P, _P]),
     "mirec_shard_plan": (c_int, [_P, _P, c_int64, c_int64, c_int64, c_int32, c_int32, c_int32,
                                  c_int64, _P, _P, _P, _P, _P, _P]),
@@ -147,7 +153,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class NativeError(RuntimeError):

@@ -21,6 +21,7 @@ OVERALL = dict(
     # MI355X build extensions
     n_gpus=None, fused_train=True, fused_eval=True, train_graph=True, profile=False,
     adam_mode='deferred', shard_tables=True,
+    neg_sampling_alias=False,   # alias-table fast mode (NON-PARITY, sampler.enable_alias)
 )
 
 SAMPLE = dict(

@@ -157,10 +157,16 @@ extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {
                      p->users, p->items, p->s0, n, p->Bc, KI, p->user_keys, p->item_keys);
   int rc = mirec::launch_status("mirec_prepare_chunk: keys");
   if (rc) return rc;
-  rc = mirec_sample_walk(p->random_list, p->L, p->pr_dev, p->user_keys, n, p->Bc, p->n_batches,
-                         p->T, p->used_ptr, p->used_cols, p->used_bits, p->n_bits, p->n_users,
-                         p->reject, p->item_keys + p->Bc, KI, p->status, p->walk_ws,
-                         p->walk_ws_bytes, stream);
+  if (p->alias_thr)
+    rc = mirec_sample_alias(p->alias_thr, p->alias_idx, p->n_alias, p->alias_seed,
+                            p->alias_counter, p->user_keys, n, p->Bc, p->T, p->used_ptr,
+                            p->used_cols, p->used_bits, p->n_bits, p->n_users, p->reject,
+                            p->item_keys + p->Bc, KI, p->status, stream);
+  else
+    rc = mirec_sample_walk(p->random_list, p->L, p->pr_dev, p->user_keys, n, p->Bc,
+                           p->n_batches, p->T, p->used_ptr, p->used_cols, p->used_bits,
+                           p->n_bits, p->n_users, p->reject, p->item_keys + p->Bc, KI,
+                           p->status, p->walk_ws, p->walk_ws_bytes, stream);
   if (rc) return rc;
   return mirec::sort_chunk_pair(p->user_keys, n, p->Bc, p->n_users, p->u_perm, p->u_uniq,
                                 p->u_seg, p->u_nu, p->item_keys, p->n_batches * KI, KI,

@@ -437,6 +437,60 @@ __global__ __launch_bounds__(256) void used_bitmap_kernel(const int64_t* __restr
   }
 }
 
+// ---- alias-table fast mode (labelled non-parity; include/mirec.h mirec_sample_alias)
+// Each draw is independent: one lane per (batch, j, k) slot, counter-based
+// random bits (splitmix64 of seed and draw id), Walker/Vose column + threshold,
+// rejection by redrawing with the next attempt number. No serial walk, so a
+// whole chunk of batches is one wide launch.
+constexpr int kAliasTries = 4096;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int32_t alias_draw(const uint32_t* __restrict__ thr,
+                                              const int32_t* __restrict__ alias, uint64_t n_cols,
+                                              uint64_t seed, uint64_t id, uint32_t attempt) {
+  const uint64_t r = mix64(seed ^ mix64(id * (uint64_t)kAliasTries + attempt));
+  const uint32_t col = (uint32_t)(((r >> 32) * n_cols) >> 32);   // multiply-shift, < n_cols
+  return (uint32_t)r < __ldg(thr + col) ? (int32_t)col : __ldg(alias + col);
+}
+
+__global__ __launch_bounds__(256) void alias_sample_kernel(
+    const uint32_t* __restrict__ thr, const int32_t* __restrict__ alias, uint64_t n_cols,
+    uint64_t seed, uint64_t counter, const int64_t* __restrict__ keys, int64_t n_keys,
+    int64_t batch_keys, int64_t num, UsedSet u, int64_t n_key_space, int reject,
+    int64_t* __restrict__ out, int64_t out_stride, int32_t* __restrict__ status) {
+  const int64_t total = n_keys * num;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    // g enumerates batches in order, slot j*Kb + k inside a batch
+    const int64_t b = g / (batch_keys * num);
+    const int64_t k0 = b * batch_keys;
+    const int64_t Kb = min(batch_keys, n_keys - k0);
+    const int64_t s = g - k0 * num;
+    const int64_t k = s % Kb;
+    const int64_t key = keys[k0 + k];
+    const uint64_t id = counter + (uint64_t)g;
+    if (key < 0 || key >= n_key_space) {
+      atomicExch(status, -2);
+      out[b * out_stride + s] = 0;
+      continue;
+    }
+    int32_t v = alias_draw(thr, alias, n_cols, seed, id, 0);
+    if (reject) {
+      uint32_t a = 1;
+      for (; is_used(u, key, v) && a < (uint32_t)kAliasTries; ++a)
+        v = alias_draw(thr, alias, n_cols, seed, id, a);
+      if (a == (uint32_t)kAliasTries && is_used(u, key, v)) atomicExch(status, -3);
+    }
+    out[b * out_stride + s] = v;
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -545,6 +599,92 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
                        masks, status_dev, rejA, rejB);
   }
   return launch_status("mirec_sample_walk");
+}
+
+// Vose's alias method in exact integer arithmetic: column capacity W = sum(counts),
+// item weight counts[i] * n; a small column s keeps floor(w_s * 2^32 / W) of its
+// 2^32 threshold units for itself and gives the rest to a large column l, whose
+// remaining weight drops by W - w_s (exact, so the last columns hold exactly W and
+// become full: threshold 2^32 - 1, alias = itself). Host-side table setup.
+extern "C" int mirec_alias_build(const int64_t* counts, int64_t n, uint32_t* thr, int32_t* alias) {
+  if (!counts || !thr || !alias || n <= 0 || n > (int64_t)UINT32_MAX) {
+    set_error("mirec_alias_build: bad arguments");
+    return -1;
+  }
+  unsigned __int128 W = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (counts[i] < 0) {
+      set_error("mirec_alias_build: negative count at %lld", (long long)i);
+      return -1;
+    }
+    W += (unsigned __int128)counts[i];
+  }
+  if (W == 0) {
+    set_error("mirec_alias_build: all counts are zero");
+    return -1;
+  }
+  std::vector<unsigned __int128> w((size_t)n);
+  std::vector<int64_t> small, large;
+  small.reserve((size_t)n);
+  large.reserve((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    w[(size_t)i] = (unsigned __int128)counts[i] * (unsigned __int128)n;
+    (w[(size_t)i] < W ? small : large).push_back(i);
+  }
+  while (!small.empty() && !large.empty()) {
+    const int64_t s = small.back(), l = large.back();
+    small.pop_back();
+    thr[s] = (uint32_t)((w[(size_t)s] << 32) / W);
+    alias[s] = (int32_t)l;
+    w[(size_t)l] -= W - w[(size_t)s];
+    if (w[(size_t)l] < W) {
+      large.pop_back();
+      small.push_back(l);
+    }
+  }
+  for (int64_t i : large) { thr[i] = UINT32_MAX; alias[i] = (int32_t)i; }
+  for (int64_t i : small) { thr[i] = UINT32_MAX; alias[i] = (int32_t)i; }  // unreachable in exact arithmetic
+  return 0;
+}
+
+extern "C" int mirec_sample_alias(const uint32_t* thr, const int32_t* alias, int64_t n_cols,
+                                  uint64_t seed, uint64_t counter, const int64_t* keys,
+                                  int64_t n_keys, int64_t batch_keys, int64_t num,
+                                  const int64_t* used_ptr, const int32_t* used_cols,
+                                  const uint32_t* used_bits, int64_t n_bits, int64_t n_key_space,
+                                  int reject, int64_t* out, int64_t out_stride,
+                                  int32_t* status_dev, void* stream) {
+  if (!thr || !alias || n_cols <= 0 || n_cols > (int64_t)UINT32_MAX || !out || !status_dev ||
+      n_keys < 0 || num < 0 || batch_keys <= 0 || (n_keys > 0 && !keys)) {
+    set_error("mirec_sample_alias: bad arguments");
+    return -1;
+  }
+  if (n_keys == 0 || num == 0) return 0;
+  if (reject && ((!used_ptr || !used_cols) && !used_bits)) {
+    set_error("mirec_sample_alias: reject=1 needs the used-id CSR or bitmap");
+    return -1;
+  }
+  if (used_bits && n_bits <= 0) {
+    set_error("mirec_sample_alias: bitmap needs n_bits > 0");
+    return -1;
+  }
+  if (out_stride == 0) out_stride = batch_keys * num;
+  if (out_stride < min(batch_keys, n_keys) * num) {
+    set_error("mirec_sample_alias: out_stride %lld < batch values", (long long)out_stride);
+    return -1;
+  }
+  UsedSet u;
+  u.ptr = used_ptr;
+  u.cols = used_cols;
+  u.bits = used_bits;
+  u.nbits = n_bits;
+  u.words = used_bits ? (n_bits + 31) / 32 : 0;
+  const int64_t total = n_keys * num;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(alias_sample_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, thr,
+                     alias, (uint64_t)n_cols, seed, counter, keys, n_keys, batch_keys, num, u,
+                     n_key_space, reject, out, out_stride, status_dev);
+  return launch_status("mirec_sample_alias");
 }
 
 // Many consecutive sample_by_key_ids calls of different sizes in one launch: call

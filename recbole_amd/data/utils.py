@@ -71,6 +71,8 @@ def data_preparation(config, dataset, save=False):
             sampler = Sampler(phases, built, train_args['distribution'])
         else:
             sampler = RepeatableSampler(phases, dataset, train_args['distribution'])
+        if config['neg_sampling_alias']:
+            sampler.enable_alias(config['seed'])
         train_kwargs['sampler'] = sampler.set_phase('train')
         train_kwargs['neg_sample_args'] = train_args
     train_data = get_data_loader('train', config, train_args)(**train_kwargs)
@@ -85,6 +87,8 @@ def data_preparation(config, dataset, save=False):
                 sampler = Sampler(phases, built, eval_args['distribution'])
             else:
                 sampler = RepeatableSampler(phases, dataset, eval_args['distribution'])
+            if config['neg_sampling_alias']:
+                sampler.enable_alias(config['seed'])
         else:
             sampler.set_distribution(eval_args['distribution'])
         test_kwargs['neg_sample_args'] = eval_args

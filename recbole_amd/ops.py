@@ -101,6 +101,52 @@ def sample_walk_segments(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: 
     return out
 
 
+def alias_build(counts) -> tuple:
+    """Host-side Vose alias table of non-negative integer counts: (thr uint32[n],
+    alias int32[n]) numpy arrays (mirec_alias_build)."""
+    counts = np.ascontiguousarray(counts, dtype=np.int64)
+    n = len(counts)
+    thr = np.empty(n, dtype=np.uint32)
+    alias = np.empty(n, dtype=np.int32)
+    check(lib().mirec_alias_build(counts.ctypes.data, n, thr.ctypes.data, alias.ctypes.data),
+          "mirec_alias_build")
+    return thr, alias
+
+
+def sample_alias(thr: torch.Tensor, alias: torch.Tensor, seed: int, counter: int,
+                 keys: torch.Tensor, num: int, used_ptr: torch.Tensor | None,
+                 used_cols: torch.Tensor | None, n_key_space: int, reject: bool,
+                 batch_keys: int | None = None, out: torch.Tensor | None = None,
+                 out_stride: int = 0, status: torch.Tensor | None = None,
+                 used_bits: torch.Tensor | None = None, n_bits: int = 0) -> torch.Tensor:
+    """Alias-table fast-mode draws (NON-PARITY, mirec_sample_alias): `thr` is the
+    uint32 threshold table viewed as int32 on the device, `alias` int32."""
+    _dev(thr, torch.int32, "thr")
+    _dev(alias, torch.int32, "alias")
+    _dev(keys, torch.int64, "keys")
+    n_keys = keys.numel()
+    if batch_keys is None:
+        batch_keys = max(n_keys, 1)
+    if out is None:
+        out = torch.empty(n_keys * num, dtype=torch.int64, device=keys.device)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=keys.device)
+    bits = reject and used_bits is not None
+    if reject and not bits:
+        _dev(used_ptr, torch.int64, "used_ptr")
+        _dev(used_cols, torch.int32, "used_cols")
+    if bits:
+        _dev(used_bits, torch.int32, "used_bits")
+    rc = lib().mirec_sample_alias(
+        ptr(thr), ptr(alias), thr.numel(), seed & (2 ** 64 - 1), counter, ptr(keys), n_keys,
+        batch_keys, num, ptr(used_ptr) if reject and not bits else None,
+        ptr(used_cols) if reject and not bits else None, ptr(used_bits) if bits else None,
+        n_bits if bits else 0, n_key_space, 1 if reject else 0, ptr(out), out_stride,
+        ptr(status), stream_handle())
+    check(rc, "mirec_sample_alias")
+    return out
+
+
 def used_bitmap(used_ptr: torch.Tensor, used_cols: torch.Tensor, n_keys: int,
                 n_bits: int) -> torch.Tensor:
     """Per-key used-id bitmap [n_keys, ceil(n_bits/32)] (int32 words) of a CSR."""

@@ -58,6 +58,53 @@ class AbstractSampler(object):
         self._rl_dev = None
         self._pr_dev = None
         self._pr_host = 0
+        if getattr(self, 'alias', None) is not None:
+            self._build_alias()
+
+    # ------------------------------------------------------------ alias fast mode
+    def enable_alias(self, seed=0):
+        """Switch to the alias-table FAST MODE (labelled NON-PARITY, north_star
+        (c); config `neg_sampling_alias`): i.i.d. draws from the distribution the
+        walk follows — p(v) proportional to the number of times v appears in
+        random_list — with the same rejection of used ids, but not the reference's
+        value sequence. Every draw is independent, so a chunk of batches is one
+        wide launch instead of a serial walk (mirec_sample_alias). Deterministic
+        for a seed; random_pr is left untouched."""
+        self.alias_seed = int(seed) & (2 ** 64 - 1)
+        self._alias_ctr = 0
+        self._build_alias()
+        return self
+
+    def _build_alias(self):
+        counts = np.bincount(np.asarray(self.random_list, dtype=np.int64),
+                             minlength=self.n_items)
+        self.alias = ops.alias_build(counts)
+        self._alias_dev = None
+
+    def alias_args(self, device, n_draws):
+        """(thr, alias, seed, counter) for n_draws draws; advances the counter."""
+        if self._alias_dev is None or self._alias_dev[0].device != torch.device(device):
+            thr, idx = self.alias
+            self._alias_dev = (torch.as_tensor(thr.view(np.int32), device=device),
+                               torch.as_tensor(idx, device=device))
+        c = self._alias_ctr
+        self._alias_ctr += int(n_draws)
+        return self._alias_dev[0], self._alias_dev[1], self.alias_seed, c
+
+    def _alias_draw(self, keys, num, batch_keys=None, out=None, out_stride=0):
+        up, uc = self._used_dev()
+        bits, n_bits = self._used_bits()
+        thr, idx, seed, c = self.alias_args(self.device, keys.numel() * int(num))
+        return ops.sample_alias(thr, idx, seed, c, keys, int(num), up, uc, self.n_users,
+                                up is not None, batch_keys=batch_keys, out=out,
+                                out_stride=out_stride, status=self._status, used_bits=bits,
+                                n_bits=n_bits)
+
+    def _phase_alias(self, phase):
+        # a phase copy draws its own stream (seed mixed with the phase index)
+        if self.alias is not None:
+            self.alias_seed = (self.alias_seed * 0x9E3779B97F4A7C15 +
+                               1 + self.phases.index(phase)) & (2 ** 64 - 1)
 
     def get_random_list(self):
         raise NotImplementedError('method [get_random_list] should be implemented')
@@ -77,6 +124,8 @@ class AbstractSampler(object):
             self._status = torch.zeros(1, dtype=torch.int32, device=device)
             self._ws = None
         return self
+
+    alias = None
 
     @property
     def random_pr(self):
@@ -108,6 +157,9 @@ class AbstractSampler(object):
         self._status.zero_()
         if s == -2:
             raise ValueError('user_id out of range in negative sampling')
+        if self.alias is not None:
+            raise RuntimeError('alias negative sampling found no free item for a user within '
+                               '4096 draws')
         raise RuntimeError('negative sampling did not terminate: a user has no free item the '
                            'walk over random_list can reach')
 
@@ -129,6 +181,10 @@ class AbstractSampler(object):
         if keys.dim() == 0:
             keys = keys.view(1)
         keys = keys.to(device=self.device, dtype=torch.int64).contiguous()
+        if self.alias is not None:
+            out = self._alias_draw(keys, num)
+            self.check_status()
+            return out
         up, uc = self._used_dev()
         bits, n_bits = self._used_bits()
         reject = up is not None
@@ -144,6 +200,9 @@ class AbstractSampler(object):
         out[b*out_stride:] (default stride batch_keys*num) in the j*Kb + k layout."""
         if self._rl_dev is None:
             self.to_device(keys_dev.device)
+        if self.alias is not None:
+            return self._alias_draw(keys_dev, num, batch_keys=batch_keys, out=out,
+                                    out_stride=out_stride)
         up, uc = self._used_dev()
         bits, n_bits = self._used_bits()
         return ops.sample_walk(self._rl_dev, self._pr_dev, keys_dev, int(num), up, uc,
@@ -167,6 +226,15 @@ class AbstractSampler(object):
         s's values at [seg_ptr[s]*num, seg_ptr[s+1]*num) in the j*K_s + k layout."""
         if self._rl_dev is None:
             self.to_device(keys_dev.device)
+        if self.alias is not None:
+            # every draw is independent: expand the keys to the output layout
+            # (call s, slot j*K_s + k -> key seg_ptr[s] + k) and draw one value each
+            sp = seg_ptr_dev.to(torch.int64)
+            K = sp[1:] - sp[:-1]
+            seg = torch.repeat_interleave(torch.arange(len(K), device=sp.device), K * int(num))
+            q = torch.arange(seg.numel(), device=sp.device) - sp[seg] * int(num)
+            ekeys = keys_dev[sp[seg] + q % K[seg]].contiguous()
+            return self._alias_draw(ekeys, 1)
         up, uc = self._used_dev()
         bits, n_bits = self._used_bits()
         return ops.sample_walk_segments(self._rl_dev, self._pr_dev, keys_dev, seg_ptr_dev,
@@ -248,6 +316,7 @@ class Sampler(AbstractSampler):
             raise ValueError(f'Phase [{phase}] not exist.')
         new = copy.copy(self)
         new.phase = phase
+        new._phase_alias(phase)
         new._used_dev_cache = self._used_dev_cache
         new._pr_host = self.random_pr
         if self._pr_dev is not None:
@@ -325,6 +394,7 @@ class RepeatableSampler(AbstractSampler):
             raise ValueError(f'Phase [{phase}] not exist.')
         new = copy.copy(self)
         new.phase = phase
+        new._phase_alias(phase)
         new._pr_host = self.random_pr
         if self._pr_dev is not None:
             new._pr_dev = self._pr_dev.clone()

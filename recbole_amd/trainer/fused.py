@@ -269,6 +269,11 @@ class FusedBPRTrainStep(object):
             cp = self._chunk_prep(slot)
             cp.users, cp.items = self._users.data_ptr(), self._items.data_ptr()
             cp.s0, cp.n_batches, cp.Bc = b0 * self.Bg, nb, Bc
+            samp = self.data.sampler
+            if samp.alias is not None:              # fast mode: draw ids of this chunk
+                thr, idx, cp.alias_seed, cp.alias_counter = samp.alias_args(
+                    self.device, nb * Bc * T)
+                cp.alias_thr, cp.alias_idx, cp.n_alias = thr.data_ptr(), idx.data_ptr(), thr.numel()
             check(lib().mirec_prepare_chunk(ctypes.byref(cp), self.prep_stream.cuda_stream),
                   'mirec_prepare_chunk')
             slot.ready.record(self.prep_stream)

@@ -233,8 +233,8 @@ class Trainer(AbstractTrainer):
         state = {
             'config': _plain_config(cfg),
             'epoch': epoch,
-            'cur_step': self.cur_step,
-            'best_valid_score': self.best_valid_score,
+            'cur_step': int(self.cur_step),
+            'best_valid_score': float(self.best_valid_score),
             'state_dict': self.model.state_dict(),
             'optimizer': self.optimizer.state_dict(),
         }
@@ -411,6 +411,8 @@ def _plain_config(cfg):
     def plain(v):
         if isinstance(v, enum.Enum):
             return v.name
+        if isinstance(v, np.generic):              # numpy scalars pickle as numpy objects
+            return v.item()
         if isinstance(v, (str, int, float, bool)) or v is None:
             return v
         if isinstance(v, (list, tuple)):
