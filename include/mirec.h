@@ -104,6 +104,16 @@ int mirec_sample_alias(const uint32_t* thr, const int32_t* alias, int64_t n_cols
                        int reject, int64_t* out, int64_t out_stride,
                        int32_t* status_dev, void* stream);
 
+/* Host data-pipeline primitives (CPU, HOST pointers):
+ * mirec_host_counting_order: order = stable sort permutation of keys in
+ *   [0, key_space) (grouping rows by user: dataset.py:1249-1256 _grouped_index);
+ * mirec_host_csr_build: CSR of the distinct (key, value) pairs, rows ascending
+ *   (the per-phase used-id sets, sampler.py:206-227); cols sized n by the caller;
+ *   returns the number of distinct pairs. */
+int mirec_host_counting_order(const int64_t* keys, int64_t n, int64_t key_space, int64_t* order);
+int64_t mirec_host_csr_build(const int64_t* keys, const int64_t* vals, int64_t n, int64_t n_keys,
+                             int64_t* ptr, int32_t* cols);
+
 /* Used-id bitmap of a CSR (sampler.py:206-227 used_ids as bits):
  * bits[k * ceil(n_bits/32) + v/32] bit v%32 set iff v in used[k], v < n_bits. */
 size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits);
@@ -243,6 +253,12 @@ typedef struct mirec_chunk_prep {
   uint64_t alias_seed, alias_counter;
 } mirec_chunk_prep;
 int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
+/* The two halves of mirec_prepare_chunk, for two streams (the caller orders
+ * group after walk, e.g. with an event): keys + K4 walk (or alias draws), then the
+ * K2 groupings + look-ahead lists. Splitting lets chunk c+1's walk run while
+ * chunk c is grouped. */
+int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream);
+int mirec_prepare_chunk_group(const mirec_chunk_prep* p, void* stream);
 
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of

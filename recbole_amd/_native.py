@@ -78,6 +78,8 @@ SIGNATURES = {
                                            c_size_t, _P]),
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
     "mirec_alias_build": (c_int, [_P, c_int64, _P, _P]),
+    "mirec_host_counting_order": (c_int, [_P, c_int64, c_int64, _P]),
+    "mirec_host_csr_build": (c_int64, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_sample_alias": (c_int, [_P, _P, c_int64, ctypes.c_uint64, ctypes.c_uint64, _P, c_int64,
                                    c_int64, c_int64, _P, _P, _P, c_int64, c_int64, c_int, _P,
                                    c_int64, _P, _P]),
@@ -105,6 +107,8 @@ SIGNATURES = {
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
     "mirec_prepare_chunk": (c_int, [_P, _P]),
+    "mirec_prepare_chunk_walk": (c_int, [_P, _P]),
+    "mirec_prepare_chunk_group": (c_int, [_P, _P]),
     "mirec_write_bytes": (c_int, [_P, _P, c_size_t, _P]),
     "mirec_selftest_adam_math": (c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P, _P]),
     "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,

@@ -145,12 +145,17 @@ __global__ __launch_bounds__(256) void chunk_keys_kernel(const int64_t* __restri
 
 }  // namespace mirec
 
-extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {
+static bool prep_ok(const mirec_chunk_prep* p) {
   if (!p || !p->users || !p->items || !p->user_keys || !p->item_keys || p->n_batches <= 0 ||
       p->Bc <= 0 || p->T <= 0 || p->s0 < 0) {
     mirec::set_error("mirec_prepare_chunk: bad arguments");
-    return -1;
+    return false;
   }
+  return true;
+}
+
+extern "C" int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream) {
+  if (!prep_ok(p)) return -1;
   const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
   const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
   hipLaunchKernelGGL(mirec::chunk_keys_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
@@ -158,19 +163,27 @@ extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {
   int rc = mirec::launch_status("mirec_prepare_chunk: keys");
   if (rc) return rc;
   if (p->alias_thr)
-    rc = mirec_sample_alias(p->alias_thr, p->alias_idx, p->n_alias, p->alias_seed,
-                            p->alias_counter, p->user_keys, n, p->Bc, p->T, p->used_ptr,
-                            p->used_cols, p->used_bits, p->n_bits, p->n_users, p->reject,
-                            p->item_keys + p->Bc, KI, p->status, stream);
-  else
-    rc = mirec_sample_walk(p->random_list, p->L, p->pr_dev, p->user_keys, n, p->Bc,
+    return mirec_sample_alias(p->alias_thr, p->alias_idx, p->n_alias, p->alias_seed,
+                              p->alias_counter, p->user_keys, n, p->Bc, p->T, p->used_ptr,
+                              p->used_cols, p->used_bits, p->n_bits, p->n_users, p->reject,
+                              p->item_keys + p->Bc, KI, p->status, stream);
+  return mirec_sample_walk(p->random_list, p->L, p->pr_dev, p->user_keys, n, p->Bc,
                            p->n_batches, p->T, p->used_ptr, p->used_cols, p->used_bits,
                            p->n_bits, p->n_users, p->reject, p->item_keys + p->Bc, KI,
                            p->status, p->walk_ws, p->walk_ws_bytes, stream);
-  if (rc) return rc;
+}
+
+extern "C" int mirec_prepare_chunk_group(const mirec_chunk_prep* p, void* stream) {
+  if (!prep_ok(p)) return -1;
+  const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
   return mirec::sort_chunk_pair(p->user_keys, n, p->Bc, p->n_users, p->u_perm, p->u_uniq,
                                 p->u_seg, p->u_nu, p->item_keys, p->n_batches * KI, KI,
                                 p->n_items, p->i_perm, p->i_uniq, p->i_seg, p->i_nu,
                                 p->n_batches, p->u_ahead, p->u_nah, p->i_ahead, p->i_nah,
                                 p->sort_ws, p->sort_ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {
+  const int rc = mirec_prepare_chunk_walk(p, stream);
+  return rc ? rc : mirec_prepare_chunk_group(p, stream);
 }

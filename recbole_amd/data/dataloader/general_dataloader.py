@@ -203,7 +203,13 @@ def _csr_difference(ptr_a, cols_a, ptr_b, cols_b):
     mul = int(max(cols_a.max() if len(cols_a) else 0, cols_b.max() if len(cols_b) else 0)) + 1
     ka = ra.astype(np.int64) * mul + cols_a
     kb = rb.astype(np.int64) * mul + cols_b
-    keep = ~np.isin(ka, kb)
+    # rows ascending and each row's columns ascending: ka and kb are sorted, so
+    # membership is one binary search per element of A
+    if len(kb):
+        at = np.minimum(np.searchsorted(kb, ka), len(kb) - 1)
+        keep = kb[at] != ka
+    else:
+        keep = np.ones(len(ka), dtype=bool)
     rows, cols = ra[keep], cols_a[keep]
     ptr = np.zeros(n + 1, dtype=np.int64)
     np.add.at(ptr, rows + 1, 1)

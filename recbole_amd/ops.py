@@ -1,9 +1,10 @@
 """Thin torch-tensor wrappers over the libmirec.so C-ABI (include/mirec.h).
 
-Every function here launches a hand-written gfx950 kernel on the current HIP
-stream. Inputs must already be device tensors of the stated dtype; nothing is
+Every device function here launches a hand-written gfx950 kernel on the current
+HIP stream. Inputs must already be device tensors of the stated dtype; nothing is
 copied to the host and nothing falls back to PyTorch or the CPU — a tensor on
-the wrong device or a missing library raises.
+the wrong device or a missing library raises. The host_* functions are the
+library's CPU data-pipeline primitives (numpy arrays in and out).
 """
 from __future__ import annotations
 
@@ -99,6 +100,29 @@ def sample_walk_segments(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: 
         1 if reject else 0, ptr(out), ptr(status), ptr(ws), ws.numel(), stream_handle())
     check(rc, "mirec_sample_walk_segments")
     return out
+
+
+def host_counting_order(keys, key_space: int) -> np.ndarray:
+    """Stable sort permutation of integer keys in [0, key_space) (host, O(n))."""
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    order = np.empty(len(keys), dtype=np.int64)
+    check(lib().mirec_host_counting_order(keys.ctypes.data, len(keys), int(key_space),
+                                          order.ctypes.data), "mirec_host_counting_order")
+    return order
+
+
+def host_csr_build(keys, vals, n_keys: int) -> tuple:
+    """(ptr int64[n_keys+1], cols int32) of the distinct (key, value) pairs, each
+    row ascending (host, counting pass + per-row sort)."""
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    vals = np.ascontiguousarray(vals, dtype=np.int64)
+    ptr = np.empty(int(n_keys) + 1, dtype=np.int64)
+    cols = np.empty(max(len(keys), 1), dtype=np.int32)
+    nnz = lib().mirec_host_csr_build(keys.ctypes.data, vals.ctypes.data, len(keys), int(n_keys),
+                                     ptr.ctypes.data, cols.ctypes.data)
+    if nnz < 0:
+        check(int(nnz), "mirec_host_csr_build")
+    return ptr, cols[:nnz].copy()
 
 
 def alias_build(counts) -> tuple:

@@ -256,17 +256,9 @@ class AbstractSampler(object):
 
 
 def _csr_from_pairs(n_keys, keys, values):
-    keys = np.asarray(keys, dtype=np.int64)
-    values = np.asarray(values, dtype=np.int64)
-    order = np.lexsort((values, keys))
-    k, v = keys[order], values[order]
-    if len(k):
-        keep = np.ones(len(k), dtype=bool)
-        keep[1:] = (k[1:] != k[:-1]) | (v[1:] != v[:-1])
-        k, v = k[keep], v[keep]
-    ptr = np.zeros(n_keys + 1, dtype=np.int64)
-    np.add.at(ptr, k + 1, 1)
-    return np.cumsum(ptr), v.astype(np.int32)
+    """CSR of the distinct (key, value) pairs, each row's values ascending
+    (mirec_host_csr_build: one counting pass + a sort per row)."""
+    return ops.host_csr_build(keys, values, n_keys)
 
 
 class Sampler(AbstractSampler):
@@ -301,9 +293,10 @@ class Sampler(AbstractSampler):
         out = {}
         ks, vs = [], []
         for phase, ds in zip(self.phases, self.datasets):
+            # cumulative sets (train, train+valid, all): counting pass + per-row sort
             ks.append(ds.inter_feat[self.uid_field].numpy())
             vs.append(ds.inter_feat[self.iid_field].numpy())
-            out[phase] = _csr_from_pairs(self.n_users, np.concatenate(ks), np.concatenate(vs))
+            out[phase] = ops.host_csr_build(np.concatenate(ks), np.concatenate(vs), self.n_users)
         last_ptr = out[self.phases[-1]][0]
         if (np.diff(last_ptr) + 1 == self.n_items).any():
             raise ValueError('Some users have interacted with all items, '

@@ -55,30 +55,35 @@ ADAM_MODES = ('deferred', 'streamed')
 _PREP_STREAMS = {}
 
 
-def _prep_stream_for(dev):
-    """A side stream whose hardware queue is not the current stream's.
+def _prep_streams_for(dev, n=2):
+    """n side streams whose hardware queues are neither the current stream's nor
+    each other's.
 
     HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 by
     default) round-robin; a side stream that lands on the main stream's queue
     runs in order with it, so the chunk preparation would run behind the model
-    steps instead of beside them. Probe: hold the current stream busy with a
-    spin kernel and see whether an event on the candidate completes meanwhile
-    (a dedicated high-priority or CU-masked queue avoids the sharing too, but
-    measured 4-8x slower kernels on both queues: the extra queue oversubscribes
-    the hardware queue slots). Falls back to the first candidate."""
-    key = str(dev)
-    st = _PREP_STREAMS.get(key)
-    if st is not None:
-        return st
+    steps instead of beside them (and two prep streams on one queue would run
+    the walk and the grouping in order again). Probe: hold the current stream
+    and the streams already chosen busy with spin kernels and see whether an
+    event on the candidate completes meanwhile (a dedicated high-priority or
+    CU-masked queue avoids the sharing too, but measured 4-8x slower kernels on
+    both queues: the extra queue oversubscribes the hardware queue slots). Falls
+    back to the first candidates."""
+    key = (str(dev), n)
+    got = _PREP_STREAMS.get(key)
+    if got is not None:
+        return got
     import time
     main = torch.cuda.current_stream(dev)
-    first = None
-    for _ in range(8):
+    chosen, spare = [], []
+    for _ in range(16):
+        if len(chosen) == n:
+            break
         cand = torch.cuda.Stream(device=dev)
-        first = first or cand
         torch.cuda.synchronize(dev)
-        with torch.cuda.stream(main):
-            torch.cuda._sleep(int(2.4e3 * 3000))          # ~3 ms of spinning on main
+        for busy in [main] + chosen:
+            with torch.cuda.stream(busy):
+                torch.cuda._sleep(int(2.4e3 * 3000))      # ~3 ms of spinning
         ev = torch.cuda.Event()
         with torch.cuda.stream(cand):
             torch.cuda._sleep(1)
@@ -90,12 +95,11 @@ def _prep_stream_for(dev):
                 free = True
                 break
         torch.cuda.synchronize(dev)
-        if free:
-            st = cand
-            break
-    st = st or first
-    _PREP_STREAMS[key] = st
-    return st
+        (chosen if free else spare).append(cand)
+    while len(chosen) < n:
+        chosen.append(spare.pop(0) if spare else torch.cuda.Stream(device=dev))
+    _PREP_STREAMS[key] = chosen
+    return chosen
 
 
 class _Slot(object):
@@ -124,8 +128,10 @@ class _Slot(object):
             self.i_ahead = torch.empty(C * KI, dtype=torch.int32, device=dev)
             self.i_nah = torch.zeros(C, dtype=torch.int32, device=dev)
         self.ready = torch.cuda.Event()
+        self.walked = torch.cuda.Event()
         self.free = torch.cuda.Event()
         self.free_recorded = False
+        self.group_pending = False   # walked, grouping not yet issued
         self.chunk = None            # (first global batch, n batches, global batch size)
         self.graphs = {}             # (n batches, entry, flush) -> HIP graph of the model side
 
@@ -188,9 +194,10 @@ class FusedBPRTrainStep(object):
         self.samp_ws = torch.empty(lib().mirec_sample_walk_workspace_size(self.Bg, T),
                                    dtype=torch.uint8, device=dev)
         self.sort_ws = None
-        # keys, K4 walk, K2 grouping: on a side stream that does not share the
-        # main stream's hardware queue (_prep_stream_for)
-        self.prep_stream = _prep_stream_for(dev)
+        # keys + K4 walk on one side stream, K2 grouping + look-ahead lists on a
+        # second: chunk c+1 walks while chunk c is grouped; neither shares the main
+        # stream's hardware queue (_prep_streams_for)
+        self.prep_stream, self.group_stream = _prep_streams_for(dev)
         self.zero_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
         self.loss_hist = torch.zeros(1, dtype=torch.float32, device=dev)
         self.consts = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -274,9 +281,10 @@ class FusedBPRTrainStep(object):
                 thr, idx, cp.alias_seed, cp.alias_counter = samp.alias_args(
                     self.device, nb * Bc * T)
                 cp.alias_thr, cp.alias_idx, cp.n_alias = thr.data_ptr(), idx.data_ptr(), thr.numel()
-            check(lib().mirec_prepare_chunk(ctypes.byref(cp), self.prep_stream.cuda_stream),
-                  'mirec_prepare_chunk')
-            slot.ready.record(self.prep_stream)
+            check(lib().mirec_prepare_chunk_walk(ctypes.byref(cp), self.prep_stream.cuda_stream),
+                  'mirec_prepare_chunk_walk')
+            slot.walked.record(self.prep_stream)
+            slot.group_pending = True          # the grouping half: _issue_groups
             slot.chunk = chunk
             return
         with torch.cuda.stream(self.prep_stream):
@@ -303,6 +311,16 @@ class FusedBPRTrainStep(object):
                 ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
+
+    def _prepare_group(self, slot):
+        """The grouping half of a chunk's preparation (K2 + look-ahead lists) on the
+        group stream, after the chunk's walk."""
+        self.group_stream.wait_event(slot.walked)
+        check(lib().mirec_prepare_chunk_group(ctypes.byref(slot.prep),
+                                              self.group_stream.cuda_stream),
+              'mirec_prepare_chunk_group')
+        slot.ready.record(self.group_stream)
+        slot.group_pending = False
 
     def _chunk_prep(self, slot):
         """The slot's mirec_chunk_prep descriptor (pointers fixed per slot)."""
@@ -582,7 +600,8 @@ class FusedBPRTrainStep(object):
             for k, n, e, f in variants:
                 self._graph_for(self.slots[k], n, e, f)
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
-        self._next_chunk = 0
+        self._next_chunk = 0                   # chunks whose walk (or whole prep) is issued
+        self._next_group = 0                   # chunks whose grouping is issued
         self._prep_limit = (len(self._plan) if hold_prep_from is None
                             else self._chunk_of(hold_prep_from))
         self._cur = None                       # chunk index being consumed
@@ -590,6 +609,7 @@ class FusedBPRTrainStep(object):
             s.free_recorded = False
         for _ in range(len(self.slots)):
             self._issue_prep()
+        self._issue_groups(len(self.slots))
         return nb
 
     def release_prep(self, upto=None):
@@ -604,8 +624,18 @@ class FusedBPRTrainStep(object):
         k = self._next_chunk
         if k >= min(len(self._plan), self._prep_limit):
             return
-        self._prepare(self.slots[k % len(self.slots)], self._plan[k])
+        slot = self.slots[k % len(self.slots)]
+        slot.group_pending = False
+        self._prepare(slot, self._plan[k])
         self._next_chunk += 1
+
+    def _issue_groups(self, upto):
+        """Issue the grouping halves of the walked chunks below `upto`."""
+        while self._next_group < min(self._next_chunk, upto):
+            slot = self.slots[self._next_group % len(self.slots)]
+            if slot.group_pending:
+                self._prepare_group(slot)
+            self._next_group += 1
 
     def _enter_chunk(self, k, stream):
         if self._cur == k:
@@ -621,6 +651,10 @@ class FusedBPRTrainStep(object):
         if self._next_chunk <= k:
             raise RuntimeError(f'chunk {k} is held (begin_epoch(hold_prep_from=...)): '
                                'call release_prep() first')
+        # walks of the next chunks before this chunk's grouping: the walk is the
+        # long pole of the preparation, the grouping of chunk k runs beside it
+        self._top_up_prep(k)
+        self._issue_groups(k + 1)
         stream.wait_event(self.slots[k % S].ready)
         self._cur = k
 
@@ -655,8 +689,8 @@ class FusedBPRTrainStep(object):
                 if c1 == nb and flush:
                     self._flush(stream)
                     self._current = True
-            self._top_up_prep(k)       # after the chunk's launch: the host enqueues the
-            b = b0 + c1                # model side first, the walks of later chunks behind it
+            self._issue_groups(k + len(self.slots))   # later chunks' groupings, behind
+            b = b0 + c1
 
     def _top_up_prep(self, k):
         """Prepare chunks up to k + SLOTS - 1 (their slots are free once the chunks
@@ -688,6 +722,7 @@ class FusedBPRTrainStep(object):
         n_done = self.n_batches if n_done is None else n_done
         stream = torch.cuda.current_stream(self.device)
         stream.wait_stream(self.prep_stream)
+        stream.wait_stream(self.group_stream)
         self.sync_params()
         self.opt.advance(n_done)
         self.data.pr = 0

@@ -41,6 +41,25 @@ def main(src, out=None):
                                (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3,
                                r.get('Queue_Id', '?'), r['Kernel_Name'].split('(')[0][-60:])
         for r in rows if t0 <= int(r['Start_Timestamp']) <= t1]
+    # with --hip-runtime-trace: the host API calls inside the window, interleaved
+    # (offset, duration, 'H', name), and each kernel's launch-call offset
+    api = glob.glob(f'{src}/**/*hip_api_trace.csv', recursive=True)
+    if api:
+        calls = sorted(csv.DictReader(open(api[0])), key=lambda r: int(r['Start_Timestamp']))
+        launch_at = {r['Correlation_Id']: int(r['Start_Timestamp']) for r in calls}
+        ev = [(int(r['Start_Timestamp']), '%9.1f %8.1f H  %s' % (
+            (int(r['Start_Timestamp']) - t0) / 1e3,
+            (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3, r['Function']))
+            for r in calls if t0 - 5000 <= int(r['Start_Timestamp']) <= t1]
+        for r in rows:
+            s = int(r['Start_Timestamp'])
+            if t0 <= s <= t1:
+                la = launch_at.get(r.get('Correlation_Id'))
+                ev.append((s, '%9.1f %8.1f q%s %s (launched %+.1f)' % (
+                    (s - t0) / 1e3, (int(r['End_Timestamp']) - s) / 1e3, r.get('Queue_Id', '?'),
+                    r['Kernel_Name'].split('(')[0][-50:],
+                    (la - t0) / 1e3 if la else float('nan'))))
+        res['timeline'] = [e for _, e in sorted(ev)]
     print(json.dumps({k: v for k, v in res.items() if k != 'timeline'}, indent=1))
     print('\n'.join(res['timeline']))
     if out:
