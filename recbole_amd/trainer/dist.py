@@ -7,12 +7,15 @@ its contiguous slice of the samples, and back-propagates its local mean loss sca
 gradient of the global-batch mean. The exchange per step is
   * one all-reduce (SUM) of a flat bucket of the dense gradients (MLP / transformer
     weights, dense tables) — RCCL over xGMI;
-  * one all-gather per stashed source of the deferred tables (DeepFM's token rows,
-    SASRec's item rows): the per-contribution gradient rows + keys of every rank,
-    concatenated in rank order — which is the global batch's contribution order, so
-    every rank applies the identical deferred K5 step to its replica.
-A ragged global batch (size not divisible by G) is computed whole on every rank, with
-no exchange. Tables and optimizer state are replicated (288 GB per GPU).
+  * the deferred tables (DeepFM's token rows, SASRec's item rows) ROW-SHARDED by
+    default (shard_tables; FusedAdam.shard_deferred): each contribution row goes to
+    the owner of its table row (all-to-all, source-rank order = the global batch's
+    contribution order) and only the owner updates it; forwards fetch the rows they
+    read from their owners. With shard_tables: False, one all-gather per stashed
+    source instead and every rank applies the identical deferred K5 step to its
+    replica.
+A ragged global batch (size not divisible by G) is computed whole on every rank: no
+exchange (each owner keeps the contributions to its own rows).
 
 Evaluation: the full-sort users are split into G contiguous blocks; rank g ranks its
 block with K6 and one all-gather assembles the [n_users, K] positive flags in user
@@ -48,6 +51,30 @@ def _gather_cat(t, group):
     parts = [torch.empty_like(t) for _ in range(G)]
     tdist.all_gather(parts, t, group=group)
     return torch.cat(parts)
+
+
+def all_to_all_v(send, send_counts, group):
+    """Variable-size all-to-all along dim 0: send[...] holds send_counts[g] rows for
+    rank g, in rank order; returns (the rows received, in source-rank order, and
+    the per-source counts). RCCL directly; gloo (CPU tests) host-staged."""
+    nccl = str(tdist.get_backend(group)) == 'nccl'
+    dev = send.device
+    sc = send_counts.to(torch.int64)
+    sc = sc.to(dev) if nccl else sc.cpu()
+    rc = torch.empty_like(sc)
+    tdist.all_to_all_single(rc, sc, group=group)
+    sl, rl = sc.tolist(), rc.tolist()
+    shape = tuple(send.shape[1:])
+    if nccl:
+        recv = torch.empty((sum(rl),) + shape, dtype=send.dtype, device=dev)
+        tdist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rl,
+                                input_split_sizes=sl, group=group)
+    else:
+        recv = torch.empty((sum(rl),) + shape, dtype=send.dtype)
+        tdist.all_to_all_single(recv, send.contiguous().cpu(), output_split_sizes=rl,
+                                input_split_sizes=sl, group=group)
+        recv = recv.to(dev)
+    return recv, rc.to(dev)
 
 
 class DataParallelStep(object):
@@ -97,6 +124,20 @@ class DataParallelStep(object):
                 p.grad.copy_(flat[o:o + n].view_as(p.grad))
                 o += n
         for p, ds in getattr(optimizer, '_deferred', {}).items():
+            if 'shard' in ds:
+                # row-sharded: every contribution row to the owner of its row, in
+                # source-rank order (= the global batch's order); local row ids
+                G = ds['shard']['G']
+                out = []
+                for rows, keys, _ in ds['stash']:
+                    owner = keys % G
+                    order = torch.argsort(owner, stable=True)
+                    counts = torch.bincount(owner, minlength=G)
+                    rr, _ = all_to_all_v(rows[order], counts, self.group)
+                    kk, _ = all_to_all_v(keys[order], counts, self.group)
+                    out.append((rr, kk // G, 'owned'))
+                ds['stash'] = out
+                continue
             ds['stash'] = [(_gather_cat(rows, self.group), _gather_cat(keys, self.group), None)
                            for rows, keys, _ in ds['stash']]
 

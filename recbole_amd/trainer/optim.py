@@ -274,7 +274,8 @@ class FusedAdam(torch.optim.Optimizer):
 
     def _dtable(self, p, ds, **kw):
         st = self.state[p]
-        spec = {'p': p.data, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'last': ds['last']}
+        pt = ds['shard']['p'] if 'shard' in ds else p.data
+        spec = {'p': pt, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'last': ds['last']}
         spec.update(kw)
         return ops.adam_tables([spec])
 
@@ -284,6 +285,9 @@ class FusedAdam(torch.optim.Optimizer):
         when the caller already has it, e.g. another table read by the same keys)."""
         if segs is None:
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])
+        if 'shard' in self._deferred[p]:
+            self._catch_up_sharded(p, keys)
+            return segs
         ds = self._dstate(p)
         r = self.n_steps - ds['t0']
         if r > 0 or self._g is not None:      # (graph mode at r = 0: a no-op launch)
@@ -315,10 +319,15 @@ class FusedAdam(torch.optim.Optimizer):
 
     def flush(self):
         """Complete every row of every deferred table (after it, p / m / v equal
-        the dense schedule's)."""
+        the dense schedule's). Row-sharded tables: every owner completes its shard
+        and one all-gather refreshes the full parameter on every rank (a collective:
+        every rank calls flush at the same points)."""
         for p, ds in getattr(self, '_deferred', {}).items():
             if ds['t0'] is not None:
                 self._flush_table(p, ds, self.n_steps - ds['t0'])
+            if 'shard' in ds and ds['shard']['synced'] != self.n_steps:
+                p.data.copy_(self._gather_shard(ds, ds['shard']['p'], p.shape[0]))
+                ds['shard']['synced'] = self.n_steps
 
     def _combine_stash(self, p, stash):
         """One summed gradient row per touched table row. Each source (one autograd
@@ -326,7 +335,8 @@ class FusedAdam(torch.optim.Optimizer):
         fixed order; several sources are then added row-wise in source order —
         the same sums the dense path forms (a dense gradient per Function, added
         by autograd), so both schedules stay bit-identical."""
-        n_rows = p.shape[0]
+        ds = self._deferred[p]
+        n_rows = ds['shard']['n_own'] if 'shard' in ds else p.shape[0]
         parts = []
         for rows, keys, segs in stash:
             if segs is None:
@@ -353,6 +363,18 @@ class FusedAdam(torch.optim.Optimizer):
     def _deferred_step(self, p):
         ds = self._deferred[p]
         stash, ds['stash'] = ds['stash'], []
+        if 'shard' in ds:
+            # contributions exchanged to their owners carry local row ids ('owned');
+            # a batch computed whole on every rank (ragged: no exchange) keeps this
+            # rank's rows only
+            sh = ds['shard']
+            out = []
+            for rows, keys, tag in stash:
+                if tag != 'owned':
+                    mine = (keys % sh['G']) == sh['r']
+                    rows, keys = rows[mine], keys[mine] // sh['G']
+                out.append((rows, keys, None))
+            stash = [x for x in out if x[1].numel()]
         if not stash and p.grad is None:      # table not in this step's graph: skipped
             if ds['t0'] is not None:
                 self._flush_table(p, ds, self.n_steps - ds['t0'])
@@ -363,6 +385,9 @@ class FusedAdam(torch.optim.Optimizer):
         if stash:
             rows, segs, n_keys = self._combine_stash(p, stash)
         graph = self._g is not None
+        if p.grad is not None and 'shard' in ds:
+            raise NotImplementedError('a row-sharded deferred table takes stashed gradient '
+                                      'rows only (no dense gradient)')
         if p.grad is not None:                # a dense contribution too: stream every row
             self._flush_table(p, ds, r, device_step=graph)
             st = self.state[p]
@@ -384,6 +409,81 @@ class FusedAdam(torch.optim.Optimizer):
             self._flush_table(p, ds, r + 1)
             ds['t0'] = None
 
+    # ------------------------------------------------------------------ row sharding
+    # SURVEY.md §8e for the autograd path (C4 DeepFM's token tables, C3 SASRec's item
+    # table): rank r of G owns the rows id % G == r of every deferred table — their
+    # p, m, v and step counts as [n_own, d] shards (local row id // G), and runs the
+    # deferred K5 (touched rows, catch-ups, flushes) on them only. The full parameter
+    # stays on every rank as the forward's read cache: before a forward reads rows,
+    # catch_up fetches them from their owners (all-to-all of ids, owner-side catch-up
+    # of exactly those rows, all-to-all of the rows back into the cache); after the
+    # backward, DataParallelStep.exchange sends every contribution row to its owner
+    # (all-to-all, in source-rank order = the global batch's order), so each owner
+    # applies the same sums and the same Adam step as one GPU on the global batch.
+    def shard_deferred(self, group):
+        """Row-shard the deferred tables over the ranks of `group`."""
+        import torch.distributed as tdist
+        G, r = tdist.get_world_size(group), tdist.get_rank(group)
+        if G <= 1 or not getattr(self, '_deferred', None):
+            return
+        self.flush()
+        for p, ds in self._deferred.items():
+            if 'shard' in ds:
+                continue
+            st = self.state[p]
+            own = torch.arange(r, p.shape[0], G, device=p.device)
+            ds['shard'] = {'G': G, 'r': r, 'group': group, 'own': own, 'n_own': len(own),
+                           'S': -(-p.shape[0] // G), 'p': p.data[own].contiguous(),
+                           'synced': self.n_steps}
+            st['exp_avg'] = st['exp_avg'][own].contiguous()       # this rank's moments only
+            st['exp_avg_sq'] = st['exp_avg_sq'][own].contiguous()
+            ds['last'] = torch.zeros(len(own), dtype=torch.int32, device=p.device)
+            ds['t0'], ds['marked'] = None, False
+
+    @staticmethod
+    def _gather_shard(ds, t, n_rows):
+        """The full [n_rows, ...] tensor of every rank's shard t (row id = l*G + g)."""
+        from recbole_amd.trainer.dist import _gather_cat
+        sh = ds['shard']
+        G, S = sh['G'], sh['S']
+        pad = torch.zeros((S,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[:t.shape[0]] = t
+        full = _gather_cat(pad, sh['group']).view((G, S) + tuple(t.shape[1:]))
+        return full.transpose(0, 1).reshape((G * S,) + tuple(t.shape[1:]))[:n_rows]
+
+    def _catch_up_sharded(self, p, keys):
+        """Make the rows `keys` of the cache p current: owners catch them up on their
+        shards and send them back (two all-to-alls)."""
+        from recbole_amd.trainer.dist import all_to_all_v
+        ds = self._deferred[p]
+        sh = ds['shard']
+        if sh['synced'] == self.n_steps:      # the cache is complete (after a flush): no
+            return                            # exchange (evaluation reads stay rank-local)
+        G = sh['G']
+        uniq = torch.unique(keys)
+        owner = uniq % G
+        send = uniq[torch.argsort(owner, stable=True)]
+        counts = torch.bincount(owner, minlength=G)
+        req, rcounts = all_to_all_v(send, counts, sh['group'])
+        local = req // G
+        ds = self._dstate(p)
+        r = self.n_steps - ds['t0']
+        if r > 0 and local.numel():
+            lsegs = ops.segment_sort(local.contiguous(), sh['n_own'])
+
+            class _Z:
+                perm = uniq = seg = self._dummy_i32
+                n_uniq = self._zero_i32
+            tab = self._dtable(p, ds, rows=self._dummy_f32, segs=_Z,
+                               ahead=(lsegs.uniq, lsegs.n_uniq))
+            base, off = self._sref(r, -1)
+            ops.adam_multi(tab, p.shape[1], ds['consts'], base, off,
+                           schedule='deferred', n_max_uniq=[local.numel()],
+                           **self._group_args())
+        rows = sh['p'][local]
+        back, _ = all_to_all_v(rows, rcounts, sh['group'])
+        p.data[send] = back
+
     # ------------------------------------------------------------------ (de)serialise
     def state_dict(self):
         self.flush()
@@ -392,8 +492,13 @@ class FusedAdam(torch.optim.Optimizer):
         for i, p in enumerate(params):
             st = self.state.get(p, {})
             if 'exp_avg' in st:
+                m, v = st['exp_avg'], st['exp_avg_sq']
+                ds = getattr(self, '_deferred', {}).get(p)
+                if ds is not None and 'shard' in ds:   # row-sharded: the full moments
+                    m = self._gather_shard(ds, m, p.shape[0])
+                    v = self._gather_shard(ds, v, p.shape[0])
                 state[i] = {'step': torch.tensor(float(self.n_steps)),
-                            'exp_avg': st['exp_avg'], 'exp_avg_sq': st['exp_avg_sq']}
+                            'exp_avg': m, 'exp_avg_sq': v}
         groups = []
         k = 0
         for g in self.param_groups:
@@ -418,9 +523,21 @@ class FusedAdam(torch.optim.Optimizer):
         for i, st in state_dict['state'].items():
             p = params[int(i)]
             mine = self._ensure_state(p)
+            ds = getattr(self, '_deferred', {}).get(p)
+            if ds is not None and 'shard' in ds:       # this rank's rows of the full moments
+                sh = ds['shard']
+                own = sh['own'].to(st['exp_avg'].device)
+                mine['exp_avg'].copy_(st['exp_avg'][own].to(p.device))
+                mine['exp_avg_sq'].copy_(st['exp_avg_sq'][own].to(p.device))
+                sh['p'].copy_(p.data[sh['own']])
+                sh['synced'] = None
+                continue
             mine['exp_avg'].copy_(st['exp_avg'].to(p.device))
             mine['exp_avg_sq'].copy_(st['exp_avg_sq'].to(p.device))
             steps = int(float(st['step']))
         self.n_steps = steps
+        for p, ds in getattr(self, '_deferred', {}).items():
+            if 'shard' in ds:
+                ds['shard']['synced'] = self.n_steps      # the loaded p is complete
         if self._g is not None:               # graph mode: a new window at the loaded step
             self._graph_open_window()

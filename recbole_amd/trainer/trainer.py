@@ -92,6 +92,9 @@ class Trainer(AbstractTrainer):
                 and hasattr(self.model, 'deferred_tables')):
             # sparsely read embedding tables on the deferred K5 schedule (optim.py)
             self.optimizer.enable_deferred(self.model.deferred_tables())
+            if self._dp is not None and config['shard_tables'] is not False:
+                # data parallel: the deferred tables row-sharded over the ranks (optim.py)
+                self.optimizer.shard_deferred(self._dp.group)
             # any state_dict() of the model sees complete rows
             self.model.register_state_dict_pre_hook(lambda *a, **k: self.optimizer.flush())
         self.eval_type = config['eval_type']

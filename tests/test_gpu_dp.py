@@ -22,8 +22,9 @@ CASES = {
 }
 
 
-def _pipe(name, root):
+def _pipe(name, root, shard=True):
     kw = dict(CASES[name])
+    kw['shard_tables'] = shard
     if name == 'DeepFM':
         from tests.test_gpu_deepfm import _pipeline
     elif name == 'SASRec':
@@ -35,25 +36,32 @@ def _pipe(name, root):
 
 
 def _grads(model, opt):
-    """Dense view of this step's gradients: p.grad, or the deferred stash scattered."""
+    """Dense view of this step's gradients: p.grad, or the deferred stash scattered
+    (row-sharded tables: each owner's rows, summed over the ranks)."""
+    import torch.distributed as tdist
     from recbole_amd import ops
     out = {}
     for n, p in model.named_parameters():
         if p.grad is not None:
             out[n] = p.grad.detach().cpu().numpy().copy()
         elif p in getattr(opt, '_deferred', {}):
+            ds = opt._deferred[p]
             dense = torch.zeros_like(p)
-            for rows, keys, _ in opt._deferred[p]['stash']:
+            for rows, keys, tag in ds['stash']:
+                if tag == 'owned':             # local row ids of this rank's shard
+                    keys = keys * ds['shard']['G'] + ds['shard']['r']
                 ops.segment_scatter_add(rows, ops.segment_sort(keys, p.shape[0]), dense)
+            if 'shard' in ds:
+                tdist.all_reduce(dense, group=ds['shard']['group'])
             out[n] = dense.cpu().numpy()
     return out
 
 
-def _run(name, root):
+def _run(name, root, shard=True):
     """The Trainer's generic loop (trainer.py _train_epoch) with the first step's
     exchanged gradients captured."""
     from recbole_amd.trainer import Trainer
-    config, train, valid, test, model = _pipe(name, root)
+    config, train, valid, test, model = _pipe(name, root, shard)
     tr = Trainer(config, model)
     dp = tr._dp
     model.train()
@@ -75,16 +83,20 @@ def _run(name, root):
     tr.optimizer.flush()
     metrics = tr.evaluate(test, load_best_model=False) if name == 'LightGCN' else None
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
-    return total, first, sd, metrics, dp is not None
+    osd = tr.optimizer.state_dict()          # full moments (sharded: gathered)
+    sd.update({f'opt.{i}.{k}': st[k].detach().cpu().numpy() for i, st in osd['state'].items()
+               for k in ('exp_avg', 'exp_avg_sq')})
+    sharded = any('shard' in ds for ds in getattr(tr.optimizer, '_deferred', {}).values())
+    return total, first, sd, metrics, (dp is not None, sharded)
 
 
-def _worker(rank, port, name, root, q):
+def _worker(rank, port, name, root, q, shard=True):
     import torch.distributed as tdist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     tdist.init_process_group('gloo', rank=rank, world_size=2)
     try:
         torch.cuda.set_device(0)
-        q.put((rank,) + _run(name, root))
+        q.put((rank,) + _run(name, root, shard))
     except Exception as e:                      # report instead of hanging the parent
         q.put((rank, repr(e), None, None, None, None))
         raise
@@ -92,23 +104,30 @@ def _worker(rank, port, name, root, q):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize('name', ['DeepFM', 'SASRec', 'LightGCN'])
-def test_two_ranks_match_one_process(tmp_path, name):
-    ref_loss, ref_g, ref_sd, ref_metrics, dp = _run(name, str(tmp_path / 'one'))
-    assert not dp
+def _two_ranks(tmp_path, name, shard, tag):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, name, str(tmp_path / f'r{r}'), q))
+    procs = [ctx.Process(target=_worker, args=(r, port, name, str(tmp_path / f'{tag}{r}'), q,
+                                               shard))
              for r in range(2)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=240) for _ in range(2)]
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
-    for rank, loss, g, sd, metrics, dp in outs:
+    return outs
+
+
+@pytest.mark.parametrize('name', ['DeepFM', 'SASRec', 'LightGCN'])
+def test_two_ranks_match_one_process(tmp_path, name):
+    ref_loss, ref_g, ref_sd, ref_metrics, (dp, _) = _run(name, str(tmp_path / 'one'))
+    assert not dp
+    outs = _two_ranks(tmp_path, name, True, 'r')
+    for rank, loss, g, sd, metrics, flags in outs:
         assert g is not None, loss
-        assert dp
+        assert flags[0]
+        assert flags[1] == (name != 'LightGCN')     # deferred tables row-sharded
         np.testing.assert_allclose(loss, ref_loss, rtol=1e-4)
         # the exchanged gradient of the first global batch = the one-process gradient
         assert g.keys() == ref_g.keys()
@@ -124,3 +143,22 @@ def test_two_ranks_match_one_process(tmp_path, name):
             np.testing.assert_allclose(sd[k], ref_sd[k], rtol=0, atol=5e-3, err_msg=k)
         if name == 'LightGCN':
             assert metrics == ref_metrics
+
+
+@pytest.mark.parametrize('name', ['DeepFM', 'SASRec'])
+def test_row_sharded_tables_match_replicated(tmp_path, name):
+    """Row-sharded deferred tables (owner-only K5, rows fetched from owners, contribution
+    rows all-to-all'd to owners in global order) against the replicated layout after
+    an epoch, on both ranks. Each row's contributions are summed in the same order,
+    but the fixed-order reduction cuts them into 32-position chunks at absolute
+    positions of the (shorter) owner array, so a row whose contributions cross a
+    chunk boundary may round differently, and the trajectories then agree to fp32 /
+    Adam tolerance (losses to 1e-6)."""
+    sharded = _two_ranks(tmp_path, name, True, 's')
+    replicated = _two_ranks(tmp_path, name, False, 'p')
+    for (rs, ls, _, sds, _, fs), (rp, lp, _, sdp, _, fp) in zip(sharded, replicated):
+        assert fs == (True, True) and fp == (True, False), (ls, lp)
+        np.testing.assert_allclose(ls, lp, rtol=1e-6)
+        assert sds.keys() == sdp.keys()
+        for k in sdp:
+            np.testing.assert_allclose(sds[k], sdp[k], rtol=0, atol=5e-3, err_msg=k)
