@@ -307,6 +307,8 @@ def main():
     # negative sampler: the bit-exact walk (default, the headline) or the alias-table
     # fast mode (labelled NON-PARITY: i.i.d. draws of the same distribution)
     ap.add_argument('--sampler', default='walk', choices=['walk', 'alias'])
+    # diagnostic: chunk sizes after a pipeline (re)start, e.g. 2,4,8,16,32
+    ap.add_argument('--ramp', default=None)
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -335,6 +337,8 @@ def main():
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
         dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded',
         alias=args.sampler == 'alias')
+    if args.ramp:
+        step.RAMP = tuple(int(x) for x in args.ramp.split(','))
     setup_s = time.time() - t_setup
     K, W = args.steps, args.warmup
     if K < 1 or W < 0:

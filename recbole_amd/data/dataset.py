@@ -41,6 +41,48 @@ def _stable_order(keys):
     return np.argsort(keys, kind='stable')
 
 
+def _group_layout(keys):
+    """Rows grouped by key: (rows in (group first-appearance, position) order, each
+    row's group (first-appearance rank), position in its group, group sizes in
+    first-appearance order)."""
+    order = _stable_order(keys)
+    sk = keys[order]
+    starts = np.flatnonzero(np.r_[True, sk[1:] != sk[:-1]])
+    tot = np.diff(np.r_[starts, len(sk)]).astype(np.int64)
+    gperm = np.argsort(order[starts], kind='stable')          # groups by first appearance
+    grank = np.empty(len(tot), dtype=np.int64)
+    grank[gperm] = np.arange(len(tot))
+    grp = np.repeat(np.arange(len(tot)), tot)
+    pos = np.arange(len(sk)) - np.repeat(starts, tot)
+    goff = np.empty(len(tot), dtype=np.int64)
+    goff[gperm] = np.r_[0, np.cumsum(tot[gperm])[:-1]]
+    newpos = goff[grp] + pos
+    rows = np.empty(len(sk), dtype=np.int64)
+    rows[newpos] = order
+    g_of = np.empty(len(sk), dtype=np.int64)
+    g_of[newpos] = grank[grp]
+    p_of = np.empty(len(sk), dtype=np.int64)
+    p_of[newpos] = pos
+    return rows, g_of, p_of, tot[gperm]
+
+
+def _grouped_leave_one_out(keys, leave_one_num):
+    """leave_one_out (dataset.py:1317-1337), vectorised: per group (first-appearance
+    order) legal = min(leave_one_num, size - 1); the first size - legal rows go to
+    part 0 and the last `legal` rows to parts P - legal .. P - 1 (P = leave_one_num + 1),
+    in row order."""
+    keys = np.asarray(keys)
+    P = leave_one_num + 1
+    if len(keys) == 0:
+        return [np.zeros(0, dtype=np.int64) for _ in range(P)]
+    rows, g, pos, sizes = _group_layout(keys)
+    size = sizes[g]
+    legal = np.minimum(leave_one_num, size - 1)
+    pr = size - legal
+    part = np.where(pos < pr, 0, P - legal + (pos - pr))
+    return [rows[part == q] for q in range(P)]
+
+
 def _grouped_ratio_split(keys, ratios):
     """split_by_ratio with group_by (dataset.py:1281-1315), vectorised: groups in
     first-appearance order, rows of a group in their current order, and group g's
@@ -710,16 +752,7 @@ class Dataset(object):
     def leave_one_out(self, group_by, leave_one_num=1):
         if group_by is None:
             raise ValueError('leave one out strategy require a group field')
-        nxt = [[] for _ in range(leave_one_num + 1)]
-        for g in self._grouped_index(self.inter_feat[group_by].numpy()):
-            g = list(g)
-            tot = len(g)
-            legal = min(leave_one_num, tot - 1)
-            pr = tot - legal
-            nxt[0].extend(g[:pr])
-            for i in range(legal):
-                nxt[-legal + i].append(g[pr])
-                pr += 1
+        nxt = _grouped_leave_one_out(self.inter_feat[group_by].numpy(), leave_one_num)
         self._drop_unused_col()
         return [self.copy(self.inter_feat[torch.as_tensor(np.asarray(ix, dtype=np.int64))])
                 for ix in nxt]

@@ -87,7 +87,9 @@ def _worker(rank, port, q):
     gU, gI = _rows(EU, EI, users, items[:G * B], items[G * B:], cg)
     sumU = _grouped(gU, users, NU)
     sumI = _grouped(gI.reshape(-1, D), items, NI)
-    q.put((rank, sumU, sumI, lay.gathered_losses(buf).reshape(-1).clone()))
+    # by value (numpy): a torch tensor would travel as a shared-memory handle that
+    # dies with this process
+    q.put((rank, sumU.numpy(), sumI.numpy(), lay.gathered_losses(buf).reshape(-1).numpy()))
     tdist.destroy_process_group()
 
 
@@ -121,6 +123,6 @@ def test_two_rank_exchange_equals_global_batch():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, sumU, sumI, losses in got:
-        assert torch.equal(sumU, refU), rank
-        assert torch.equal(sumI, refI), rank
-        assert torch.equal(losses, loss), rank
+        assert np.array_equal(sumU, refU.numpy()), rank
+        assert np.array_equal(sumI, refI.numpy()), rank
+        assert np.array_equal(losses, loss.numpy()), rank

@@ -127,3 +127,37 @@ def test_factorize_pieces_matches_pandas():
                                                   other, other[::-1]]))
     assert np.array_equal(got_ids, exp_ids)
     assert list(got_u) == list(exp_u)
+
+
+def _loop_loo(keys, leave_one_num):
+    groups, seen = {}, []
+    for idx, k in enumerate(keys.tolist()):
+        if k not in groups:
+            groups[k] = []
+            seen.append(k)
+        groups[k].append(idx)
+    nxt = [[] for _ in range(leave_one_num + 1)]
+    for k in seen:
+        g = groups[k]
+        tot = len(g)
+        legal = min(leave_one_num, tot - 1)
+        pr = tot - legal
+        nxt[0].extend(g[:pr])
+        for i in range(legal):
+            nxt[-legal + i].append(g[pr])
+            pr += 1
+    return [np.asarray(x, dtype=np.int64) for x in nxt]
+
+
+@pytest.mark.parametrize('leave_one_num', [1, 2, 3])
+def test_grouped_leave_one_out_matches_loop(leave_one_num):
+    from recbole_amd.data.dataset import _grouped_leave_one_out
+    rng = np.random.default_rng(leave_one_num)
+    sizes = np.r_[np.arange(1, 8), rng.integers(1, 60, 400)]
+    keys = np.repeat(rng.permutation(len(sizes)) * 3 + 1, sizes)
+    keys = keys[rng.permutation(len(keys))]
+    got = _grouped_leave_one_out(keys, leave_one_num)
+    exp = _loop_loo(keys, leave_one_num)
+    assert len(got) == len(exp)
+    for a, b in zip(got, exp):
+        assert np.array_equal(a, b)

@@ -1,5 +1,7 @@
 set -o pipefail
-timeout -k 10 300 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval > gpurun_out/bs1.log 2>&1 && \
-timeout -k 10 300 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval > gpurun_out/bs2.log 2>&1 && \
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_chain.py tests/test_gpu_e2e.py tests/test_gpu_shard.py tests/test_gpu_distributed.py tests/test_gpu_alias.py > gpurun_out/t.log 2>&1 && \
-TRACE_OPTS=--hip-runtime-trace bash tools/trace_short.sh
+for r in 4,8,16,32 2,4,8,16,32 1,2,4,8,16,32 2,6,12,24,48 3,6,12,24; do
+  for k in 1 2; do
+    timeout -k 10 200 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval --ramp $r > gpurun_out/ramp.log 2>&1 || exit 3
+    echo "$r $(grep '^{' gpurun_out/ramp.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["config"]["chunk_plan_timed"])')" | tee -a gpurun_out/ramps.txt
+  done
+done
