@@ -371,6 +371,12 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
 
+/* n device-to-device copies (src[i] -> dst[i], bytes[i]; host arrays of device
+ * pointers) in one launch per 96 copies: the per-step copy of a batch's columns into
+ * a captured training graph's static inputs (one launch instead of one per column). */
+int mirec_copy_many(const void* const* src, void* const* dst, const int64_t* bytes, int n,
+                    void* stream);
+
 /* Copy n_bytes (a multiple of 4, at most a few KiB: e.g. the mirec_ctx_field
  * descriptors of a batch) from host memory to dst_dev through kernel arguments:
  * stream-ordered, and recorded BY VALUE when the stream is being captured into a

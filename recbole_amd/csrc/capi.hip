@@ -124,6 +124,64 @@ __global__ __launch_bounds__(256) void write_bytes_kernel(uint32_t* __restrict__
 }
 }  // namespace mirec
 
+// Many device-to-device copies in one launch (the per-step copy of a batch's columns
+// into a captured graph's static inputs): up to kCopyDescs (src, dst, bytes) per
+// launch, passed by value; block b copies slice b % per of copy b / per ... with
+// 16-B vectors when src, dst and the size allow, bytes otherwise.
+constexpr int kCopyDescs = 96;
+struct CopyDescs {
+  const char* src[kCopyDescs];
+  char* dst[kCopyDescs];
+  int64_t bytes[kCopyDescs];
+};
+
+__global__ __launch_bounds__(256) void copy_many_kernel(CopyDescs d, int n, int blocks_per) {
+  const int c = blockIdx.x / blocks_per;
+  if (c >= n) return;
+  const int64_t nb = d.bytes[c];
+  const char* __restrict__ src = d.src[c];
+  char* __restrict__ dst = d.dst[c];
+  const int64_t t0 = (int64_t)(blockIdx.x % blocks_per) * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)blocks_per * blockDim.x;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t nv = nb / 16;
+    const int4* __restrict__ s4 = reinterpret_cast<const int4*>(src);
+    int4* __restrict__ d4 = reinterpret_cast<int4*>(dst);
+    for (int64_t i = t0; i < nv; i += stride) d4[i] = s4[i];
+    for (int64_t i = nv * 16 + t0; i < nb; i += stride) dst[i] = src[i];
+  } else {
+    for (int64_t i = t0; i < nb; i += stride) dst[i] = src[i];
+  }
+}
+
+extern "C" int mirec_copy_many(const void* const* src, void* const* dst, const int64_t* bytes,
+                               int n, void* stream) {
+  if (n < 0 || (n > 0 && (!src || !dst || !bytes))) {
+    set_error("mirec_copy_many: bad arguments");
+    return -1;
+  }
+  for (int off = 0; off < n; off += kCopyDescs) {
+    const int m = std::min(kCopyDescs, n - off);
+    CopyDescs d;
+    int64_t mx = 0;
+    for (int i = 0; i < m; ++i) {
+      if (bytes[off + i] < 0 || (bytes[off + i] && (!src[off + i] || !dst[off + i]))) {
+        set_error("mirec_copy_many: bad descriptor %d", off + i);
+        return -1;
+      }
+      d.src[i] = (const char*)src[off + i];
+      d.dst[i] = (char*)dst[off + i];
+      d.bytes[i] = bytes[off + i];
+      mx = std::max(mx, bytes[off + i]);
+    }
+    // blocks per copy: enough 16-B lanes for the largest copy, at most 64
+    const int per = (int)std::max<int64_t>(1, std::min<int64_t>(64, (mx / 16 + 255) / 256));
+    hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)(m * per)), dim3(256), 0,
+                       (hipStream_t)stream, d, m, per);
+  }
+  return launch_status("mirec_copy_many");
+}
+
 extern "C" int mirec_write_bytes(void* dst_dev, const void* src_host, size_t n_bytes,
                                  void* stream) {
   if ((n_bytes && (!dst_dev || !src_host)) || (n_bytes & 3) || ((uintptr_t)dst_dev & 3)) {

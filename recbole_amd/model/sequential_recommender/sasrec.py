@@ -152,6 +152,12 @@ class _SampledSoftmaxFn(torch.autograd.Function):
 
 class SASRec(SequentialRecommender):
 
+    # the training step has no host synchronisation or host-side branching on device
+    # values (K9a / K9b / K3 launches with host-known sizes, deferred catch-ups on the
+    # device step counter, dropout through torch's capture-aware generator): the
+    # trainer may capture it in a HIP graph (trainer/graph_step.py)
+    graph_step_safe = True
+
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
         self.n_layers = config['n_layers']

@@ -102,6 +102,25 @@ def sample_walk_segments(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: 
     return out
 
 
+def copy_many(dst: list, src: list) -> None:
+    """dst[i].copy_(src[i]) for same-size contiguous device tensors, in one launch
+    (mirec_copy_many)."""
+    n = len(dst)
+    if n == 0:
+        return
+    S = (ctypes.c_void_p * n)()
+    D = (ctypes.c_void_p * n)()
+    N = (ctypes.c_int64 * n)()
+    for i, (d, s) in enumerate(zip(dst, src)):
+        if not (d.is_cuda and s.is_cuda and d.is_contiguous() and s.is_contiguous()):
+            raise NativeError("copy_many: contiguous device tensors only")
+        nb = d.numel() * d.element_size()
+        if s.numel() * s.element_size() != nb:
+            raise ValueError(f"copy_many: size mismatch at {i}")
+        S[i], D[i], N[i] = s.data_ptr(), d.data_ptr(), nb
+    check(lib().mirec_copy_many(S, D, N, n, stream_handle()), "mirec_copy_many")
+
+
 def host_counting_order(keys, key_space: int) -> np.ndarray:
     """Stable sort permutation of integer keys in [0, key_space) (host, O(n))."""
     keys = np.ascontiguousarray(keys, dtype=np.int64)

@@ -235,12 +235,20 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
     if ADAM_MODE == 'deferred':
         opt.enable_deferred(model.deferred_tables())
     it = [0]
+    gs = None
+    if GRAPH_STEP:                 # the Trainer's captured step (trainer/graph_step.py)
+        from recbole_amd.trainer.graph_step import GraphedTrainStep
+        gs = GraphedTrainStep(model, opt)
 
     def step():
         b = batches[it[0] % n_batches]
         it[0] += 1
+        # the data side (the loader's K4 walk of 100 negatives per sequence) stays eager
         neg = ops.sample_walk(random_list, pr, b['user_id'], n_neg, None, None, 1_000_000, False)
         b.interaction['neg_item_id'] = neg
+        if gs is not None:
+            gs.step(b)
+            return
         opt.zero_grad()
         loss = model.calculate_loss(b)
         loss.backward()
@@ -393,7 +401,7 @@ def main():
     ap.add_argument('--out', default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--adam-mode', default='deferred', choices=['deferred', 'streamed'])
-    ap.add_argument('--eager-step', action='store_true', help='C4 without the captured step')
+    ap.add_argument('--eager-step', action='store_true', help='C3 / C4 without the captured step')
     args = ap.parse_args()
     global CPU_BASELINE, ADAM_MODE, GRAPH_STEP
     CPU_BASELINE = not args.no_cpu_baseline
