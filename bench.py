@@ -309,6 +309,8 @@ def main():
     ap.add_argument('--sampler', default='walk', choices=['walk', 'alias'])
     # diagnostic: chunk sizes after a pipeline (re)start, e.g. 2,4,8,16,32
     ap.add_argument('--ramp', default=None)
+    # diagnostic: steps between deferred-Adam full flushes (default FLUSH_EVERY)
+    ap.add_argument('--flush-every', type=int, default=None)
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -339,6 +341,8 @@ def main():
         alias=args.sampler == 'alias')
     if args.ramp:
         step.RAMP = tuple(int(x) for x in args.ramp.split(','))
+    if args.flush_every:
+        step.FLUSH_EVERY = args.flush_every
     setup_s = time.time() - t_setup
     K, W = args.steps, args.warmup
     if K < 1 or W < 0:
@@ -349,7 +353,9 @@ def main():
     # K2 grouping of every timed step (the first timed chunk's serially, the rest on
     # the prep stream beside the model side, as in steady state).
     M = step.C                                 # per-kernel measurement window after it
-    nb = step.begin_epoch(cuts=(W, W + K, W + K + M), hold_prep_from=W)
+    # every row complete at the end of the timed region and of the measurement window
+    nb = step.begin_epoch(cuts=(W, W + K, W + K + M), hold_prep_from=W,
+                          flush_at=(W + K, W + K + M))
     if W + K + M > nb:
         raise SystemExit(f'steps+warmup exceed one epoch ({nb} batches)')
     step.run_batches(0, W)

@@ -153,6 +153,13 @@ class FusedBPRTrainStep(object):
     CHUNK = 64
     SLOTS = 3                     # chunk buffers in flight (walk, grouping, model)
     RAMP = (4, 8, 16, 32)         # chunk sizes after a (re)start of the prep pipeline
+    # deferred schedule: steps between full-table flushes (every row complete;
+    # parameters are also complete at every epoch end / sync_params()). Rarer
+    # flushes let idle rows reach the cheap replay regime (adam.hip
+    # p_update_vanishes) but lengthen the lags the per-step kernel replays when a
+    # row is touched, and its slowest wave sets the step time: measured on C2 (64
+    # warm-up + 256 steps) 18.0 M positives/s at 64, 12.4 M at 256, 12.3 M at 1,024.
+    FLUSH_EVERY = 64
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None):
@@ -247,15 +254,17 @@ class FusedBPRTrainStep(object):
 
     def _chunk_flags(self, plan):
         """(entry, flush) per chunk of the deferred schedule: a chunk flushes every
-        row at its end once C or more steps have run since the last flush (and
-        before a ragged batch / the end); a chunk after one that did not flush
+        row at its end once max(C, FLUSH_EVERY) or more steps have run since the last
+        flush (and before a ragged batch / the end); a chunk after one that did not flush
         starts with an entry catch-up of the rows its first batch reads."""
         flags, since = [], 0
-        for i, (_, nb, Bc) in enumerate(plan):
+        at = getattr(self, '_flush_at', set())
+        for i, (b0, nb, Bc) in enumerate(plan):
             entry = since > 0
             since += nb
             nxt_full = i + 1 < len(plan) and plan[i + 1][2] == self.Bg
-            flush = since >= self.C or not nxt_full
+            flush = (since >= max(self.C, self.FLUSH_EVERY) or not nxt_full
+                     or b0 + nb in at)
             if flush:
                 since = 0
             flags.append((entry, flush))
@@ -555,12 +564,13 @@ class FusedBPRTrainStep(object):
         return g
 
     # ------------------------------------------------------------------ epoch API
-    def begin_epoch(self, cuts=(), hold_prep_from=None):
+    def begin_epoch(self, cuts=(), hold_prep_from=None, flush_at=()):
         """Shuffle (reference order of RNG use), stage the epoch's Adam constants,
         and start preparing the first chunks; returns the number of (global) batches.
 
         cuts: batch indices at which a chunk must start (bench.py cuts at the
-        warm-up / timed / measurement boundaries). hold_prep_from: batch index
+        warm-up / timed / measurement boundaries). flush_at: batch indices (chunk
+        ends) where the deferred schedule also completes every row. hold_prep_from: batch index
         whose chunk (and every later one) is not prepared until release_prep() —
         so a timed region that starts there contains its own chunks' sampler walk
         and grouping."""
@@ -592,6 +602,7 @@ class FusedBPRTrainStep(object):
                 ops.zero_state_marks(m, v, last, self._adam_args[3])
         ramps = (0,) if hold_prep_from is None else (0, int(hold_prep_from))
         self._plan, self._plan_starts = self._chunks(cuts, ramps), None
+        self._flush_at = set(int(b) for b in flush_at)
         self._flags = self._chunk_flags(self._plan)
         if self.use_graph:                      # capture up front: capture synchronizes
             S = len(self.slots)
@@ -995,10 +1006,10 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         super()._finish(c0, n_steps, Bc, stream)
 
     # ------------------------------------------------------------ epoch API
-    def begin_epoch(self, cuts=(), hold_prep_from=None):
+    def begin_epoch(self, cuts=(), hold_prep_from=None, flush_at=()):
         self.status.zero_()
         self._load_shards()
-        return super().begin_epoch(cuts=cuts, hold_prep_from=hold_prep_from)
+        return super().begin_epoch(cuts=cuts, hold_prep_from=hold_prep_from, flush_at=flush_at)
 
     def end_epoch(self, n_done=None):
         losses = super().end_epoch(n_done)
