@@ -236,6 +236,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
           }
         }
       }
+      WALK_MARK(3, tp);                       // round 0 values + membership (thread 0)
       // exclusive scan of the packed per-j counts (each field < 2^16: Kb <= 1024)
       const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
       uint64_t incl = packed;
@@ -263,6 +264,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
         base_j += cj;
       }
       nrej = base_j;
+      WALK_MARK(4, tp);                       // round 0 scan
     } else
     for (int64_t base = 0; base < total; base += (int64_t)kSampThreads * kPer) {
       const int64_t t0 = base + (int64_t)threadIdx.x * kPer;

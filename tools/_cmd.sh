@@ -1,7 +1,9 @@
 set -o pipefail
-for c in 32 48 64 96; do
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-eval --chunk $c > gpurun_out/fe.log 2>&1 || { tail -20 gpurun_out/fe.log; exit 3; }
-  echo "default C=$c $(grep '^{' gpurun_out/fe.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["us_per_step"])')" | tee -a gpurun_out/fc.txt
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-eval --chunk $c --warmup 5 --steps 20 > gpurun_out/fe.log 2>&1 || { tail -20 gpurun_out/fe.log; exit 3; }
-  echo "short C=$c $(grep '^{' gpurun_out/fe.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" | tee -a gpurun_out/fc.txt
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_kernels.py tests/test_gpu_chain.py tests/test_gpu_popularity.py tests/test_gpu_fixtures.py tests/test_gpu_sampled_eval.py > gpurun_out/wt.log 2>&1 || { tail -30 gpurun_out/wt.log; exit 3; }
+tail -2 gpurun_out/wt.log
+for k in 1 2 3; do
+timeout -k 10 200 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval > gpurun_out/bs.log 2>&1 || exit 4
+grep '^{' gpurun_out/bs.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("short", d["value"])'
 done
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-eval > gpurun_out/bs.log 2>&1 || exit 5
+grep '^{' gpurun_out/bs.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("default", d["value"])'

@@ -47,7 +47,11 @@ def main():
         f(buf, 0)
         us = e0.elapsed_time(e1) * 1e3 / nb
         v = list(buf)
-        tot = sum(v[:3]) or 1
+        tot = (sum(v[:5]) or 1)
+        ck = us / (tot / nb)                  # us per clock (the batch time covers every phase)
+        print(f'   us/batch: setup {v[0] / nb * ck:.2f}, round-0 values+membership '
+              f'{v[3] / nb * ck:.2f}, round-0 scan {v[4] / nb * ck:.2f}, round-0 tail '
+              f'{v[1] / nb * ck:.2f}, refills {v[2] / nb * ck:.2f}', flush=True)
         print(f'rep {rep}: {us:.2f} us/batch; clocks/batch setup {v[0]/nb:.0f} round0 {v[1]/nb:.0f} '
               f'refill {v[2]/nb:.0f} (frac {v[0]/tot:.2f}/{v[1]/tot:.2f}/{v[2]/tot:.2f}); per batch: '
               f'pending after round 0 {v[8]/nb:.1f}, wide rounds {v[9]/nb:.2f}, tail entry '
