@@ -584,6 +584,21 @@ int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const f
                                const float* gamma, const float* mean, const float* rstd,
                                const float* grad_out, float* dx, float* ditem,
                                float* part_gamma, float* part_beta, void* stream);
+/* K9c  LayerNorm(a + b) of the transformer blocks' residual connections (layers.py
+ * MultiHeadAttention / FeedForward, reference layers.py:338-552) in one pass, and its
+ * backward (dx = d(a + b), per-block dgamma / dbeta partials as K9a, summed with
+ * mirec_colsum_f32). a, b, out, grad_out, dx: [n, d] rows; d in {32,64,128,256}. */
+int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                         const float* gamma, const float* beta, float eps, float* out,
+                         float* mean, float* rstd, void* stream);
+/* GELU (erf form) of the feed-forward block, forward and backward, elementwise. */
+int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream);
+int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, float* dx, void* stream);
+int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                         const float* gamma, const float* mean, const float* rstd,
+                         const float* grad_out, float* dx, float* part_gamma, float* part_beta,
+                         void* stream);
+
 /* K9c: sampled evaluation (uni-N) of a sequential model — rank[q] = number of the
  * m sampled items neg[q*m .. q*m+m) (row-major: the sampler's per-row walk order)
  * whose score <seq_out[q], E[i]> is greater than or equal to the positive's (exact

@@ -141,6 +141,132 @@ __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
   }
 }
 
+// K9c  residual + LayerNorm of the transformer blocks (layers.py MultiHeadAttention /
+//   FeedForward: LayerNorm(hidden + input_tensor), reference layers.py:338-552):
+//   y = LayerNorm(a + b) in one pass (the sum is never written), and its backward
+//   from the saved mean / rstd with x = a + b recomputed; same arithmetic as K9a.
+template <int D>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(
+    const float* __restrict__ A, const float* __restrict__ Bv, int64_t n_rows,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    float* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int LPR = D / 4, GPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane % LPR;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t r = wave * GPW + g;
+  if (r >= n_rows) return;
+  const float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
+  const float4 b = reinterpret_cast<const float4*>(Bv + r * D)[l];
+  float4 x = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  const float mean = lane_group_sum<LPR>(sum4(x)) * (1.0f / D);
+  float4 c = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+  const float var = lane_group_sum<LPR>(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) *
+                    (1.0f / D);
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+  const float4 bt = reinterpret_cast<const float4*>(beta)[l];
+  float4 y;
+  y.x = c.x * rstd * gm.x + bt.x;
+  y.y = c.y * rstd * gm.y + bt.y;
+  y.z = c.z * rstd * gm.z + bt.z;
+  y.w = c.w * rstd * gm.w + bt.w;
+  reinterpret_cast<float4*>(out + r * D)[l] = y;
+  if (l == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void add_ln_bwd_kernel(
+    const float* __restrict__ A, const float* __restrict__ Bv, int64_t n_rows,
+    const float* __restrict__ gamma, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gy, float* __restrict__ dx,
+    float* __restrict__ part_gamma, float* __restrict__ part_beta) {
+  constexpr int LPR = D / 4, GPW = 64 / LPR;
+  __shared__ float4 red_g[4 * GPW][LPR];
+  __shared__ float4 red_b[4 * GPW][LPR];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane / LPR, l = lane % LPR;
+  const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+  float4 ag = make_float4(0.f, 0.f, 0.f, 0.f), ab = ag;
+  const int64_t base = (int64_t)blockIdx.x * kLnRowsPerBlock;
+  for (int i = w * GPW + g; i < kLnRowsPerBlock; i += 4 * GPW) {
+    const int64_t r = base + i;
+    if (r >= n_rows) break;
+    const float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
+    const float4 b = reinterpret_cast<const float4*>(Bv + r * D)[l];
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float4 xh;
+    xh.x = (a.x + b.x - mean) * rstd;
+    xh.y = (a.y + b.y - mean) * rstd;
+    xh.z = (a.z + b.z - mean) * rstd;
+    xh.w = (a.w + b.w - mean) * rstd;
+    const float4 gv = reinterpret_cast<const float4*>(gy + r * D)[l];
+    const float4 gg = make_float4(gv.x * gm.x, gv.y * gm.y, gv.z * gm.z, gv.w * gm.w);
+    const float m1 = lane_group_sum<LPR>(sum4(gg)) * (1.0f / D);
+    const float m2 =
+        lane_group_sum<LPR>(gg.x * xh.x + gg.y * xh.y + gg.z * xh.z + gg.w * xh.w) *
+        (1.0f / D);
+    float4 o;
+    o.x = rstd * (gg.x - m1 - xh.x * m2);
+    o.y = rstd * (gg.y - m1 - xh.y * m2);
+    o.z = rstd * (gg.z - m1 - xh.z * m2);
+    o.w = rstd * (gg.w - m1 - xh.w * m2);
+    reinterpret_cast<float4*>(dx + r * D)[l] = o;
+    ag.x += gv.x * xh.x;
+    ag.y += gv.y * xh.y;
+    ag.z += gv.z * xh.z;
+    ag.w += gv.w * xh.w;
+    ab.x += gv.x;
+    ab.y += gv.y;
+    ab.z += gv.z;
+    ab.w += gv.w;
+  }
+  red_g[w * GPW + g][l] = ag;
+  red_b[w * GPW + g][l] = ab;
+  __syncthreads();
+  if (threadIdx.x < LPR) {
+    float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
+    for (int q = 0; q < 4 * GPW; ++q) {
+      const float4 a = red_g[q][threadIdx.x], b = red_b[q][threadIdx.x];
+      sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
+      sb.x += b.x; sb.y += b.y; sb.z += b.z; sb.w += b.w;
+    }
+    reinterpret_cast<float4*>(part_gamma + (int64_t)blockIdx.x * D)[threadIdx.x] = sg;
+    reinterpret_cast<float4*>(part_beta + (int64_t)blockIdx.x * D)[threadIdx.x] = sb;
+  }
+}
+
+// GELU of the feed-forward block (layers.py FeedForward.gelu, erf form):
+//   y = x * 0.5 * (1 + erf(x / sqrt(2)))   (torch's op order; x / sqrt(2) as its
+//   scalar division, multiplication by the reciprocal), and
+//   dx = g * (0.5 * (1 + erf(u)) + x * exp(-u^2) / sqrt(2 pi)),  u = x / sqrt(2).
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const float* __restrict__ x,
+                                                       int64_t n, float* __restrict__ y) {
+  const float rs2 = (float)(1.0 / 1.4142135623730951);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    y[i] = v * 0.5f * (1.0f + erff(v * rs2));
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ g, int64_t n,
+                                                       float* __restrict__ dx) {
+  const float rs2 = (float)(1.0 / 1.4142135623730951);
+  const float k = (float)(0.3989422804014327);      // 1 / sqrt(2 pi)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    const float u = v * rs2;
+    dx[i] = g[i] * (0.5f * (1.0f + erff(u)) + v * k * expf(-u * u));
+  }
+}
+
 // K9b. items: pos [B] and negs [N*B] (layout j*B + b, the sampler's).
 template <int D>
 __global__ __launch_bounds__(256) void sampled_softmax_kernel(
@@ -274,6 +400,93 @@ extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_ite
   }
 #undef MIREC_LNB
   return launch_status("mirec_seq_embed_ln_bwd_f32");
+}
+
+extern "C" int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                    const float* gamma, const float* beta, float eps, float* out,
+                                    float* mean, float* rstd, void* stream) {
+  if (n == 0) return 0;
+  if (!a || !b || !gamma || !beta || !out || !mean || !rstd || n < 0) {
+    set_error("mirec_add_ln_fwd_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+#define MIREC_ALF(DD)                                                                        \
+  case DD: {                                                                                 \
+    constexpr int GPW = 64 / (DD / 4);                                                       \
+    const int64_t waves = (n + GPW - 1) / GPW;                                               \
+    hipLaunchKernelGGL(add_ln_fwd_kernel<DD>, dim3((unsigned)((waves + 3) / 4)), dim3(256),  \
+                       0, st, a, b, n, gamma, beta, eps, out, mean, rstd);                   \
+  } break;
+  switch (d) {
+    MIREC_ALF(32)
+    MIREC_ALF(64)
+    MIREC_ALF(128)
+    MIREC_ALF(256)
+    default:
+      set_error("mirec_add_ln_fwd_f32: hidden size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_ALF
+  return launch_status("mirec_add_ln_fwd_f32");
+}
+
+extern "C" int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                    const float* gamma, const float* mean, const float* rstd,
+                                    const float* grad_out, float* dx, float* part_gamma,
+                                    float* part_beta, void* stream) {
+  if (n == 0) return 0;
+  if (!a || !b || !gamma || !mean || !rstd || !grad_out || !dx || !part_gamma || !part_beta ||
+      n < 0) {
+    set_error("mirec_add_ln_bwd_f32: bad arguments");
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grd((unsigned)mirec_seq_embed_ln_partials(n));
+#define MIREC_ALB(DD)                                                                        \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(add_ln_bwd_kernel<DD>, grd, dim3(256), 0, st, a, b, n, gamma, mean,   \
+                       rstd, grad_out, dx, part_gamma, part_beta);                           \
+    break;
+  switch (d) {
+    MIREC_ALB(32)
+    MIREC_ALB(64)
+    MIREC_ALB(128)
+    MIREC_ALB(256)
+    default:
+      set_error("mirec_add_ln_bwd_f32: hidden size %d not in {32,64,128,256}", d);
+      return -1;
+  }
+#undef MIREC_ALB
+  return launch_status("mirec_add_ln_bwd_f32");
+}
+
+static unsigned elem_grid(int64_t n) {
+  const int64_t g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 256 * 32 ? 256 * 32 : g));
+}
+
+extern "C" int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream) {
+  if (n == 0) return 0;
+  if (!x || !y || n < 0) {
+    set_error("mirec_gelu_fwd_f32: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(elem_grid(n)), dim3(256), 0, (hipStream_t)stream, x,
+                     n, y);
+  return launch_status("mirec_gelu_fwd_f32");
+}
+
+extern "C" int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, float* dx,
+                                  void* stream) {
+  if (n == 0) return 0;
+  if (!x || !g || !dx || n < 0) {
+    set_error("mirec_gelu_bwd_f32: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(elem_grid(n)), dim3(256), 0, (hipStream_t)stream, x,
+                     g, n, dx);
+  return launch_status("mirec_gelu_bwd_f32");
 }
 
 extern "C" int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table,

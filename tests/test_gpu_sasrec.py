@@ -4,6 +4,8 @@ oracle's torch-CPU restatement (sasrec.py:25-158, layers.py:338-552), dropout 0.
 Tolerances: fp32 1e-4 relative on losses and outputs (north_star); gradients
 1e-4 relative + 1e-6 absolute (the transformer in between is the same op
 sequence on both sides)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -216,3 +218,34 @@ def test_fused_sampled_eval_matches_generic(tmp_path):
     valid.pr = 0
     tr.evaluate(valid, load_best_model=False)           # the fused path end to end
     assert sm.random_pr == pr_generic
+
+
+@pytest.mark.parametrize('d', [32, 64, 128, 256])
+def test_add_layernorm_and_gelu_match_torch(dev, d):
+    """K9c LayerNorm(a + b) forward / backward and the GELU kernels against torch
+    fp32 (nn.LayerNorm over the materialised sum; the erf formula of layers.py)."""
+    from recbole_amd.model.layers import _AddLNFn, _GeluFn
+    g = torch.Generator(device='cpu').manual_seed(d)
+    n = 3000
+    a = torch.randn(n, d, generator=g).to(dev).requires_grad_()
+    b = torch.randn(n, d, generator=g).to(dev).requires_grad_()
+    ln = torch.nn.LayerNorm(d, eps=1e-12).to(dev)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(d, generator=g))
+        ln.bias.copy_(torch.randn(d, generator=g))
+    gy = torch.randn(n, d, generator=g).to(dev)
+    y = _AddLNFn.apply(a, b, ln.weight, ln.bias, 1e-12)
+    ga, gb, gw, gbias = torch.autograd.grad(y, (a, b, ln.weight, ln.bias), gy)
+    a2, b2 = a.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    y2 = ln(a2 + b2)
+    ra, rb, rw, rbias = torch.autograd.grad(y2, (a2, b2, ln.weight, ln.bias), gy)
+    for got, ref in ((y, y2), (ga, ra), (gb, rb), (gw, rw), (gbias, rbias)):
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+    x = (torch.randn(n, d, generator=g) * 3).to(dev).requires_grad_()
+    yg = _GeluFn.apply(x)
+    (gx,) = torch.autograd.grad(yg, x, gy)
+    x2 = x.detach().clone().requires_grad_()
+    yr = x2 * 0.5 * (1.0 + torch.erf(x2 / math.sqrt(2.0)))
+    (rx,) = torch.autograd.grad(yr, x2, gy)
+    torch.testing.assert_close(yg, yr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gx, rx, rtol=1e-4, atol=1e-5)
