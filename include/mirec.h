@@ -584,7 +584,7 @@ int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const f
                                const float* gamma, const float* mean, const float* rstd,
                                const float* grad_out, float* dx, float* ditem,
                                float* part_gamma, float* part_beta, void* stream);
-/* K9c  LayerNorm(a + b) of the transformer blocks' residual connections (layers.py
+/* K9d  LayerNorm(a + b) of the transformer blocks' residual connections (layers.py
  * MultiHeadAttention / FeedForward, reference layers.py:338-552) in one pass, and its
  * backward (dx = d(a + b), per-block dgamma / dbeta partials as K9a, summed with
  * mirec_colsum_f32). a, b, out, grad_out, dx: [n, d] rows; d in {32,64,128,256}. */

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void segment_scatter_add_kernel(
 // ---------------------------------------------------------------------------
 // Large single-batch sorts (n > kLdsMax: the autograd paths of the context and
 // sequential models group 10^5..10^6 contributions per step). Device-wide
-// stable LSD radix sort, 4-bit digits, one tile of kRadixTile keys per block:
+// stable LSD radix sort, 5-bit digits, one tile of kRadixTile keys per block:
 //   upsweep   per-tile digit histogram            -> hist[digit * n_tiles + tile]
 //   scan      exclusive scan of hist (digit-major) -> global destination bases
 //   downsweep stable in-tile ranking (blocked layout, per-thread digit counts
@@ -280,7 +280,8 @@ __global__ __launch_bounds__(256) void segment_scatter_add_kernel(
 constexpr int kRadixThreads = 256;
 constexpr int kRadixIpt = 8;
 constexpr int kRadixTile = kRadixThreads * kRadixIpt;
-constexpr int kRadixBins = 16;
+constexpr int kRadixBits = 5;     // digit width: 5 passes for 25-bit key spaces (was 4 bits, 7)
+constexpr int kRadixBins = 1 << kRadixBits;
 
 __global__ __launch_bounds__(kRadixThreads) void radix_init_kernel(
     const int64_t* __restrict__ keys, int n, int32_t* __restrict__ k32, int32_t* __restrict__ v32) {
@@ -448,9 +449,9 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
   int g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(radix_init_kernel, dim3(g), dim3(256), 0, st, keys, n, kA, vA);
-  const int passes = nbits == 0 ? 0 : (nbits + 3) / 4;
+  const int passes = nbits == 0 ? 0 : (nbits + kRadixBits - 1) / kRadixBits;
   for (int p = 0; p < passes; ++p) {
-    const int shift = 4 * p;
+    const int shift = kRadixBits * p;
     hipLaunchKernelGGL(radix_upsweep_kernel, dim3(tiles), dim3(kRadixThreads), 0, st, kA, n,
                        shift, tiles, hist);
     hipLaunchKernelGGL(scan_exclusive_kernel, dim3(1), dim3(1024), 0, st, hist,

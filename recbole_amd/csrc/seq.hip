@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
   }
 }
 
-// K9c  residual + LayerNorm of the transformer blocks (layers.py MultiHeadAttention /
+// K9d  residual + LayerNorm of the transformer blocks (layers.py MultiHeadAttention /
 //   FeedForward: LayerNorm(hidden + input_tensor), reference layers.py:338-552):
 //   y = LayerNorm(a + b) in one pass (the sum is never written), and its backward
 //   from the saved mean / rstd with x = a + b recomputed; same arithmetic as K9a.

@@ -194,7 +194,7 @@ def linear(module, x):
 
 
 class _AddLNFn(torch.autograd.Function):
-    """LayerNorm(a + b) (K9c, mirec_add_ln_fwd/bwd_f32): the residual sum is never
+    """LayerNorm(a + b) (K9d, mirec_add_ln_fwd/bwd_f32): the residual sum is never
     materialised; the backward returns the same dx for both inputs."""
 
     @staticmethod
@@ -233,7 +233,7 @@ class _AddLNFn(torch.autograd.Function):
 
 
 def add_layer_norm(hidden, input_tensor, ln):
-    """ln(hidden + input_tensor) — the fused K9c kernel on the GPU (fp32, d in
+    """ln(hidden + input_tensor) — the fused K9d kernel on the GPU (fp32, d in
     {32, 64, 128, 256}), the module itself otherwise."""
     if (hidden.is_cuda and hidden.dtype == torch.float32 and hidden.shape[-1] in (32, 64, 128, 256)
             and ln.elementwise_affine and hidden.shape == input_tensor.shape):

@@ -222,7 +222,7 @@ def test_fused_sampled_eval_matches_generic(tmp_path):
 
 @pytest.mark.parametrize('d', [32, 64, 128, 256])
 def test_add_layernorm_and_gelu_match_torch(dev, d):
-    """K9c LayerNorm(a + b) forward / backward and the GELU kernels against torch
+    """K9d LayerNorm(a + b) forward / backward and the GELU kernels against torch
     fp32 (nn.LayerNorm over the materialised sum; the erf formula of layers.py)."""
     from recbole_amd.model.layers import _AddLNFn, _GeluFn
     g = torch.Generator(device='cpu').manual_seed(d)
