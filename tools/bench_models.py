@@ -395,8 +395,8 @@ def bench_c5(dev, scale=1.0, d=256, n_layers=2, K=10, sample_users=131072):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--configs', default='C3,C4,C5')
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=64)
+    ap.add_argument('--warmup', type=int, default=8)
     ap.add_argument('--scale', type=float, default=1.0)
     ap.add_argument('--out', default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
