@@ -262,6 +262,9 @@ class _GeluFn(torch.autograd.Function):
         return dx
 
 
+SDPA = True     # MultiHeadAttention through torch's fused scaled_dot_product_attention
+
+
 class MultiHeadAttention(nn.Module):
     """layers.py:338-407 (same parameters and op sequence; library GEMMs)."""
 
@@ -290,12 +293,20 @@ class MultiHeadAttention(nn.Module):
         q = self.transpose_for_scores(linear(self.query, input_tensor))
         k = self.transpose_for_scores(linear(self.key, input_tensor))
         v = self.transpose_for_scores(linear(self.value, input_tensor))
-        scores = torch.matmul(q, k.transpose(-1, -2))
-        scores = scores / math.sqrt(self.attention_head_size)
-        scores = scores + attention_mask
-        probs = nn.Softmax(dim=-1)(scores)
-        probs = self.attn_dropout(probs)
-        ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
+        if input_tensor.is_cuda and SDPA:
+            # softmax(q k^T / sqrt(dh) + mask) with dropout on the weights, @ v: the same
+            # computation in torch's fused attention (no copies of the permuted q, k, v)
+            p = self.attn_dropout.p if self.training else 0.0
+            ctx = nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=attention_mask,
+                                                             dropout_p=p)
+            ctx = ctx.permute(0, 2, 1, 3).contiguous()
+        else:
+            scores = torch.matmul(q, k.transpose(-1, -2))
+            scores = scores / math.sqrt(self.attention_head_size)
+            scores = scores + attention_mask
+            probs = nn.Softmax(dim=-1)(scores)
+            probs = self.attn_dropout(probs)
+            ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
         ctx = ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
         hidden = self.out_dropout(linear(self.dense, ctx))
         return add_layer_norm(hidden, input_tensor, self.LayerNorm)

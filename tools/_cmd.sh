@@ -1,3 +1,5 @@
 set -o pipefail
-timeout -k 10 1100 python tools/bench_models.py --out gpurun_out/r02_models.json > gpurun_out/models.log 2>&1 || { tail -30 gpurun_out/models.log; exit 3; }
-grep '^{' gpurun_out/models.log | cut -c1-200
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_sasrec.py tests/test_gpu_graph_step.py tests/test_gpu_dp.py > gpurun_out/st.log 2>&1 || { tail -40 gpurun_out/st.log; exit 3; }
+tail -2 gpurun_out/st.log
+timeout -k 10 400 python tools/bench_models.py --configs C3 --no-cpu-baseline > gpurun_out/c3g.log 2>&1 || { tail -20 gpurun_out/c3g.log; exit 4; }
+grep '^{' gpurun_out/c3g.log | cut -c1-250
