@@ -175,8 +175,19 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   const int c = threadIdx.x % CB, r = threadIdx.x / CB;
   const int64_t j = (int64_t)blockIdx.x * CB + c;
   float s = 0.f;
-  if (j < m)
-    for (int64_t i = r; i < n; i += RG) s += x[i * m + j];
+  if (j < m) {
+    // 8 rows' loads in flight per thread, added in the same (row) order
+    constexpr int U = 8;
+    int64_t i = r;
+    for (; i + (U - 1) * RG < n; i += U * RG) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = x[(i + u * RG) * m + j];
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += v[u];
+    }
+    for (; i < n; i += RG) s += x[i * m + j];
+  }
   part[r][c] = s;
   __syncthreads();
   if (r == 0 && j < m) {
