@@ -218,6 +218,16 @@ int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
                                int64_t key_space, int32_t* perm, int32_t* uniq, int32_t* seg,
                                int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
 
+/* The same single sort (mirec_segment_sort outputs) for keys that come in blocks of
+ * block_n (<= 8,192) with every key of block b below every key of block b+1 (e.g.
+ * DeepFM's token keys, field-major at increasing table offsets): each block sorted
+ * in LDS, then concatenated — two launches instead of a device-wide radix sort.
+ * Workspace: mirec_segment_sort_blocks_workspace_size(n, block_n). */
+size_t mirec_segment_sort_blocks_workspace_size(int64_t n, int64_t block_n);
+int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t block_n, int64_t key_space,
+                              int32_t* perm, int32_t* uniq, int32_t* seg, int32_t* n_uniq_dev,
+                              void* ws, size_t ws_bytes, void* stream);
+
 /* Look-ahead lists of the deferred Adam: for b < n_batches-1,
  * out[b*stride ..) = uniq(b+1) \ uniq(b) ascending, n_out[b] its length, where
  * uniq(b) = uniq[b*stride .. + n_uniq[b]) (the batched segment-sort layout);

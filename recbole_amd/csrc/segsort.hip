@@ -171,6 +171,32 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
                     blockIdx.x, L);
 }
 
+// Block-partitioned sort (keys in n_blocks blocks of block_n, every key of block b
+// below every key of block b+1 — DeepFM's token keys, one block per field at its
+// table offset): each block sorted in LDS by its own workgroup, then concatenated —
+// the global stable sort, in two launches instead of a device-wide radix sort.
+__global__ __launch_bounds__(256) void blocks_concat_kernel(
+    const int32_t* __restrict__ perm_t, const int32_t* __restrict__ uniq_t,
+    const int32_t* __restrict__ seg_t, const int32_t* __restrict__ nu_t, int64_t n,
+    int block_n, int n_blocks, int32_t* __restrict__ perm, int32_t* __restrict__ uniq,
+    int32_t* __restrict__ seg, int32_t* __restrict__ n_uniq) {
+  const int b = blockIdx.x;
+  int off = 0;
+  for (int c = 0; c < b; ++c) off += nu_t[c];
+  const int nu = nu_t[b];
+  const int64_t base = (int64_t)b * block_n;
+  const int nb = (int)min((int64_t)block_n, n - base);
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) perm[base + i] = (int32_t)base + perm_t[base + i];
+  for (int i = threadIdx.x; i < nu; i += blockDim.x) {
+    uniq[off + i] = uniq_t[base + i];
+    seg[off + i] = (int32_t)base + seg_t[(int64_t)b * (block_n + 1) + i];
+  }
+  if (b == n_blocks - 1 && threadIdx.x == 0) {
+    seg[off + nu] = (int32_t)n;
+    n_uniq[0] = off + nu;
+  }
+}
+
 // Two batched sorts in one launch (the user and the item keys of a chunk):
 // workgroups [0, nbA) sort table A's batches, the rest table B's.
 struct SortJob {
@@ -665,6 +691,40 @@ extern "C" int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_
                        (int32_t*)ws);
   }
   return launch_status("mirec_segment_sort");
+}
+
+extern "C" size_t mirec_segment_sort_blocks_workspace_size(int64_t n, int64_t block_n) {
+  if (n <= 0 || block_n <= 0) return 256;
+  const int64_t nb = (n + block_n - 1) / block_n;
+  return (size_t)(2 * nb * block_n + nb * (block_n + 1) + nb) * sizeof(int32_t) + 256;
+}
+
+extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t block_n,
+                                         int64_t key_space, int32_t* perm, int32_t* uniq,
+                                         int32_t* seg, int32_t* n_uniq_dev, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  if (n <= 0 || block_n <= 0 || block_n > kLdsMax || key_space <= 0 ||
+      key_space > INT32_MAX || n > INT32_MAX || !keys || !perm || !uniq || !seg || !n_uniq_dev) {
+    set_error("mirec_segment_sort_blocks: bad arguments (0 < block_n <= %d)", kLdsMax);
+    return -1;
+  }
+  if (!ws || ws_bytes < mirec_segment_sort_blocks_workspace_size(n, block_n)) {
+    set_error("mirec_segment_sort_blocks: workspace too small");
+    return -1;
+  }
+  const int64_t nb = (n + block_n - 1) / block_n;
+  int32_t* perm_t = (int32_t*)ws;
+  int32_t* uniq_t = perm_t + nb * block_n;
+  int32_t* seg_t = uniq_t + nb * block_n;
+  int32_t* nu_t = seg_t + nb * (block_n + 1);
+  int nbits = 0;
+  while (nbits < 31 && ((int64_t)1 << nbits) < key_space) ++nbits;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys, n,
+                     (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
+  hipLaunchKernelGGL(blocks_concat_kernel, dim3((unsigned)nb), dim3(256), 0, st, perm_t, uniq_t,
+                     seg_t, nu_t, n, (int)block_n, (int)nb, perm, uniq, seg, n_uniq_dev);
+  return launch_status("mirec_segment_sort_blocks");
 }
 
 extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,

@@ -28,6 +28,8 @@ class FieldLayout:
         self.seq_names = list(seq_names)
         self.float_names = list(float_names)
         self.token_offsets = [int(x) for x in token_offsets] if len(token_names) else []
+        # field-major keys (id + offset) then fall in increasing, disjoint ranges per field
+        self.blocks_ok = all(a < b for a, b in zip(self.token_offsets, self.token_offsets[1:]))
         self.n_fields = len(self.token_names) + len(self.seq_names) + len(self.float_names)
         self._dev_offsets = {}
 
@@ -141,7 +143,11 @@ class _CtxFMFn(torch.autograd.Function):
             keys.view(len(layout.token_names), B).copy_(
                 torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
                 + off.unsqueeze(1))
-            ctx.segs = h.catch_up(T, keys)
+            # one key block per field (ranges increase with the field offsets): K2
+            # sorts each field's B keys in LDS instead of a device-wide radix sort
+            blocks = B if (layout.blocks_ok and 0 < B <= 8192 and len(layout.token_names) > 1) \
+                else None
+            ctx.segs = h.catch_up(T, keys, blocks=blocks)
             h1 = getattr(T1, '_mirec_deferred', None)
             if h1 is not None:                # the first-order [V, 1] table, same rows
                 h1.catch_up(T1, keys, ctx.segs)

@@ -363,6 +363,20 @@ def segment_sort(keys: torch.Tensor, key_space: int, segs: Segments | None = Non
     return segs
 
 
+def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int) -> Segments:
+    """segment_sort for keys in blocks of block_n whose key ranges increase block to
+    block (every key of block b below every key of block b+1): same outputs, each
+    block sorted in LDS (mirec_segment_sort_blocks)."""
+    _dev(keys, torch.int64, "keys")
+    n = keys.numel()
+    segs = Segments(n, keys.device, lib().mirec_segment_sort_blocks_workspace_size(n, block_n))
+    rc = lib().mirec_segment_sort_blocks(ptr(keys), n, block_n, key_space, ptr(segs.perm),
+                                         ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq),
+                                         ptr(segs.ws), segs.ws.numel(), stream_handle())
+    check(rc, "mirec_segment_sort_blocks")
+    return segs
+
+
 def segment_sort_batched(keys: torch.Tensor, batch_n: int, key_space: int, perm, uniq, seg,
                          n_uniq, ws=None):
     """K2 over consecutive batches of `batch_n` keys, one workgroup per batch."""

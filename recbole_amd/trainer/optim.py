@@ -279,11 +279,15 @@ class FusedAdam(torch.optim.Optimizer):
         spec.update(kw)
         return ops.adam_tables([spec])
 
-    def catch_up(self, p, keys, segs=None):
+    def catch_up(self, p, keys, segs=None, blocks=None):
         """Make the rows `keys` (int64, any order / duplicates) current before a
         forward pass reads them; returns their K2 grouping (`segs`: the grouping
-        when the caller already has it, e.g. another table read by the same keys)."""
-        if segs is None:
+        when the caller already has it, e.g. another table read by the same keys;
+        `blocks`: the keys come in blocks of this size with increasing key ranges,
+        which K2 then sorts block by block in LDS)."""
+        if segs is None and blocks:
+            segs = ops.segment_sort_blocks(keys.contiguous(), int(blocks), p.shape[0])
+        elif segs is None:
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])
         if 'shard' in self._deferred[p]:
             self._catch_up_sharded(p, keys)

@@ -713,3 +713,27 @@ def test_adam_fast_math_selftest(dev):
     sq_bad, sq_n, dv_bad, dv_n = out.cpu().tolist()
     assert sq_n > 2 ** 24 and dv_n > 2 ** 24
     assert sq_bad == 0 and dv_bad == 0, (sq_bad, dv_bad)
+
+
+@pytest.mark.parametrize('block_n,n_blocks,space', [(2048, 26, 1 << 25), (100, 7, 1000), (8192, 3, 1 << 20), (513, 4, 2100)])
+def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
+    """mirec_segment_sort_blocks on keys in blocks of increasing key ranges (DeepFM's
+    field-major token keys) gives exactly the device-wide segment_sort's outputs,
+    incl. a ragged last block."""
+    from recbole_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(block_n)
+    edges = torch.linspace(0, space, n_blocks + 1).long()
+    parts = []
+    n = block_n * n_blocks - block_n // 3
+    for b in range(n_blocks):
+        m = min(block_n, n - b * block_n)
+        lo, hi = int(edges[b]), int(edges[b + 1])
+        parts.append(lo + torch.randint(0, max(1, min(hi - lo, 50 + b * 997)), (m,), generator=g))
+    keys = torch.cat(parts).to(dev)
+    a = ops.segment_sort(keys, space)
+    b = ops.segment_sort_blocks(keys, block_n, space)
+    nu = int(a.n_uniq.item())
+    assert int(b.n_uniq.item()) == nu
+    assert torch.equal(a.perm[:n], b.perm[:n])
+    assert torch.equal(a.uniq[:nu], b.uniq[:nu])
+    assert torch.equal(a.seg[:nu + 1], b.seg[:nu + 1])
