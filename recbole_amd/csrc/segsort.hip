@@ -17,7 +17,10 @@
 
 namespace mirec {
 
-constexpr int kSortThreads = 1024;
+#ifndef MIREC_SORT_THREADS
+#define MIREC_SORT_THREADS 1024
+#endif
+constexpr int kSortThreads = MIREC_SORT_THREADS;   // profiling variants: tools/build_variant.sh
 constexpr int kLdsMax = 8192;
 constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
 
