@@ -7,7 +7,7 @@
 // contributions, which K5 (adam.hip) or the dense scatter below sums in that
 // fixed order — bitwise reproducible, no float atomics.
 //
-// The sort runs in ONE workgroup (1024 lanes): n is a training batch's
+// The sort runs in ONE workgroup (512 lanes): n is a training batch's
 // contribution count (C2: 512 user keys, 2,560 item keys), far too small to
 // fill the chip, and the sort depends only on ids, so the trainer runs it
 // ahead of the model step on a side stream.  Up to kLdsMax keys the whole
@@ -18,9 +18,13 @@
 namespace mirec {
 
 #ifndef MIREC_SORT_THREADS
-#define MIREC_SORT_THREADS 1024
+#define MIREC_SORT_THREADS 512
 #endif
-constexpr int kSortThreads = MIREC_SORT_THREADS;   // profiling variants: tools/build_variant.sh
+// 512 lanes: each 4-bit pass pays a fixed cross-wave cost (wave scan, per-wave totals,
+// two barriers) that grows with the wave count — one C2 batch (512 user keys / 2,560 item
+// keys) sorts in 14.7 / 20.3 us with 8 waves against 27.1 / 29.1 us with 16
+// (tools/probe_segsort.py, variants by tools/build_variant.sh -DMIREC_SORT_THREADS=N).
+constexpr int kSortThreads = MIREC_SORT_THREADS;
 constexpr int kLdsMax = 8192;
 constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
 
