@@ -25,6 +25,11 @@ namespace mirec {
 // keys) sorts in 14.7 / 20.3 us with 8 waves against 27.1 / 29.1 us with 16
 // (tools/probe_segsort.py, variants by tools/build_variant.sh -DMIREC_SORT_THREADS=N).
 constexpr int kSortThreads = MIREC_SORT_THREADS;
+#ifndef MIREC_SORT_DIGIT_BITS
+#define MIREC_SORT_DIGIT_BITS 4
+#endif
+constexpr int kDigitBits = MIREC_SORT_DIGIT_BITS;      // radix digit width of the LDS sort
+constexpr int kDigitWords = (1 << kDigitBits) / 4;     // four 16-bit counters per 64-bit word
 constexpr int kLdsMax = 8192;
 constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
 
@@ -67,7 +72,7 @@ __device__ void emit_segments(KeyPtr skey, int n, int32_t* __restrict__ uniq,
 struct SortLds {
   int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
   int scan[kSortThreads / 64 + 1];
-  uint64_t wtot[kSortThreads / 64][4];   // per-wave packed digit counts
+  uint64_t wtot[kSortThreads / 64][(1 << MIREC_SORT_DIGIT_BITS) / 4];  // per-wave packed digit counts
 };
 
 __device__ __forceinline__ void segsort_lds_batch(
@@ -104,35 +109,38 @@ __device__ __forceinline__ void segsort_lds_batch(
   // destination of an item is (items of smaller digits) + (items of its digit
   // before it) — the same permutation as the 1-bit splits, in a quarter of the
   // passes.
-  for (int shift = 0; shift < nbits; shift += 4) {
-    uint64_t c[4] = {0ull, 0ull, 0ull, 0ull};
+  for (int shift = 0; shift < nbits; shift += kDigitBits) {
+    constexpr int kMask = (1 << kDigitBits) - 1;
+    uint64_t c[kDigitWords];
+#pragma unroll
+    for (int w = 0; w < kDigitWords; ++w) c[w] = 0ull;
     for (int i = lo; i < hi; ++i) {
-      const int d = (ks[i] >> shift) & 15;
+      const int d = (ks[i] >> shift) & kMask;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) c[w] += (d >> 2) == w ? 1ull << (16 * (d & 3)) : 0ull;
+      for (int w = 0; w < kDigitWords; ++w) c[w] += (d >> 2) == w ? 1ull << (16 * (d & 3)) : 0ull;
     }
-    uint64_t inc[4];
+    uint64_t inc[kDigitWords];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) inc[w] = c[w];
+    for (int w = 0; w < kDigitWords; ++w) inc[w] = c[w];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < kDigitWords; ++w) {
         const uint64_t y = __shfl_up(inc[w], off, 64);
         if (lane >= off) inc[w] += y;
       }
     }
     if (lane == 63) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) L.wtot[wid][w] = inc[w];
+      for (int w = 0; w < kDigitWords; ++w) L.wtot[wid][w] = inc[w];
     }
     __syncthreads();
-    uint64_t ex[4], tot[4];
+    uint64_t ex[kDigitWords], tot[kDigitWords];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { ex[w] = inc[w] - c[w]; tot[w] = 0ull; }
+    for (int w = 0; w < kDigitWords; ++w) { ex[w] = inc[w] - c[w]; tot[w] = 0ull; }
     for (int v = 0; v < nw; ++v) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < kDigitWords; ++w) {
         const uint64_t x = L.wtot[v][w];
         ex[w] += v < wid ? x : 0ull;
         tot[w] += x;
@@ -143,12 +151,12 @@ __device__ __forceinline__ void segsort_lds_batch(
     };
     for (int i = lo; i < hi; ++i) {
       const int32_t kv = ks[i];
-      const int d = (kv >> shift) & 15;
+      const int d = (kv >> shift) & kMask;
       const int w = d >> 2, f = 16 * (d & 3);
       int base = 0;
       uint64_t e = 0ull;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < kDigitWords; ++q) {
         base += q < w ? fsum(tot[q]) : 0;
         if (q == w) {
           base += fsum(tot[q] & ((1ull << f) - 1ull));

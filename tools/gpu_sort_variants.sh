@@ -4,7 +4,7 @@
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sortv
-for v in sort256 sort512 default; do
+for v in ${VARIANTS:-d5 d6 default}; do
   if [ $v = default ]; then L=recbole_amd/_lib/libmirec.so; else L=recbole_amd/_lib/alt/$v.so; fi
   MIREC_LIB=$L timeout -k 10 120 python tools/probe_segsort.py > gpurun_out/sortv/$v.probe 2>&1 || exit 3
   MIREC_LIB=$L timeout -k 10 200 python bench.py --warmup 5 --steps 20 --no-cpu-baseline > gpurun_out/sortv/$v.bench 2>&1 || exit 4
