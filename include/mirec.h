@@ -645,7 +645,13 @@ int mirec_shard_keys(const int64_t* ids, int64_t n, int32_t G, int64_t S, int64_
  *   pos[nb, (2+T)*B]     requester side (slice = rank): local slot ls (users k',
  *                        items n + j*n + k', n = this slice's positives) -> o*cap + idx
  *   bwd_src[nb, G*cap]   requester side: message (rank, o) entry idx -> local slot ls;
- *                        padding 0. */
+ *                        padding 0.
+ *   status[2]            (accumulated, zero it first) [0] = -4 if any message of any
+ *                        rank exceeded cap, [1] = max over launches of the largest
+ *                        message (rows). Every rank counts every message, so all ranks
+ *                        see the same status. An overflowing slot gets position 0 in
+ *                        map2 / pos (in range, never read out of bounds); its batch must
+ *                        be re-planned with cap >= status[1] before it runs. */
 int mirec_shard_plan(const int64_t* users, const int64_t* items, int64_t n_batches, int64_t Bc,
                      int64_t B, int32_t T, int32_t G, int32_t rank, int64_t cap,
                      int64_t* fwd_rows, int32_t* map2, int64_t* pos, int32_t* bwd_src,

@@ -26,7 +26,9 @@ import yaml
 from recbole_amd.config.defaults import (DATASET_DEFAULTS, MODEL_DEFAULTS, OVERALL, SAMPLE,
                                          TYPE_DATASET_PRESETS, TYPE_PRESETS)
 from recbole_amd.evaluator import group_metrics, individual_metrics
-from recbole_amd.utils import EvaluatorType, InputType, ModelType, get_model
+from recbole_amd.utils import (EvaluatorType, InputType, ModelType, dataset_arguments,
+                               evaluation_arguments, general_arguments, get_model,
+                               training_arguments)
 
 
 def _yaml_loader():
@@ -66,6 +68,9 @@ class Config(object):
 
     def __init__(self, model=None, dataset=None, config_file_list=None, config_dict=None):
         self.yaml_loader = _yaml_loader()
+        # parameter categories of the printout (configurator.py:85-88)
+        self.parameters = {'General': general_arguments, 'Training': training_arguments,
+                           'Evaluation': evaluation_arguments, 'Dataset': dataset_arguments}
         self.file_config_dict = self._load_config_files(config_file_list)
         self.variable_config_dict = {k: _convert(v) for k, v in (config_dict or {}).items()}
         self.cmd_config_dict = self._load_cmd_line()
@@ -205,8 +210,26 @@ class Config(object):
             raise TypeError('index must be a str.')
         return key in self.final_config_dict
 
+    def __getstate__(self):            # the YAML loader class is local: rebuilt on load
+        state = dict(self.__dict__)
+        state.pop('yaml_loader', None)
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self.yaml_loader = _yaml_loader()
+
     def __str__(self):
-        return '\n'.join(f'{k} = {v}' for k, v in self.final_config_dict.items()) + '\n'
+        # one block per category, then everything uncategorised (configurator.py:342-360)
+        listed = {k for keys in self.parameters.values() for k in keys}
+        blocks = []
+        for category, keys in self.parameters.items():
+            lines = [f'{k} = {v}' for k, v in self.final_config_dict.items() if k in keys]
+            blocks.append(f'{category} Hyper Parameters:\n' + '\n'.join(lines))
+        rest = [f'{k} = {v}' for k, v in self.final_config_dict.items()
+                if k not in listed and k not in ('model', 'dataset', 'config_files')]
+        blocks.append('Other Hyper Parameters: \n' + '\n'.join(rest))
+        return '\n' + '\n\n'.join(blocks) + '\n\n'
 
     def __repr__(self):
         return self.__str__()

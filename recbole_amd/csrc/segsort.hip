@@ -11,8 +11,10 @@
 // contribution count (C2: 512 user keys, 2,560 item keys), far too small to
 // fill the chip, and the sort depends only on ids, so the trainer runs it
 // ahead of the model step on a side stream.  Up to kLdsMax keys the whole
-// sort lives in LDS (1-bit stable splits, one block scan per bit); larger n
-// uses the same algorithm over global ping-pong buffers.
+// sort lives in LDS (stable kDigitBits-bit digit passes, packed per-thread digit
+// counts, one block scan per pass). Larger batches: one large batch takes a
+// device-wide LSD radix sort (upsweep histograms, scan, stable downsweep), several
+// take one workgroup each over global ping-pong buffers (1-bit stable splits).
 #include "common.h"
 
 namespace mirec {
@@ -32,6 +34,11 @@ constexpr int kDigitBits = MIREC_SORT_DIGIT_BITS;      // radix digit width of t
 constexpr int kDigitWords = (1 << kDigitBits) / 4;     // four 16-bit counters per 64-bit word
 constexpr int kLdsMax = 8192;
 constexpr int kIpt = kLdsMax / kSortThreads;  // items per thread in the LDS path
+// knobs of the probing builds (tools/build_variant.sh): digits of 2..6 bits (kDigitWords
+// packed words of four 16-bit counters each), whole waves dividing the LDS capacity
+static_assert(kDigitBits >= 2 && kDigitBits <= 6, "MIREC_SORT_DIGIT_BITS must be in [2, 6]");
+static_assert(kSortThreads % 64 == 0 && kSortThreads <= 1024 && kLdsMax % kSortThreads == 0,
+              "MIREC_SORT_THREADS: a multiple of 64, at most 1024, dividing kLdsMax");
 
 __host__ __device__ __forceinline__ int nbits_for(int64_t key_space) {
   int b = 0;
@@ -72,8 +79,10 @@ __device__ void emit_segments(KeyPtr skey, int n, int32_t* __restrict__ uniq,
 struct SortLds {
   int32_t kA[kLdsMax], vA[kLdsMax], kB[kLdsMax], vB[kLdsMax];
   int scan[kSortThreads / 64 + 1];
-  uint64_t wtot[kSortThreads / 64][(1 << MIREC_SORT_DIGIT_BITS) / 4];  // per-wave packed digit counts
+  uint64_t wtot[kSortThreads / 64][kDigitWords];  // per-wave packed digit counts
 };
+// the two-job kernel (segsort_lds2_kernel) holds one SortLds; gfx950 has 160 KiB per CU
+static_assert(sizeof(SortLds) <= 160 * 1024, "SortLds exceeds the gfx950 LDS");
 
 __device__ __forceinline__ void segsort_lds_batch(
     const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n, int nbits,
@@ -102,12 +111,12 @@ __device__ __forceinline__ void segsort_lds_batch(
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
-  // Stable LSD passes of 4-bit digits (a blocked arrangement: thread t owns
+  // Stable LSD passes of kDigitBits-bit digits (a blocked arrangement: thread t owns
   // positions [lo, hi)). Per-digit counts travel packed, four 16-bit fields per
-  // 64-bit word (n <= 8192 < 2^16: no carries), so one wave scan of four words
+  // 64-bit word (n <= 8192 < 2^16: no carries), so one wave scan of kDigitWords words
   // and one barrier give every thread its per-digit exclusive prefix; the
   // destination of an item is (items of smaller digits) + (items of its digit
-  // before it) — the same permutation as the 1-bit splits, in a quarter of the
+  // before it) — the same permutation as 1-bit splits, in 1/kDigitBits of the
   // passes.
   for (int shift = 0; shift < nbits; shift += kDigitBits) {
     constexpr int kMask = (1 << kDigitBits) - 1;
@@ -396,7 +405,8 @@ __global__ __launch_bounds__(kRadixThreads) void radix_downsweep_kernel(
   const int base = blockIdx.x * kRadixTile;
   tile_counts(k, n, base, shift, cnt, my, &nmy);
   __syncthreads();
-  // exclusive scan of cnt (bin-major, 4096 entries): 16 per thread, then a block scan
+  // exclusive scan of cnt (thread-major, kRadixBins per thread: kRadixBins * kRadixThreads
+  // entries), each thread's own bins serially, then a block scan of the thread totals
   const int t = threadIdx.x;
   int loc[kRadixBins];
   int s = 0;

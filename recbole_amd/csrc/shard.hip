@@ -106,7 +106,12 @@ __global__ __launch_bounds__(kPlanThreads) void shard_plan_kernel(
     }
     if (act) {
       if (idx >= cap) {
+        // no room in the message: the slot gets a harmless in-range position (row 0
+        // of the first message) so no kernel reads outside the buffers; the chunk is
+        // re-planned with a larger cap before it runs (status, ShardedBPRTrainStep)
         overflow = 1;
+        if (o == r) m2[t] = 0;
+        if (g == r) ps[ls] = 0;
       } else {
         const int64_t local = id / G;
         if (o == r) {                                   // owner side: rows to send to g
@@ -128,6 +133,14 @@ __global__ __launch_bounds__(kPlanThreads) void shard_plan_kernel(
       for (int64_t i = cnt + threadIdx.x; i < cap; i += kPlanThreads) fr[(int64_t)g * cap + i] = 0;
     if (g == r)
       for (int64_t i = cnt + threadIdx.x; i < cap; i += kPlanThreads) bs[(int64_t)q * cap + i] = 0;
+  }
+  // status[0] = -4 if any message of this (batch, slice) overflowed, status[1] = the
+  // largest message (rows) — every rank's launch counts every (slice, owner) message,
+  // so every rank sees the same status without a collective
+  if (threadIdx.x == 0) {
+    int most = 0;
+    for (int q = 0; q < G; ++q) most = max(most, run[q]);
+    atomicMax(status + 1, most);
   }
   if (overflow) atomicExch(status, -4);
 }

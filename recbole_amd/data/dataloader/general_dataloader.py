@@ -1,6 +1,7 @@
 """General-recommendation loaders (mirror of
 recbole/data/dataloader/general_dataloader.py:24-378 and
-neg_sample_mixin.py:19-140).
+neg_sample_mixin.py:19-140 — the mixins live in
+neg_sample_mixin.py, as in the reference).
 
 Train batches are slices of the (shuffled) train table kept resident in HBM;
 negatives come from the device walk (K4). The full-sort loader builds, per
@@ -17,9 +18,9 @@ import numpy as np
 import torch
 
 from recbole_amd.data.dataloader.abstract_dataloader import AbstractDataLoader
+from recbole_amd.data.dataloader.neg_sample_mixin import NegSampleByMixin, NegSampleMixin
 from recbole_amd.data.interaction import Interaction, cat_interactions
-from recbole_amd.utils import (DataLoaderType, EvaluatorType, FeatureSource, FeatureType,
-                               InputType)
+from recbole_amd.utils import DataLoaderType, InputType
 
 
 def _loader_device(config):
@@ -41,52 +42,6 @@ class GeneralDataLoader(AbstractDataLoader):
         cur = self.dataset[self.pr:self.pr + self.step]
         self.pr += self.step
         return cur
-
-
-class NegSampleMixin(AbstractDataLoader):
-    dl_type = DataLoaderType.NEGSAMPLE
-
-    def __init__(self, config, dataset, sampler, neg_sample_args, batch_size=1,
-                 dl_format=InputType.POINTWISE, shuffle=False):
-        if neg_sample_args['strategy'] not in ['by', 'full']:
-            raise ValueError(f"Neg_sample strategy [{neg_sample_args['strategy']}] has not been implemented.")
-        self.sampler = sampler
-        self.neg_sample_args = neg_sample_args
-        super().__init__(config, dataset, batch_size=batch_size, dl_format=dl_format,
-                         shuffle=shuffle)
-
-    def setup(self):
-        self._batch_size_adaptation()
-
-
-class NegSampleByMixin(NegSampleMixin):
-
-    def __init__(self, config, dataset, sampler, neg_sample_args, batch_size=1,
-                 dl_format=InputType.POINTWISE, shuffle=False):
-        if neg_sample_args['strategy'] != 'by':
-            raise ValueError('neg_sample strategy in GeneralInteractionBasedDataLoader() should be `by`')
-        self.user_inter_in_one_batch = (sampler.phase != 'train') and (
-            config['eval_type'] != EvaluatorType.INDIVIDUAL)
-        self.neg_sample_by = neg_sample_args['by']
-        if dl_format == InputType.POINTWISE:
-            self.times = 1 + self.neg_sample_by
-            self.sampling_func = self._neg_sample_by_point_wise_sampling
-            self.label_field = config['LABEL_FIELD']
-            dataset.set_field_property(self.label_field, FeatureType.FLOAT,
-                                       FeatureSource.INTERACTION, 1)
-        elif dl_format == InputType.PAIRWISE:
-            self.times = self.neg_sample_by
-            self.sampling_func = self._neg_sample_by_pair_wise_sampling
-            self.neg_prefix = config['NEG_PREFIX']
-            iid_field = config['ITEM_ID_FIELD']
-            self.neg_item_id = self.neg_prefix + iid_field
-            cols = [iid_field] if dataset.item_feat is None else dataset.item_feat.columns
-            for c in cols:
-                dataset.copy_field_property(self.neg_prefix + c, c)
-        else:
-            raise ValueError(f'`neg sampling by` with dl_format [{dl_format}] not been implemented.')
-        super().__init__(config, dataset, sampler, neg_sample_args, batch_size=batch_size,
-                         dl_format=dl_format, shuffle=shuffle)
 
 
 class GeneralNegSampleDataLoader(NegSampleByMixin):

@@ -19,8 +19,8 @@ import numpy as np
 import torch
 
 from recbole_amd.data.dataloader.abstract_dataloader import AbstractDataLoader
-from recbole_amd.data.dataloader.general_dataloader import (NegSampleByMixin, NegSampleMixin,
-                                                            _loader_device)
+from recbole_amd.data.dataloader.general_dataloader import _loader_device
+from recbole_amd.data.dataloader.neg_sample_mixin import NegSampleByMixin, NegSampleMixin
 from recbole_amd.data.interaction import Interaction, cat_interactions
 from recbole_amd.utils import DataLoaderType, FeatureSource, FeatureType, InputType
 

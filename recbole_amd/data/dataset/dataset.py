@@ -164,11 +164,25 @@ def _factorize(pieces):
     return new_ids, np.array(order, dtype=object)
 
 
+def _pandas_na_tokens():
+    """The strings pd.read_csv reads as missing by default (its na_values); Arrow's
+    own default list lacks 'None' and '<NA>'."""
+    try:
+        from pandas._libs.parsers import STR_NA_VALUES
+        return sorted(STR_NA_VALUES)
+    except ImportError:                          # the documented pandas default list
+        return ['', '#N/A', '#N/A N/A', '#NA', '-1.#IND', '-1.#QNAN', '-NaN', '-nan', '1.#IND',
+                '1.#QNAN', '<NA>', 'N/A', 'NA', 'NULL', 'NaN', 'None', 'n/a', 'nan', 'null']
+
+
+_PANDAS_NA_TOKENS = _pandas_na_tokens()
+
+
 def _read_atomic(filepath, sep, usecols, dtype, cat_cols=()):
     """pd.read_csv(filepath, delimiter=sep, usecols=usecols, dtype=dtype) as the
     reference reads an atomic file (dataset.py:342-408), parsed by Arrow's
-    multi-threaded CSV reader: token columns as strings (empty -> missing, like
-    pandas' NaN), float columns as float64, then the same pandas frame (object
+    multi-threaded CSV reader: token columns as strings (pandas' missing-value tokens,
+    quoted or not, -> missing, like its NaN), float columns as float64, then the same pandas frame (object
     columns of str). Float fields are parsed correctly rounded (pandas' default
     parser may differ in the last bit for inputs of more than ~15 significant digits;
     atomic-file ratings, timestamps and prices are exact either way). Columns in
@@ -185,8 +199,9 @@ def _read_atomic(filepath, sep, usecols, dtype, cat_cols=()):
             filepath, parse_options=pacsv.ParseOptions(delimiter=sep),
             convert_options=pacsv.ConvertOptions(column_types=types,
                                                  include_columns=list(usecols),
+                                                 null_values=_PANDAS_NA_TOKENS,
                                                  strings_can_be_null=True,
-                                                 quoted_strings_can_be_null=False))
+                                                 quoted_strings_can_be_null=True))
     except pa.ArrowInvalid:
         # ragged rows (pandas fills missing trailing fields with NaN; Arrow refuses)
         return pd.read_csv(filepath, delimiter=sep, usecols=usecols, dtype=dtype)

@@ -11,7 +11,7 @@ import copy
 
 import numpy as np
 
-from recbole_amd.data.dataset import Dataset
+from recbole_amd.data.dataset.dataset import Dataset
 
 
 class SequentialDataset(Dataset):

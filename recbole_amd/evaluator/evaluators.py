@@ -1,13 +1,14 @@
 """Evaluators (mirror of recbole/evaluator/evaluators.py:37-370,
-abstract_evaluator.py:18-120). TopKEvaluator.collect keeps the reference's
+abstract_evaluator.py:18-120 — the base classes live in
+abstract_evaluator.py). TopKEvaluator.collect keeps the reference's
 score-matrix contract for models without a fused scorer; the fused full-sort
 path feeds `evaluate_pos_idx` with the K6 kernel's positive flags directly."""
 from collections import ChainMap
 
 import numpy as np
 import torch
-from torch.nn.utils.rnn import pad_sequence
 
+from recbole_amd.evaluator.abstract_evaluator import GroupedEvaluator, IndividualEvaluator
 from recbole_amd.evaluator.metrics import (metrics_dict, pattern_codes, topk_metric_rows,
                                            uses_patterns)
 
@@ -18,15 +19,7 @@ group_metrics = ChainMap(topk_metrics, rank_metrics)
 individual_metrics = ChainMap(loss_metrics)
 
 
-class BaseEvaluator(object):
-
-    def __init__(self, config, metrics):
-        self.metrics = metrics
-        self.full = ('full' in config['eval_setting'])
-        self.precision = config['metric_decimal_place']
-
-
-class TopKEvaluator(BaseEvaluator):
+class TopKEvaluator(GroupedEvaluator):
 
     def __init__(self, config, metrics):
         super().__init__(config, metrics)
@@ -44,18 +37,8 @@ class TopKEvaluator(BaseEvaluator):
         else:
             raise TypeError('The topk must be a integer, list')
 
-    # score-matrix contract (abstract_evaluator.py:65-95, evaluators.py:53-76)
-    def get_score_matrix(self, scores_tensor, user_len_list):
-        if self.full:
-            return scores_tensor.view(len(user_len_list), -1)
-        scores_list = torch.split(scores_tensor, list(user_len_list), dim=0)
-        padding = pad_sequence(scores_list, batch_first=True, padding_value=-np.inf)
-        if padding.shape[1] < max(self.topk):
-            new = torch.full((padding.shape[0], max(self.topk)), -np.inf, device=padding.device)
-            new[:, :padding.shape[1]] = padding
-            padding = new
-        return padding
-
+    # the score-matrix contract (get_score_matrix) is GroupedEvaluator's
+    # (abstract_evaluator.py:65-95); collect = evaluators.py:53-76
     def collect(self, interaction, scores_tensor):
         user_len_list = interaction.user_len_list
         scores = torch.flip(self.get_score_matrix(scores_tensor, user_len_list), dims=[-1])
@@ -127,7 +110,7 @@ class TopKEvaluator(BaseEvaluator):
         return out
 
 
-class LossEvaluator(BaseEvaluator):
+class LossEvaluator(IndividualEvaluator):
 
     def __init__(self, config, metrics):
         super().__init__(config, metrics)
@@ -136,7 +119,7 @@ class LossEvaluator(BaseEvaluator):
     def collect(self, interaction, pred_scores):
         trues = interaction[self.label_field].to(pred_scores.device)
         assert len(trues) == len(pred_scores)
-        return torch.stack((trues.float(), pred_scores.detach().float()), dim=1)
+        return self.get_score_matrix(trues.float(), pred_scores.float())
 
     def evaluate(self, batch_matrix_list, *args):
         concat = torch.cat(batch_matrix_list, dim=0).cpu().numpy()

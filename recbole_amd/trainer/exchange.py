@@ -116,6 +116,12 @@ class ShardLayout(object):
         bwd[(o * cap + idx)[req]] = ls[req].to(torch.int32)
         return fwd, map2, pos, bwd, over
 
+    def largest_message(self, users: torch.Tensor, items: torch.Tensor) -> int:
+        """Rows of the largest (slice, owner) message of one batch (plan status[1])."""
+        _, ids, _, g, _ = self.slots(users, items)
+        msg = g * self.G + ids % self.G
+        return int(torch.bincount(msg).max())
+
     def own(self, uniq: torch.Tensor, seg: torch.Tensor, perm: torch.Tensor,
             map2: torch.Tensor, map_off: int, S: int, rank: int):
         """Rank `rank`'s slice of one batch's sorted keyed uniq list: (local rows,

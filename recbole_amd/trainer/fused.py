@@ -40,6 +40,7 @@ complete after end_epoch() / sync_params().
 from __future__ import annotations
 
 import ctypes
+import logging
 import math
 
 import numpy as np
@@ -563,6 +564,15 @@ class FusedBPRTrainStep(object):
             slot.graphs[key] = g
         return g
 
+    def _capture_variants(self):
+        """Capture the model-side graph of every (slot, size, entry, flush) variant the
+        epoch's chunk plan uses."""
+        S = len(self.slots)
+        variants = sorted({(k % S, n, e, f) for k, ((_, n, Bc), (e, f)) in
+                           enumerate(zip(self._plan, self._flags)) if Bc == self.Bg})
+        for k, n, e, f in variants:
+            self._graph_for(self.slots[k], n, e, f)
+
     # ------------------------------------------------------------------ epoch API
     def begin_epoch(self, cuts=(), hold_prep_from=None, flush_at=()):
         """Shuffle (reference order of RNG use), stage the epoch's Adam constants,
@@ -605,11 +615,7 @@ class FusedBPRTrainStep(object):
         self._flush_at = set(int(b) for b in flush_at)
         self._flags = self._chunk_flags(self._plan)
         if self.use_graph:                      # capture up front: capture synchronizes
-            S = len(self.slots)
-            variants = sorted({(k % S, n, e, f) for k, ((_, n, Bc), (e, f)) in
-                               enumerate(zip(self._plan, self._flags)) if Bc == self.Bg})
-            for k, n, e, f in variants:
-                self._graph_for(self.slots[k], n, e, f)
+            self._capture_variants()
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
         self._next_chunk = 0                   # chunks whose walk (or whole prep) is issued
         self._next_group = 0                   # chunks whose grouping is issued
@@ -791,32 +797,32 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         G, B, T, d, dev = self.G, self.B, self.times, self.d, self.device
         self.SU, self.SI = -(-self.nU // G), -(-self.nI // G)
         # rows per (slice, owner) message: the slice's (2+T)*B slots spread over G
-        # owners (cyclic ownership); overflow is detected (status -4), never silent
+        # owners (cyclic ownership); a chunk whose plan overflows is re-planned with a
+        # larger cap before it runs (_enter_chunk), never run on a truncated plan
         self.cap = int(cap or min((2 + T) * B,
                                   math.ceil(self.CAP_SLACK * (2 + T) * B / G) + 64))
-        M = G * self.cap
         self.shU = [torch.zeros(self.SU, d, device=dev) for _ in range(3)]   # p, m, v
         self.shI = [torch.zeros(self.SI, d, device=dev) for _ in range(3)]
         self.lastU = torch.zeros(self.SU, dtype=torch.int32, device=dev)
         self.lastI = torch.zeros(self.SI, dtype=torch.int32, device=dev)
-        solo = dist is None                  # one rank, no process group: no collectives
-        self.sendF = torch.empty(M, d, device=dev)
-        self.recvF = self.sendF if solo else torch.empty(M, d, device=dev)
+        self._solo = dist is None            # one rank, no process group: no collectives
         self.xloc = torch.empty((2 + T) * B, d, device=dev)
-        self.sendB = torch.empty(M, d, device=dev)
-        self.recvB = self.sendB if solo else torch.empty(M, d, device=dev)
         self.loss_g = torch.empty(G * self.C * B, dtype=torch.float32, device=dev)
         self.loss_mine = torch.zeros(self.C * B, dtype=torch.float32, device=dev)
-        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(2, dtype=torch.int32, device=dev)    # epoch backstop
+        self.cap_growths = 0
         Bg, KI = self.Bg, (1 + T) * self.Bg
         C = self.C
         for sl in self.slots:
             sl.u_keyed = torch.empty(C * Bg, dtype=torch.int64, device=dev)
             sl.i_keyed = torch.empty(C * KI, dtype=torch.int64, device=dev)
-            sl.fwd_rows = torch.empty(C * M, dtype=torch.int64, device=dev)
             sl.map2 = torch.empty(C * (Bg + KI), dtype=torch.int32, device=dev)
             sl.pos = torch.empty(C * (2 + T) * B, dtype=torch.int64, device=dev)
-            sl.bwd_src = torch.empty(C * M, dtype=torch.int32, device=dev)
+            # this chunk's plan status ([overflow, largest message]), read by the host
+            # before the chunk's model side is launched (_enter_chunk)
+            sl.plan_status = torch.zeros(2, dtype=torch.int32, device=dev)
+            sl.plan_status_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+            sl.planned = torch.cuda.Event()
             for tag, per in (('u', Bg), ('i', KI)):
                 setattr(sl, f'own_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_seg', torch.empty(C * (per + 1), dtype=torch.int32,
@@ -825,8 +831,21 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                 setattr(sl, f'perm2_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_ah', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_nah', torch.zeros(C, dtype=torch.int32, device=dev))
+        self._alloc_exchange()
         self._n_max = (ctypes.c_int64 * 2)(min(Bg, self.SU), min(KI, self.SI))
         self._fill_tables()
+
+    def _alloc_exchange(self):
+        """Buffers sized by `cap`: the two all-to-all send / receive buffers and the
+        per-slot message plans."""
+        M, d, dev = self.G * self.cap, self.d, self.device
+        self.sendF = torch.empty(M, d, device=dev)
+        self.recvF = self.sendF if self._solo else torch.empty(M, d, device=dev)
+        self.sendB = torch.empty(M, d, device=dev)
+        self.recvB = self.sendB if self._solo else torch.empty(M, d, device=dev)
+        for sl in self.slots:
+            sl.fwd_rows = torch.empty(self.C * M, dtype=torch.int64, device=dev)
+            sl.bwd_src = torch.empty(self.C * M, dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ shards <-> full tensors
     def _owned_ids(self, n, S):
@@ -905,21 +924,79 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                                                     slot.i_nu, ws=self.sort_ws)
             ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
             ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
-            check(L.mirec_shard_plan(users.data_ptr(), items.data_ptr(), nb, Bc, self.B, T, G, r,
-                                     self.cap, slot.fwd_rows.data_ptr(), slot.map2.data_ptr(),
-                                     slot.pos.data_ptr(), slot.bwd_src.data_ptr(),
-                                     self.status.data_ptr(), st), 'mirec_shard_plan')
-            for tag, per, off, S in (('u', Bc, 0, self.SU), ('i', KI, Bc, self.SI)):
-                g_ = lambda n: getattr(slot, n).data_ptr()
-                check(L.mirec_shard_own(g_(f'{tag}_uniq'), g_(f'{tag}_seg'), g_(f'{tag}_nu'),
-                                        g_(f'{tag}_perm'), per, nb, g_(f'{tag}_ahead'),
-                                        g_(f'{tag}_nah'), slot.map2.data_ptr(), Bc + KI, off,
-                                        S, r, g_(f'own_{tag}'), g_(f'own_{tag}_seg'),
-                                        g_(f'own_{tag}_n'), g_(f'perm2_{tag}'),
-                                        g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), st),
-                      'mirec_shard_own')
+            self._plan_chunk(slot, chunk, st)
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
+
+    def _plan_chunk(self, slot, chunk, st):
+        """Exchange plans of a walked + grouped chunk and this rank's slice of its
+        grouping (on stream `st`); the plan status goes to pinned host memory."""
+        _, nb, Bc = chunk
+        T, G, r = self.times, self.G, self.rank
+        KI = (1 + T) * Bc
+        L = lib()
+        users = slot.user_keys[:nb * Bc]
+        items = slot.item_keys[:nb * KI]
+        slot.plan_status.zero_()
+        check(L.mirec_shard_plan(users.data_ptr(), items.data_ptr(), nb, Bc, self.B, T, G, r,
+                                 self.cap, slot.fwd_rows.data_ptr(), slot.map2.data_ptr(),
+                                 slot.pos.data_ptr(), slot.bwd_src.data_ptr(),
+                                 slot.plan_status.data_ptr(), st), 'mirec_shard_plan')
+        for tag, per, off, S in (('u', Bc, 0, self.SU), ('i', KI, Bc, self.SI)):
+            g_ = lambda n: getattr(slot, n).data_ptr()
+            check(L.mirec_shard_own(g_(f'{tag}_uniq'), g_(f'{tag}_seg'), g_(f'{tag}_nu'),
+                                    g_(f'{tag}_perm'), per, nb, g_(f'{tag}_ahead'),
+                                    g_(f'{tag}_nah'), slot.map2.data_ptr(), Bc + KI, off,
+                                    S, r, g_(f'own_{tag}'), g_(f'own_{tag}_seg'),
+                                    g_(f'own_{tag}_n'), g_(f'perm2_{tag}'),
+                                    g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), st),
+                  'mirec_shard_own')
+        # epoch backstop: overflow flag (min: -4 < 0) and the largest message (max)
+        torch.minimum(self.status[:1], slot.plan_status[:1], out=self.status[:1])
+        torch.maximum(self.status[1:], slot.plan_status[1:], out=self.status[1:])
+        slot.plan_status_host.copy_(slot.plan_status, non_blocking=True)
+        slot.planned.record(torch.cuda.current_stream(self.device))
+
+    def _enter_chunk(self, k, stream):
+        """Before chunk k's model side is enqueued: its plan must fit `cap`. Every rank
+        counts every message, so all ranks see the same status and grow `cap` to the
+        same value (no collective); the chunk and the prepared ones after it are
+        re-planned. No step ever runs on an overflowed plan."""
+        new = self._cur != k
+        super()._enter_chunk(k, stream)
+        if not new:
+            return
+        slot = self.slots[k % len(self.slots)]
+        slot.planned.synchronize()
+        over, most = (int(x) for x in slot.plan_status_host)
+        if over == -4:
+            self._grow_cap(most)
+
+    def _grow_cap(self, most):
+        """Larger messages: reallocate the cap-sized buffers, re-plan every prepared
+        chunk from its walked keys and recapture the chunk graphs."""
+        T, B = self.times, self.B
+        new_cap = min((2 + T) * B, max(most, math.ceil(self.CAP_SLACK * self.cap)))
+        logger = logging.getLogger()
+        logger.warning(f'row exchange: a (slice, owner) message of {most} rows exceeds '
+                       f'cap={self.cap}; re-planning with cap={new_cap}')
+        torch.cuda.synchronize(self.device)
+        self.cap = new_cap
+        self.cap_growths += 1
+        self._alloc_exchange()
+        self._fill_tables()
+        self.status.zero_()
+        for q in range(self._cur, self._next_chunk):           # prepared chunks, in order
+            slot = self.slots[q % len(self.slots)]
+            with torch.cuda.stream(self.prep_stream):
+                self._plan_chunk(slot, self._plan[q], self.prep_stream.cuda_stream)
+        torch.cuda.synchronize(self.device)
+        if int(self.slots[self._cur % len(self.slots)].plan_status_host[0]) == -4:
+            raise RuntimeError('row exchange plan still overflows after re-planning')
+        for slot in self.slots:                                 # later chunks: checked on entry
+            slot.graphs = {}
+        if self.use_graph:
+            self._capture_variants()
 
     # ------------------------------------------------------------ model side
     def _fill_tables(self):
@@ -1013,9 +1090,9 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
 
     def end_epoch(self, n_done=None):
         losses = super().end_epoch(n_done)
-        if int(self.status.item()) == -4:
+        if int(self.status[0].item()) == -4:                 # backstop: _enter_chunk re-plans
             raise RuntimeError(f'row exchange overflow: a (slice, owner) message exceeded '
-                               f'cap={self.cap} rows; construct with a larger cap')
+                               f'cap={self.cap} rows')
         self._store_shards()
         return losses
 

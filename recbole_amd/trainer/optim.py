@@ -527,6 +527,7 @@ class FusedAdam(torch.optim.Optimizer):
         for i, st in state_dict['state'].items():
             p = params[int(i)]
             mine = self._ensure_state(p)
+            steps = int(float(st['step']))     # every entry, row-sharded tables included
             ds = getattr(self, '_deferred', {}).get(p)
             if ds is not None and 'shard' in ds:       # this rank's rows of the full moments
                 sh = ds['shard']
@@ -538,7 +539,6 @@ class FusedAdam(torch.optim.Optimizer):
                 continue
             mine['exp_avg'].copy_(st['exp_avg'].to(p.device))
             mine['exp_avg_sq'].copy_(st['exp_avg_sq'].to(p.device))
-            steps = int(float(st['step']))
         self.n_steps = steps
         for p, ds in getattr(self, '_deferred', {}).items():
             if 'shard' in ds:

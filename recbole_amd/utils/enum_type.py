@@ -19,6 +19,14 @@ class DataLoaderType(Enum):
     NEGSAMPLE = 3
 
 
+class KGDataLoaderState(Enum):
+    """Knowledge-aware loader states (kept for enum / checkpoint compatibility; the
+    knowledge-aware loaders themselves are outside this build)."""
+    RSKG = 1
+    RS = 2
+    KG = 3
+
+
 class EvaluatorType(Enum):
     RANKING = 1
     INDIVIDUAL = 2

@@ -59,12 +59,12 @@ def test_shard_plan_and_own_match_spec(dev, G, Bc):
         map2 = torch.full((Bc + KI,), -7, dtype=torch.int32, device=dev)
         pos = torch.full(((2 + T) * B,), -1, dtype=torch.int64, device=dev)
         bwd = torch.empty(M, dtype=torch.int32, device=dev)
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
         check(L.mirec_shard_plan(ud.data_ptr(), idv.data_ptr(), 1, Bc, B, T, G, r, cap,
                                  fwd.data_ptr(), map2.data_ptr(), pos.data_ptr(), bwd.data_ptr(),
                                  status.data_ptr(), st), 'plan')
         efwd, emap, epos, ebwd, over = lay.plan(users, items, r)
-        assert not over and int(status.item()) == 0
+        assert not over and status.tolist() == [0, lay.largest_message(users, items)]
         assert torch.equal(fwd.cpu(), efwd)
         assert torch.equal(bwd.cpu(), ebwd)
         n_r = max(0, min(B, Bc - r * B))
@@ -90,15 +90,21 @@ def test_shard_plan_and_own_match_spec(dev, G, Bc):
             assert torch.equal(own.cpu()[:k], e_own)
             assert torch.equal(oseg.cpu()[:k + 1], e_seg)
             assert torch.equal(p2.cpu()[e_p], e_p2)
-    if G > 1:                                                  # a too-small cap is reported
-        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    # a too-small cap is reported on every rank (with the largest message), and the
+    # overflowing slots get the in-range position 0 instead of stale values
+    for r in range(G):
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
         bufs = [torch.empty(G * 2, dtype=torch.int64, device=dev),
-                torch.empty(Bc + KI, dtype=torch.int32, device=dev),
-                torch.empty((2 + T) * B, dtype=torch.int64, device=dev),
+                torch.full((Bc + KI,), 1 << 30, dtype=torch.int32, device=dev),
+                torch.full(((2 + T) * B,), 1 << 40, dtype=torch.int64, device=dev),
                 torch.empty(G * 2, dtype=torch.int32, device=dev)]
-        check(L.mirec_shard_plan(ud.data_ptr(), idv.data_ptr(), 1, Bc, B, T, G, 0, 2,
+        check(L.mirec_shard_plan(ud.data_ptr(), idv.data_ptr(), 1, Bc, B, T, G, r, 2,
                                  *[b.data_ptr() for b in bufs], status.data_ptr(), st), 'plan')
-        assert int(status.item()) == -4
+        assert status.tolist() == [-4, lay.largest_message(users, items)]
+        n_r = max(0, min(B, Bc - r * B))
+        assert int(bufs[2][:(2 + T) * n_r].max()) < 2 * G
+        owned = (torch.cat([users, items]) % G == r).to(dev)
+        assert int(bufs[1][owned].max()) < 2 * G
 
 
 def _pipeline(root, batch_rows):
@@ -134,7 +140,29 @@ def test_sharded_solo_equals_fused(tmp_path, graph):
         assert torch.equal(a, b)
 
 
-def _worker(rank, port, root, q):
+@pytest.mark.parametrize('graph', [True, False])
+def test_sharded_cap_overflow_replans(tmp_path, graph):
+    """A cap below the largest message: the chunk is re-planned with a larger cap
+    before it runs (no step on a truncated plan; graphs recaptured) — results
+    bit-identical to the fused single-GPU step."""
+    cap = 64
+    from recbole_amd.trainer.fused import FusedBPRTrainStep, ShardedBPRTrainStep
+    from recbole_amd.trainer.optim import FusedAdam
+    out = []
+    for cls, kw in ((FusedBPRTrainStep, {}), (ShardedBPRTrainStep, {'cap': cap})):
+        config, train, valid, test, model = _pipeline(str(tmp_path), 512)
+        opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
+        step = cls(model, opt, train, chunk=CHUNK, use_graph=graph, **kw)
+        out.append(_train(step))
+        if kw:
+            assert step.cap_growths >= 1 and step.cap > cap
+    (ta, la), (tb, lb) = out
+    assert la == lb
+    for a, b in zip(ta, tb):
+        assert torch.equal(a, b)
+
+
+def _worker(rank, port, root, q, cap=None):
     import torch.distributed as tdist
     from recbole_amd.trainer.fused import ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
@@ -144,21 +172,25 @@ def _worker(rank, port, root, q):
         torch.cuda.set_device(0)
         config, train, valid, test, model = _pipeline(root, 256)
         opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
-        step = ShardedBPRTrainStep(model, opt, train, chunk=CHUNK, dist=tdist.group.WORLD)
+        step = ShardedBPRTrainStep(model, opt, train, chunk=CHUNK, dist=tdist.group.WORLD,
+                                   cap=cap)
         tensors, losses = _train(step)
+        assert cap is None or step.cap_growths >= 1
         q.put((rank, step.Bg, step.SU, [t.numpy() for t in tensors], losses))
     finally:
         tdist.destroy_process_group()
 
 
-def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path):
+@pytest.mark.parametrize('cap', [None, 40])
+def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap):
+    """cap=40: both ranks detect the same overflow and grow cap identically."""
     from recbole_amd.trainer.fused import FusedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     root = str(tmp_path)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, root, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=600) for _ in range(2)]

@@ -37,7 +37,7 @@ def _loop_split(keys, ratios):
 @pytest.mark.parametrize('ratios', [[0.8, 0.1, 0.1], [0.5, 0.5], [1.0], [0.7, 0.2, 0.05, 0.05],
                                     [0.1, 0.1, 0.8]])
 def test_grouped_ratio_split_matches_loop(ratios):
-    from recbole_amd.data.dataset import _grouped_ratio_split
+    from recbole_amd.data.dataset.dataset import _grouped_ratio_split
     rng = np.random.default_rng(len(ratios))
     sizes = np.r_[np.arange(1, 25), rng.integers(1, 200, 300)]
     keys = np.repeat(rng.permutation(len(sizes)) * 7 + 3, sizes)
@@ -80,7 +80,7 @@ def test_cumulative_csr_matches_unique():
 
 def test_counting_order_is_stable_argsort():
     from recbole_amd import ops
-    from recbole_amd.data.dataset import _stable_order
+    from recbole_amd.data.dataset.dataset import _stable_order
     rng = np.random.default_rng(1)
     for n, space in ((0, 5), (10, 3), (100000, 7000), (50000, 60)):
         k = rng.integers(0, space, n)
@@ -91,13 +91,20 @@ def test_counting_order_is_stable_argsort():
 
 
 def test_atomic_reader_matches_pandas(tmp_path):
+    """_read_atomic == pd.read_csv (the reference's reader, dataset.py:342-408),
+    missing-value tokens included (quoted or not), for the token, float and
+    token_seq columns; also through the categorical (code) path."""
     import pandas as pd
-    from recbole_amd.data.dataset import _read_atomic
+    from recbole_amd.data.dataset.dataset import _read_atomic
     f = tmp_path / 'x.inter'
     f.write_text('user_id:token\titem_id:token\trating:float\tname:token_seq\tts:float\n'
                  '1\t007\t4.5\ta b\t878887116\n'
                  'x\t\t\t\t1.0000000000000002\n'
-                 '"q"\t12\t3\tc\t-0\n')
+                 '"q"\t12\t3\tc\t-0\n'
+                 # pandas' missing-value tokens (None, <NA>, a quoted empty field, NA)
+                 'None\t<NA>\tNone\t""\tNA\n'
+                 '""\tNA\t<NA>\tnull\t2\n'
+                 '"NA"\tn/a\t1\tNone\t3\n')
     cols = ['user_id:token', 'item_id:token', 'rating:float', 'name:token_seq', 'ts:float']
     dt = {c: (np.float64 if c.endswith(':float') else str) for c in cols}
     got = _read_atomic(str(f), '\t', cols, dt)
@@ -111,11 +118,17 @@ def test_atomic_reader_matches_pandas(tmp_path):
                 assert isinstance(a, float) and np.isnan(a), (c, a)
             else:
                 assert a == b and type(a) is type(b), (c, a, b)
+    cat = _read_atomic(str(f), '\t', cols, dt, cat_cols=('user_id:token', 'item_id:token'))
+    for c in ('user_id:token', 'item_id:token'):
+        g = np.asarray(cat[c], dtype=object)
+        e = exp[c].values
+        assert [x if isinstance(x, str) else None for x in g] == \
+            [x if isinstance(x, str) else None for x in e], c
 
 
 def test_factorize_pieces_matches_pandas():
     import pandas as pd
-    from recbole_amd.data.dataset import _factorize
+    from recbole_amd.data.dataset.dataset import _factorize
     rng = np.random.default_rng(4)
     toks = np.array([f't{x}' for x in rng.integers(0, 40, 500)], dtype=object)
     toks[rng.integers(0, 500, 20)] = np.nan
@@ -151,7 +164,7 @@ def _loop_loo(keys, leave_one_num):
 
 @pytest.mark.parametrize('leave_one_num', [1, 2, 3])
 def test_grouped_leave_one_out_matches_loop(leave_one_num):
-    from recbole_amd.data.dataset import _grouped_leave_one_out
+    from recbole_amd.data.dataset.dataset import _grouped_leave_one_out
     rng = np.random.default_rng(leave_one_num)
     sizes = np.r_[np.arange(1, 8), rng.integers(1, 60, 400)]
     keys = np.repeat(rng.permutation(len(sizes)) * 3 + 1, sizes)
