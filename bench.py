@@ -58,29 +58,85 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
     return u[order], i[order], n_users + 1, n_items + 1
 
 
+C2_NAME = 'c2-synth'
+
+
+def write_c2_inter(path, u, i, seed=2020):
+    """The synthetic interactions as an atomic `.inter` file in the ml-20m layout
+    (user_id:token, item_id:token, rating:float, timestamp:float; tab separated), so the
+    benchmark's dataset goes through the reference's loading path (dataset.py:342-408
+    read, 908-928 factorize remap, 1281-1315 RO_RS split). Arrow's CSV writer; the
+    header is written as the reference's atomic files spell it."""
+    import pyarrow as pa
+    import pyarrow.csv as pacsv
+    rng = np.random.default_rng(seed + 1)
+    rating = rng.integers(1, 11, len(u)) / 2.0
+    ts = (789652009 + np.sort(rng.integers(0, 600_000_000, len(u)))).astype(np.float64)
+    tb = pa.table({'u': u, 'i': i, 'r': rating, 't': ts})
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + '.part'
+    with open(tmp, 'wb') as f:
+        f.write(b'user_id:token\titem_id:token\trating:float\ttimestamp:float\n')
+        pacsv.write_csv(tb, f, pacsv.WriteOptions(include_header=False, delimiter='\t'))
+    os.replace(tmp, path)
+
+
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
-                   dist=None, chunk=None, sharded=False, alias=False):
+                   dist=None, chunk=None, sharded=False, alias=False, fused_step=None,
+                   source='file'):
+    """C2 through the drop-in path. source='file' (default): the synthetic interactions
+    are written as an atomic file (MIREC_BENCH_DATA, default /tmp/mirec_bench; reused
+    when present) and built by create_dataset -> data_preparation, the reference's
+    pipeline; source='memory': Dataset.from_interactions of the same arrays (no file).
+    The step object carries the setup timings (step.setup_info)."""
     from recbole_amd.config import Config
-    from recbole_amd.data import data_preparation
+    from recbole_amd.data import create_dataset, data_preparation
     from recbole_amd.data.dataset import Dataset
     from recbole_amd.model.general_recommender import BPR
     from recbole_amd.trainer.fused import FusedBPRTrainStep, ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     from recbole_amd.utils import init_seed
-    config = Config(model='BPR', dataset='synthetic-ml20m', config_dict={
-        'data_path': ROOT, 'embedding_size': d, 'training_neg_sample_num': neg,
-        'train_batch_size': batch_rows, 'eval_setting': 'RO_RS,full', 'use_gpu': True,
-        'state': 'ERROR', 'neg_sampling_alias': alias})
+    info = {'source': source}
+    root = os.environ.get('MIREC_BENCH_DATA', '/tmp/mirec_bench')
+    path = os.path.join(root, C2_NAME, f'{C2_NAME}.inter')
+    cd = {'data_path': root if source == 'file' else ROOT, 'embedding_size': d,
+          'training_neg_sample_num': neg, 'train_batch_size': batch_rows,
+          'eval_setting': 'RO_RS,full', 'use_gpu': True, 'state': 'ERROR',
+          'neg_sampling_alias': alias,
+          'load_col': {'inter': ['user_id', 'item_id', 'rating', 'timestamp']}}
+    t = time.perf_counter()
+    if source == 'memory' or not os.path.exists(path):
+        u, i, nU, nI = make_c2(seed)
+        info['generate_s'] = round(time.perf_counter() - t, 2)
+        if source == 'file':
+            t = time.perf_counter()
+            write_c2_inter(path, u, i, seed)
+            info['write_s'] = round(time.perf_counter() - t, 2)
+    if source == 'file':
+        info['file'] = path
+        info['file_mb'] = round(os.path.getsize(path) / 2 ** 20, 1)
+    config = Config(model='BPR', dataset=C2_NAME if source == 'file' else 'synthetic-ml20m',
+                    config_dict=cd)
     config['device'] = dev
     init_seed(config['seed'], config['reproducibility'])
-    u, i, nU, nI = make_c2(seed)
-    ds = Dataset.from_interactions(config, u, i, nU, nI)
+    t = time.perf_counter()
+    if source == 'file':
+        ds = create_dataset(config)
+    else:
+        ds = Dataset.from_interactions(config, u, i, nU, nI)
+    info['create_dataset_s'] = round(time.perf_counter() - t, 2)
+    t = time.perf_counter()
     train, valid, test = data_preparation(config, ds)
+    info['data_preparation_s'] = round(time.perf_counter() - t, 2)
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
-    cls = ShardedBPRTrainStep if sharded else FusedBPRTrainStep
-    return config, train, test, model, opt, cls(model, opt, train, adam_mode=adam_mode,
-                                                dist=dist, chunk=chunk)
+    if sharded:
+        step = ShardedBPRTrainStep(model, opt, train, adam_mode=adam_mode, dist=dist, chunk=chunk)
+    else:
+        step = FusedBPRTrainStep(model, opt, train, adam_mode=adam_mode, dist=dist, chunk=chunk,
+                                 fused_step=fused_step)
+    step.setup_info = info
+    return config, train, test, model, opt, step
 
 
 def pmc_bytes(substr):
@@ -140,22 +196,36 @@ def roofline(step, events, uniq, d, M):
     kernels_us = {k: round(float(np.mean(v)) * 1e6, 2) for k, v in per.items()}
     R, B, T = d * 4, step.B, step.times
     rowsI = (1 + T) * B
-    bpr_bytes = 2 * (B + rowsI) * R + (B + rowsI) * 8 + B * 4
-    t_bpr = kernels_us['bpr'] * 1e-6
-    tb, _ = pmc_bytes(f'bpr_fwd_bwd_kernel<{d}>')
-    bpr = {'kernel': f'K3 bpr_fwd_bwd<{d}>', 'bound': 'hbm', 'traffic': tb,
-           'achieved': round(bpr_bytes / t_bpr / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-           'frac': round(bpr_bytes / t_bpr / 1e9 / HBM_PEAK_GBS, 4),
-           'bytes_per_launch': bpr_bytes, 'avg_launch_us': kernels_us['bpr']}
-    # K5 kernel time: touched updates + look-ahead catch-ups (side stream, beside K3) + flush
-    t_adam = sum(per.get('adam', [])) + sum(per.get('ahead', [])) + sum(per.get('flush', []))
+    fused = 'step' in per                      # K35: BPR + Adam step + look-ahead, one launch
+    bpr = None
+    if 'bpr' in per:
+        bpr_bytes = 2 * (B + rowsI) * R + (B + rowsI) * 8 + B * 4
+        t_bpr = kernels_us['bpr'] * 1e-6
+        tb, _ = pmc_bytes(f'bpr_fwd_bwd_kernel<{d}>')
+        bpr = {'kernel': f'K3 bpr_fwd_bwd<{d}>', 'bound': 'hbm', 'traffic': tb,
+               'achieved': round(bpr_bytes / t_bpr / 1e9, 1), 'peak': HBM_PEAK_GBS,
+               'unit': 'GB/s', 'frac': round(bpr_bytes / t_bpr / 1e9 / HBM_PEAK_GBS, 4),
+               'bytes_per_launch': bpr_bytes, 'avg_launch_us': kernels_us['bpr']}
+    # kernel time of the window's dense-Adam work: the per-step launches (K5 touched rows +
+    # look-ahead, or K35 which also holds the BPR forward/backward), entry catch-ups and
+    # the closing flush
+    step_key = 'step' if fused else 'adam'
+    t_adam = sum(per.get(step_key, [])) + sum(per.get('ahead', [])) + sum(per.get('flush', []))
     rows = getattr(step, 'SU', step.nU) + getattr(step, 'SI', step.nI)   # this rank's table rows
     flops = rows * d * M * ADAM_FLOPS
+    if fused:   # + the BPR arithmetic K35 also does: (1+T) dots of 2d and 8d per pair
+        flops += M * B * ((1 + T) * 2 * d + T * 8 * d)
     tf = flops / t_adam / 1e12
     flush_k = 'adam_flush_row_kernel' if d >= 64 else 'adam_flush_kernel'
-    name = ('K5 deferred dense Adam: adam_deferred_kernel<%d, float> x %d + %s<%d> x %d'
-            % (d, len(per.get('adam', [])) + len(per.get('ahead', [])), flush_k, d,
-               len(per.get('flush', []))))
+    per_k = f'bpr_adam_step_kernel<{d}>' if fused else f'adam_deferred_kernel<{d},'
+    nd, nf = len(per.get(step_key, [])) + len(per.get('ahead', [])), len(per.get('flush', []))
+    if fused:
+        name = ('K35 bpr_adam_step_kernel<%d> x %d (BPR fwd/bwd + touched-row Adam + '
+                'look-ahead, one launch per step) + %s<%d> x %d (+ entry catch-up x %d)'
+                % (d, len(per['step']), flush_k, d, nf, len(per.get('ahead', []))))
+    else:
+        name = ('K5 deferred dense Adam: adam_deferred_kernel<%d, float> x %d + %s<%d> x %d'
+                % (d, nd, flush_k, d, nf))
     if step.adam_mode == 'streamed':
         name = f'K5 adam_multi_kernel<{d}> x {len(per.get("adam", []))} (streamed dense Adam)'
     adam = {'kernel': name, 'bound': 'valu', 'achieved': round(tf, 2),
@@ -163,18 +233,18 @@ def roofline(step, events, uniq, d, M):
             'traffic': None, 'flops_per_window': flops, 'window_steps': M,
             'window_kernel_us': round(t_adam * 1e6, 1),
             'us_per_step': round(t_adam * 1e6 / M, 2),
-            'flops_formula': '(table rows on this rank) * d * steps * 13'}
-    nd, nf = len(per.get('adam', [])) + len(per.get('ahead', [])), len(per.get('flush', []))
+            'flops_formula': '(table rows on this rank) * d * steps * 13'
+                             + (' + steps * B * ((1+T)*2d + 8dT) (BPR)' if fused else '')}
     if step.adam_mode == 'deferred':
-        bd, src = pmc_bytes(f'adam_deferred_kernel<{d},')
+        bd, src = pmc_bytes(per_k)
         bf, _ = pmc_bytes(f'{flush_k}<{d}>')
-        vd, td, bd_busy, vsrc = pmc_valu_insts(f'adam_deferred_kernel<{d},')
+        vd, td, bd_busy, vsrc = pmc_valu_insts(per_k)
         vf, tf_, bf_busy, _ = pmc_valu_insts(f'{flush_k}<{d}>')
         if bd_busy is not None and bf_busy is not None:
-            # measured VALU pipe occupancy of the two K5 kernels (PMC pass, tools/
-            # prof_pmc.sh: 4 * SQ_ACTIVE_INST_VALU / (SIMDs * clock * duration))
-            adam.update({'valu_busy_frac_deferred': bd_busy, 'valu_busy_frac_flush': bf_busy,
-                         'valu_source': vsrc})
+            # measured VALU pipe occupancy of the per-step kernel and the flush (PMC pass,
+            # tools/prof_pmc.sh: 4 * SQ_ACTIVE_INST_VALU / (SIMDs * clock * duration))
+            adam.update({'valu_busy_frac_' + ('step' if fused else 'deferred'): bd_busy,
+                         'valu_busy_frac_flush': bf_busy, 'valu_source': vsrc})
         if vd is not None and vf is not None:
             insts = nd * vd + nf * vf
             trans = nd * td + nf * tf_
@@ -246,12 +316,13 @@ def _cpu_model():
 def cpu_baseline(train, step_obj, d, neg, steps, warmup=20, runs=3):
     """SURVEY.md §8d protocol: the oracle's faithful CPU restatement of the
     reference step, `warmup` untimed steps then `steps` timed steps, median of
-    `runs` runs, torch threads = the host's cores (capped at 16: the box's share)."""
+    `runs` runs, torch threads = the CPUs this job may use (sched_getaffinity capped by
+    the cgroup CPU quota, oracle.cpu_baseline.host_threads; recorded in the JSON)."""
     from oracle import cpu_baseline as cb
     users = train.dataset.inter_feat['user_id'].cpu().numpy()
     items = train.dataset.inter_feat['item_id'].cpu().numpy()
     ptr, cols = train.sampler.used_csr['train']
-    threads = min(16, os.cpu_count() or 1)
+    threads, how = cb.host_threads()
     vals, dts = [], []
     for r in range(runs):
         pps, dt, used = cb.time_bpr_steps(users, items, ptr, cols, train.sampler.random_list,
@@ -262,7 +333,7 @@ def cpu_baseline(train, step_obj, d, neg, steps, warmup=20, runs=3):
     return {'value': round(float(np.median(vals)), 1), 'unit': 'positives/s', 'cores': used,
             'kind': 'port', 'runs': [round(v, 1) for v in vals],
             'nproc': os.cpu_count(), 'cpu_model': _cpu_model(),
-            'torch_threads': used,
+            'torch_threads': used, 'threads_derivation': how,
             'sample': f'median of {runs} runs of {warmup} warm-up + {steps} timed C2 steps '
                       f'({steps * step_obj.B} positives x {neg} negatives per run) of the oracle '
                       f'restatement: Python rejection sampler + torch-CPU nn.Embedding/BPRLoss/'
@@ -311,6 +382,10 @@ def main():
     ap.add_argument('--ramp', default=None)
     # diagnostic: steps between deferred-Adam full flushes (default FLUSH_EVERY)
     ap.add_argument('--flush-every', type=int, default=None)
+    # diagnostic: the K3 + K5 launches per step instead of the one-launch K35 step
+    ap.add_argument('--no-fused-step', action='store_true')
+    # diagnostic: the synthetic interactions in memory instead of the atomic-file path
+    ap.add_argument('--in-memory', action='store_true')
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -338,7 +413,8 @@ def main():
     config, train, test, model, opt, step = build_workload(
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
         dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded',
-        alias=args.sampler == 'alias')
+        alias=args.sampler == 'alias', fused_step=False if args.no_fused_step else None,
+        source='memory' if args.in_memory else 'file')
     if args.ramp:
         step.RAMP = tuple(int(x) for x in args.ramp.split(','))
     if args.flush_every:
@@ -445,7 +521,9 @@ def main():
         'kernels_us': kernels_us,
         'ranks': per_rank,
         'adam_mode': step.adam_mode,
+        'fused_step': bool(getattr(step, 'fused_step', False)),
         'setup_s': round(setup_s, 1),
+        'setup': step.setup_info,
     }
     if not args.no_eval and rank == 0:
         from recbole_amd.trainer.fused import fused_full_sort_eval

@@ -341,6 +341,9 @@ typedef struct mirec_adam_table {
   int32_t* last;            /* deferred schedule: steps applied per row    */
   const int32_t* ahead_uniq;   /* deferred: rows the next batch reads, sorted */
   const int32_t* ahead_n_uniq; /* device count of ahead_uniq (NULL = none)    */
+  float* p_alt;             /* deferred / flush: parity buffer of p (or NULL): the
+                               state after t applied steps lives in t & 1 ? p_alt : p
+                               (mirec_bpr_adam_step_f32); the flush also completes p */
 } mirec_adam_table;
 
 /* Streamed schedule: every row of every table, step index
@@ -375,11 +378,36 @@ int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n_tables,
 
 /* Flush of the deferred schedule: every row r of every table with
  * last[r] < t = step_base_dev[0] + step_off replays steps last[r]..t-1 with a
- * zero gradient; last[r] = t. After it, p, m, v equal the streamed result. */
+ * zero gradient; last[r] = t. After it, p, m, v equal the streamed result.
+ * With p_alt (parity buffers, d >= 64): rows are read from their state's buffer and
+ * written to t & 1 ? p_alt : p and to p; rows already current at an odd t are copied
+ * p_alt -> p — afterwards p holds every row (the parameter tensor is complete). */
 int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
                          const float* step_consts_dev, const int32_t* step_base_dev,
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
+
+/* K35 — one training step of the fused BPR path in ONE launch: BPR forward + backward
+ * (mirec_bpr_fwd_bwd_f32's arithmetic) and the deferred Adam step
+ * (mirec_adam_deferred_f32's arithmetic) of every touched row, and the look-ahead
+ * replays — results bit-identical to those two launches. Replaces, as one kernel,
+ * BPR.calculate_loss + BPRLoss + the embedding backward + optim.Adam.step (bpr.py:74-83,
+ * loss.py:43-49, trainer.py:157-174). tables[0] = users (grouping of user[0..Bc),
+ * contribution k = positive k), tables[1] = items (grouping of items[0..(1+T)Bc), the
+ * pairwise slots: positive k at k, negative j of k at Bc + j*Bc + k); each table needs
+ * p and p_alt (parity buffers: the state after t steps lives in t & 1 ? p_alt : p), m,
+ * v, last, perm / uniq / seg / n_uniq and optionally the look-ahead list; `rows` and
+ * `dense_grad` are unused / NULL. The step s = step_base_dev[0] + step_off reads every
+ * row from buffer s & 1 (all rows the batch reads must be complete through s - 1) and
+ * writes touched + look-ahead rows at state s + 1 to buffer (s + 1) & 1; zero-state rows
+ * must hold the same p in both buffers. loss_k[k] = sum_j -log(gamma + sigmoid(x_kj)).
+ * d in {64, 128, 256}; T >= 1. */
+int mirec_bpr_adam_step_f32(const mirec_adam_table* tables, const int64_t* n_max_uniq,
+                            int32_t d, const int64_t* user, const int64_t* items, int64_t Bc,
+                            int32_t T, float gamma, float grad_scale, float* loss_k,
+                            const float* step_consts_dev, const int32_t* step_base_dev,
+                            int32_t step_off, double beta1, double beta2, double eps,
+                            double weight_decay, void* stream);
 
 /* n device-to-device copies (src[i] -> dst[i], bytes[i]; host arrays of device
  * pointers) in one launch per 96 copies: the per-step copy of a batch's columns into

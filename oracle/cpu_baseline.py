@@ -36,6 +36,37 @@ class _LazySets(object):
         return s
 
 
+def host_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity),
+    capped by the cgroup CPU quota when one is set (cgroup v2 cpu.max, v1 cfs quota) — the
+    host share a job on the GPU box actually gets, not the machine's core count. Returns
+    (threads, record) with how the number was derived (written into the bench JSON)."""
+    import math
+    import os
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    quota = None
+    for path, parse in (('/sys/fs/cgroup/cpu.max', lambda t: t.split()),
+                        ('/sys/fs/cgroup/cpu/cpu.cfs_quota_us', None)):
+        try:
+            txt = open(path).read().strip()
+        except OSError:
+            continue
+        if parse is not None:
+            q, per = parse(txt)
+            if q != 'max':
+                quota = int(q) / int(per)
+        else:
+            q = int(txt)
+            per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            if q > 0:
+                quota = q / per
+        break
+    threads = aff if quota is None else max(1, min(aff, math.floor(quota)))
+    return threads, {'sched_getaffinity': aff, 'cgroup_cpu_quota': quota,
+                     'os_cpu_count': os.cpu_count(), 'threads': threads,
+                     'derivation': 'min(len(sched_getaffinity(0)), floor(cgroup CPU quota))'}
+
+
 def time_bpr_steps(users, items, used_ptr, used_cols, random_list, n_users, n_items, d, B, T,
                    steps=20, warmup=3, lr=1e-3, threads=None, seed=0):
     """Returns (positives_per_second, seconds_timed, threads_used)."""

@@ -45,7 +45,7 @@ class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
                 ('perm', _P), ('uniq', _P), ('seg', _P), ('n_uniq', _P), ('dense_grad', _P),
-                ('last', _P), ('ahead_uniq', _P), ('ahead_n_uniq', _P)]
+                ('last', _P), ('ahead_uniq', _P), ('ahead_n_uniq', _P), ('p_alt', _P)]
 
 
 class ChunkPrep(ctypes.Structure):
@@ -136,6 +136,10 @@ SIGNATURES = {
                                         _P]),
     "mirec_adam_flush_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
+    "mirec_bpr_adam_step_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, _P,
+                                        c_int64, c_int32, ctypes.c_float, ctypes.c_float, _P,
+                                        _P, _P, c_int32, c_double, c_double, c_double,
+                                        c_double, _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
     "mirec_chunk_finish": (c_int, [_P, c_int64, c_int64, c_int32, c_float, _P, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,

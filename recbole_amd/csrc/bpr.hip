@@ -12,7 +12,7 @@
 //   g = -(1/R) / (gamma + s);  dx = g * (1 - s) * s;  d pos = dx, d neg = -dx
 //   du = dx*p - dx*n, dp = dx*u, dn = -dx*u   (summed over the rows of a key
 //   by the segment reduction, K2/K5).
-#include "common.h"
+#include "bpr_math.h"
 
 namespace mirec {
 
@@ -49,36 +49,6 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, int lane, co
   } else {
     p[0] = x[0];
   }
-}
-
-template <int LPR>
-__device__ __forceinline__ float group_sum(float x) {
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-  return x;
-}
-
-__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
-  return ((a.x * b.x + a.y * b.y) + a.z * b.z) + a.w * b.w;
-}
-
-// Gradient contributions of one (positive, negative) row from its coefficient
-// dx = d loss / d (pos_score - neg_score): du += dx*p - dx*n, dp += dx*u,
-// dn = -dx*u, every product and sum rounded on its own. Shared by K3 and the
-// data-parallel rebuild (bpr_contrib_kernel), so both produce the same bits.
-__device__ __forceinline__ void pair_contrib(float4& gu, float4& gp, float4& gn, float dx,
-                                             const float4& u, const float4& p,
-                                             const float4& n) {
-#pragma clang fp contract(off)
-  gu.x += dx * p.x - dx * n.x;
-  gu.y += dx * p.y - dx * n.y;
-  gu.z += dx * p.z - dx * n.z;
-  gu.w += dx * p.w - dx * n.w;
-  gp.x += dx * u.x;
-  gp.y += dx * u.y;
-  gp.z += dx * u.z;
-  gp.w += dx * u.w;
-  gn = make_float4(-dx * u.x, -dx * u.y, -dx * u.z, -dx * u.w);
 }
 
 // D/4 lanes per positive (one float4 of every row per lane: 16-B loads, a 512-B
@@ -137,12 +107,9 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     for (int q = 0; q < NB; ++q) {
       const int j = j0 + q;
       if (j < times) {
-        const float x = sp - sn[q];
-        const float s = 1.f / (1.f + expf(-x));
-        const float gs = gamma + s;
-        lsum += -logf(gs);
-        const float gg = ng / gs;
-        const float dx = (gg * (1.f - s)) * s;
+        const BprCoef cf = bpr_coef(sp, sn[q], gamma, ng);
+        lsum += cf.nll;
+        const float dx = cf.dx;
         float4 gn;
         pair_contrib(gu, gp, gn, dx, u, p, n[q]);
         const int64_t r = (int64_t)j * B + k;

@@ -532,7 +532,28 @@ def adam_tables(specs):
             au, an = s["ahead"]
             t.ahead_uniq = ptr(_dev(au, torch.int32, "ahead_uniq"))
             t.ahead_n_uniq = ptr(_dev(an, torch.int32, "ahead_n_uniq"))
+        if s.get("p_alt") is not None:            # parity buffer (bpr_adam_step)
+            t.p_alt = ptr(_dev(s["p_alt"], torch.float32, "p_alt"))
+        if s.get("segs") is None and s.get("grouping") is not None:   # no gradient rows
+            g = s["grouping"]
+            t.perm, t.uniq, t.seg, t.n_uniq = ptr(g.perm), ptr(g.uniq), ptr(g.seg), ptr(g.n_uniq)
     return arr
+
+
+def bpr_adam_step(tables, n_max_uniq, d: int, user, items, Bc: int, times: int, grad_scale: float,
+                  loss_k, step_consts, step_base, step_off: int = 0, gamma: float = 1e-10,
+                  beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+    """K35: one training step (BPR forward/backward + the touched rows' deferred Adam
+    step + look-ahead) in one launch; tables = adam_tables([users, items]) with p_alt and
+    `grouping` (K2 of user / items without gradient rows)."""
+    import ctypes
+    for n_, t_ in (("user", user), ("items", items)):
+        _dev(t_, torch.int64, n_)
+    nm = (ctypes.c_int64 * 2)(*n_max_uniq)
+    rc = lib().mirec_bpr_adam_step_f32(tables, nm, d, ptr(user), ptr(items), Bc, times, gamma,
+                                       grad_scale, ptr(loss_k), ptr(step_consts), ptr(step_base),
+                                       step_off, beta1, beta2, eps, weight_decay, stream_handle())
+    check(rc, "mirec_bpr_adam_step_f32")
 
 
 def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,

@@ -163,7 +163,7 @@ class FusedBPRTrainStep(object):
     FLUSH_EVERY = 64
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
-                 adam_mode='deferred', dist=None):
+                 adam_mode='deferred', dist=None, fused_step=None):
         if adam_mode not in ADAM_MODES:
             raise ValueError(f'adam_mode must be one of {ADAM_MODES}, got {adam_mode!r}')
         self.model = model
@@ -222,6 +222,17 @@ class FusedBPRTrainStep(object):
         if deferred:
             self.lastU = torch.zeros(self.nU, dtype=torch.int32, device=dev)
             self.lastI = torch.zeros(self.nI, dtype=torch.int32, device=dev)
+        # K35 (csrc/step.hip): the model side of a step in ONE launch (BPR + the touched
+        # rows' Adam + look-ahead), bit-identical to K3 + K5. One GPU, deferred schedule;
+        # needs the parity buffers of p (state after t steps in t & 1 ? alt : p)
+        if fused_step is None:
+            fused_step = deferred and G == 1 and d in (64, 128, 256)
+        if fused_step and not (deferred and G == 1 and d in (64, 128, 256)):
+            raise ValueError('fused_step needs adam_mode="deferred", one rank and d in '
+                             '{64, 128, 256}')
+        self.fused_step = bool(fused_step)
+        self.pU_alt = torch.empty_like(self.pU.data) if self.fused_step else None
+        self.pI_alt = torch.empty_like(self.pI.data) if self.fused_step else None
         self._n_max = (ctypes.c_int64 * 2)(self.Bg, (1 + T) * self.Bg)
         g = self.opt.param_groups[0]
         self._adam_args = (g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'])
@@ -380,6 +391,9 @@ class FusedBPRTrainStep(object):
             t[0].last, t[1].last = self.lastU.data_ptr(), self.lastI.data_ptr()
         else:
             t[0].last = t[1].last = None
+        fs = getattr(self, 'fused_step', False)
+        t[0].p_alt = self.pU_alt.data_ptr() if fs else None
+        t[1].p_alt = self.pI_alt.data_ptr() if fs else None
 
     def _adam_state(self):
         """(m, v, deferred step counts) of each table."""
@@ -436,7 +450,7 @@ class FusedBPRTrainStep(object):
                                               self.xchg.data_ptr() + 4 * lay.coef0, B, lay.W,
                                               gU, gI, st), 'mirec_bpr_contrib_f32')
             self._record('contrib', stream, contrib)
-        else:
+        elif not self.fused_step:
             def bpr():
                 check(L.mirec_bpr_fwd_bwd_f32(self.pU.data_ptr(), self.nU, self.pI.data_ptr(),
                                               self.nI, d, user_g, keys_g, keys_g + 8 * Bc, Bc,
@@ -461,6 +475,18 @@ class FusedBPRTrainStep(object):
         else:
             t[0].ahead_uniq = t[0].ahead_n_uniq = t[1].ahead_uniq = t[1].ahead_n_uniq = None
 
+        if self.fused_step and not sharded:
+            # K35: BPR + touched-row Adam + look-ahead in one launch (no gradient rows)
+            def fused():
+                check(L.mirec_bpr_adam_step_f32(t, self._n_max, d, user_g, keys_g, Bc, T, 1e-10,
+                                                self._grad_scale(Bc), loss_p,
+                                                self.consts.data_ptr(),
+                                                self.step_idx.data_ptr(), step_off,
+                                                *self._adam_args, st), 'mirec_bpr_adam_step_f32')
+            self._record('step', stream, fused)
+            if self.kernel_events is not None:
+                self.kernel_uniq.append(torch.stack([slot.u_nu[c], slot.i_nu[c]]))
+            return
         if self.adam_mode == 'deferred':
             def adam():
                 check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
@@ -610,6 +636,9 @@ class FusedBPRTrainStep(object):
         if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
             for m, v, last in self._adam_state():   # zero-state rows: marked (adam.hip)
                 ops.zero_state_marks(m, v, last, self._adam_args[3])
+        if self.fused_step:                    # parity buffers: state 0 (and every
+            self.pU_alt.copy_(self.pU.data)    # zero-state row) valid in both
+            self.pI_alt.copy_(self.pI.data)
         ramps = (0,) if hold_prep_from is None else (0, int(hold_prep_from))
         self._plan, self._plan_starts = self._chunks(cuts, ramps), None
         self._flush_at = set(int(b) for b in flush_at)
@@ -793,7 +822,7 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         if adam_mode != 'deferred':
             raise ValueError('the row-sharded step runs the deferred Adam schedule')
         super().__init__(model, optimizer, train_data, chunk=chunk, use_graph=use_graph,
-                         adam_mode=adam_mode, dist=dist)
+                         adam_mode=adam_mode, dist=dist, fused_step=False)
         G, B, T, d, dev = self.G, self.B, self.times, self.d, self.device
         self.SU, self.SI = -(-self.nU // G), -(-self.nI // G)
         # rows per (slice, owner) message: the slice's (2+T)*B slots spread over G

@@ -148,10 +148,12 @@ class Trainer(AbstractTrainer):
                 # shard_tables: False asks for replicas
                 cls = (ShardedBPRTrainStep if self._dp is not None and mode == 'deferred'
                        and self.config['shard_tables'] is not False else FusedBPRTrainStep)
+                # fused_step (K35, one launch per step): None = where it applies
+                kw = {} if cls is ShardedBPRTrainStep else {'fused_step': self.config['fused_step']}
                 self._fused_step = cls(
                     self.model, self.optimizer, train_data,
                     use_graph=self.config['train_graph'] is not False, adam_mode=mode,
-                    dist=self._dp.group if self._dp is not None else None)
+                    dist=self._dp.group if self._dp is not None else None, **kw)
             losses = self._fused_step.run_epoch()
             total = None
             for v in losses:

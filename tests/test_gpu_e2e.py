@@ -105,16 +105,21 @@ def test_fit_matches_oracle(tmp_path, fused):
                                m.item_embedding.weight.detach(), rtol=1e-3, atol=2e-5)
 
 
-def test_fused_adam_schedules_bitwise_identical(tmp_path):
-    """Deferred and streamed dense Adam, graph-replayed chunks and eager steps:
-    identical bits in the weights, the optimizer state and the losses."""
+@pytest.mark.parametrize('d', [64, 256])
+def test_fused_adam_schedules_bitwise_identical(tmp_path, d):
+    """Deferred and streamed dense Adam, graph-replayed chunks and eager steps, the
+    one-launch K35 step (parity buffers) and the K3 + K5 launches: identical bits in the
+    weights, the optimizer state and the losses."""
     from recbole_amd.trainer.fused import FusedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     out = {}
-    for mode, graph in (('streamed', True), ('deferred', True), ('deferred', False)):
-        config, train, valid, test, model = _pipeline(tmp_path)
+    for mode, graph, k35 in (('streamed', True, False), ('deferred', True, True),
+                             ('deferred', False, True), ('deferred', True, False)):
+        config, train, valid, test, model = _pipeline(tmp_path, embedding_size=d)
         opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
-        fs = FusedBPRTrainStep(model, opt, train, chunk=8, use_graph=graph, adam_mode=mode)
+        fs = FusedBPRTrainStep(model, opt, train, chunk=8, use_graph=graph, adam_mode=mode,
+                               fused_step=k35)
+        assert fs.fused_step == k35
         losses = []
         for _ in range(2):
             nb = fs.begin_epoch()
@@ -122,8 +127,8 @@ def test_fused_adam_schedules_bitwise_identical(tmp_path):
             fs.run_batches(11, nb)
             losses += fs.end_epoch()
         st = [opt.state[p][k].cpu() for p in (fs.pU, fs.pI) for k in ('exp_avg', 'exp_avg_sq')]
-        out[(mode, graph)] = ([fs.pU.detach().cpu(), fs.pI.detach().cpu()] + st, losses)
-    ref_t, ref_l = out[('streamed', True)]
+        out[(mode, graph, k35)] = ([fs.pU.detach().cpu(), fs.pI.detach().cpu()] + st, losses)
+    ref_t, ref_l = out[('streamed', True, False)]
     for key, (ts, ls) in out.items():
         assert ls == ref_l, key
         for a, b in zip(ref_t, ts):

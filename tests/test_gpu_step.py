@@ -1,0 +1,149 @@
+"""K35 (csrc/step.hip, mirec_bpr_adam_step_f32): one launch per BPR training step —
+the owners of the touched rows form their own gradient contributions (BPR forward +
+backward, bpr.py:74-83, loss.py:43-49), add them in grouping order and apply the
+deferred Adam step, and the look-ahead rows replay — bit for bit against the two
+launches it replaces (K3 mirec_bpr_fwd_bwd_f32 + K5 mirec_adam_deferred_f32), on
+tables held in parity buffers (state t in buffer t & 1).
+
+Cases: d in {64, 128, 256}; T = 3 and 4 (a partial negative group); an even and an odd
+step; duplicate users; a hot item with 40 positive slots (10 contribution rounds of
+the block's 4 lane groups); look-ahead rows lagging 0..7 steps, in their parity
+buffer with the other buffer poisoned (NaN); zero-state rows."""
+import numpy as np
+import pytest
+import torch
+
+from recbole_amd import ops
+from recbole_amd.ops import ADAM_ZERO_STATE, Segments
+
+pytestmark = pytest.mark.gpu
+
+
+def _consts(dev, n=32):
+    from recbole_amd.trainer.optim import FusedAdam
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(4, device=dev))], lr=1e-3)
+    return torch.as_tensor(opt.step_constants(1, n).reshape(-1), device=dev)
+
+
+def _grouping(keys, space):
+    segs = Segments(keys.numel(), keys.device)
+    ws = ops.segment_sort_batched(keys, keys.numel(), space, segs.perm, segs.uniq, segs.seg,
+                                  segs.n_uniq)
+    segs.ws = ws
+    return segs
+
+
+@pytest.mark.parametrize('d,T,s', [(64, 3, 6), (128, 4, 7), (128, 4, 10), (256, 3, 9)])
+def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
+    g = torch.Generator().manual_seed(d * 100 + T * 10 + s)
+    nU, nI, Bc = 257, 301, 96
+    # batch 0 (the step) and batch 1 (whose rows the look-ahead completes)
+    user0 = torch.randint(0, nU, (Bc,), generator=g)
+    user0[5] = user0[17] = user0[60]                       # a user with 3 positives
+    user1 = torch.randint(0, nU, (Bc,), generator=g)
+    items0 = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
+    items0[:40] = 7                                         # hot item: 40 positive slots
+    items0[Bc + 3] = 7                                      # ... and a negative slot
+    items1 = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
+    pU = torch.randn(nU, d, generator=g) * 0.1
+    pI = torch.randn(nI, d, generator=g) * 0.1
+    mU, vU = torch.randn(nU, d, generator=g) * 1e-3, torch.rand(nU, d, generator=g) * 1e-5
+    mI, vI = torch.randn(nI, d, generator=g) * 1e-3, torch.rand(nI, d, generator=g) * 1e-5
+    # step counts: rows batch 0 reads are current (s); others lag 0..7; some zero-state
+    lastU = s - torch.randint(0, 8, (nU,), generator=g, dtype=torch.int32)
+    lastI = s - torch.randint(0, 8, (nI,), generator=g, dtype=torch.int32)
+    lastU[user0] = s
+    lastI[items0] = s
+    for m, v, last, read in ((mU, vU, lastU, user0), (mI, vI, lastI, items0)):
+        zs = torch.zeros(last.numel(), dtype=torch.bool)
+        zs[torch.randint(0, last.numel(), (last.numel() // 6,), generator=g)] = True
+        zs[read] = zs[read] & (torch.arange(read.numel()) % 2 == 0)   # some read rows too
+        m[zs], v[zs] = 0.0, 0.0
+        last[zs] = ADAM_ZERO_STATE
+    to = lambda x: x.to(dev)
+    consts = _consts(dev)
+    base = torch.tensor([s - 3], dtype=torch.int32, device=dev)     # step = base + 3
+    grad_scale = float(np.float32(1.0) / np.float32(Bc * T))
+
+    gu0, gi0 = _grouping(to(user0), nU), _grouping(to(items0), nI)
+    gu1, gi1 = _grouping(to(user1), nU), _grouping(to(items1), nI)
+    ahead = []
+    for a, b, n in ((gu0, gu1, nU), (gi0, gi1, nI)):
+        # rows batch 1 reads and batch 0 does not touch (the chunk layout of 2 batches)
+        stride = max(a.uniq.numel(), b.uniq.numel())
+        U = torch.zeros(2 * stride, dtype=torch.int32, device=dev)
+        N = torch.zeros(2, dtype=torch.int32, device=dev)
+        U[:a.uniq.numel()] = a.uniq
+        U[stride:stride + b.uniq.numel()] = b.uniq
+        N[0], N[1] = a.n_uniq[0], b.n_uniq[0]
+        out = torch.zeros(2 * stride, dtype=torch.int32, device=dev)
+        n_out = torch.zeros(2, dtype=torch.int32, device=dev)
+        ops.uniq_ahead_diff(U, N, stride, 2, out, n_out)
+        ahead.append((out[:stride].clone(), n_out[:1].clone()))
+    assert int(ahead[0][1]) > 0 and int(ahead[1][1]) > 0
+
+    # ---- reference: K3 on the single current tables, then K5 deferred
+    rU, rI = to(pU.clone()), to(pI.clone())
+    rmU, rvU, rmI, rvI = to(mU.clone()), to(vU.clone()), to(mI.clone()), to(vI.clone())
+    rlU, rlI = to(lastU.clone()), to(lastI.clone())
+    o = ops.bpr_fwd_bwd(rU, rI, to(user0), to(items0[:Bc]), to(items0[Bc:]), T,
+                        grad_scale=grad_scale)
+    tabs = ops.adam_tables([
+        {'p': rU, 'm': rmU, 'v': rvU, 'rows': o['gU'], 'segs': gu0, 'last': rlU,
+         'ahead': ahead[0]},
+        {'p': rI, 'm': rmI, 'v': rvI, 'rows': o['gI'], 'segs': gi0, 'last': rlI,
+         'ahead': ahead[1]}])
+    ops.adam_multi(tabs, d, consts, base, 3, schedule='deferred',
+                   n_max_uniq=[Bc, (1 + T) * Bc])
+
+    # ---- K35 on parity buffers: row state t in buffer t & 1, the other one poisoned
+    bufs = []
+    for p, last in ((pU, lastU), (pI, lastI)):
+        P = [torch.full_like(p, float('nan')), torch.full_like(p, float('nan'))]
+        for par in (0, 1):
+            sel = (last & 1) == par
+            P[par][sel] = p[sel]
+        zs = last == ADAM_ZERO_STATE                       # zero-state: both buffers
+        P[0][zs], P[1][zs] = p[zs], p[zs]
+        bufs.append([to(P[0]), to(P[1])])
+    fmU, fvU, fmI, fvI = to(mU.clone()), to(vU.clone()), to(mI.clone()), to(vI.clone())
+    flU, flI = to(lastU.clone()), to(lastI.clone())
+    tabs2 = ops.adam_tables([
+        {'p': bufs[0][0], 'p_alt': bufs[0][1], 'm': fmU, 'v': fvU, 'grouping': gu0,
+         'last': flU, 'ahead': ahead[0]},
+        {'p': bufs[1][0], 'p_alt': bufs[1][1], 'm': fmI, 'v': fvI, 'grouping': gi0,
+         'last': flI, 'ahead': ahead[1]}])
+    loss_k = torch.full((Bc,), float('nan'), device=dev)
+    ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, to(user0), to(items0), Bc, T, grad_scale,
+                      loss_k, consts, base, 3)
+    torch.cuda.synchronize()
+
+    assert torch.equal(loss_k, o['loss_k'])
+    for (P, rp), rl, fl, (rm, fm), (rv, fv) in (
+            ((bufs[0], rU), rlU, flU, (rmU, fmU), (rvU, fvU)),
+            ((bufs[1], rI), rlI, flI, (rmI, fmI), (rvI, fvI))):
+        assert torch.equal(rl, fl)
+        assert torch.equal(rm, fm) and torch.equal(rv, fv)
+        moved = (fl == s + 1)                              # touched + look-ahead rows
+        assert int(moved.sum()) > 0
+        wb = P[(s + 1) & 1]
+        assert torch.equal(wb[moved], rp[moved])
+        # rows not moved keep their state in their own buffer
+        keep = ~moved & (fl != ADAM_ZERO_STATE)
+        src = torch.where(((fl & 1) == 1)[:, None], P[1], P[0])
+        assert torch.equal(src[keep], rp[keep])
+
+
+def test_bpr_adam_step_rejects_bad_tables(dev):
+    from recbole_amd._native import NativeError
+    d, Bc, T = 64, 8, 2
+    p = torch.zeros(10, d, device=dev)
+    g = _grouping(torch.zeros(Bc, dtype=torch.int64, device=dev), 10)
+    tabs = ops.adam_tables([{'p': p, 'm': p, 'v': p, 'grouping': g,
+                             'last': torch.zeros(10, dtype=torch.int32, device=dev)}] * 2)
+    consts = _consts(dev)
+    base = torch.zeros(1, dtype=torch.int32, device=dev)
+    with pytest.raises(NativeError):            # no parity buffer
+        ops.bpr_adam_step(tabs, [Bc, 3 * Bc], d, torch.zeros(Bc, dtype=torch.int64, device=dev),
+                          torch.zeros(3 * Bc, dtype=torch.int64, device=dev), Bc, T, 0.1,
+                          torch.zeros(Bc, device=dev), consts, base)

@@ -55,19 +55,28 @@ class StubDataset:
         return self._num[field]
 
 
+MARKERS = os.environ.get('MODELS_MARKERS') == '1'   # trace markers (tools/step_breakdown.py)
+
+
 def _timed(fn, steps, warmup, opt=None):
     """Mean wall time per step over `steps` steps; with a deferred optimizer the
-    flush that completes every row is inside the timed region (no work skipped)."""
+    flush that completes every row is inside the timed region (no work skipped).
+    MODELS_MARKERS=1: two 1-cycle spin kernels bracket the timed region in a kernel
+    trace (tools/step_breakdown.py)."""
     for _ in range(warmup):
         fn()
     if opt is not None:
         opt.flush()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if MARKERS:
+        torch.cuda._sleep(1)
     for _ in range(steps):
         fn()
     if opt is not None:
         opt.flush()
+    if MARKERS:
+        torch.cuda._sleep(1)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps
 
@@ -171,14 +180,18 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
     cpu = None
     if CPU_BASELINE:
         from oracle import cpu_baseline as cb
-        thr = min(16, os.cpu_count() or 1)
-        sps, dt, used = cb.time_deepfm_steps(batches, [f'C{j}' for j in range(26)],
-                                             [nums[f'C{j}'] for j in range(26)],
-                                             [f'I{j}' for j in range(13)], d, [128, 128, 128],
-                                             steps=3, threads=thr)
+        thr, how = cb.host_threads()
+        runs = [cb.time_deepfm_steps(batches, [f'C{j}' for j in range(26)],
+                                     [nums[f'C{j}'] for j in range(26)],
+                                     [f'I{j}' for j in range(13)], d, [128, 128, 128],
+                                     steps=5, threads=thr) for _ in range(3)]
+        sps, used = float(np.median([r[0] for r in runs])), runs[0][2]
         cpu = {'value': round(sps, 1), 'unit': 'samples/s', 'cores': used, 'kind': 'port',
-               'sample': f'3 C4 steps of the oracle restatement on torch CPU (DeepFMCPU + dense '
-                         f'optim.Adam over every table), {dt:.1f} s'}
+               'threads_derivation': how, 'runs': [round(r[0], 1) for r in runs],
+               'sample': f'median of 3 runs of 1 warm-up + 5 timed C4 steps of the oracle '
+                         f'restatement on torch CPU (DeepFMCPU + dense optim.Adam over every '
+                         f'table; a bounded sample: one step moves the 2.1 GB tables several '
+                         f'times), {sum(r[1] for r in runs):.1f} s timed in all'}
     return {
         'cpu_baseline': cpu,
         'adam_mode': ADAM_MODE, 'graph_step': bool(GRAPH_STEP),
@@ -272,12 +285,16 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
     cpu = None
     if CPU_BASELINE:
         from oracle import cpu_baseline as cb
-        thr = min(16, os.cpu_count() or 1)
-        sps, dt, used = cb.time_sasrec_steps(batches, random_list.cpu().numpy(), n_items, L, d,
-                                             n_neg, steps=2, threads=thr)
+        thr, how = cb.host_threads()
+        runs = [cb.time_sasrec_steps(batches, random_list.cpu().numpy(), n_items, L, d, n_neg,
+                                     steps=2, threads=thr) for _ in range(3)]
+        sps, used = float(np.median([r[0] for r in runs])), runs[0][2]
         cpu = {'value': round(sps, 1), 'unit': 'sequences/s', 'cores': used, 'kind': 'port',
-               'sample': f'2 C3 steps of the oracle restatement on torch CPU (numpy walk, '
-                         f'SASRecCPU + sampled softmax, dense optim.Adam), {dt:.1f} s'}
+               'threads_derivation': how, 'runs': [round(r[0], 1) for r in runs],
+               'sample': f'median of 3 runs of 1 warm-up + 2 timed C3 steps of the oracle '
+                         f'restatement on torch CPU (numpy walk, SASRecCPU + sampled softmax, '
+                         f'dense optim.Adam over the 1.5 GB item table; a bounded sample), '
+                         f'{sum(r[1] for r in runs):.1f} s timed in all'}
     return {
         'cpu_baseline': cpu,
         'adam_mode': ADAM_MODE,
@@ -363,13 +380,16 @@ def bench_c5(dev, scale=1.0, d=256, n_layers=2, K=10, sample_users=131072):
     cpu = None
     if CPU_BASELINE:
         from oracle import cpu_baseline as cb
-        thr = min(16, os.cpu_count() or 1)
+        thr, how = cb.host_threads()
         nc = 512
-        ups, dt, used = cb.time_full_sort_users(Uq[:nc].cpu(), out_i.cpu(), nc, K=K,
-                                                threads=thr)
+        uq, it = Uq[:nc].cpu(), out_i.cpu()
+        runs = [cb.time_full_sort_users(uq, it, nc, K=K, threads=thr) for _ in range(3)]
+        ups, used = float(np.median([r[0] for r in runs])), runs[0][2]
         cpu = {'value': round(ups, 1), 'unit': 'users/s', 'cores': used, 'kind': 'port',
-               'sample': f'{nc} users ranked on torch CPU as the reference does (U[u] @ I^T, '
-                         f'pad mask, flip + topk), {dt:.1f} s'}
+               'threads_derivation': how, 'runs': [round(r[0], 1) for r in runs],
+               'sample': f'median of 3 runs of {nc} users ranked on torch CPU as the reference '
+                         f'does (U[u] @ I^T, pad mask, flip + topk), '
+                         f'{sum(r[1] for r in runs):.1f} s timed in all'}
     return {
         'cpu_baseline': cpu,
         'config': 'C5', 'metric': 'full-sort eval users/s', 'value': round(n / tf, 1),
