@@ -261,6 +261,8 @@ typedef struct mirec_chunk_prep {
   /* alias fast mode (alias_thr != NULL): mirec_sample_alias replaces the walk */
   const uint32_t* alias_thr; const int32_t* alias_idx; int64_t n_alias;
   uint64_t alias_seed, alias_counter;
+  /* K35 records (u_rec != NULL): mirec_step_records after the groupings */
+  int32_t *u_rec, *u_crec, *i_rec, *i_crec;
 } mirec_chunk_prep;
 int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
 /* The two halves of mirec_prepare_chunk, for two streams (the caller orders
@@ -392,22 +394,40 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
  * (mirec_adam_deferred_f32's arithmetic) of every touched row, and the look-ahead
  * replays — results bit-identical to those two launches. Replaces, as one kernel,
  * BPR.calculate_loss + BPRLoss + the embedding backward + optim.Adam.step (bpr.py:74-83,
- * loss.py:43-49, trainer.py:157-174). tables[0] = users (grouping of user[0..Bc),
- * contribution k = positive k), tables[1] = items (grouping of items[0..(1+T)Bc), the
- * pairwise slots: positive k at k, negative j of k at Bc + j*Bc + k); each table needs
- * p and p_alt (parity buffers: the state after t steps lives in t & 1 ? p_alt : p), m,
- * v, last, perm / uniq / seg / n_uniq and optionally the look-ahead list; `rows` and
- * `dense_grad` are unused / NULL. The step s = step_base_dev[0] + step_off reads every
+ * loss.py:43-49, trainer.py:157-174). tables[0] = users (grouping of the batch's user
+ * keys, contribution k = positive k), tables[1] = items (grouping of its (1+T)*Bc item
+ * keys, the pairwise slots: positive k at k, negative j of k at Bc + j*Bc + k); each
+ * table needs p and p_alt (parity buffers: the state after t steps lives in
+ * t & 1 ? p_alt : p), m, v, last, n_uniq and optionally the look-ahead list; `rows` and
+ * `dense_grad` are unused / NULL. The touched rows come as the records of
+ * mirec_step_records (u_rec / i_rec: one per touched-row slot; u_crec / i_crec: one per
+ * grouped position) of this batch. The step s = step_base_dev[0] + step_off reads every
  * row from buffer s & 1 (all rows the batch reads must be complete through s - 1) and
  * writes touched + look-ahead rows at state s + 1 to buffer (s + 1) & 1; zero-state rows
  * must hold the same p in both buffers. loss_k[k] = sum_j -log(gamma + sigmoid(x_kj)).
- * d in {64, 128, 256}; T >= 1. */
+ * items = the batch's item keys (read only for negatives past the 4th). d in
+ * {64, 128, 256}; T >= 1. */
 int mirec_bpr_adam_step_f32(const mirec_adam_table* tables, const int64_t* n_max_uniq,
-                            int32_t d, const int64_t* user, const int64_t* items, int64_t Bc,
-                            int32_t T, float gamma, float grad_scale, float* loss_k,
+                            int32_t d, const int64_t* items, int64_t Bc, int32_t T, float gamma,
+                            float grad_scale, float* loss_k, const int32_t* u_rec,
+                            const int32_t* u_crec, const int32_t* i_rec, const int32_t* i_crec,
                             const float* step_consts_dev, const int32_t* step_base_dev,
                             int32_t step_off, double beta1, double beta2, double eps,
                             double weight_decay, void* stream);
+/* The K35 records of n_batches consecutive batches (strides per batch: Bc user keys,
+ * (1+T)*Bc item keys; the groupings of mirec_segment_sort_batched / the chunk
+ * preparation). Contribution record (8 int32) per grouped position i: positive k,
+ * negative slot j (-1 for a user slot or a positive slot), user id, positive item id,
+ * the first 4 negatives' ids (ids clamped to the table as K3 clamps them). Row record
+ * (20 int32) per touched-row slot u: row id, first position, contribution count, 0,
+ * then the records of its first two contributions. u_rec / i_rec: per batch Bc /
+ * (1+T)*Bc slots x 20 int32; u_crec / i_crec: per batch Bc / (1+T)*Bc positions x 8. */
+int mirec_step_records(const int64_t* user_keys, const int64_t* item_keys, int64_t n_batches,
+                       int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
+                       const int32_t* u_perm, const int32_t* u_uniq, const int32_t* u_seg,
+                       const int32_t* u_nu, const int32_t* i_perm, const int32_t* i_uniq,
+                       const int32_t* i_seg, const int32_t* i_nu, int32_t* u_rec,
+                       int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, void* stream);
 
 /* n device-to-device copies (src[i] -> dst[i], bytes[i]; host arrays of device
  * pointers) in one launch per 96 copies: the per-step copy of a batch's columns into

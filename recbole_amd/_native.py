@@ -62,7 +62,8 @@ class ChunkPrep(ctypes.Structure):
                 ('i_perm', _P), ('i_uniq', _P), ('i_seg', _P), ('i_nu', _P),
                 ('u_ahead', _P), ('u_nah', _P), ('i_ahead', _P), ('i_nah', _P),
                 ('alias_thr', _P), ('alias_idx', _P), ('n_alias', c_int64),
-                ('alias_seed', ctypes.c_uint64), ('alias_counter', ctypes.c_uint64)]
+                ('alias_seed', ctypes.c_uint64), ('alias_counter', ctypes.c_uint64),
+                ('u_rec', _P), ('u_crec', _P), ('i_rec', _P), ('i_crec', _P)]
 
 
 # Every symbol include/mirec.h declares: name -> (restype, argtypes)
@@ -136,10 +137,12 @@ SIGNATURES = {
                                         _P]),
     "mirec_adam_flush_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
-    "mirec_bpr_adam_step_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, _P,
-                                        c_int64, c_int32, ctypes.c_float, ctypes.c_float, _P,
-                                        _P, _P, c_int32, c_double, c_double, c_double,
-                                        c_double, _P]),
+    "mirec_bpr_adam_step_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, c_int64,
+                                        c_int32, ctypes.c_float, ctypes.c_float, _P, _P, _P,
+                                        _P, _P, _P, _P, c_int32, c_double, c_double,
+                                        c_double, c_double, _P]),
+    "mirec_step_records": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64, _P, _P,
+                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
     "mirec_chunk_finish": (c_int, [_P, c_int64, c_int64, c_int32, c_float, _P, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,

@@ -540,19 +540,38 @@ def adam_tables(specs):
     return arr
 
 
-def bpr_adam_step(tables, n_max_uniq, d: int, user, items, Bc: int, times: int, grad_scale: float,
-                  loss_k, step_consts, step_base, step_off: int = 0, gamma: float = 1e-10,
-                  beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_users: int,
+                 n_items: int, gu, gi):
+    """K35 records (mirec_step_records) of n_batches batches from their K2 groupings
+    gu / gi (Segments or any object with perm, uniq, seg, n_uniq; per-batch strides Bc
+    and (1+T)*Bc): (u_rec, u_crec, i_rec, i_crec) int32 device tensors."""
+    for n_, t_ in (("user_keys", user_keys), ("item_keys", item_keys)):
+        _dev(t_, torch.int64, n_)
+    dev = user_keys.device
+    KI = (1 + times) * Bc
+    out = [torch.empty(n_batches * n * w, dtype=torch.int32, device=dev)
+           for n, w in ((Bc, 20), (Bc, 8), (KI, 20), (KI, 8))]
+    rc = lib().mirec_step_records(ptr(user_keys), ptr(item_keys), n_batches, Bc, times, n_users,
+                                  n_items, ptr(gu.perm), ptr(gu.uniq), ptr(gu.seg),
+                                  ptr(gu.n_uniq), ptr(gi.perm), ptr(gi.uniq), ptr(gi.seg),
+                                  ptr(gi.n_uniq), *[ptr(o) for o in out], stream_handle())
+    check(rc, "mirec_step_records")
+    return out
+
+
+def bpr_adam_step(tables, n_max_uniq, d: int, items, Bc: int, times: int, grad_scale: float,
+                  loss_k, records, step_consts, step_base, step_off: int = 0,
+                  gamma: float = 1e-10, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
     """K35: one training step (BPR forward/backward + the touched rows' deferred Adam
     step + look-ahead) in one launch; tables = adam_tables([users, items]) with p_alt and
-    `grouping` (K2 of user / items without gradient rows)."""
+    a grouping (n_uniq); records = step_records(...) of this batch."""
     import ctypes
-    for n_, t_ in (("user", user), ("items", items)):
-        _dev(t_, torch.int64, n_)
+    _dev(items, torch.int64, "items")
     nm = (ctypes.c_int64 * 2)(*n_max_uniq)
-    rc = lib().mirec_bpr_adam_step_f32(tables, nm, d, ptr(user), ptr(items), Bc, times, gamma,
-                                       grad_scale, ptr(loss_k), ptr(step_consts), ptr(step_base),
-                                       step_off, beta1, beta2, eps, weight_decay, stream_handle())
+    rc = lib().mirec_bpr_adam_step_f32(tables, nm, d, ptr(items), Bc, times, gamma, grad_scale,
+                                       ptr(loss_k), *[ptr(r) for r in records], ptr(step_consts),
+                                       ptr(step_base), step_off, beta1, beta2, eps, weight_decay,
+                                       stream_handle())
     check(rc, "mirec_bpr_adam_step_f32")
 
 

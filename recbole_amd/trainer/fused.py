@@ -50,6 +50,9 @@ from recbole_amd import ops
 from recbole_amd._native import AdamTable, check, lib
 from recbole_amd.trainer.exchange import ExchangeLayout
 
+# K35 record widths (int32 per touched-row slot / per grouped position, include/mirec.h
+# mirec_step_records)
+REC_ROW, REC_CONTRIB = 20, 8
 ADAM_MODES = ('deferred', 'streamed')
 
 
@@ -128,6 +131,7 @@ class _Slot(object):
             self.u_nah = torch.zeros(C, dtype=torch.int32, device=dev)
             self.i_ahead = torch.empty(C * KI, dtype=torch.int32, device=dev)
             self.i_nah = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.records = None          # K35 row / contribution records (FusedBPRTrainStep)
         self.ready = torch.cuda.Event()
         self.walked = torch.cuda.Event()
         self.free = torch.cuda.Event()
@@ -233,6 +237,12 @@ class FusedBPRTrainStep(object):
         self.fused_step = bool(fused_step)
         self.pU_alt = torch.empty_like(self.pU.data) if self.fused_step else None
         self.pI_alt = torch.empty_like(self.pI.data) if self.fused_step else None
+        if self.fused_step:          # K35 records per slot (mirec_step_records, prep stream)
+            KIg = (1 + T) * self.Bg
+            for sl in self.slots:
+                sl.records = [torch.empty(self.C * n * w, dtype=torch.int32, device=dev)
+                              for n, w in ((self.Bg, REC_ROW), (self.Bg, REC_CONTRIB),
+                                           (KIg, REC_ROW), (KIg, REC_CONTRIB))]
         self._n_max = (ctypes.c_int64 * 2)(self.Bg, (1 + T) * self.Bg)
         g = self.opt.param_groups[0]
         self._adam_args = (g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'])
@@ -373,6 +383,8 @@ class FusedBPRTrainStep(object):
             if self.adam_mode == 'deferred':
                 setattr(cp, f'{tag}_ahead', getattr(slot, f'{tag}_ahead').data_ptr())
                 setattr(cp, f'{tag}_nah', getattr(slot, f'{tag}_nah').data_ptr())
+        if slot.records is not None:
+            cp.u_rec, cp.u_crec, cp.i_rec, cp.i_crec = (r.data_ptr() for r in slot.records)
         slot.prep = cp
         return cp
 
@@ -476,10 +488,15 @@ class FusedBPRTrainStep(object):
             t[0].ahead_uniq = t[0].ahead_n_uniq = t[1].ahead_uniq = t[1].ahead_n_uniq = None
 
         if self.fused_step and not sharded:
-            # K35: BPR + touched-row Adam + look-ahead in one launch (no gradient rows)
+            # K35: BPR + touched-row Adam + look-ahead in one launch (no gradient rows),
+            # the touched rows from the chunk's records (built on the prep stream)
+            rec = [r.data_ptr() + 4 * c * n * w for r, (n, w) in zip(
+                slot.records, ((Bc, REC_ROW), (Bc, REC_CONTRIB), (KI, REC_ROW),
+                               (KI, REC_CONTRIB)))]
+
             def fused():
-                check(L.mirec_bpr_adam_step_f32(t, self._n_max, d, user_g, keys_g, Bc, T, 1e-10,
-                                                self._grad_scale(Bc), loss_p,
+                check(L.mirec_bpr_adam_step_f32(t, self._n_max, d, keys_g, Bc, T, 1e-10,
+                                                self._grad_scale(Bc), loss_p, *rec,
                                                 self.consts.data_ptr(),
                                                 self.step_idx.data_ptr(), step_off,
                                                 *self._adam_args, st), 'mirec_bpr_adam_step_f32')

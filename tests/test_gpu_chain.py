@@ -34,7 +34,7 @@ def _train_arrays(train):
 
 def test_c2_chunk_chain_from_seed(dev):
     import bench
-    config, train, test, model, opt, step = bench.build_workload(dev)
+    config, train, test, model, opt, step = bench.build_workload(dev, source='memory')
     tu, ti = _train_arrays(train)
     rl = np.asarray(train.sampler.random_list).copy()
     init = [p.detach().cpu().clone() for p in (step.pU, step.pI)]

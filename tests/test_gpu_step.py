@@ -5,9 +5,10 @@ deferred Adam step, and the look-ahead rows replay — bit for bit against the t
 launches it replaces (K3 mirec_bpr_fwd_bwd_f32 + K5 mirec_adam_deferred_f32), on
 tables held in parity buffers (state t in buffer t & 1).
 
-Cases: d in {64, 128, 256}; T = 3 and 4 (a partial negative group); an even and an odd
-step; duplicate users; a hot item with 40 positive slots (10 contribution rounds of
-the block's 4 lane groups); look-ahead rows lagging 0..7 steps, in their parity
+Cases: d in {64, 128, 256}; T = 3, 4 and 6 (a partial negative group; negatives past
+the 4 a contribution record holds); an even and an odd
+step; duplicate users; a hot item with 40 or 80 positive slots (20 / 40 contribution
+rounds; 80 refills the block's staged id table); look-ahead rows lagging 0..7 steps, in their parity
 buffer with the other buffer poisoned (NaN); zero-state rows."""
 import numpy as np
 import pytest
@@ -33,7 +34,8 @@ def _grouping(keys, space):
     return segs
 
 
-@pytest.mark.parametrize('d,T,s', [(64, 3, 6), (128, 4, 7), (128, 4, 10), (256, 3, 9)])
+@pytest.mark.parametrize('d,T,s', [(64, 3, 6), (128, 4, 7), (128, 4, 10), (256, 3, 9),
+                                   (128, 6, 8)])
 def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
     g = torch.Generator().manual_seed(d * 100 + T * 10 + s)
     nU, nI, Bc = 257, 301, 96
@@ -42,7 +44,8 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
     user0[5] = user0[17] = user0[60]                       # a user with 3 positives
     user1 = torch.randint(0, nU, (Bc,), generator=g)
     items0 = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
-    items0[:40] = 7                                         # hot item: 40 positive slots
+    hot = 40 if s % 2 == 0 else 80                          # > 64: two id-table refills
+    items0[:hot] = 7                                        # hot item: `hot` positive slots
     items0[Bc + 3] = 7                                      # ... and a negative slot
     items1 = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
     pU = torch.randn(nU, d, generator=g) * 0.1
@@ -114,8 +117,9 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
         {'p': bufs[1][0], 'p_alt': bufs[1][1], 'm': fmI, 'v': fvI, 'grouping': gi0,
          'last': flI, 'ahead': ahead[1]}])
     loss_k = torch.full((Bc,), float('nan'), device=dev)
-    ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, to(user0), to(items0), Bc, T, grad_scale,
-                      loss_k, consts, base, 3)
+    recs = ops.step_records(to(user0), to(items0), 1, Bc, T, nU, nI, gu0, gi0)
+    ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, to(items0), Bc, T, grad_scale, loss_k, recs,
+                      consts, base, 3)
     torch.cuda.synchronize()
 
     assert torch.equal(loss_k, o['loss_k'])
@@ -143,7 +147,8 @@ def test_bpr_adam_step_rejects_bad_tables(dev):
                              'last': torch.zeros(10, dtype=torch.int32, device=dev)}] * 2)
     consts = _consts(dev)
     base = torch.zeros(1, dtype=torch.int32, device=dev)
+    z = torch.zeros(3 * Bc, dtype=torch.int64, device=dev)
+    recs = ops.step_records(z[:Bc], z, 1, Bc, T, 10, 10, g, _grouping(z, 10))
     with pytest.raises(NativeError):            # no parity buffer
-        ops.bpr_adam_step(tabs, [Bc, 3 * Bc], d, torch.zeros(Bc, dtype=torch.int64, device=dev),
-                          torch.zeros(3 * Bc, dtype=torch.int64, device=dev), Bc, T, 0.1,
-                          torch.zeros(Bc, device=dev), consts, base)
+        ops.bpr_adam_step(tabs, [Bc, 3 * Bc], d, z, Bc, T, 0.1, torch.zeros(Bc, device=dev), recs,
+                          consts, base)

@@ -1,0 +1,26 @@
+#!/bin/bash
+# K35 one-wave-per-row: parity tests, bitwise chain, then driver-window benches with
+# ramp / K2 variants and a kernel trace of the driver window. Stops at the first failure.
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r3c
+mkdir -p $O
+T="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu"
+timeout -k 10 600 $T tests/test_gpu_step.py tests/test_gpu_e2e.py tests/test_gpu_chain.py > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 10
+b() {  # tag, args...
+  local tag=$1; shift
+  timeout -k 10 300 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval --in-memory "$@" > $O/$tag 2>&1 || exit 4
+  echo "$tag: $(grep -o '"value": [0-9.]*' $O/$tag | head -n1) $(grep -o '"kernels_us": {[^}]*}' $O/$tag | head -n1)"
+}
+b short_r4a; b short_r4b
+b short_r1a --ramp 1,2,4,8,16,32; b short_r1b --ramp 1,2,4,8,16,32
+b short_r2a --ramp 2,4,8,16,32
+MIREC_LIB=recbole_amd/_lib/alt/k2bs.so b short_k2bs_a
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval > $O/default 2>&1 || exit 5
+echo "default: $(grep -o '"value": [0-9.]*' $O/default | head -n1) $(grep -o '"kernels_us": {[^}]*}' $O/default | head -n1)"
+BENCH_MARKERS=1 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- \
+  python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval > $O/trace.log 2>&1 || exit 6
+python tools/check_timed_window.py $O/trace $O/timed_window.json > $O/tw.txt
+head -60 $O/tw.txt
+echo done
