@@ -522,6 +522,7 @@ def main():
         'ranks': per_rank,
         'adam_mode': step.adam_mode,
         'fused_step': bool(getattr(step, 'fused_step', False)),
+        'flush_every': int(getattr(step, 'FLUSH_EVERY', 0)),
         'setup_s': round(setup_s, 1),
         'setup': step.setup_info,
     }

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 12
+#define MIREC_ABI_VERSION 13
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -398,10 +398,18 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
  * keys, contribution k = positive k), tables[1] = items (grouping of its (1+T)*Bc item
  * keys, the pairwise slots: positive k at k, negative j of k at Bc + j*Bc + k); each
  * table needs p and p_alt (parity buffers: the state after t steps lives in
- * t & 1 ? p_alt : p), m, v, last, n_uniq and optionally the look-ahead list; `rows` and
+ * t & 1 ? p_alt : p), m, v, last, n_uniq and optionally the look-ahead list (n_max_uniq:
+ * bounds of both, the grid is sized by them); `rows` and
  * `dense_grad` are unused / NULL. The touched rows come as the records of
- * mirec_step_records (u_rec / i_rec: one per touched-row slot; u_crec / i_crec: one per
- * grouped position) of this batch. The step s = step_base_dev[0] + step_off reads every
+ * mirec_step_records (u_rec / i_rec: the batch's record region; u_crec / i_crec: one per
+ * grouped position) of this batch. Rows with more than 2 contributions are split: their
+ * contributions are formed by several blocks of the launch, which hand the vectors over
+ * through u_part / i_part (scratch, Bc / (1+T)*Bc positions x d floats) and count in on
+ * u_join / i_join (2*Bc / 2*(1+T)*Bc int32: per row slot, then per look-ahead slot —
+ * at d >= 128 a look-ahead row is replayed by two blocks, the second to finish marks
+ * it; all ZERO before the first launch, every launch leaves them zero). The sums keep
+ * the grouping order, so split rows give the same bits.
+ * The step s = step_base_dev[0] + step_off reads every
  * row from buffer s & 1 (all rows the batch reads must be complete through s - 1) and
  * writes touched + look-ahead rows at state s + 1 to buffer (s + 1) & 1; zero-state rows
  * must hold the same p in both buffers. loss_k[k] = sum_j -log(gamma + sigmoid(x_kj)).
@@ -411,6 +419,7 @@ int mirec_bpr_adam_step_f32(const mirec_adam_table* tables, const int64_t* n_max
                             int32_t d, const int64_t* items, int64_t Bc, int32_t T, float gamma,
                             float grad_scale, float* loss_k, const int32_t* u_rec,
                             const int32_t* u_crec, const int32_t* i_rec, const int32_t* i_crec,
+                            float* u_part, int32_t* u_join, float* i_part, int32_t* i_join,
                             const float* step_consts_dev, const int32_t* step_base_dev,
                             int32_t step_off, double beta1, double beta2, double eps,
                             double weight_decay, void* stream);
@@ -418,20 +427,22 @@ int mirec_bpr_adam_step_f32(const mirec_adam_table* tables, const int64_t* n_max
  * (1+T)*Bc item keys; the groupings of mirec_segment_sort_batched / the chunk
  * preparation). Contribution record (8 int32) per grouped position i: positive k,
  * negative slot j (-1 for a user slot or a positive slot), user id, positive item id,
- * the first 4 negatives' ids (ids clamped to the table as K3 clamps them). Row record
- * (20 int32) per touched-row slot u: row id, first position, contribution count, 0,
- * then the records of its first two contributions. u_rec / i_rec: per batch Bc /
- * (1+T)*Bc slots x 20 int32; u_crec / i_crec: per batch Bc / (1+T)*Bc positions x 8. */
+ * the first 4 negatives' ids (ids clamped to the table as K3 clamps them). Record
+ * region per batch and table (mirec_step_record_ints(per) int32, per = Bc or
+ * (1+T)*Bc): per row records (20 int32: row id, first position, contribution count,
+ * share count, the records of its first two contributions), then 256 share records of
+ * split rows (24 int32: row slot, share, first position, count, row id, share count,
+ * 0, 0, the share's two contribution records), then the number of share records.
+ * u_crec / i_crec: per batch Bc / (1+T)*Bc positions x 8 int32. */
 int mirec_step_records(const int64_t* user_keys, const int64_t* item_keys, int64_t n_batches,
                        int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
                        const int32_t* u_perm, const int32_t* u_uniq, const int32_t* u_seg,
                        const int32_t* u_nu, const int32_t* i_perm, const int32_t* i_uniq,
                        const int32_t* i_seg, const int32_t* i_nu, int32_t* u_rec,
                        int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, void* stream);
+/* int32 per batch of one table's record region for per keys per batch (-1 if per < 0). */
+int64_t mirec_step_record_ints(int64_t per);
 
-/* n device-to-device copies (src[i] -> dst[i], bytes[i]; host arrays of device
- * pointers) in one launch per 96 copies: the per-step copy of a batch's columns into
- * a captured training graph's static inputs (one launch instead of one per column). */
 int mirec_copy_many(const void* const* src, void* const* dst, const int64_t* bytes, int n,
                     void* stream);
 

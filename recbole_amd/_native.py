@@ -139,8 +139,9 @@ SIGNATURES = {
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
     "mirec_bpr_adam_step_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, c_int64,
                                         c_int32, ctypes.c_float, ctypes.c_float, _P, _P, _P,
-                                        _P, _P, _P, _P, c_int32, c_double, c_double,
-                                        c_double, c_double, _P]),
+                                        _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_double,
+                                        c_double, c_double, c_double, _P]),
+    "mirec_step_record_ints": (c_int64, [c_int64]),
     "mirec_step_records": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64, _P, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
@@ -172,7 +173,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class NativeError(RuntimeError):

@@ -262,13 +262,13 @@ __device__ __forceinline__ void incr_steps(const float (*me)[N], const float (*v
 // a group only moves m and v. The test runs at the first step of every group
 // outside that state (as adam_replay's every 4th step); a group whose four steps
 // do not all pass goes step by step. Full steps use the fast-path sqrt /
-// division of adam_math.h.
-template <typename V>
+// division of adam_math.h. G = steps per group (8: eight chains in flight for a
+// thread holding one element).
+template <typename V, int G = 4>
 __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1,
                                                 const float* __restrict__ consts,
                                                 const AdamConsts& k) {
   constexpr int N = Lanes<V>::n;
-  constexpr int G = 4;
   int s = __builtin_amdgcn_readfirstlane(s0);
   if (s >= s1) return;
   bool skipping = false;
@@ -374,7 +374,7 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
       for (int j = 0; j < G; ++j) one_step(me[j], ve[j], sc[j], j == 0);
     }
   }
-  for (int j = 0; s < s1; ++s, ++j) {           // the last s1 - s < 4 steps
+  for (int j = 0; s < s1; ++s, ++j) {           // the last s1 - s < G steps
     const StepConsts sc = step_consts(consts, s);
     float me[N], ve[N];
 #pragma unroll
@@ -396,11 +396,11 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
 
 // Replay dispatch: whole-wave rows in the common configuration take
 // adam_replay_row, everything else the general adam_replay.
-template <typename V, bool kRowWave>
+template <typename V, bool kRowWave, int G = 4>
 __device__ __forceinline__ void replay(V& p, V& m, V& v, int s0, int s1,
                                        const float* __restrict__ consts, const AdamConsts& k) {
   if (kRowWave && k.wd == 0.f && k.lerp_small)
-    adam_replay_row(p, m, v, s0, s1, consts, k);
+    adam_replay_row<V, G>(p, m, v, s0, s1, consts, k);
   else
     adam_replay(p, m, v, s0, s1, consts, k);
 }

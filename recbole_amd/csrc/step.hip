@@ -43,7 +43,11 @@ struct StepLaunch {
   mirec_adam_table t[2];       // [0] users, [1] items: p (+ p_alt), m, v, last, grouping
   const int32_t* rec[2];       // row records per touched-row slot (mirec_step_records)
   const int32_t* crec[2];      // contribution records per grouped position
-  int64_t block_start[5];      // segments: ahead U, ahead I, touched U, touched I, end
+  float* part[2];              // contribution vectors of split rows, per position x D
+  int32_t* join[2];            // arrivals per row slot of split rows, then per look-ahead
+                               // slot at join_ahead (zero between launches)
+  int64_t join_ahead[2];
+  int64_t block_start[7];      // segments: shares U, I, look-ahead U, I, touched U, I, end
 };
 
 // rows of one contribution of the positive k: u = EU[user[k]], p = EI[items[k]],
@@ -61,7 +65,7 @@ __device__ __forceinline__ int64_t clamp_id(int64_t id, int64_t n) {
 // (look-ahead), and at the end,
 // into a buffer of their own that no other code reads. No stamp executes in the product.
 #if defined(MIREC_STEP_STAMPS)
-constexpr int kStampBlocks = 16384;
+constexpr int kStampBlocks = 32768;
 __device__ unsigned long long g_step_stamps[kStampBlocks * 4];
 #define MIREC_STAMP(slot)                                                                  \
   do {                                                                                     \
@@ -82,13 +86,35 @@ __device__ unsigned long long g_step_stamps[kStampBlocks * 4];
 // dependent loads (its record, then the rows) instead of four (segment, perm, ids,
 // rows). Contribution record (8 int32): positive k, negative slot j (-1: the positive
 // or the user slot), user id, positive item id, the negatives' ids (the first 4; more
-// are read from the keys). Row record (kRowRec int32) per touched-row slot u: row id,
-// first position i0, contribution count, 0, then the records of its first kRecInline
-// contributions; the others are at crec[i0 + c].
+// are read from the keys). Row record (kRowRec int32) per touched-row slot x: row id,
+// first position i0, contribution count nc, share count nsh, then the records of its
+// first kRecInline contributions; the others are at crec[i0 + c].
+//
+// Split rows. A row with more than kShare contributions (a hot item: its positives and
+// negative slots) would take ceil(nc / NG) dependent rounds in one block — the long
+// pole of the launch. Its contributions are dealt out in shares of kShare: share 0 to
+// the row's own block, shares 1..nsh-1 to blocks of the launch's "share" segment (task
+// records below, one per share, carrying the share's contribution records inline).
+// Every participant writes its contribution vectors to part[(i0 + c) * D] and counts
+// itself in on join[x]; the last to arrive sums ALL nc vectors in grouping order (the
+// same sequential sum as an unsplit row) and applies the Adam step. At most
+// kSplitCap shares per (table, batch) are dealt out; the contributions of shares past
+// the cap stay with the row's own block.
+//
+// Record region per (table, batch), rec_ints(per) int32: per row records, kSplitCap
+// task records {x, share j, i0, nc}, {row, nsh, 0, 0}, the share's contribution
+// records, then the task count.
 constexpr int kRecInts = 8;
 constexpr int kRecInline = 2;
 constexpr int kRowRec = 4 + kRecInline * kRecInts;
+constexpr int kShare = kRecInline;      // contributions per share of a split row
+constexpr int kTaskRec = 8 + kShare * kRecInts;
+constexpr int kSplitCap = 256;          // shares dealt out per (table, batch)
 constexpr int kStepExtraCap = 62;       // extra records staged in LDS per touched row
+
+__host__ __device__ constexpr int64_t rec_ints(int64_t per) {
+  return per * kRowRec + (int64_t)kSplitCap * kTaskRec + 4;
+}
 
 __device__ __forceinline__ void contrib_record(int q, int tb, int Bc, int T,
                                                const int64_t* __restrict__ user,
@@ -114,8 +140,8 @@ __device__ __forceinline__ void contrib_record(int q, int tb, int Bc, int T,
   reinterpret_cast<int4*>(out)[1] = make_int4(r[4], r[5], r[6], r[7]);
 }
 
-// One block per (table, batch): row records of the batch's touched-row slots and
-// contribution records of its grouped positions.
+// One block per (table, batch): row records of the batch's touched-row slots, task
+// records of the shares of its split rows, contribution records of its positions.
 __global__ __launch_bounds__(256) void step_records_kernel(
     const int64_t* __restrict__ ukeys, const int64_t* __restrict__ ikeys, int n_batches, int Bc,
     int T, int64_t nU, int64_t nI, const int32_t* __restrict__ u_perm,
@@ -124,6 +150,7 @@ __global__ __launch_bounds__(256) void step_records_kernel(
     const int32_t* __restrict__ i_uniq, const int32_t* __restrict__ i_seg,
     const int32_t* __restrict__ i_nu, int32_t* __restrict__ u_rec, int32_t* __restrict__ u_crec,
     int32_t* __restrict__ i_rec, int32_t* __restrict__ i_crec) {
+  __shared__ int scan_lds[256 / 64 + 1];
   const int tb = blockIdx.x >= (unsigned)n_batches;
   const int b = tb ? blockIdx.x - n_batches : blockIdx.x;
   const int KI = (1 + T) * Bc;
@@ -134,23 +161,71 @@ __global__ __launch_bounds__(256) void step_records_kernel(
   const int32_t* __restrict__ uniq = (tb ? i_uniq : u_uniq) + (int64_t)b * per;
   const int32_t* __restrict__ seg = (tb ? i_seg : u_seg) + (int64_t)b * (per + 1);
   const int nu = (tb ? i_nu : u_nu)[b];
-  int32_t* __restrict__ rec = (tb ? i_rec : u_rec) + (int64_t)b * per * kRowRec;
+  int32_t* __restrict__ rec = (tb ? i_rec : u_rec) + (int64_t)b * rec_ints(per);
+  int32_t* __restrict__ task = rec + (int64_t)per * kRowRec;
   int32_t* __restrict__ crec = (tb ? i_crec : u_crec) + (int64_t)b * per * kRecInts;
   const int n = seg[nu];
   for (int i = threadIdx.x; i < n; i += blockDim.x)
     contrib_record(perm[i], tb, Bc, T, user, items, nU, nI, crec + (int64_t)i * kRecInts);
-  for (int x = threadIdx.x; x < nu; x += blockDim.x) {
-    const int i0 = seg[x], i1 = seg[x + 1];
+  int dealt = 0;                                   // shares dealt out so far (block-uniform)
+  for (int x0 = 0; x0 < nu; x0 += blockDim.x) {
+    const int x = x0 + threadIdx.x;
+    int i0 = 0, nc = 0;
+    if (x < nu) {
+      i0 = seg[x];
+      nc = seg[x + 1] - i0;
+    }
+    const int want = nc > kShare ? (nc + kShare - 1) / kShare - 1 : 0;
+    int total;
+    const int base = dealt + block_exclusive_scan(want, scan_lds, &total);
+    dealt += total;
+    if (x >= nu) continue;
+    const int got = max(0, min(want, kSplitCap - base));
+    const int nsh = 1 + got;
     int32_t* r = rec + (int64_t)x * kRowRec;
-    reinterpret_cast<int4*>(r)[0] = make_int4(uniq[x], i0, i1 - i0, 0);
+    reinterpret_cast<int4*>(r)[0] = make_int4(uniq[x], i0, nc, nsh);
     for (int c = 0; c < kRecInline; ++c)
-      if (i0 + c < i1) contrib_record(perm[i0 + c], tb, Bc, T, user, items, nU, nI,
-                                      r + 4 + c * kRecInts);
+      if (c < nc) contrib_record(perm[i0 + c], tb, Bc, T, user, items, nU, nI,
+                                 r + 4 + c * kRecInts);
+    for (int j = 1; j <= got; ++j) {
+      int32_t* tr = task + (int64_t)(base + j - 1) * kTaskRec;
+      reinterpret_cast<int4*>(tr)[0] = make_int4(x, j, i0, nc);
+      reinterpret_cast<int4*>(tr)[1] = make_int4(uniq[x], nsh, 0, 0);
+      for (int c = 0; c < kShare; ++c)
+        if (j * kShare + c < nc)
+          contrib_record(perm[i0 + j * kShare + c], tb, Bc, T, user, items, nU, nI,
+                         tr + 8 + c * kRecInts);
+    }
   }
+  if (threadIdx.x == 0) task[(int64_t)kSplitCap * kTaskRec] = min(dealt, kSplitCap);
+}
+
+// Hand-off of a split row's contribution vectors between the blocks of one launch
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off form: write-through
+// agent-scope stores, every storing wave drained before one lane's agent-scope add, the
+// last adder told by the returned value, agent-scope loads): no fence needed.
+__device__ __forceinline__ void part_store(float* p, float4 a) {
+  auto q = (__attribute__((address_space(1))) unsigned long long*)(p);
+  const unsigned long long lo =
+      (unsigned long long)__float_as_uint(a.x) | ((unsigned long long)__float_as_uint(a.y) << 32);
+  const unsigned long long hi =
+      (unsigned long long)__float_as_uint(a.z) | ((unsigned long long)__float_as_uint(a.w) << 32);
+  __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void part_load(const float* p, float& a) {
+  auto q = (const __attribute__((address_space(1))) unsigned int*)(p);
+  a = __uint_as_float(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void part_load(const float* p, float2& a) {
+  auto q = (const __attribute__((address_space(1))) unsigned long long*)(p);
+  const unsigned long long w = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a = make_float2(__uint_as_float((unsigned)w), __uint_as_float((unsigned)(w >> 32)));
 }
 
 template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
+template <typename V> struct AheadVec { using T = float; };
 
 template <int D>
 __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_adam_step_kernel(
@@ -162,13 +237,16 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
   constexpr int TPB = D / EPT;             // threads per block (one row)
   constexpr int LPR = D / 4;               // lanes per contribution (float4 each, K3's layout)
   constexpr int NG = TPB / LPR;            // contributions in flight per block
+  constexpr int kAheadHalves = EPT;        // look-ahead blocks per row (one element per thread)
   __shared__ float cont[NG][D];
+  __shared__ int s_last;
   MIREC_STAMP(0);
   int si = 0;
 #pragma unroll
-  for (int q = 1; q < 4; ++q)
+  for (int q = 1; q < 6; ++q)
     if ((int64_t)blockIdx.x >= L.block_start[q]) si = q;
-  const bool ahead = si < 2;
+  const int kind = si >> 1;                // 0 share of a split row, 1 look-ahead, 2 touched
+  const bool ahead = kind == 1;
   const int tb = si & 1;                   // 0 users, 1 items
   const mirec_adam_table& T_ = L.t[tb];
   const int u = (int)((int64_t)blockIdx.x - L.block_start[si]);
@@ -176,22 +254,38 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
   const int grp = t / LPR;
   const int l = t - grp * LPR;
   // first load level, all independent of each other: the count and the row id (look-
-  // ahead) or the row record (touched: row, first position, count, and this lane
-  // group's inline contribution record); u < the launch's bound, so the loads stay in
-  // the buffers even past the count
-  const int n = ahead ? T_.ahead_n_uniq[0] : T_.n_uniq[0];
-  const int32_t* __restrict__ R = L.rec[tb] + (int64_t)u * kRowRec;
-  int4 hdr = make_int4(0, 0, 0, 0), ra = hdr, rb = hdr;
+  // ahead), the row record (touched: row, i0, nc, nsh and this lane group's inline
+  // contribution record) or the task record (share j of row slot x); u < the
+  // launch's bound, so the loads stay in the buffers even past the count
+  const int per = tb ? (1 + T) * Bc : Bc;
+  const int32_t* __restrict__ R = L.rec[tb];
+  int4 h0 = make_int4(0, 0, 0, 0), h1 = h0, ra = h0, rb = h0;
+  int n;
   int64_t row;
-  if (ahead) {
-    row = T_.ahead_uniq[u];
+  if (ahead) {                             // two blocks per row when a thread holds 2
+    n = T_.ahead_n_uniq[0] * kAheadHalves;
+    row = T_.ahead_uniq[u / kAheadHalves];
   } else {
-    hdr = reinterpret_cast<const int4*>(R)[0];
-    if (grp < kRecInline) {
-      ra = reinterpret_cast<const int4*>(R + 4 + grp * kRecInts)[0];
-      rb = reinterpret_cast<const int4*>(R + 4 + grp * kRecInts)[1];
+    const int32_t* __restrict__ Q;
+    if (kind == 2) {
+      n = T_.n_uniq[0];
+      Q = R + (int64_t)u * kRowRec;
+      h0 = reinterpret_cast<const int4*>(Q)[0];              // row, i0, nc, nsh
+      row = h0.x;
+      Q += 4;
+    } else {
+      const int32_t* __restrict__ task = R + (int64_t)per * kRowRec;
+      n = task[(int64_t)kSplitCap * kTaskRec];
+      Q = task + (int64_t)u * kTaskRec;
+      h0 = reinterpret_cast<const int4*>(Q)[0];              // x, j, i0, nc
+      h1 = reinterpret_cast<const int4*>(Q)[1];              // row, nsh
+      row = h1.x;
+      Q += 8;
     }
-    row = hdr.x;
+    if (grp < kRecInline) {
+      ra = reinterpret_cast<const int4*>(Q + grp * kRecInts)[0];
+      rb = reinterpret_cast<const int4*>(Q + grp * kRecInts)[1];
+    }
   }
   const int st = step_base[0] + step_off;
   if (u >= n) return;                      // block-uniform
@@ -209,29 +303,46 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
 
   if (ahead) {
     // rows the next step reads and this one does not touch: replay last..st (zero
-    // gradient), as adam_deferred_kernel's look-ahead segment
+    // gradient), as adam_deferred_kernel's look-ahead segment. The replay is a chain of
+    // dependent steps per element: with two elements per thread the row goes to two
+    // blocks of one element per thread (half the chain work per wave, eight steps'
+    // sqrt / division chains in flight); the second half to finish marks the row.
     if (raw == kZeroState || raw > st) return;    // current at every step / already done
-    V p = reinterpret_cast<const V*>(Pr[raw & 1])[off];
-    V m = reinterpret_cast<const V*>(T_.m)[off];
-    V v = reinterpret_cast<const V*>(T_.v)[off];
+    using H = typename AheadVec<V>::T;
+    const int64_t offh = row * (D / Lanes<H>::n) + (u % kAheadHalves) * TPB + t;
+    H p = reinterpret_cast<const H*>(Pr[raw & 1])[offh];
+    H m = reinterpret_cast<const H*>(T_.m)[offh];
+    H v = reinterpret_cast<const H*>(T_.v)[offh];
     MIREC_STAMP(2);
-    replay<V, true>(p, m, v, raw, st, consts, k);
-    V z;
-    memset(&z, 0, sizeof(V));
+    replay<H, true, kAheadHalves == 2 ? 8 : 4>(p, m, v, raw, st, consts, k);
+    H z;
+    memset(&z, 0, sizeof(H));
     adam_vec(p, m, v, z, step_consts(consts, st), k);   // step st: zero gradient
-    __syncthreads();                               // every thread read `last`
-    reinterpret_cast<V*>(Pw)[off] = p;
-    reinterpret_cast<V*>(T_.m)[off] = m;
-    reinterpret_cast<V*>(T_.v)[off] = v;
-    if (t == 0) T_.last[row] = st + 1;
+    reinterpret_cast<H*>(Pw)[offh] = p;
+    reinterpret_cast<H*>(T_.m)[offh] = m;
+    reinterpret_cast<H*>(T_.v)[offh] = v;
+    if (kAheadHalves == 1) {
+      __syncthreads();                             // every thread read `last`
+      if (t == 0) T_.last[row] = st + 1;
+    } else {
+      // both halves read `last` before the first one counts in (its replay used it)
+      __syncthreads();
+      if (t == 0) {
+        int32_t* j = L.join[tb] + L.join_ahead[tb] + u / kAheadHalves;
+        if (__hip_atomic_fetch_add(j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+          __hip_atomic_store(j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          T_.last[row] = st + 1;
+        }
+      }
+    }
     MIREC_STAMP(3);
     return;
   }
 
-  // ---- touched row: own state in flight while the contributions are formed. Every
-  // row a step reads is complete through st - 1 (look-ahead / entry catch-up / flush)
-  // or in the zero state (the same p in both buffers), so its p is in buffer st & 1;
-  // a row behind (never, by that invariant) reloads from its own buffer below.
+  // ---- touched row (or one share of it): own state in flight while the contributions
+  // are formed. Every row a step reads is complete through st - 1 (look-ahead / entry
+  // catch-up / flush) or in the zero state (the same p in both buffers), so its p is in
+  // buffer st & 1; a row behind (never, by that invariant) reloads from its own buffer.
   const int last = raw == kZeroState ? st : raw;
   V p = reinterpret_cast<const V*>(Pr[st & 1])[off];
   V m = reinterpret_cast<const V*>(T_.m)[off];
@@ -242,30 +353,42 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
     EU = L.t[0].p_alt;
     EI = L.t[1].p_alt;
   }
-  const int i0 = hdr.y, nc = hdr.z;
+  // this block's contributions: i = 0..cnt-1 -> grouping position c(i). Share j >= 1:
+  // c = j*kShare + i. The row's own block (j = 0): share 0, then the contributions past
+  // the dealt-out shares (c = i + (nsh-1)*kShare for i >= kShare).
+  const int x = kind == 2 ? u : h0.x;
+  const int j = kind == 2 ? 0 : h0.y;
+  const int i0 = kind == 2 ? h0.y : h0.z;
+  const int nc = kind == 2 ? h0.z : h0.w;
+  const int nsh = kind == 2 ? h0.w : h1.y;
+  const bool split = nsh > 1;                      // block-uniform
+  const int cnt = j ? min(kShare, nc - j * kShare)
+                    : min(kShare, nc) + max(0, nc - nsh * kShare);
+  const int cskip = (nsh - 1) * kShare;
   const float ng = -grad_scale;
+  float* __restrict__ part = L.part[tb] + (int64_t)i0 * D;
   V g;
   memset(&g, 0, sizeof(V));
   // records of contributions kRecInline.. into LDS (one level, beside round 0's rows)
   __shared__ int4 xrec[kStepExtraCap][2];
-  if (nc > kRecInline) {                           // block-uniform
-    const int32_t* __restrict__ C = L.crec[tb] + (int64_t)(i0 + kRecInline) * kRecInts;
-    for (int c = t; c < min(nc - kRecInline, kStepExtraCap); c += TPB) {
-      xrec[c][0] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[0];
-      xrec[c][1] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[1];
+  if (cnt > kRecInline) {                          // block-uniform (own block only)
+    const int32_t* __restrict__ C = L.crec[tb] + (int64_t)(i0 + cskip) * kRecInts;
+    for (int c = kRecInline + t; c < min(cnt, kRecInline + kStepExtraCap); c += TPB) {
+      xrec[c - kRecInline][0] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[0];
+      xrec[c - kRecInline][1] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[1];
     }
     __syncthreads();
   }
-  for (int base = 0; base < nc; base += NG) {
-    const int c = base + grp;
-    if (c < nc) {
-      int4 r0 = ra, r1 = rb;                        // contribution c's record
-      if (c >= kRecInline) {
-        if (c - kRecInline < kStepExtraCap) {
-          r0 = xrec[c - kRecInline][0];
-          r1 = xrec[c - kRecInline][1];
+  for (int base = 0; base < cnt; base += NG) {
+    const int i = base + grp;
+    if (i < cnt) {
+      int4 r0 = ra, r1 = rb;                        // contribution i's record
+      if (i >= kRecInline) {
+        if (i - kRecInline < kStepExtraCap) {
+          r0 = xrec[i - kRecInline][0];
+          r1 = xrec[i - kRecInline][1];
         } else {
-          const int32_t* C = L.crec[tb] + (int64_t)(i0 + c) * kRecInts;
+          const int32_t* C = L.crec[tb] + (int64_t)(i0 + cskip + i) * kRecInts;
           r0 = reinterpret_cast<const int4*>(C)[0];
           r1 = reinterpret_cast<const int4*>(C)[1];
         }
@@ -286,20 +409,20 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
           float4 nv[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int j = j0 + e;
+            const int jj = j0 + e;
             nv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (j < T) {
-              const int64_t nid = j < 4 ? (int64_t)nid4[e]
-                                        : clamp_id(items[Bc + (int64_t)j * Bc + kk],
-                                                   L.t[1].n_rows);
+            if (jj < T) {
+              const int64_t nid = jj < 4 ? (int64_t)nid4[e]
+                                         : clamp_id(items[Bc + (int64_t)jj * Bc + kk],
+                                                    L.t[1].n_rows);
               nv[e] = reinterpret_cast<const float4*>(EI + nid * D)[l];
             }
           }
           const float sp = group_sum<LPR>(dot4(uv, pv));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int j = j0 + e;
-            if (j < T) {
+            const int jj = j0 + e;
+            if (jj < T) {
               const float sn = group_sum<LPR>(dot4(uv, nv[e]));
               const BprCoef cf = bpr_coef(sp, sn, gamma, ng);
               lsum += cf.nll;
@@ -312,17 +435,56 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
         }
         if (tb == 0 && l == 0 && loss_k) loss_k[kk] = lsum;   // one user slot per positive
       }
-      *reinterpret_cast<float4*>(&cont[grp][4 * l]) = acc;
+      if (split) {
+        const int c = i < kShare ? j * kShare + i : cskip + i;
+        part_store(part + (int64_t)c * D + 4 * l, acc);
+      } else {
+        *reinterpret_cast<float4*>(&cont[grp][4 * l]) = acc;
+      }
+    }
+    if (!split) {
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < NG; ++h)
+        if (base + h < cnt) {
+          const V cv = *reinterpret_cast<const V*>(&cont[h][EPT * t]);
+#pragma unroll
+          for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv, e);
+        }
+      __syncthreads();                               // cont is rewritten next round
+    }
+  }
+  if (split) {
+    // every storing wave drained, then one lane counts the block in; the last of the
+    // row's nsh participants sums all nc vectors in grouping order and steps the row
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const int arrived =
+          __hip_atomic_fetch_add(L.join[tb] + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = arrived == nsh - 1;
+      if (s_last)                                    // every participant has counted in
+        __hip_atomic_store(L.join[tb] + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if (!s_last) return;                             // block-uniform
+    const float* __restrict__ pe = part + EPT * t;
+    int c = 0;
+    for (; c + 8 <= nc; c += 8) {
+      V cv[8];
 #pragma unroll
-    for (int h = 0; h < NG; ++h)
-      if (base + h < nc) {
-        const V cv = *reinterpret_cast<const V*>(&cont[h][EPT * t]);
+      for (int h = 0; h < 8; ++h) part_load(pe + (int64_t)(c + h) * D, cv[h]);
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv, e);
-      }
-    __syncthreads();                                 // cont is rewritten next round
+      for (int h = 0; h < 8; ++h)
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv[h], e);
+    }
+    for (; c < nc; ++c) {
+      V cv;
+      part_load(pe + (int64_t)c * D, cv);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv, e);
+    }
   }
   if (last < st) {                                   // behind (not expected): own buffer
     p = reinterpret_cast<const V*>(Pr[last & 1])[off];
@@ -368,19 +530,23 @@ extern "C" int mirec_step_records(const int64_t* user_keys, const int64_t* item_
   return launch_status("mirec_step_records");
 }
 
+extern "C" int64_t mirec_step_record_ints(int64_t per) { return per < 0 ? -1 : rec_ints(per); }
+
 extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
                                        const int64_t* n_max_uniq, int32_t d,
                                        const int64_t* items, int64_t Bc, int32_t T, float gamma,
                                        float grad_scale, float* loss_k, const int32_t* u_rec,
                                        const int32_t* u_crec, const int32_t* i_rec,
-                                       const int32_t* i_crec, const float* step_consts_dev,
+                                       const int32_t* i_crec, float* u_part, int32_t* u_join,
+                                       float* i_part, int32_t* i_join,
+                                       const float* step_consts_dev,
                                        const int32_t* step_base_dev, int32_t step_off,
                                        double beta1, double beta2, double eps,
                                        double weight_decay, void* stream) {
   const char* what = "mirec_bpr_adam_step_f32";
   if (!tables || !n_max_uniq || !items || Bc < 0 || T < 1 || !step_consts_dev ||
       (int64_t)(1 + T) * Bc > INT32_MAX || !u_rec || !u_crec || !i_rec || !i_crec ||
-      !step_base_dev || ((uintptr_t)step_consts_dev & 15) != 0) {
+      !u_part || !u_join || !i_part || !i_join || !step_base_dev || ((uintptr_t)step_consts_dev & 15) != 0) {
     set_error("%s: bad arguments", what);
     return -1;
   }
@@ -404,18 +570,30 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   L.crec[0] = u_crec;
   L.rec[1] = i_rec;
   L.crec[1] = i_crec;
-  // segments: look-ahead rows first (their replays are the longest chains), then touched
+  L.part[0] = u_part;
+  L.join[0] = u_join;
+  L.part[1] = i_part;
+  L.join[1] = i_join;
+  L.join_ahead[0] = Bc;                           // join: [row slots | look-ahead slots]
+  L.join_ahead[1] = (int64_t)(1 + T) * Bc;
+  // segments: the shares of split rows first (their row's step waits for them), then
+  // the look-ahead rows (their replays are long chains), then the touched rows
+  if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
   int64_t b = 0;
   L.block_start[0] = b;
-  b += L.t[0].ahead_uniq ? n_max_uniq[0] : 0;
+  b += kSplitCap;
   L.block_start[1] = b;
-  b += L.t[1].ahead_uniq ? n_max_uniq[1] : 0;
+  b += kSplitCap;
   L.block_start[2] = b;
-  b += n_max_uniq[0];
+  const int halves = d >= 128 ? 2 : 1;            // look-ahead blocks per row
+  b += L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0;
   L.block_start[3] = b;
-  b += n_max_uniq[1];
+  b += L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0;
   L.block_start[4] = b;
-  if (b == 0) return 0;
+  b += n_max_uniq[0];
+  L.block_start[5] = b;
+  b += n_max_uniq[1];
+  L.block_start[6] = b;
   AdamConsts k;
   k.omb1 = (float)(1.0 - beta1);
   k.omb1m1 = k.omb1 - 1.0f;

@@ -549,8 +549,8 @@ def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_us
         _dev(t_, torch.int64, n_)
     dev = user_keys.device
     KI = (1 + times) * Bc
-    out = [torch.empty(n_batches * n * w, dtype=torch.int32, device=dev)
-           for n, w in ((Bc, 20), (Bc, 8), (KI, 20), (KI, 8))]
+    out = [torch.empty(n_batches * n, dtype=torch.int32, device=dev)
+           for n in (step_record_ints(Bc), Bc * 8, step_record_ints(KI), KI * 8)]
     rc = lib().mirec_step_records(ptr(user_keys), ptr(item_keys), n_batches, Bc, times, n_users,
                                   n_items, ptr(gu.perm), ptr(gu.uniq), ptr(gu.seg),
                                   ptr(gu.n_uniq), ptr(gi.perm), ptr(gi.uniq), ptr(gi.seg),
@@ -559,17 +559,39 @@ def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_us
     return out
 
 
+def step_record_ints(per: int) -> int:
+    """int32 per batch of one table's K35 record region (mirec_step_record_ints)."""
+    n = lib().mirec_step_record_ints(per)
+    if n < 0:
+        raise ValueError(f"step_record_ints: bad per {per}")
+    return n
+
+
+def step_scratch(Bc: int, times: int, d: int, device):
+    """K35 hand-off scratch (u_part, u_join, i_part, i_join): contribution vectors of
+    split rows per grouped position, and zeroed arrival counters per row slot and per
+    look-ahead slot; reusable by every launch of the same stream (each launch leaves
+    the counters zero)."""
+    KI = (1 + times) * Bc
+    return [torch.empty(Bc * d, dtype=torch.float32, device=device),
+            torch.zeros(2 * Bc, dtype=torch.int32, device=device),
+            torch.empty(KI * d, dtype=torch.float32, device=device),
+            torch.zeros(2 * KI, dtype=torch.int32, device=device)]
+
+
 def bpr_adam_step(tables, n_max_uniq, d: int, items, Bc: int, times: int, grad_scale: float,
-                  loss_k, records, step_consts, step_base, step_off: int = 0,
+                  loss_k, records, scratch, step_consts, step_base, step_off: int = 0,
                   gamma: float = 1e-10, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
     """K35: one training step (BPR forward/backward + the touched rows' deferred Adam
     step + look-ahead) in one launch; tables = adam_tables([users, items]) with p_alt and
-    a grouping (n_uniq); records = step_records(...) of this batch."""
+    a grouping (n_uniq); records = step_records(...) of this batch; scratch =
+    step_scratch(Bc, times, d)."""
     import ctypes
     _dev(items, torch.int64, "items")
     nm = (ctypes.c_int64 * 2)(*n_max_uniq)
     rc = lib().mirec_bpr_adam_step_f32(tables, nm, d, ptr(items), Bc, times, gamma, grad_scale,
-                                       ptr(loss_k), *[ptr(r) for r in records], ptr(step_consts),
+                                       ptr(loss_k), *[ptr(r) for r in records],
+                                       *[ptr(x) for x in scratch], ptr(step_consts),
                                        ptr(step_base), step_off, beta1, beta2, eps, weight_decay,
                                        stream_handle())
     check(rc, "mirec_bpr_adam_step_f32")

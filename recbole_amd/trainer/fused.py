@@ -52,7 +52,7 @@ from recbole_amd.trainer.exchange import ExchangeLayout
 
 # K35 record widths (int32 per touched-row slot / per grouped position, include/mirec.h
 # mirec_step_records)
-REC_ROW, REC_CONTRIB = 20, 8
+REC_CONTRIB = 8
 ADAM_MODES = ('deferred', 'streamed')
 
 
@@ -237,12 +237,13 @@ class FusedBPRTrainStep(object):
         self.fused_step = bool(fused_step)
         self.pU_alt = torch.empty_like(self.pU.data) if self.fused_step else None
         self.pI_alt = torch.empty_like(self.pI.data) if self.fused_step else None
+        self._rec_w = {}
         if self.fused_step:          # K35 records per slot (mirec_step_records, prep stream)
-            KIg = (1 + T) * self.Bg
             for sl in self.slots:
-                sl.records = [torch.empty(self.C * n * w, dtype=torch.int32, device=dev)
-                              for n, w in ((self.Bg, REC_ROW), (self.Bg, REC_CONTRIB),
-                                           (KIg, REC_ROW), (KIg, REC_CONTRIB))]
+                sl.records = [torch.empty(self.C * w, dtype=torch.int32, device=dev)
+                              for w in self._rec_ints(self.Bg)]
+            # split rows' hand-off scratch (one launch at a time on the compute stream)
+            self._step_scratch = ops.step_scratch(self.Bg, T, d, dev)
         self._n_max = (ctypes.c_int64 * 2)(self.Bg, (1 + T) * self.Bg)
         g = self.opt.param_groups[0]
         self._adam_args = (g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'])
@@ -389,6 +390,15 @@ class FusedBPRTrainStep(object):
         return cp
 
     # ------------------------------------------------------------------ model side
+    def _rec_ints(self, Bc):
+        """int32 per batch of the four K35 record buffers for batches of Bc positives."""
+        w = self._rec_w.get(Bc)
+        if w is None:
+            KI = (1 + self.times) * Bc
+            w = self._rec_w[Bc] = (ops.step_record_ints(Bc), Bc * REC_CONTRIB,
+                                   ops.step_record_ints(KI), KI * REC_CONTRIB)
+        return w
+
     def _fill_tables(self):
         """Per-table pointers that do not depend on the batch."""
         stU = self.opt.state[self.pU]
@@ -490,9 +500,8 @@ class FusedBPRTrainStep(object):
         if self.fused_step and not sharded:
             # K35: BPR + touched-row Adam + look-ahead in one launch (no gradient rows),
             # the touched rows from the chunk's records (built on the prep stream)
-            rec = [r.data_ptr() + 4 * c * n * w for r, (n, w) in zip(
-                slot.records, ((Bc, REC_ROW), (Bc, REC_CONTRIB), (KI, REC_ROW),
-                               (KI, REC_CONTRIB)))]
+            rec = [r.data_ptr() + 4 * c * w for r, w in zip(slot.records, self._rec_ints(Bc))]
+            rec += [x.data_ptr() for x in self._step_scratch]
 
             def fused():
                 check(L.mirec_bpr_adam_step_f32(t, self._n_max, d, keys_g, Bc, T, 1e-10,

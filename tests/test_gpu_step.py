@@ -6,10 +6,13 @@ launches it replaces (K3 mirec_bpr_fwd_bwd_f32 + K5 mirec_adam_deferred_f32), on
 tables held in parity buffers (state t in buffer t & 1).
 
 Cases: d in {64, 128, 256}; T = 3, 4 and 6 (a partial negative group; negatives past
-the 4 a contribution record holds); an even and an odd
-step; duplicate users; a hot item with 40 or 80 positive slots (20 / 40 contribution
-rounds; 80 refills the block's staged id table); look-ahead rows lagging 0..7 steps, in their parity
-buffer with the other buffer poisoned (NaN); zero-state rows."""
+the 4 a contribution record holds); an even and an odd step; duplicate users; a hot
+item with 40 or 80 positive slots (a split row: its contributions dealt out in shares
+of 2 to other blocks of the launch, the last to arrive sums them); batches whose items
+come from 3 or 5 ids (more shares than the 256 a batch deals out: the rest stay with
+the row's own block, past its 62 staged records); look-ahead rows lagging 0..7 steps, in
+their parity buffer with the other buffer poisoned (NaN); zero-state rows. After the
+launch the arrival counters are zero again."""
 import numpy as np
 import pytest
 import torch
@@ -34,16 +37,20 @@ def _grouping(keys, space):
     return segs
 
 
-@pytest.mark.parametrize('d,T,s', [(64, 3, 6), (128, 4, 7), (128, 4, 10), (256, 3, 9),
-                                   (128, 6, 8)])
-def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
+@pytest.mark.parametrize('d,T,s,Bc,few', [(64, 3, 6, 96, 0), (128, 4, 7, 96, 0),
+                                          (128, 4, 10, 96, 0), (256, 3, 9, 96, 0),
+                                          (128, 6, 8, 96, 0), (128, 4, 12, 640, 5),
+                                          (64, 3, 11, 640, 3)])
+def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
     g = torch.Generator().manual_seed(d * 100 + T * 10 + s)
-    nU, nI, Bc = 257, 301, 96
+    nU, nI = 257, 301
     # batch 0 (the step) and batch 1 (whose rows the look-ahead completes)
     user0 = torch.randint(0, nU, (Bc,), generator=g)
     user0[5] = user0[17] = user0[60]                       # a user with 3 positives
     user1 = torch.randint(0, nU, (Bc,), generator=g)
     items0 = torch.randint(1, nI, ((1 + T) * Bc,), generator=g)
+    if few:                                                 # every item row a split row
+        items0 = torch.randint(1, 1 + few, ((1 + T) * Bc,), generator=g)
     hot = 40 if s % 2 == 0 else 80                          # > 64: two id-table refills
     items0[:hot] = 7                                        # hot item: `hot` positive slots
     items0[Bc + 3] = 7                                      # ... and a negative slot
@@ -118,9 +125,11 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s):
          'last': flI, 'ahead': ahead[1]}])
     loss_k = torch.full((Bc,), float('nan'), device=dev)
     recs = ops.step_records(to(user0), to(items0), 1, Bc, T, nU, nI, gu0, gi0)
+    scratch = ops.step_scratch(Bc, T, d, dev)
     ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, to(items0), Bc, T, grad_scale, loss_k, recs,
-                      consts, base, 3)
+                      scratch, consts, base, 3)
     torch.cuda.synchronize()
+    assert int(scratch[1].abs().sum()) == 0 and int(scratch[3].abs().sum()) == 0
 
     assert torch.equal(loss_k, o['loss_k'])
     for (P, rp), rl, fl, (rm, fm), (rv, fv) in (
@@ -151,4 +160,4 @@ def test_bpr_adam_step_rejects_bad_tables(dev):
     recs = ops.step_records(z[:Bc], z, 1, Bc, T, 10, 10, g, _grouping(z, 10))
     with pytest.raises(NativeError):            # no parity buffer
         ops.bpr_adam_step(tabs, [Bc, 3 * Bc], d, z, Bc, T, 0.1, torch.zeros(Bc, device=dev), recs,
-                          consts, base)
+                          ops.step_scratch(Bc, T, d, dev), consts, base)

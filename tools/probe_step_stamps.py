@@ -3,7 +3,8 @@ per-block real-time stamps (MIREC_LIB=recbole_amd/_lib/alt/step_stamps.so, built
 `tools/build_variant.sh step_stamps -DMIREC_STEP_STAMPS`), one eager step at a time on
 the C2 workload. Per launch: the spread of block start times (dispatch), and per block
 class (look-ahead rows, touched user rows, touched item rows) the time from entry to
-the first load levels, to the end of the contributions / loads, and to the end — as
+the first load levels, to the end of the contributions / loads, and to the end (shares of
+split rows: the end of the last arriver only) — as
 quantiles over the blocks, in microseconds (100 MHz stamps: 10 ns resolution). The
 stamp build's own run time is not quoted anywhere: its shares are what count.
 
@@ -40,8 +41,11 @@ def main():
     step.run_batches(0, args.warmup)
     torch.cuda.synchronize()
     nU_max, nI_max = step._n_max[0], step._n_max[1]
-    starts = [0, nU_max, nU_max + nI_max, 2 * nU_max + nI_max, 2 * (nU_max + nI_max)]
-    buf = np.zeros(16384 * 4, dtype=np.uint64)
+    cap = 256                                        # shares per (table, batch): step.hip kSplitCap
+    starts = [0, cap, 2 * cap]                       # segments: shares U, I, ahead U, I, touched U, I
+    for n in (nU_max, nI_max, nU_max, nI_max):
+        starts.append(starts[-1] + n)
+    buf = np.zeros(32768 * 4, dtype=np.uint64)
     out = []
     for b in range(args.warmup, args.warmup + args.steps):
         L.mirec_step_stamps_clear()
@@ -55,10 +59,10 @@ def main():
         rec = {'batch': b, 'makespan_us': round((st[live, 3].max() - t0) * TICK_US, 2),
                'dispatch_spread_us': np.round(np.quantile(
                    (st[st[:, 0] > 0, 0] - t0) * TICK_US, [0.5, 0.9, 1.0]), 2).tolist()}
-        for name, (a, e) in (('ahead_users', (starts[0], starts[1])),
-                             ('ahead_items', (starts[1], starts[2])),
-                             ('touched_users', (starts[2], starts[3])),
-                             ('touched_items', (starts[3], starts[4]))):
+        names = ('share_users', 'share_items', 'ahead_users', 'ahead_items', 'touched_users',
+                 'touched_items')
+        for q, name in enumerate(names):
+            a, e = starts[q], starts[q + 1]
             s = st[a:e][live[a:e]]
             if len(s) == 0:
                 rec[name] = None
