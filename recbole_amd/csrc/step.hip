@@ -140,40 +140,55 @@ __device__ __forceinline__ void contrib_record(int q, int tb, int Bc, int T,
   reinterpret_cast<int4*>(out)[1] = make_int4(r[4], r[5], r[6], r[7]);
 }
 
-// One block per (table, batch): row records of the batch's touched-row slots, task
-// records of the shares of its split rows, contribution records of its positions.
-__global__ __launch_bounds__(256) void step_records_kernel(
+struct RecJob {   // one table's groupings and record buffers
+  const int32_t* perm; const int32_t* uniq; const int32_t* seg; const int32_t* nu;
+  int32_t* rec; int32_t* crec;
+};
+
+// Contribution records of every grouped position: grid (position blocks, 2 * batches),
+// 256 positions per block — three dependent loads (perm, then the keys), no serial loop.
+__global__ __launch_bounds__(256) void step_contrib_records_kernel(
     const int64_t* __restrict__ ukeys, const int64_t* __restrict__ ikeys, int n_batches, int Bc,
-    int T, int64_t nU, int64_t nI, const int32_t* __restrict__ u_perm,
-    const int32_t* __restrict__ u_uniq, const int32_t* __restrict__ u_seg,
-    const int32_t* __restrict__ u_nu, const int32_t* __restrict__ i_perm,
-    const int32_t* __restrict__ i_uniq, const int32_t* __restrict__ i_seg,
-    const int32_t* __restrict__ i_nu, int32_t* __restrict__ u_rec, int32_t* __restrict__ u_crec,
-    int32_t* __restrict__ i_rec, int32_t* __restrict__ i_crec) {
-  __shared__ int scan_lds[256 / 64 + 1];
-  const int tb = blockIdx.x >= (unsigned)n_batches;
-  const int b = tb ? blockIdx.x - n_batches : blockIdx.x;
+    int T, int64_t nU, int64_t nI, RecJob U, RecJob I) {
+  const int tb = blockIdx.y >= (unsigned)n_batches;
+  const int b = tb ? blockIdx.y - n_batches : blockIdx.y;
+  const RecJob& J = tb ? I : U;
   const int KI = (1 + T) * Bc;
   const int per = tb ? KI : Bc;
-  const int64_t* __restrict__ user = ukeys + (int64_t)b * Bc;
-  const int64_t* __restrict__ items = ikeys + (int64_t)b * KI;
-  const int32_t* __restrict__ perm = (tb ? i_perm : u_perm) + (int64_t)b * per;
-  const int32_t* __restrict__ uniq = (tb ? i_uniq : u_uniq) + (int64_t)b * per;
-  const int32_t* __restrict__ seg = (tb ? i_seg : u_seg) + (int64_t)b * (per + 1);
-  const int nu = (tb ? i_nu : u_nu)[b];
-  int32_t* __restrict__ rec = (tb ? i_rec : u_rec) + (int64_t)b * rec_ints(per);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= per) return;
+  const int32_t* __restrict__ seg = J.seg + (int64_t)b * (per + 1);
+  if (i >= seg[J.nu[b]]) return;
+  contrib_record(J.perm[(int64_t)b * per + i], tb, Bc, T, ukeys + (int64_t)b * Bc,
+                 ikeys + (int64_t)b * KI, nU, nI, J.crec + ((int64_t)b * per + i) * kRecInts);
+}
+
+// Row records of the touched-row slots and share records of split rows, one block of
+// 1024 threads per (table, batch): the contribution records are copied from crec
+// (step_contrib_records_kernel), the shares dealt out in row-slot order (a block scan).
+constexpr int kRowRecThreads = 1024;
+__global__ __launch_bounds__(kRowRecThreads) void step_row_records_kernel(int n_batches, int Bc,
+                                                                          int T, RecJob U,
+                                                                          RecJob I) {
+  __shared__ int scan_lds[kRowRecThreads / 64 + 1];
+  const int tb = blockIdx.x >= (unsigned)n_batches;
+  const int b = tb ? blockIdx.x - n_batches : blockIdx.x;
+  const RecJob& J = tb ? I : U;
+  const int per = tb ? (1 + T) * Bc : Bc;
+  const int32_t* __restrict__ uniq = J.uniq + (int64_t)b * per;
+  const int32_t* __restrict__ seg = J.seg + (int64_t)b * (per + 1);
+  const int nu = J.nu[b];
+  int32_t* __restrict__ rec = J.rec + (int64_t)b * rec_ints(per);
   int32_t* __restrict__ task = rec + (int64_t)per * kRowRec;
-  int32_t* __restrict__ crec = (tb ? i_crec : u_crec) + (int64_t)b * per * kRecInts;
-  const int n = seg[nu];
-  for (int i = threadIdx.x; i < n; i += blockDim.x)
-    contrib_record(perm[i], tb, Bc, T, user, items, nU, nI, crec + (int64_t)i * kRecInts);
+  const int4* __restrict__ crec = reinterpret_cast<const int4*>(J.crec + (int64_t)b * per * kRecInts);
   int dealt = 0;                                   // shares dealt out so far (block-uniform)
-  for (int x0 = 0; x0 < nu; x0 += blockDim.x) {
+  for (int x0 = 0; x0 < nu; x0 += kRowRecThreads) {
     const int x = x0 + threadIdx.x;
-    int i0 = 0, nc = 0;
+    int i0 = 0, nc = 0, row = 0;
     if (x < nu) {
       i0 = seg[x];
       nc = seg[x + 1] - i0;
+      row = uniq[x];
     }
     const int want = nc > kShare ? (nc + kShare - 1) / kShare - 1 : 0;
     int total;
@@ -182,19 +197,20 @@ __global__ __launch_bounds__(256) void step_records_kernel(
     if (x >= nu) continue;
     const int got = max(0, min(want, kSplitCap - base));
     const int nsh = 1 + got;
-    int32_t* r = rec + (int64_t)x * kRowRec;
-    reinterpret_cast<int4*>(r)[0] = make_int4(uniq[x], i0, nc, nsh);
-    for (int c = 0; c < kRecInline; ++c)
-      if (c < nc) contrib_record(perm[i0 + c], tb, Bc, T, user, items, nU, nI,
-                                 r + 4 + c * kRecInts);
+    int4* r = reinterpret_cast<int4*>(rec + (int64_t)x * kRowRec);
+    r[0] = make_int4(row, i0, nc, nsh);
+    for (int c = 0; c < kRecInline && c < nc; ++c) {
+      r[1 + 2 * c] = crec[2 * (i0 + c)];
+      r[2 + 2 * c] = crec[2 * (i0 + c) + 1];
+    }
     for (int j = 1; j <= got; ++j) {
-      int32_t* tr = task + (int64_t)(base + j - 1) * kTaskRec;
-      reinterpret_cast<int4*>(tr)[0] = make_int4(x, j, i0, nc);
-      reinterpret_cast<int4*>(tr)[1] = make_int4(uniq[x], nsh, 0, 0);
-      for (int c = 0; c < kShare; ++c)
-        if (j * kShare + c < nc)
-          contrib_record(perm[i0 + j * kShare + c], tb, Bc, T, user, items, nU, nI,
-                         tr + 8 + c * kRecInts);
+      int4* tr = reinterpret_cast<int4*>(task + (int64_t)(base + j - 1) * kTaskRec);
+      tr[0] = make_int4(x, j, i0, nc);
+      tr[1] = make_int4(row, nsh, 0, 0);
+      for (int c = 0; c < kShare && j * kShare + c < nc; ++c) {
+        tr[2 + 2 * c] = crec[2 * (i0 + j * kShare + c)];
+        tr[3 + 2 * c] = crec[2 * (i0 + j * kShare + c) + 1];
+      }
     }
   }
   if (threadIdx.x == 0) task[(int64_t)kSplitCap * kTaskRec] = min(dealt, kSplitCap);
@@ -516,17 +532,25 @@ extern "C" int mirec_step_records(const int64_t* user_keys, const int64_t* item_
                                   const int32_t* i_seg, const int32_t* i_nu, int32_t* u_rec,
                                   int32_t* u_crec, int32_t* i_rec, int32_t* i_crec,
                                   void* stream) {
-  if (n_batches < 0 || Bc < 0 || T < 1 || (int64_t)(1 + T) * Bc > INT32_MAX || n_users <= 0 ||
-      n_items <= 0 || !user_keys || !item_keys || !u_perm || !u_uniq || !u_seg || !u_nu ||
+  if (n_batches < 0 || n_batches > 32767 || Bc < 0 || T < 1 ||
+      (int64_t)(1 + T) * Bc > INT32_MAX || n_users <= 0 || n_items <= 0 || !user_keys || !item_keys || !u_perm || !u_uniq || !u_seg || !u_nu ||
       !i_perm || !i_uniq || !i_seg || !i_nu || !u_rec || !u_crec || !i_rec || !i_crec) {
     set_error("mirec_step_records: bad arguments");
     return -1;
   }
   if (n_batches == 0 || Bc == 0) return 0;
-  hipLaunchKernelGGL(step_records_kernel, dim3((unsigned)(2 * n_batches)), dim3(256), 0,
+  const RecJob U = {u_perm, u_uniq, u_seg, u_nu, u_rec, u_crec};
+  const RecJob I = {i_perm, i_uniq, i_seg, i_nu, i_rec, i_crec};
+  const int64_t KI = (1 + T) * Bc;
+  hipLaunchKernelGGL(step_contrib_records_kernel,
+                     dim3((unsigned)((KI + 255) / 256), (unsigned)(2 * n_batches)), dim3(256), 0,
                      (hipStream_t)stream, user_keys, item_keys, (int)n_batches, (int)Bc, T,
-                     n_users, n_items, u_perm, u_uniq, u_seg, u_nu, i_perm, i_uniq, i_seg, i_nu,
-                     u_rec, u_crec, i_rec, i_crec);
+                     n_users, n_items, U, I);
+  const int rc = launch_status("mirec_step_records");
+  if (rc) return rc;
+  hipLaunchKernelGGL(step_row_records_kernel, dim3((unsigned)(2 * n_batches)),
+                     dim3(kRowRecThreads), 0, (hipStream_t)stream, (int)n_batches, (int)Bc, T, U,
+                     I);
   return launch_status("mirec_step_records");
 }
 

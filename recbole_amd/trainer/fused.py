@@ -277,17 +277,20 @@ class FusedBPRTrainStep(object):
 
     def _chunk_flags(self, plan):
         """(entry, flush) per chunk of the deferred schedule: a chunk flushes every
-        row at its end once max(C, FLUSH_EVERY) or more steps have run since the last
-        flush (and before a ragged batch / the end); a chunk after one that did not flush
-        starts with an entry catch-up of the rows its first batch reads."""
+        row at its end once FLUSH_EVERY or more steps have run since the last flush, or
+        when the next chunk would take the count past 1.5 x FLUSH_EVERY (the ramp's
+        4 + 8 + 16 + 32 steps flush before the first 64-step chunk instead of after it),
+        and before a ragged batch / the end; a chunk after one that did not flush starts
+        with an entry catch-up of the rows its first batch reads."""
         flags, since = [], 0
         at = getattr(self, '_flush_at', set())
         for i, (b0, nb, Bc) in enumerate(plan):
             entry = since > 0
             since += nb
             nxt_full = i + 1 < len(plan) and plan[i + 1][2] == self.Bg
-            flush = (since >= max(self.C, self.FLUSH_EVERY) or not nxt_full
-                     or b0 + nb in at)
+            nxt_nb = plan[i + 1][1] if i + 1 < len(plan) else 0
+            flush = (since >= self.FLUSH_EVERY or since + nxt_nb > self.FLUSH_EVERY * 3 // 2
+                     or not nxt_full or b0 + nb in at)
             if flush:
                 since = 0
             flags.append((entry, flush))
