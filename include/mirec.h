@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 13
+#define MIREC_ABI_VERSION 14
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -591,7 +591,10 @@ int mirec_gather_scale_rows_f32(const float* table, int64_t n_rows, int32_t d,
  *   token_seq: grad[(b*L + t)*d + k] = mask * ge / (count + 1e-8), grad1[b*L+t] = mask*g_fm[b];
  *   float: grad[b*grad_ld + k] = ge * x_b, grad1[b*grad1_ld] = g_fm[b] * x_b
  *          (column-sum them over b).
- * 1 <= d <= 64.
+ * 1 <= d <= 64. work: mirec_ctx_fm_work_floats(B, n_fields, d) floats written by the
+ * forward (per-field first-order terms, then S_bk) and read by the backward of the same
+ * batch. The forward is two launches (a gather over every (sample, field) pair, then
+ * the per-sample sums in field order), the backward one over every (sample, field).
  * ------------------------------------------------------------------------- */
 typedef struct mirec_ctx_field {
   int32_t kind;
@@ -609,11 +612,13 @@ typedef struct mirec_ctx_field {
   int64_t grad1_ld;  /* stride of grad1 for kinds 0 and 2 */
 } mirec_ctx_field;
 
+size_t mirec_ctx_fm_work_floats(int64_t B, int32_t n_fields, int32_t d);
 int mirec_ctx_fm_fwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields, int64_t B,
-                         int32_t d, const float* bias, float* concat, float* y_fm, void* stream);
+                         int32_t d, const float* bias, float* concat, float* y_fm, float* work,
+                         void* stream);
 int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields, int64_t B,
                          int32_t d, const float* concat, const float* g_concat,
-                         const float* g_fm, void* stream);
+                         const float* g_fm, const float* work, void* stream);
 
 /* sigmoid + nn.BCELoss (DeepFM.forward / calculate_loss, deepfm.py:66-73):
  * z = y_fm + y_deep (y_deep may be NULL); prob = sigmoid(z);

@@ -156,8 +156,9 @@ SIGNATURES = {
     "mirec_spmm_csr_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
                                    _P, _P, c_int64, _P, ctypes.POINTER(RowsRef),
                                    ctypes.POINTER(SpmmEpilogue), _P]),
-    "mirec_ctx_fm_fwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P]),
-    "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P]),
+    "mirec_ctx_fm_work_floats": (c_size_t, [c_int64, c_int32, c_int32]),
+    "mirec_ctx_fm_fwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P, _P]),
+    "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P, _P]),
     "mirec_sigmoid_bce_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
     "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
     "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
@@ -173,7 +174,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 class NativeError(RuntimeError):

@@ -38,7 +38,9 @@ __device__ __forceinline__ int wave_sum_i(int x) {
 
 // Block-wide exclusive scan of one int per thread (blockDim.x <= 1024,
 // multiple of 64). `lds` needs blockDim.x/64 + 1 ints. Returns the exclusive
-// prefix; *total gets the block sum. Contains __syncthreads().
+// prefix; *total gets the block sum. Contains __syncthreads(). Every lane reads
+// the wave totals in one burst of LDS loads (no serial pass by one thread between
+// two more barriers).
 __device__ __forceinline__ int block_exclusive_scan(int x, int* lds, int* total) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -52,20 +54,15 @@ __device__ __forceinline__ int block_exclusive_scan(int x, int* lds, int* total)
   }
   if (lane == 63) lds[wid] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int w = 0; w < nw; ++w) {
-      int t = lds[w];
-      lds[w] = acc;
-      acc += t;
-    }
-    lds[nw] = acc;
+  int pre = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int t = lds[w];
+    pre += w < wid ? t : 0;
+    tot += t;
   }
-  __syncthreads();
-  int excl = lds[wid] + v - x;
-  *total = lds[nw];
-  __syncthreads();
-  return excl;
+  __syncthreads();                      // lds is reused by the next scan
+  *total = tot;
+  return pre + v - x;
 }
 
 // Binary search for `key` in sorted cols[lo, hi).

@@ -38,99 +38,122 @@ __device__ __forceinline__ int64_t clamp_row(int64_t r, int64_t n) {
   return r < 0 ? 0 : (r >= n ? n - 1 : r);
 }
 
-// Forward: concat[b, f*d + k], keys of token fields, y_fm[b].
+// Forward, two launches. (1) gather: one block row per field (blockIdx.y = f, so the
+// field descriptor is block-uniform), LPS lanes per sample: the field's row (token),
+// masked mean (token_seq) or scaled row (float) -> concat[b, f, :], its first-order
+// term -> fo[b, f], the token row id -> keys. Every (sample, field) pair is independent:
+// B * F groups in flight instead of B. (2) reduce, LPS lanes per sample: the FM sums
+// S = sum_f e, Q = sum_f e^2 and the first-order sums by kind, all in field order (the
+// one-kernel order), y_fm; S is kept for the backward.
 template <int LPS>
-__global__ __launch_bounds__(kCtxThreads) void ctx_fm_fwd_kernel(
+__global__ __launch_bounds__(kCtxThreads) void ctx_fm_gather_kernel(
     const mirec_ctx_field* __restrict__ fields, int n_fields, int64_t B, int d,
-    const float* __restrict__ bias, float* __restrict__ concat, float* __restrict__ y_fm) {
+    float* __restrict__ concat, float* __restrict__ fo) {
   constexpr int SPW = 64 / LPS;
   const int lane = threadIdx.x & 63;
   const int k = lane % LPS;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t b = wave * SPW + lane / LPS;
+  const int f = blockIdx.y;
+  const int64_t b = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / LPS;
+  if (b >= B) return;
+  const bool col = k < d;
+  const int64_t F = n_fields;
+  const mirec_ctx_field fd = fields[f];
+  float e = 0.f, w1 = 0.f;
+  if (fd.kind == 0) {
+    const int64_t r = clamp_row(fd.ids[b] + fd.offset, fd.n_rows);
+    if (col) e = fd.table[r * d + k];
+    w1 = fd.table1[r];
+    if (fd.keys && k == 0) fd.keys[b] = r;
+  } else if (fd.kind == 1) {
+    const int64_t* ids = fd.ids + b * fd.seq_len;
+    float sum = 0.f, cnt = 0.f;
+    for (int t = 0; t < fd.seq_len; ++t) {
+      const int64_t id = ids[t];
+      const float msk = id != 0 ? 1.f : 0.f;
+      const int64_t r = clamp_row(id, fd.n_rows);
+      if (col) sum += fd.table[r * d + k] * msk;
+      w1 += fd.table1[r] * msk;
+      cnt += msk;
+    }
+    e = sum / (cnt + 1e-8f);
+  } else {
+    const float x = fd.vals[b];
+    if (col) e = fd.table[fd.offset * d + k] * x;
+    w1 = fd.table1[fd.offset] * x;
+  }
+  if (col) concat[(b * F + f) * d + k] = e;
+  if (k == 0) fo[b * F + f] = w1;
+}
+
+template <int LPS>
+__global__ __launch_bounds__(kCtxThreads) void ctx_fm_reduce_kernel(
+    const mirec_ctx_field* __restrict__ fields, int n_fields, int64_t B, int d,
+    const float* __restrict__ bias, const float* __restrict__ concat,
+    const float* __restrict__ fo, float* __restrict__ y_fm, float* __restrict__ fm_sum) {
+  constexpr int SPW = 64 / LPS;
+  const int lane = threadIdx.x & 63;
+  const int k = lane % LPS;
+  const int64_t b = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / LPS;
   if (b >= B) return;   // whole groups exit together; no cross-group shuffles below
   const bool col = k < d;
   const int64_t F = n_fields;
   float S = 0.f, Q = 0.f;
   float fo_float = 0.f, fo_tok = 0.f, fo_seq = 0.f;
   for (int f = 0; f < n_fields; ++f) {
-    const mirec_ctx_field fd = fields[f];
-    float e = 0.f;
-    if (fd.kind == 0) {
-      const int64_t r = clamp_row(fd.ids[b] + fd.offset, fd.n_rows);
-      if (col) e = fd.table[r * d + k];
-      fo_tok += fd.table1[r];
-      if (fd.keys && k == 0) fd.keys[b] = r;
-    } else if (fd.kind == 1) {
-      const int64_t* ids = fd.ids + b * fd.seq_len;
-      float sum = 0.f, cnt = 0.f, w = 0.f;
-      for (int t = 0; t < fd.seq_len; ++t) {
-        const int64_t id = ids[t];
-        const float msk = id != 0 ? 1.f : 0.f;
-        const int64_t r = clamp_row(id, fd.n_rows);
-        if (col) sum += fd.table[r * d + k] * msk;
-        w += fd.table1[r] * msk;
-        cnt += msk;
-      }
-      e = sum / (cnt + 1e-8f);
-      fo_seq += w;
-    } else {
-      const float x = fd.vals[b];
-      if (col) e = fd.table[fd.offset * d + k] * x;
-      fo_float += fd.table1[fd.offset] * x;
-    }
-    if (col) concat[(b * F + f) * d + k] = e;
+    const int kind = fields[f].kind;
+    const float e = col ? concat[(b * F + f) * d + k] : 0.f;
+    const float w1 = fo[b * F + f];
+    if (kind == 0) fo_tok += w1;
+    else if (kind == 1) fo_seq += w1;
+    else fo_float += w1;
     S += e;
     Q += e * e;
   }
+  if (col) fm_sum[b * d + k] = S;
   const float fm = 0.5f * group_sum<LPS>(col ? S * S - Q : 0.f);
   if (k == 0) y_fm[b] = ((fo_float + fo_tok) + fo_seq) + bias[0] + fm;
 }
 
-// Backward. g_concat: dL/d concat [B, F*d] (may be NULL = 0); g_fm: dL/d y_fm [B].
+// Backward, one block row per field as the gather. g_concat: dL/d concat [B, F*d] (may
+// be NULL = 0); g_fm: dL/d y_fm [B]; fm_sum: the forward's S.
 // grad_e = g_concat + g_fm * (S_k - e) (d fm / d e_fk = S_k - e_fk).
 template <int LPS>
 __global__ __launch_bounds__(kCtxThreads) void ctx_fm_bwd_kernel(
     const mirec_ctx_field* __restrict__ fields, int n_fields, int64_t B, int d,
     const float* __restrict__ concat, const float* __restrict__ g_concat,
-    const float* __restrict__ g_fm) {
+    const float* __restrict__ g_fm, const float* __restrict__ fm_sum) {
   constexpr int SPW = 64 / LPS;
   const int lane = threadIdx.x & 63;
   const int k = lane % LPS;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t b = wave * SPW + lane / LPS;
+  const int f = blockIdx.y;
+  const int64_t b = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / LPS;
   if (b >= B) return;
   const bool col = k < d;
   const int64_t F = n_fields;
-  float S = 0.f;
-  if (col)
-    for (int f = 0; f < n_fields; ++f) S += concat[(b * F + f) * d + k];
   const float gf = g_fm[b];
-  for (int f = 0; f < n_fields; ++f) {
-    const mirec_ctx_field fd = fields[f];
-    float ge = 0.f;
-    if (col) {
-      const int64_t c = (b * F + f) * d + k;
-      ge = (g_concat ? g_concat[c] : 0.f) + gf * (S - concat[c]);
+  const mirec_ctx_field fd = fields[f];
+  float ge = 0.f;
+  if (col) {
+    const int64_t c = (b * F + f) * d + k;
+    ge = (g_concat ? g_concat[c] : 0.f) + gf * (fm_sum[b * d + k] - concat[c]);
+  }
+  if (fd.kind == 0) {
+    if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge;
+    if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf;
+  } else if (fd.kind == 1) {
+    const int64_t* ids = fd.ids + b * fd.seq_len;
+    float cnt = 0.f;
+    for (int t = 0; t < fd.seq_len; ++t) cnt += ids[t] != 0 ? 1.f : 0.f;
+    const float gm = ge / (cnt + 1e-8f);
+    for (int t = 0; t < fd.seq_len; ++t) {
+      const float msk = ids[t] != 0 ? 1.f : 0.f;
+      if (col && fd.grad) fd.grad[(b * fd.seq_len + t) * d + k] = gm * msk;
+      if (k == 0 && fd.grad1) fd.grad1[b * fd.seq_len + t] = gf * msk;
     }
-    if (fd.kind == 0) {
-      if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge;
-      if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf;
-    } else if (fd.kind == 1) {
-      const int64_t* ids = fd.ids + b * fd.seq_len;
-      float cnt = 0.f;
-      for (int t = 0; t < fd.seq_len; ++t) cnt += ids[t] != 0 ? 1.f : 0.f;
-      const float gm = ge / (cnt + 1e-8f);
-      for (int t = 0; t < fd.seq_len; ++t) {
-        const float msk = ids[t] != 0 ? 1.f : 0.f;
-        if (col && fd.grad) fd.grad[(b * fd.seq_len + t) * d + k] = gm * msk;
-        if (k == 0 && fd.grad1) fd.grad1[b * fd.seq_len + t] = gf * msk;
-      }
-    } else {
-      const float x = fd.vals[b];
-      if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge * x;
-      if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf * x;
-    }
+  } else {
+    const float x = fd.vals[b];
+    if (col && fd.grad) fd.grad[b * fd.grad_ld + k] = ge * x;
+    if (k == 0 && fd.grad1) fd.grad1[b * fd.grad1_ld] = gf * x;
   }
 }
 
@@ -206,42 +229,62 @@ static unsigned ctx_grid(int64_t B, int lps) {
 
 using namespace mirec;
 
-#define MIREC_CTX_DISPATCH(KERNEL, ...)                                                       \
+#define MIREC_CTX_DISPATCH(KERNEL, NY, ...)                                                   \
   do {                                                                                        \
     hipStream_t st = (hipStream_t)stream;                                                     \
+    const unsigned ny = (unsigned)(NY);                                                       \
     if (d <= 4)                                                                               \
-      hipLaunchKernelGGL(KERNEL<4>, dim3(ctx_grid(B, 4)), dim3(kCtxThreads), 0, st, __VA_ARGS__);   \
+      hipLaunchKernelGGL(KERNEL<4>, dim3(ctx_grid(B, 4), ny), dim3(kCtxThreads), 0, st,       \
+                         __VA_ARGS__);                                                        \
     else if (d <= 8)                                                                          \
-      hipLaunchKernelGGL(KERNEL<8>, dim3(ctx_grid(B, 8)), dim3(kCtxThreads), 0, st, __VA_ARGS__);   \
+      hipLaunchKernelGGL(KERNEL<8>, dim3(ctx_grid(B, 8), ny), dim3(kCtxThreads), 0, st,       \
+                         __VA_ARGS__);                                                        \
     else if (d <= 16)                                                                         \
-      hipLaunchKernelGGL(KERNEL<16>, dim3(ctx_grid(B, 16)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+      hipLaunchKernelGGL(KERNEL<16>, dim3(ctx_grid(B, 16), ny), dim3(kCtxThreads), 0, st,     \
+                         __VA_ARGS__);                                                        \
     else if (d <= 32)                                                                         \
-      hipLaunchKernelGGL(KERNEL<32>, dim3(ctx_grid(B, 32)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+      hipLaunchKernelGGL(KERNEL<32>, dim3(ctx_grid(B, 32), ny), dim3(kCtxThreads), 0, st,     \
+                         __VA_ARGS__);                                                        \
     else                                                                                      \
-      hipLaunchKernelGGL(KERNEL<64>, dim3(ctx_grid(B, 64)), dim3(kCtxThreads), 0, st, __VA_ARGS__); \
+      hipLaunchKernelGGL(KERNEL<64>, dim3(ctx_grid(B, 64), ny), dim3(kCtxThreads), 0, st,     \
+                         __VA_ARGS__);                                                        \
   } while (0)
+
+extern "C" size_t mirec_ctx_fm_work_floats(int64_t B, int32_t n_fields, int32_t d) {
+  return B < 0 || n_fields < 0 || d < 0 ? 0 : (size_t)B * ((size_t)n_fields + (size_t)d);
+}
 
 extern "C" int mirec_ctx_fm_fwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields,
                                     int64_t B, int32_t d, const float* bias, float* concat,
-                                    float* y_fm, void* stream) {
+                                    float* y_fm, float* work, void* stream) {
   if (B == 0) return 0;
-  if (!fields_dev || n_fields <= 0 || B < 0 || d < 1 || d > 64 || !bias || !concat || !y_fm) {
-    set_error("mirec_ctx_fm_fwd_f32: bad arguments (1 <= d <= 64)");
+  if (!fields_dev || n_fields <= 0 || n_fields > 65535 || B < 0 || d < 1 || d > 64 || !bias ||
+      !concat || !y_fm || !work) {
+    set_error("mirec_ctx_fm_fwd_f32: bad arguments (1 <= d <= 64, 1 <= fields <= 65535)");
     return -1;
   }
-  MIREC_CTX_DISPATCH(ctx_fm_fwd_kernel, fields_dev, n_fields, B, d, bias, concat, y_fm);
+  float* fo = work;
+  float* fm_sum = work + B * n_fields;
+  MIREC_CTX_DISPATCH(ctx_fm_gather_kernel, n_fields, fields_dev, n_fields, B, d, concat, fo);
+  const int rc = launch_status("mirec_ctx_fm_fwd_f32: gather");
+  if (rc) return rc;
+  MIREC_CTX_DISPATCH(ctx_fm_reduce_kernel, 1, fields_dev, n_fields, B, d, bias, concat, fo, y_fm,
+                     fm_sum);
   return launch_status("mirec_ctx_fm_fwd_f32");
 }
 
 extern "C" int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields,
                                     int64_t B, int32_t d, const float* concat,
-                                    const float* g_concat, const float* g_fm, void* stream) {
+                                    const float* g_concat, const float* g_fm, const float* work,
+                                    void* stream) {
   if (B == 0) return 0;
-  if (!fields_dev || n_fields <= 0 || B < 0 || d < 1 || d > 64 || !concat || !g_fm) {
-    set_error("mirec_ctx_fm_bwd_f32: bad arguments (1 <= d <= 64)");
+  if (!fields_dev || n_fields <= 0 || n_fields > 65535 || B < 0 || d < 1 || d > 64 || !concat ||
+      !g_fm || !work) {
+    set_error("mirec_ctx_fm_bwd_f32: bad arguments (1 <= d <= 64, 1 <= fields <= 65535)");
     return -1;
   }
-  MIREC_CTX_DISPATCH(ctx_fm_bwd_kernel, fields_dev, n_fields, B, d, concat, g_concat, g_fm);
+  MIREC_CTX_DISPATCH(ctx_fm_bwd_kernel, n_fields, fields_dev, n_fields, B, d, concat, g_concat,
+                     g_fm, work + B * n_fields);
   return launch_status("mirec_ctx_fm_bwd_f32");
 }
 

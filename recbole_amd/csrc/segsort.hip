@@ -110,7 +110,7 @@ __device__ __forceinline__ void segsort_lds_batch(
   const int hi = min(n, lo + ipt);
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
+  constexpr int nw = kSortThreads / 64;  // every launch of these kernels: kSortThreads lanes
   // Stable LSD passes of kDigitBits-bit digits (a blocked arrangement: thread t owns
   // positions [lo, hi)). Per-digit counts travel packed, four 16-bit fields per
   // 64-bit word (n <= 8192 < 2^16: no carries), so one wave scan of kDigitWords words
@@ -147,6 +147,7 @@ __device__ __forceinline__ void segsort_lds_batch(
     uint64_t ex[kDigitWords], tot[kDigitWords];
 #pragma unroll
     for (int w = 0; w < kDigitWords; ++w) { ex[w] = inc[w] - c[w]; tot[w] = 0ull; }
+#pragma unroll
     for (int v = 0; v < nw; ++v) {
 #pragma unroll
       for (int w = 0; w < kDigitWords; ++w) {

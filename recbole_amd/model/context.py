@@ -117,10 +117,15 @@ def ctx_fm_forward(layout, interaction, tables, B, d, bias, keys=None):
     fields_dev = _upload(arr, dev)
     concat = torch.empty(B, layout.n_fields, d, dtype=torch.float32, device=dev)
     y_fm = torch.empty(B, dtype=torch.float32, device=dev)
-    rc = lib().mirec_ctx_fm_fwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(bias), ptr(concat),
-                                    ptr(y_fm), stream_handle())
+    # first-order terms + FM sums of the batch: written here, read by the backward
+    work = torch.empty(max(1, lib().mirec_ctx_fm_work_floats(B, layout.n_fields, d)),
+                       dtype=torch.float32, device=dev)
+    with ops.timed_launch('ctx_fm_fwd'):
+        rc = lib().mirec_ctx_fm_fwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(bias),
+                                        ptr(concat), ptr(y_fm), ptr(work), stream_handle())
     check(rc, "mirec_ctx_fm_fwd_f32")
     keep.append(fields_dev)
+    keep.append(work)
     return concat, y_fm, keep
 
 
@@ -154,7 +159,8 @@ class _CtxFMFn(torch.autograd.Function):
         else:
             ctx.segs = None
             h1 = None
-        concat, y_fm, _ = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
+        concat, y_fm, keep = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
+        ctx.fm_work = keep[-1]
         ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
         ctx.deferred_T = T if h is not None else None
         ctx.deferred_T1 = T1 if h1 is not None else None
@@ -180,8 +186,10 @@ class _CtxFMFn(torch.autograd.Function):
         arr, keep = build_fields(layout, ctx.interaction, tables, grads)
         fields_dev = _upload(arr, dev)
         gc = None if g_concat is None else g_concat.contiguous()
-        rc = lib().mirec_ctx_fm_bwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(concat),
-                                        ptr(gc), ptr(g_fm), stream_handle())
+        with ops.timed_launch('ctx_fm_bwd'):
+            rc = lib().mirec_ctx_fm_bwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(concat),
+                                            ptr(gc), ptr(g_fm), ptr(ctx.fm_work),
+                                            stream_handle())
         check(rc, "mirec_ctx_fm_bwd_f32")
         dT = dT1 = dEf = dEf1 = None
         if nt:

@@ -15,6 +15,32 @@ import torch
 
 from recbole_amd._native import NativeError, check, lib, ptr, stream_handle
 
+# Per-launch HIP events of named kernels, collected while a dict is installed here
+# ({name: [(start, end), ...]}; tools/bench_models.py): the measuring tool times a
+# model step's dominant kernel on the stream it runs on. None: no events.
+KERNEL_EVENTS = None
+
+
+class timed_launch(object):
+    """`with timed_launch(name): <one native launch>` — records a start / end event pair
+    on the current stream when KERNEL_EVENTS holds `name` (nothing otherwise)."""
+
+    def __init__(self, name):
+        self.name = name
+        self.ev = None
+
+    def __enter__(self):
+        if KERNEL_EVENTS is not None and self.name in KERNEL_EVENTS:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ev is not None:
+            self.ev[1].record()
+            KERNEL_EVENTS[self.name].append(self.ev)
+        return False
+
 
 def _dev(t: torch.Tensor, dtype, name: str) -> torch.Tensor:
     if not isinstance(t, torch.Tensor):

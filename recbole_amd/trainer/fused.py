@@ -726,10 +726,11 @@ class FusedBPRTrainStep(object):
         if self._next_chunk <= k:
             raise RuntimeError(f'chunk {k} is held (begin_epoch(hold_prep_from=...)): '
                                'call release_prep() first')
-        # walks of the next chunks before this chunk's grouping: the walk is the
-        # long pole of the preparation, the grouping of chunk k runs beside it
-        self._top_up_prep(k)
+        # this chunk's grouping first (its stream waits for the walk on the GPU; issued
+        # later, the host's enqueue of the next walks would delay it), then the walks of
+        # the next chunks (the same walk stream: they start as this chunk's walk ends)
         self._issue_groups(k + 1)
+        self._top_up_prep(k)
         stream.wait_event(self.slots[k % S].ready)
         self._cur = k
 

@@ -81,6 +81,54 @@ def _timed(fn, steps, warmup, opt=None):
     return (time.perf_counter() - t0) / steps
 
 
+def _window_events(step, names, steps=8):
+    """HIP events around the named native launches (ops.timed_launch) over `steps`
+    eager steps enqueued behind a spin kernel (the host enqueues the whole window
+    before the GPU reaches it, so an event pair brackets its kernel only). Returns
+    {name: (launches per step, mean launch us)}."""
+    from recbole_amd import ops
+    ops.KERNEL_EVENTS = {n: [] for n in names}
+    try:
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(2.4e3 * 1500 * steps))
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ev = ops.KERNEL_EVENTS
+    finally:
+        ops.KERNEL_EVENTS = None
+    return {n: (len(v) / steps, float(np.mean([a.elapsed_time(b) * 1e3 for a, b in v])))
+            for n, v in ev.items() if v}
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed models PMC summary
+    (profiles/r*_models_pmc.json, tools/models_pmc.py), or None."""
+    import glob
+    import json
+    paths = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_models_pmc.json')))
+    if not paths:
+        return None, None
+    rec = json.load(open(paths[-1])).get(kernel)
+    return (rec['traffic'], os.path.basename(paths[-1])) if rec else (None, None)
+
+
+def _step_breakdown(config):
+    """The committed per-step kernel breakdown of the timed step (rocprofv3 kernel
+    trace, tools/step_breakdown.py): profiles/r*_<config>_step.json, newest."""
+    import glob
+    import json
+    paths = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_{config}_step.json')))
+    if not paths:
+        return None
+    r = json.load(open(paths[-1]))
+    return {'source': os.path.basename(paths[-1]), 'wall_us_per_step': r['wall_us_per_step'],
+            'kernel_us_per_step': r['kernel_us_per_step'],
+            'launches_per_step': r['launches_per_step'], 'dominant': r['dominant'],
+            'top5': [{k: x[k] for k in ('kernel', 'us_per_step', 'launches_per_step')}
+                     for x in r['kernels'][:5]]}
+
+
 def _event_time(fn, reps=10):
     ts = []
     for _ in range(reps):
@@ -161,22 +209,24 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
 
     t = _timed(step, steps, warmup, opt)
     V = sum(nums[f'C{j}'] for j in range(26))
-    # dominant kernel: dense Adam over the [V, 16] token table (K5, HBM-bound):
-    # algorithmic bytes per step = p, m, v, g read + p, m, v written = 7 * V * d * 4
-    T = model.token_embedding_table.embedding.weight
-    st = opt._ensure_state(T)
-    g = torch.zeros_like(T)
-    from recbole_amd import ops
-    consts, idx = opt.prepare_window(1, dev)
-    ta = _event_time(lambda: ops.adam_step(T.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
-                                           dense_grad=g))
-    adam_bytes = 7 * T.numel() * 4
-    # K8 forward on one batch: rows read (26 token rows of d floats + 26 first-order
-    # weights + 26 ids + 13 floats) + concat written (39 * d) + y_fm
-    b0 = batches[0]
-    Tw, T1, Ef, Ef1, bias, seq, seq1 = model._fm_params()
-    tk = _event_time(lambda: _CtxFMFn.apply(model.field_layout, b0, Tw, T1, Ef, Ef1, bias))
-    k8_bytes = B * (26 * (d * 4 + 4 + 8) + 13 * 4 + 39 * d * 4 + 4)
+    # the timed step's dominant kernel (profiles/r03_C4_step.json: ctx_fm_bwd_kernel, K8
+    # backward), timed live on its stream over eager steps of the same batches.
+    # Algorithmic bytes per launch: concat + g_concat read (39 fields x d floats per
+    # sample), g_fm read, gradient rows written (26 token + 13 float fields x d floats)
+    # and the first-order gradients (39 floats) per sample.
+    def eager():
+        b = batches[it[0] % n_batches]
+        it[0] += 1
+        opt.zero_grad()
+        model.calculate_loss(b).backward()
+        opt.step()
+    ev = _window_events(eager, ('ctx_fm_bwd', 'ctx_fm_fwd'))
+    opt.flush()
+    bwd_n, bwd_us = ev['ctx_fm_bwd']
+    fwd_n, fwd_us = ev['ctx_fm_fwd']
+    bwd_bytes = B * (2 * 39 * d * 4 + 4 + 39 * d * 4 + 39 * 4)
+    fwd_bytes = B * (26 * (d * 4 + 4 + 8) + 13 * 4 + 39 * d * 4 + 4 + 26 * 8)
+    traffic, tsrc = _pmc_traffic('ctx_fm_bwd_kernel')
     cpu = None
     if CPU_BASELINE:
         from oracle import cpu_baseline as cb
@@ -200,15 +250,21 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
         'workload': f'DeepFM Criteo-shape: 13 float + 26 token fields, vocab {V:,} '
                     f'(incl. PADs), d={d}, MLP 624-128-128-128-1, dropout 0.2, BCE, dense Adam',
         'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) ids, log-normal floats, seeded)',
-        'roofline': {'kernel': 'K5 dense Adam over the [V,16] token table (adam_multi_kernel<16>)',
-                     'bound': 'hbm', 'achieved': round(adam_bytes / ta / 1e9, 1),
+        'step_breakdown': _step_breakdown('C4'),
+        'roofline': {'kernel': 'ctx_fm_bwd_kernel<16> (K8 backward; the timed step\'s dominant '
+                               'kernel)', 'bound': 'hbm',
+                     'achieved': round(bwd_bytes / (bwd_us * 1e-6) / 1e9, 1),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(adam_bytes / ta / 1e9 / HBM_PEAK_GBS, 4),
-                     'bytes_per_launch': adam_bytes, 'launch_us': round(ta * 1e6, 1)},
-        'k8_fwd': {'kernel': 'K8 ctx_fm_fwd (field gather + first order + FM)',
-                   'bound': 'hbm', 'achieved': round(k8_bytes / tk / 1e9, 1),
-                   'unit': 'GB/s', 'bytes_per_launch': k8_bytes,
-                   'launch_us_incl_host': round(tk * 1e6, 1)},
+                     'frac': round(bwd_bytes / (bwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     'traffic': traffic, 'traffic_source': tsrc,
+                     'bytes_per_launch': bwd_bytes, 'launch_us': round(bwd_us, 2),
+                     'launches_per_step': bwd_n,
+                     'timing': 'HIP events around each launch on its stream, 8 eager steps'},
+        'k8_fwd': {'kernel': 'ctx_fm_fwd_kernel<16> (K8 forward: field gather + first order + '
+                             'FM)', 'bound': 'hbm',
+                   'achieved': round(fwd_bytes / (fwd_us * 1e-6) / 1e9, 1),
+                   'unit': 'GB/s', 'bytes_per_launch': fwd_bytes, 'launch_us': round(fwd_us, 2),
+                   'launches_per_step': fwd_n},
     }
 
 
@@ -275,12 +331,21 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
     neg = ops.sample_walk(random_list, pr, b0['user_id'], n_neg, None, None, 1_000_000, False)
     tk = _event_time(lambda: _SampledSoftmaxFn.apply(S, W, b0['item_id'], neg))
     k9_bytes = B * (1 + n_neg) * (d * 4 + 8 + d * 4) + B * d * 4 * 2
-    st = opt._ensure_state(W)
-    g = torch.zeros_like(W)
-    consts, idx = opt.prepare_window(1, dev)
-    ta = _event_time(lambda: ops.adam_step(W.data, st['exp_avg'], st['exp_avg_sq'], consts, idx,
-                                           dense_grad=g))
-    adam_bytes = 7 * W.numel() * 4
+    # the timed step's dominant kernel (profiles/r03_C3_step.json): the attention backward
+    # of torch's fused scaled_dot_product_attention (a library kernel, 2 launches per step:
+    # one per layer), timed live with HIP events at the step's shapes (B x heads x L x
+    # d/heads, the model's additive mask, its attention dropout). FLOPs per launch: the
+    # flash backward's five L x L x dh matmuls (S recomputed, dV, dP, dQ, dK).
+    H = config['n_heads']
+    dh = d // H
+    seq0 = b0['item_id_list']
+    mask = model.get_attention_mask(seq0)
+    p_drop = model.trm_encoder.layer[0].multi_head_attention.attn_dropout.p
+    q, k, v = (torch.randn(B, H, L, dh, device=dev, requires_grad=True) for _ in range(3))
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p_drop)
+    go = torch.randn_like(o)
+    ta = _event_time(lambda: torch.autograd.grad(o, (q, k, v), go, retain_graph=True))
+    attn_flops = 5 * 2 * B * H * L * L * dh
     flops = 86.3e6 * B    # transformer fwd+bwd per sequence
     cpu = None
     if CPU_BASELINE:
@@ -305,11 +370,17 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
                     f'negatives, dense Adam',
         'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) items, Poisson(20)+4 lengths, seeded)',
         'transformer_tflops_at_step_rate': round(flops / t / 1e12, 2),
-        'roofline': {'kernel': 'K5 dense Adam over the [I,128] item table (adam_multi_kernel<128>)',
-                     'bound': 'hbm', 'achieved': round(adam_bytes / ta / 1e9, 1),
-                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(adam_bytes / ta / 1e9 / HBM_PEAK_GBS, 4),
-                     'bytes_per_launch': adam_bytes, 'launch_us': round(ta * 1e6, 1)},
+        'step_breakdown': _step_breakdown('C3'),
+        'roofline': {'kernel': 'attention backward of torch scaled_dot_product_attention '
+                               '(bwd_kernel_fuse, library; the timed step\'s dominant kernel)',
+                     'bound': 'mfma', 'achieved': round(attn_flops / ta / 1e12, 2),
+                     'peak': 157.3, 'unit': 'TFLOP/s',
+                     'frac': round(attn_flops / ta / 1e12 / 157.3, 4),
+                     'flops_per_launch': attn_flops, 'launch_us': round(ta * 1e6, 1),
+                     'timing': 'HIP events around torch.autograd.grad of one attention at the '
+                               'step shapes (median of 10)',
+                     'note': 'fp32 dense peak; our own largest kernel in the step is listed in '
+                             'step_breakdown'},
         'k9b': {'kernel': f'K9b sampled_softmax<{d}> ({n_neg} negatives)', 'bound': 'hbm',
                 'achieved': round(k9_bytes / tk / 1e9, 1), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': k9_bytes,
