@@ -433,13 +433,16 @@ int mirec_bpr_adam_step_f32(const mirec_adam_table* tables, const int64_t* n_max
  * share count, the records of its first two contributions), then 256 share records of
  * split rows (24 int32: row slot, share, first position, count, row id, share count,
  * 0, 0, the share's two contribution records), then the number of share records.
- * u_crec / i_crec: per batch Bc / (1+T)*Bc positions x 8 int32. */
+ * u_crec / i_crec: per batch Bc / (1+T)*Bc positions x 8 int32. u_ahead .. i_nah
+ * (all four or none): the look-ahead lists of mirec_uniq_ahead_diff, formed in the same
+ * launch (one launch of three block roles after the groupings). */
 int mirec_step_records(const int64_t* user_keys, const int64_t* item_keys, int64_t n_batches,
                        int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
                        const int32_t* u_perm, const int32_t* u_uniq, const int32_t* u_seg,
                        const int32_t* u_nu, const int32_t* i_perm, const int32_t* i_uniq,
                        const int32_t* i_seg, const int32_t* i_nu, int32_t* u_rec,
-                       int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, void* stream);
+                       int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, int32_t* u_ahead,
+                       int32_t* u_nah, int32_t* i_ahead, int32_t* i_nah, void* stream);
 /* int32 per batch of one table's record region for per keys per batch (-1 if per < 0). */
 int64_t mirec_step_record_ints(int64_t per);
 

@@ -143,7 +143,8 @@ SIGNATURES = {
                                         c_double, c_double, c_double, _P]),
     "mirec_step_record_ints": (c_int64, [c_int64]),
     "mirec_step_records": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64, _P, _P,
-                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                   _P]),
     "mirec_step_finish": (c_int, [_P, c_int64, c_float, _P, _P, _P]),
     "mirec_chunk_finish": (c_int, [_P, c_int64, c_int64, c_int32, c_float, _P, _P, _P, _P]),
     "mirec_fullsort_topk_f32": (c_int, [_P, c_int64, _P, c_int64, c_int32, _P, _P, _P, _P,

@@ -176,17 +176,22 @@ extern "C" int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream)
 extern "C" int mirec_prepare_chunk_group(const mirec_chunk_prep* p, void* stream) {
   if (!prep_ok(p)) return -1;
   const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
+  // with K35 records the look-ahead lists come from the records launch (one launch
+  // after the sort instead of two)
+  const bool rec = p->u_rec != nullptr;
   const int rc = mirec::sort_chunk_pair(p->user_keys, n, p->Bc, p->n_users, p->u_perm,
                                         p->u_uniq, p->u_seg, p->u_nu, p->item_keys,
                                         p->n_batches * KI, KI, p->n_items, p->i_perm, p->i_uniq,
-                                        p->i_seg, p->i_nu, p->n_batches, p->u_ahead, p->u_nah,
-                                        p->i_ahead, p->i_nah, p->sort_ws, p->sort_ws_bytes,
-                                        (hipStream_t)stream);
-  if (rc || !p->u_rec) return rc;
+                                        p->i_seg, p->i_nu, p->n_batches,
+                                        rec ? nullptr : p->u_ahead, p->u_nah,
+                                        rec ? nullptr : p->i_ahead, p->i_nah, p->sort_ws,
+                                        p->sort_ws_bytes, (hipStream_t)stream);
+  if (rc || !rec) return rc;
   return mirec_step_records(p->user_keys, p->item_keys, p->n_batches, p->Bc, (int32_t)p->T,
                             p->n_users, p->n_items, p->u_perm, p->u_uniq, p->u_seg, p->u_nu,
                             p->i_perm, p->i_uniq, p->i_seg, p->i_nu, p->u_rec, p->u_crec,
-                            p->i_rec, p->i_crec, stream);
+                            p->i_rec, p->i_crec, p->u_ahead, p->u_ahead ? p->u_nah : nullptr,
+                            p->i_ahead, p->i_ahead ? p->i_nah : nullptr, stream);
 }
 
 extern "C" int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream) {

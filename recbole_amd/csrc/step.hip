@@ -36,6 +36,7 @@
 // the number of elements a thread holds.
 #include "adam_core.h"
 #include "bpr_math.h"
+#include "ahead.h"
 
 namespace mirec {
 
@@ -140,49 +141,54 @@ __device__ __forceinline__ void contrib_record(int q, int tb, int Bc, int T,
   reinterpret_cast<int4*>(out)[1] = make_int4(r[4], r[5], r[6], r[7]);
 }
 
-struct RecJob {   // one table's groupings and record buffers
+struct RecJob {   // one table's groupings, record buffers and look-ahead lists
   const int32_t* perm; const int32_t* uniq; const int32_t* seg; const int32_t* nu;
-  int32_t* rec; int32_t* crec;
+  int32_t* rec; int32_t* crec; int32_t* ahead; int32_t* nah;
 };
 
-// Contribution records of every grouped position: grid (position blocks, 2 * batches),
-// 256 positions per block — three dependent loads (perm, then the keys), no serial loop.
-__global__ __launch_bounds__(256) void step_contrib_records_kernel(
+// The K35 side of a chunk's preparation, after its K2 groupings, in ONE launch of
+// kPrepThreads-lane blocks with three roles (no role reads another's output):
+//   [0, 2nb)          look-ahead list of (table, batch) (ahead.h; skipped without lists);
+//   [2nb, 4nb)        row records of (table, batch) and the share records of its split
+//                     rows, shares dealt in row-slot order by a block scan; the inline
+//                     contribution records are formed here from the keys;
+//   [4nb, 4nb + 2nb*PC) contribution records of PC position blocks per (table, batch).
+constexpr int kPrepThreads = 512;
+__global__ __launch_bounds__(kPrepThreads) void step_prep_kernel(
     const int64_t* __restrict__ ukeys, const int64_t* __restrict__ ikeys, int n_batches, int Bc,
-    int T, int64_t nU, int64_t nI, RecJob U, RecJob I) {
-  const int tb = blockIdx.y >= (unsigned)n_batches;
-  const int b = tb ? blockIdx.y - n_batches : blockIdx.y;
+    int T, int64_t nU, int64_t nI, RecJob U, RecJob I, int PC) {
+  __shared__ int32_t a_lds[kDiffLds];
+  __shared__ int scan_lds[kPrepThreads / 64 + 1];
+  const int nb2 = 2 * n_batches;
+  const int role = blockIdx.x < (unsigned)nb2 ? 0 : blockIdx.x < (unsigned)(2 * nb2) ? 1 : 2;
+  const int q = role < 2 ? blockIdx.x - role * nb2 : (blockIdx.x - 2 * nb2) / PC;
+  const int tb = q >= n_batches;
+  const int b = tb ? q - n_batches : q;
   const RecJob& J = tb ? I : U;
   const int KI = (1 + T) * Bc;
   const int per = tb ? KI : Bc;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= per) return;
-  const int32_t* __restrict__ seg = J.seg + (int64_t)b * (per + 1);
-  if (i >= seg[J.nu[b]]) return;
-  contrib_record(J.perm[(int64_t)b * per + i], tb, Bc, T, ukeys + (int64_t)b * Bc,
-                 ikeys + (int64_t)b * KI, nU, nI, J.crec + ((int64_t)b * per + i) * kRecInts);
-}
-
-// Row records of the touched-row slots and share records of split rows, one block of
-// 1024 threads per (table, batch): the contribution records are copied from crec
-// (step_contrib_records_kernel), the shares dealt out in row-slot order (a block scan).
-constexpr int kRowRecThreads = 1024;
-__global__ __launch_bounds__(kRowRecThreads) void step_row_records_kernel(int n_batches, int Bc,
-                                                                          int T, RecJob U,
-                                                                          RecJob I) {
-  __shared__ int scan_lds[kRowRecThreads / 64 + 1];
-  const int tb = blockIdx.x >= (unsigned)n_batches;
-  const int b = tb ? blockIdx.x - n_batches : blockIdx.x;
-  const RecJob& J = tb ? I : U;
-  const int per = tb ? (1 + T) * Bc : Bc;
-  const int32_t* __restrict__ uniq = J.uniq + (int64_t)b * per;
+  const int64_t* __restrict__ user = ukeys + (int64_t)b * Bc;
+  const int64_t* __restrict__ items = ikeys + (int64_t)b * KI;
+  if (role == 0) {
+    if (J.ahead)
+      uniq_ahead_diff_batch(J.uniq, J.nu, per, n_batches, J.ahead, J.nah, b, a_lds, scan_lds);
+    return;
+  }
+  const int32_t* __restrict__ perm = J.perm + (int64_t)b * per;
   const int32_t* __restrict__ seg = J.seg + (int64_t)b * (per + 1);
   const int nu = J.nu[b];
+  if (role == 2) {
+    const int i = ((blockIdx.x - 2 * nb2) % PC) * kPrepThreads + threadIdx.x;
+    if (i < per && i < seg[nu])
+      contrib_record(perm[i], tb, Bc, T, user, items, nU, nI,
+                     J.crec + ((int64_t)b * per + i) * kRecInts);
+    return;
+  }
+  const int32_t* __restrict__ uniq = J.uniq + (int64_t)b * per;
   int32_t* __restrict__ rec = J.rec + (int64_t)b * rec_ints(per);
   int32_t* __restrict__ task = rec + (int64_t)per * kRowRec;
-  const int4* __restrict__ crec = reinterpret_cast<const int4*>(J.crec + (int64_t)b * per * kRecInts);
   int dealt = 0;                                   // shares dealt out so far (block-uniform)
-  for (int x0 = 0; x0 < nu; x0 += kRowRecThreads) {
+  for (int x0 = 0; x0 < nu; x0 += kPrepThreads) {
     const int x = x0 + threadIdx.x;
     int i0 = 0, nc = 0, row = 0;
     if (x < nu) {
@@ -197,20 +203,17 @@ __global__ __launch_bounds__(kRowRecThreads) void step_row_records_kernel(int n_
     if (x >= nu) continue;
     const int got = max(0, min(want, kSplitCap - base));
     const int nsh = 1 + got;
-    int4* r = reinterpret_cast<int4*>(rec + (int64_t)x * kRowRec);
-    r[0] = make_int4(row, i0, nc, nsh);
-    for (int c = 0; c < kRecInline && c < nc; ++c) {
-      r[1 + 2 * c] = crec[2 * (i0 + c)];
-      r[2 + 2 * c] = crec[2 * (i0 + c) + 1];
-    }
+    int32_t* r = rec + (int64_t)x * kRowRec;
+    reinterpret_cast<int4*>(r)[0] = make_int4(row, i0, nc, nsh);
+    for (int c = 0; c < kRecInline && c < nc; ++c)
+      contrib_record(perm[i0 + c], tb, Bc, T, user, items, nU, nI, r + 4 + c * kRecInts);
     for (int j = 1; j <= got; ++j) {
-      int4* tr = reinterpret_cast<int4*>(task + (int64_t)(base + j - 1) * kTaskRec);
-      tr[0] = make_int4(x, j, i0, nc);
-      tr[1] = make_int4(row, nsh, 0, 0);
-      for (int c = 0; c < kShare && j * kShare + c < nc; ++c) {
-        tr[2 + 2 * c] = crec[2 * (i0 + j * kShare + c)];
-        tr[3 + 2 * c] = crec[2 * (i0 + j * kShare + c) + 1];
-      }
+      int32_t* tr = task + (int64_t)(base + j - 1) * kTaskRec;
+      reinterpret_cast<int4*>(tr)[0] = make_int4(x, j, i0, nc);
+      reinterpret_cast<int4*>(tr)[1] = make_int4(row, nsh, 0, 0);
+      for (int c = 0; c < kShare && j * kShare + c < nc; ++c)
+        contrib_record(perm[i0 + j * kShare + c], tb, Bc, T, user, items, nU, nI,
+                       tr + 8 + c * kRecInts);
     }
   }
   if (threadIdx.x == 0) task[(int64_t)kSplitCap * kTaskRec] = min(dealt, kSplitCap);
@@ -531,26 +534,23 @@ extern "C" int mirec_step_records(const int64_t* user_keys, const int64_t* item_
                                   const int32_t* i_perm, const int32_t* i_uniq,
                                   const int32_t* i_seg, const int32_t* i_nu, int32_t* u_rec,
                                   int32_t* u_crec, int32_t* i_rec, int32_t* i_crec,
-                                  void* stream) {
+                                  int32_t* u_ahead, int32_t* u_nah, int32_t* i_ahead,
+                                  int32_t* i_nah, void* stream) {
   if (n_batches < 0 || n_batches > 32767 || Bc < 0 || T < 1 ||
       (int64_t)(1 + T) * Bc > INT32_MAX || n_users <= 0 || n_items <= 0 || !user_keys || !item_keys || !u_perm || !u_uniq || !u_seg || !u_nu ||
-      !i_perm || !i_uniq || !i_seg || !i_nu || !u_rec || !u_crec || !i_rec || !i_crec) {
+      !i_perm || !i_uniq || !i_seg || !i_nu || !u_rec || !u_crec || !i_rec || !i_crec ||
+      !u_ahead != !u_nah || !u_ahead != !i_ahead || !i_ahead != !i_nah) {
     set_error("mirec_step_records: bad arguments");
     return -1;
   }
   if (n_batches == 0 || Bc == 0) return 0;
-  const RecJob U = {u_perm, u_uniq, u_seg, u_nu, u_rec, u_crec};
-  const RecJob I = {i_perm, i_uniq, i_seg, i_nu, i_rec, i_crec};
+  const RecJob U = {u_perm, u_uniq, u_seg, u_nu, u_rec, u_crec, u_ahead, u_nah};
+  const RecJob I = {i_perm, i_uniq, i_seg, i_nu, i_rec, i_crec, i_ahead, i_nah};
   const int64_t KI = (1 + T) * Bc;
-  hipLaunchKernelGGL(step_contrib_records_kernel,
-                     dim3((unsigned)((KI + 255) / 256), (unsigned)(2 * n_batches)), dim3(256), 0,
-                     (hipStream_t)stream, user_keys, item_keys, (int)n_batches, (int)Bc, T,
-                     n_users, n_items, U, I);
-  const int rc = launch_status("mirec_step_records");
-  if (rc) return rc;
-  hipLaunchKernelGGL(step_row_records_kernel, dim3((unsigned)(2 * n_batches)),
-                     dim3(kRowRecThreads), 0, (hipStream_t)stream, (int)n_batches, (int)Bc, T, U,
-                     I);
+  const int PC = (int)((KI + kPrepThreads - 1) / kPrepThreads);
+  hipLaunchKernelGGL(step_prep_kernel, dim3((unsigned)(4 * n_batches + 2 * n_batches * PC)),
+                     dim3(kPrepThreads), 0, (hipStream_t)stream, user_keys, item_keys,
+                     (int)n_batches, (int)Bc, T, n_users, n_items, U, I, PC);
   return launch_status("mirec_step_records");
 }
 

@@ -580,7 +580,8 @@ def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_us
     rc = lib().mirec_step_records(ptr(user_keys), ptr(item_keys), n_batches, Bc, times, n_users,
                                   n_items, ptr(gu.perm), ptr(gu.uniq), ptr(gu.seg),
                                   ptr(gu.n_uniq), ptr(gi.perm), ptr(gi.uniq), ptr(gi.seg),
-                                  ptr(gi.n_uniq), *[ptr(o) for o in out], stream_handle())
+                                  ptr(gi.n_uniq), *[ptr(o) for o in out], None, None, None, None,
+                                  stream_handle())
     check(rc, "mirec_step_records")
     return out
 

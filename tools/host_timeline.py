@@ -25,7 +25,7 @@ def main():
     from recbole_amd.trainer import fused as F
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    _, _, _, _, _, step = bench.build_workload(dev)
+    _, _, _, _, _, step = bench.build_workload(dev, source='memory')
     W, K = args.warmup, args.steps
     marks = []
     t_ref = [0.0]
@@ -41,6 +41,19 @@ def main():
         orig_prepare(slot, chunk)
         mark('prepare out')
     step._prepare = prepare
+
+    def wrap(name):
+        orig = getattr(step, name)
+
+        def f(*a, **kw):
+            mark(f'{name} in')
+            r = orig(*a, **kw)
+            mark(f'{name} out')
+            return r
+        setattr(step, name, f)
+    for name in ('_enter_chunk', '_prepare_group', '_issue_groups', '_top_up_prep', '_entry',
+                 '_flush', '_finish'):
+        wrap(name)
     for rep in range(args.reps):
         M = step.C
         nb = step.begin_epoch(cuts=(W, W + K, W + K + M), hold_prep_from=W)
@@ -48,7 +61,9 @@ def main():
         torch.cuda.synchronize()
         marks.clear()
         t_ref[0] = t0 = time.perf_counter()
-        step.release_prep()
+        torch.cuda._sleep(1)
+        mark('marker')
+        step.release_prep(upto=W + K)
         mark('released')
         step.run_batches(W, W + K)
         mark('run_batches out')
