@@ -144,7 +144,8 @@ def pmc_bytes(substr):
     newest committed PMC summary (profiles/*_pmc.json, tools/summarize_prof.py:
     FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json'))
+                   if 'models_pmc' not in f)
     if not files:
         return None, None
     data = json.load(open(files[-1]))
@@ -159,7 +160,8 @@ def pmc_valu_insts(substr):
     name contains `substr` (SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32 pass of
     tools/prof_pmc.sh), or (None, None)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))[::-1]:
+    for path in sorted(f for f in glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json'))
+                       if 'models_pmc' not in f)[::-1]:
         for k, v in json.load(open(path)).items():
             if substr in k and 'sq_insts_valu_per_launch' in v:
                 return (v['sq_insts_valu_per_launch'],
