@@ -529,13 +529,18 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
 
 // ---------------------------------------------------------------------------
 // Chunked segmented scatter-add (hot rows: a Zipf head row may own 10^4..10^5
-// contributions, far too many for one wave to sum serially). The sorted
-// contribution positions are cut into chunks of scat_chunk(d); a group of G lanes
-// per chunk sums runs of equal segment in position order. A segment wholly
-// inside a chunk is added to dense directly; a segment crossing chunk
-// boundaries leaves a tail partial in its first chunk and head partials in the
-// following ones, which the fixup kernel (one owner per segment: the boundary
-// it first crosses) adds in chunk order. Deterministic, no float atomics.
+// contributions, far too many for one wave to sum serially). Every segment is cut
+// into pieces of CH = scat_chunk(d) positions counted from ITS OWN start, so a row's
+// sum depends only on its own contributions and their order — not on where the row
+// sits in the sorted array (a row-sharded owner's shorter array gives the one-process
+// sums bit for bit). Work is dealt by absolute chunks of CH positions: the group of G
+// lanes of chunk c sums every piece that STARTS in c (reading past c's end when the
+// piece does) — the pieces of the segments that start in c, plus at most one later
+// piece of the segment that started before c. A one-piece segment is written
+// directly; a longer one leaves its first piece in tail[chunk of its start] and
+// piece k in head[that chunk + k] (at most one of each per chunk), which the fixup
+// kernel (owner: the block of the first boundary after the segment's start) adds in
+// piece order. Deterministic, no float atomics.
 // positions per chunk: short chunks for wide rows (more lane groups in flight),
 // longer ones for narrow rows; the workspace is sized for the smallest
 __host__ __device__ __forceinline__ int scat_chunk(int d) { return d == 1 ? 8 : 32; }
@@ -567,19 +572,15 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
   if (p0 >= n) return;
   const int p1 = min(n, p0 + CH);
   constexpr int MAXC = DMAX / G;    // columns per lane, d <= DMAX
-  int u = seg_of(seg, nu, p0);
-  int p = p0;
-  while (p < p1) {
-    const int s0 = seg[u], e = seg[u + 1];
-    const int q1 = min(e, p1);
-    float acc[MAXC];
+  // sums positions [q0, q1) of one segment into acc (loads 4 positions ahead of the adds)
+  auto piece = [&](int q0, int q1, float* acc) {
+    int q = q0;
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
-    // one run of equal segment: loads issued 4 positions ahead of the adds
-    for (; p + 4 <= q1; p += 4) {
+    for (; q + 4 <= q1; q += 4) {
       int pr[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) pr[t] = perm[p + t];
+      for (int t = 0; t < 4; ++t) pr[t] = perm[q + t];
       float v[4][MAXC];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -593,36 +594,44 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
 #pragma unroll
         for (int j = 0; j < MAXC; ++j) acc[j] += v[t][j];
     }
-    for (; p < q1; ++p) {
-      const float* r = rows + (int64_t)perm[p] * d;
+    for (; q < q1; ++q) {
+      const float* r = rows + (int64_t)perm[q] * d;
 #pragma unroll
       for (int j = 0; j < MAXC; ++j) {
         const int col = l + j * G;
         if (col < d) acc[j] += r[col];
       }
     }
-    const bool started_before = s0 < p0;
-    const bool ends_after = e > p1;
-    float* dst;
-    if (!started_before && !ends_after) {
-      const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
-      dst = (row >= 0 && row < n_rows) ? dense + row * d : nullptr;
+  };
+  auto store = [&](float* dst, const float* acc, bool add) {
 #pragma unroll
-      for (int j = 0; j < MAXC; ++j) {
-        const int col = l + j * G;
-        if (dst && col < d) {
-          if (compact) dst[col] = acc[j]; else dst[col] += acc[j];
-        }
-      }
-    } else {
-      dst = (started_before ? head : tail) + (int64_t)c * d;
-#pragma unroll
-      for (int j = 0; j < MAXC; ++j) {
-        const int col = l + j * G;
-        if (col < d) dst[col] = acc[j];
+    for (int j = 0; j < MAXC; ++j) {
+      const int col = l + j * G;
+      if (dst && col < d) {
+        if (add) dst[col] += acc[j]; else dst[col] = acc[j];
       }
     }
+  };
+  float acc[MAXC];
+  int u = seg_of(seg, nu, p0);
+  if (seg[u] < p0) {                       // the segment that started before this chunk
+    const int s0 = seg[u], e = seg[u + 1];
+    const int ps = s0 + (p0 - s0 + CH - 1) / CH * CH;   // its next piece start >= p0
+    if (ps < p1 && ps < e) {
+      piece(ps, min(e, ps + CH), acc);
+      store(head + (int64_t)c * d, acc, false);
+    }
     ++u;
+  }
+  for (; u < nu && seg[u] < p1; ++u) {     // the segments that start in this chunk
+    const int s0 = seg[u], e = seg[u + 1];
+    piece(s0, min(e, s0 + CH), acc);
+    if (e - s0 <= CH) {
+      const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
+      store((row >= 0 && row < n_rows) ? dense + row * d : nullptr, acc, !compact);
+    } else {
+      store(tail + (int64_t)c * d, acc, false);
+    }
   }
 }
 
@@ -643,8 +652,9 @@ __global__ __launch_bounds__(256) void scatter_fixup_kernel(
   if (q >= n) return;
   const int u = seg_of(seg, nu, q);
   const int s0 = seg[u], e = seg[u + 1];
-  if (s0 == q || s0 < (b - 1) * CH) return;   // not crossing, or not the owner
-  const int kend = (e - 1) / CH;
+  // owner: a segment of more than one piece that starts in chunk b - 1
+  if (s0 == q || s0 < (b - 1) * CH || e - s0 <= CH) return;
+  const int kend = b - 2 + (e - s0 + CH - 1) / CH;     // chunk holding its last piece's start
   const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
   if (row < 0 || row >= n_rows) return;
   int cw = 1;

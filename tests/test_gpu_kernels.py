@@ -700,6 +700,36 @@ def test_large_segment_sort_and_hot_row_scatter(dev, n, key_space, d):
     torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize('d', [1, 16, 128])
+def test_segment_reduce_independent_of_position(dev, d):
+    """The chunked fixed-order reduction cuts each row's contributions into pieces
+    counted from the row's own first contribution, so a row's sum does not depend on
+    where its contributions sit in the sorted array: the same rows behind 0..63 extra
+    contributions of smaller keys (a row-sharded owner's shorter or longer array)
+    give bit-identical sums, rows of 1..700 contributions included."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(d)
+    lens = np.r_[1, 2, 31, 32, 33, 64, 65, 97, 300, 700, rng.integers(1, 90, 40)]
+    keys = np.repeat(np.arange(100, 100 + len(lens)), lens).astype(np.int64)
+    rows = torch.randn(len(keys), d, generator=torch.Generator().manual_seed(d))
+    ref = None
+    for shift in (0, 1, 5, 17, 31, 32, 63):
+        k = np.r_[rng.integers(0, 100, shift), keys].astype(np.int64)
+        r = torch.cat([torch.randn(shift, d), rows])
+        segs = ops.segment_sort(torch.as_tensor(k, device=dev), 100 + len(lens))
+        out, osegs = ops.segment_reduce(r.to(dev), segs)
+        nu = int(osegs.n_uniq.item())
+        uniq = osegs.uniq[:nu].cpu().numpy()
+        got = out[:nu].cpu()[uniq >= 100]
+        assert got.shape[0] == len(lens)
+        if ref is None:
+            ref = got
+            exp = torch.zeros(len(lens), d, dtype=torch.float64).index_add_(
+                0, torch.as_tensor(keys - 100), rows.double())
+            torch.testing.assert_close(got.double(), exp, rtol=1e-5, atol=1e-4)
+        assert torch.equal(got, ref), shift
+
+
 def test_adam_fast_math_selftest(dev):
     """The K5 replay's fast sqrt / division (csrc/adam_math.h) equal sqrtf and IEEE
     division bit for bit on this GPU: every 64th float of the fast sqrt range plus
