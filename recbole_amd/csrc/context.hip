@@ -99,15 +99,28 @@ __global__ __launch_bounds__(kCtxThreads) void ctx_fm_reduce_kernel(
   const int64_t F = n_fields;
   float S = 0.f, Q = 0.f;
   float fo_float = 0.f, fo_tok = 0.f, fo_seq = 0.f;
-  for (int f = 0; f < n_fields; ++f) {
-    const int kind = fields[f].kind;
-    const float e = col ? concat[(b * F + f) * d + k] : 0.f;
-    const float w1 = fo[b * F + f];
-    if (kind == 0) fo_tok += w1;
-    else if (kind == 1) fo_seq += w1;
-    else fo_float += w1;
-    S += e;
-    Q += e * e;
+  // eight fields' loads in flight, then their sums in field order
+  constexpr int U = 8;
+  for (int f0 = 0; f0 < n_fields; f0 += U) {
+    float e[U], w1[U];
+    int kind[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int f = f0 + j;
+      const bool ok = f < n_fields;
+      kind[j] = ok ? fields[f].kind : -1;
+      e[j] = ok && col ? concat[(b * F + f) * d + k] : 0.f;
+      w1[j] = ok ? fo[b * F + f] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (kind[j] < 0) break;
+      if (kind[j] == 0) fo_tok += w1[j];
+      else if (kind[j] == 1) fo_seq += w1[j];
+      else fo_float += w1[j];
+      S += e[j];
+      Q += e[j] * e[j];
+    }
   }
   if (col) fm_sum[b * d + k] = S;
   const float fm = 0.5f * group_sum<LPS>(col ? S * S - Q : 0.f);
