@@ -115,7 +115,7 @@ extern "C" int mirec_chunk_finish(const float* loss_k, int64_t n, int64_t stride
 
 // ---- small host -> device writes that a graph capture records by value
 namespace mirec {
-constexpr int kPayloadWords = 768;     // 3 KiB of kernel arguments per launch
+constexpr int kPayloadWords = 992;     // 3,968 B of kernel arguments per launch (< 4 KiB)
 struct Payload { uint32_t w[kPayloadWords]; };
 
 __global__ __launch_bounds__(256) void write_bytes_kernel(uint32_t* __restrict__ dst, Payload p,

@@ -108,10 +108,25 @@ def _upload(arr, device):
     return out
 
 
-def ctx_fm_forward(layout, interaction, tables, B, d, bias, keys=None):
+def _grad_buffers(layout, interaction, B, d, keys, dev):
+    """The backward's per-contribution gradient buffers (written by K8's backward)."""
+    nt, nf = len(layout.token_names), len(layout.float_names)
+    E = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)
+    seq_ids = [_col(interaction, n, torch.int64) for n in layout.seq_names]
+    return {'B': B, 'keys': keys,
+            'T': E(nt * B, d) if nt else None, 'T1': E(nt * B, 1) if nt else None,
+            'Ef': E(B, nf * d) if nf else None, 'Ef1': E(B, nf) if nf else None,
+            'seq': [E(ids.numel(), d) for ids in seq_ids],
+            'seq1': [E(ids.numel(), 1) for ids in seq_ids]}
+
+
+def ctx_fm_forward(layout, interaction, tables, B, d, bias, keys=None, grads=None):
+    """K8 forward. grads (the backward's buffers, _grad_buffers): the field descriptors
+    then also carry the gradient pointers, so the backward reuses them (one descriptor
+    upload per step instead of two)."""
     dev = bias.device
-    arr, keep = build_fields(layout, interaction, tables)
-    if keys is not None:
+    arr, keep = build_fields(layout, interaction, tables, grads)
+    if keys is not None and grads is None:
         for i in range(len(layout.token_names)):
             arr[i].keys = ptr(keys) + 8 * i * B
     fields_dev = _upload(arr, dev)
@@ -159,8 +174,12 @@ class _CtxFMFn(torch.autograd.Function):
         else:
             ctx.segs = None
             h1 = None
-        concat, y_fm, keep = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys)
-        ctx.fm_work = keep[-1]
+        grads = None
+        if any(ctx.needs_input_grad[2:]):
+            grads = _grad_buffers(layout, interaction, B, d, keys, bias.device)
+        concat, y_fm, keep = ctx_fm_forward(layout, interaction, tables, B, d, bias.detach(), keys,
+                                            grads)
+        ctx.fm_work, ctx.fields_dev, ctx.grads, ctx.keep = keep[-1], keep[-2], grads, keep
         ctx.layout, ctx.interaction, ctx.tables, ctx.B, ctx.d = layout, interaction, tables, B, d
         ctx.deferred_T = T if h is not None else None
         ctx.deferred_T1 = T1 if h1 is not None else None
@@ -176,15 +195,8 @@ class _CtxFMFn(torch.autograd.Function):
         if g_fm is None:
             g_fm = torch.zeros(B, dtype=torch.float32, device=dev)
         g_fm = g_fm.contiguous()
-        E = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)
         seq_ids = [_col(ctx.interaction, n, torch.int64) for n in layout.seq_names]
-        grads = {'B': B, 'keys': keys,
-                 'T': E(nt * B, d) if nt else None, 'T1': E(nt * B, 1) if nt else None,
-                 'Ef': E(B, nf * d) if nf else None, 'Ef1': E(B, nf) if nf else None,
-                 'seq': [E(ids.numel(), d) for ids in seq_ids],
-                 'seq1': [E(ids.numel(), 1) for ids in seq_ids]}
-        arr, keep = build_fields(layout, ctx.interaction, tables, grads)
-        fields_dev = _upload(arr, dev)
+        grads, fields_dev = ctx.grads, ctx.fields_dev    # descriptors of the forward
         gc = None if g_concat is None else g_concat.contiguous()
         with ops.timed_launch('ctx_fm_bwd'):
             rc = lib().mirec_ctx_fm_bwd_f32(ptr(fields_dev), layout.n_fields, B, d, ptr(concat),
@@ -220,7 +232,7 @@ class _CtxFMFn(torch.autograd.Function):
                                                 torch.zeros_like(tables['seq'][i])))
             dseq1.append(ops.segment_scatter_add(grads['seq1'][i], segs,
                                                  torch.zeros_like(tables['seq1'][i])))
-        del keep
+        ctx.keep = ctx.grads = ctx.fields_dev = None      # the forward's buffers: done
         return (None, None, dT, dT1, dEf, dEf1, dbias, *dseq, *dseq1)
 
 
