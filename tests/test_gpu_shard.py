@@ -102,9 +102,11 @@ def test_shard_plan_and_own_match_spec(dev, G, Bc):
                                  *[b.data_ptr() for b in bufs], status.data_ptr(), st), 'plan')
         assert status.tolist() == [-4, lay.largest_message(users, items)]
         n_r = max(0, min(B, Bc - r * B))
-        assert int(bufs[2][:(2 + T) * n_r].max()) < 2 * G
+        if n_r:                          # a ragged batch leaves the last ranks no positives
+            assert int(bufs[2][:(2 + T) * n_r].max()) < 2 * G
         owned = (torch.cat([users, items]) % G == r).to(dev)
-        assert int(bufs[1][owned].max()) < 2 * G
+        if bool(owned.any()):
+            assert int(bufs[1][owned].max()) < 2 * G
 
 
 def _pipeline(root, batch_rows):
