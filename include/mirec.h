@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 14
+#define MIREC_ABI_VERSION 15
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -633,6 +633,49 @@ int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* l
 
 /* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
 int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K10  DeepFM's deep part (recbole/model/layers.py:30-86 MLPLayers: Dropout -> Linear
+ * -> ReLU per hidden layer; deepfm.py:40-43,61 deep_predict_layer) on fp32 MFMA:
+ * one forward launch and two backward launches (data gradient through every layer,
+ * then every dW / db tile; fixed summation orders). Layer l maps dims[l] -> dims[l+1]
+ * with W[l] the nn.Linear weight [dims[l+1], dims[l]] (16-B aligned) and b[l] its
+ * bias (or NULL); dropout[l]: Dropout(p) before layer l; relu[l]: ReLU after it (every
+ * hidden layer must have it). Widths <= 1024, multiples of 4 except dims[n_layers].
+ * Dropout (training): element e of layer l's input is kept iff
+ *   splitmix64(splitmix64(seed + counter[0]) ^ (e*8 + l)) >> 32 < keep_threshold
+ * and scaled by `scale`; the forward advances counter[0] by one (last block; `arrive`
+ * is zero-initialised device scratch). Saved for the backward: xs[l] = layer l's input
+ * after its dropout [B, dims[l]] (xs[0] may be NULL when layer 0 has no dropout: the
+ * backward then reads x), mask0 = layer 0's keep flags [B, dims[0]] (dropout[0] only).
+ * Backward: dy = d loss / d y [B, dims[n_layers]]; gz[l] [B, dims[l+1]] scratch for
+ * l < n_layers - 1; writes gx [B, dims[0]], dW[l], db[l] (when non-NULL).
+ * ------------------------------------------------------------------------- */
+#define MIREC_MLP_MAX_LAYERS 6
+typedef struct mirec_mlp {
+  int32_t n_layers;
+  int32_t dims[MIREC_MLP_MAX_LAYERS + 1];
+  int32_t dropout[MIREC_MLP_MAX_LAYERS];
+  int32_t relu[MIREC_MLP_MAX_LAYERS];
+  int32_t tile_start[MIREC_MLP_MAX_LAYERS];   /* set by mirec_mlp_bwd_f32 */
+  uint32_t keep_threshold;
+  float scale;
+  uint64_t seed;
+  int64_t* counter;
+  int32_t* arrive;
+  const float* W[MIREC_MLP_MAX_LAYERS];
+  const float* b[MIREC_MLP_MAX_LAYERS];
+  float* xs[MIREC_MLP_MAX_LAYERS];
+  uint8_t* mask0;
+  float* gz[MIREC_MLP_MAX_LAYERS];
+  float* dW[MIREC_MLP_MAX_LAYERS];
+  float* db[MIREC_MLP_MAX_LAYERS];
+} mirec_mlp;
+
+int mirec_mlp_fwd_f32(const mirec_mlp* mlp, const float* x, int64_t B, float* y, int32_t train,
+                      void* stream);
+int mirec_mlp_bwd_f32(const mirec_mlp* mlp, const float* x, const float* dy, int64_t B, float* gx,
+                      void* stream);
 
 /* ---------------------------------------------------------------------------
  * K9  Sequential recommender (SASRec) embedding block and sampled softmax.

@@ -41,6 +41,20 @@ class CtxField(ctypes.Structure):
                 ('grad1_ld', c_int64)]
 
 
+MLP_MAX_LAYERS = 6
+
+
+class MlpDesc(ctypes.Structure):
+    """struct mirec_mlp (include/mirec.h, K10)."""
+    _L = MLP_MAX_LAYERS
+    _fields_ = [('n_layers', c_int32), ('dims', c_int32 * (_L + 1)), ('dropout', c_int32 * _L),
+                ('relu', c_int32 * _L), ('tile_start', c_int32 * _L),
+                ('keep_threshold', ctypes.c_uint32), ('scale', c_float),
+                ('seed', ctypes.c_uint64), ('counter', _P), ('arrive', _P),
+                ('W', _P * _L), ('b', _P * _L), ('xs', _P * _L), ('mask0', _P),
+                ('gz', _P * _L), ('dW', _P * _L), ('db', _P * _L)]
+
+
 class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
@@ -162,6 +176,8 @@ SIGNATURES = {
     "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P, _P]),
     "mirec_sigmoid_bce_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
     "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
+    "mirec_mlp_fwd_f32": (c_int, [_P, _P, c_int64, _P, c_int32, _P]),
+    "mirec_mlp_bwd_f32": (c_int, [_P, _P, _P, c_int64, _P, _P]),
     "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
                                            _P, c_float, _P, _P, _P, _P]),
     "mirec_seq_embed_ln_partials": (c_int64, [c_int64]),
@@ -175,7 +191,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class NativeError(RuntimeError):

@@ -2,7 +2,8 @@
 
 y = sigmoid(first_order + FM + MLP(concat of field rows)), nn.BCELoss. The
 field embedding, first-order term and FM term run in the fused K8 kernel
-(ContextRecommender.fm_fields); the MLP is library GEMMs (nn.Linear); the
+(ContextRecommender.fm_fields); MLPLayers + deep_predict_layer run in K10
+(model/mlp.py: one forward, two backward launches on fp32 MFMA); the
 sigmoid + BCE and its gradient run in mirec_sigmoid_bce_f32. Same modules and
 init (xavier_normal_ weights, zero biases, apply order) as the reference.
 """
@@ -12,6 +13,7 @@ from torch.nn.init import constant_, xavier_normal_
 from recbole_amd.model.abstract_recommender import ContextRecommender
 from recbole_amd.model.context import _SigmoidBCEFn, sigmoid_prob
 from recbole_amd.model.layers import BaseFactorizationMachine, MLPLayers
+from recbole_amd.model.mlp import deep_forward
 
 
 class DeepFM(ContextRecommender):
@@ -43,7 +45,7 @@ class DeepFM(ContextRecommender):
     def _logits(self, interaction):
         concat, y_fm = self.fm_fields(interaction)
         B = concat.shape[0]
-        y_deep = self.deep_predict_layer(self.mlp_layers(concat.view(B, -1)))
+        y_deep = deep_forward(self.mlp_layers, self.deep_predict_layer, concat.view(B, -1))
         return y_fm, y_deep
 
     def forward(self, interaction):
