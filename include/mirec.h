@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIREC_ABI_VERSION 15
+#define MIREC_ABI_VERSION 18
 
 int mirec_abi_version(void);
 const char* mirec_last_error(void);
@@ -289,6 +289,14 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
 int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,
                              const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq_dev,
                              int64_t n, float* out, void* ws, size_t ws_bytes, void* stream);
+/* Two sources grouped by the same segments in one pass (DeepFM's [V, d] token rows and
+ * [V, 1] first-order weights): out = mirec_segment_reduce_f32(rows, d, ...) and out1 =
+ * the same for rows1 with d = 1, bit for bit. 2 <= d <= 16; ws: at least
+ * mirec_segment_scatter_add_workspace_size(n, d + 1) bytes. */
+int mirec_segment_reduce2_f32(const float* rows, int32_t d, const float* rows1,
+                              const int32_t* perm, const int32_t* uniq, const int32_t* seg,
+                              const int32_t* n_uniq_dev, int64_t n, float* out, float* out1,
+                              void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K5  Dense Adam over every row, with the gradient supplied in compact form.
@@ -325,6 +333,19 @@ int mirec_adam_flat_f32(float* p, float* m, float* v, int64_t n, const float* gr
                         const float* step_consts_dev, const int32_t* step_idx_dev,
                         double beta1, double beta2, double eps, double weight_decay,
                         void* stream);
+/* Up to 16 flat parameters with dense gradients in one launch (the same per-element
+ * step as mirec_adam_flat_f32 / the streamed K5: bit-identical results). */
+typedef struct mirec_flat_param {
+  float* p;
+  float* m;
+  float* v;
+  const float* g;
+  int64_t n;
+} mirec_flat_param;
+int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t n_params,
+                              const float* step_consts_dev, const int32_t* step_idx_dev,
+                              double beta1, double beta2, double eps, double weight_decay,
+                              void* stream);
 
 /* Several tables in ONE launch (e.g. the user and the item embedding of BPR),
  * same arithmetic per table. `tables` is a HOST array of n_tables <= 4
@@ -388,7 +409,6 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
                          const float* step_consts_dev, const int32_t* step_base_dev,
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
-
 /* K35 — one training step of the fused BPR path in ONE launch: BPR forward + backward
  * (mirec_bpr_fwd_bwd_f32's arithmetic) and the deferred Adam step
  * (mirec_adam_deferred_f32's arithmetic) of every touched row, and the look-ahead

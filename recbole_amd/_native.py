@@ -55,6 +55,11 @@ class MlpDesc(ctypes.Structure):
                 ('gz', _P * _L), ('dW', _P * _L), ('db', _P * _L)]
 
 
+class FlatParam(ctypes.Structure):
+    """struct mirec_flat_param (include/mirec.h)."""
+    _fields_ = [('p', _P), ('m', _P), ('v', _P), ('g', _P), ('n', c_int64)]
+
+
 class AdamTable(ctypes.Structure):
     """struct mirec_adam_table (include/mirec.h)."""
     _fields_ = [('p', _P), ('m', _P), ('v', _P), ('n_rows', c_int64), ('rows', _P),
@@ -136,12 +141,16 @@ SIGNATURES = {
     "mirec_selftest_adam_math": (c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P, _P]),
     "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,
                                          _P]),
+    "mirec_segment_reduce2_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P,
+                                          c_size_t, _P]),
     "mirec_segment_scatter_add_workspace_size": (c_size_t, [c_int64, c_int32]),
     "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
                                               c_int64, _P, c_size_t, _P]),
     "mirec_adam_sparse_grad_f32": (c_int, [_P, _P, _P, c_int64, c_int32, _P, _P, _P, _P, _P,
                                            c_int64, _P, _P, _P, c_double, c_double, c_double,
                                            c_double, _P]),
+    "mirec_adam_flat_multi_f32": (c_int, [ctypes.POINTER(FlatParam), c_int32, _P, _P, c_double,
+                                          c_double, c_double, c_double, _P]),
     "mirec_adam_flat_f32": (c_int, [_P, _P, _P, c_int64, _P, _P, _P, c_double, c_double,
                                     c_double, c_double, _P]),
     "mirec_adam_multi_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
@@ -191,7 +200,7 @@ SIGNATURES = {
     "mirec_gather_scale_rows_f32": (c_int, [_P, c_int64, c_int32, _P, c_int64, _P, _P, _P]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 18
 
 
 class NativeError(RuntimeError):

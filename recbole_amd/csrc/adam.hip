@@ -477,7 +477,79 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flat_kernel(
   }
 }
 
+// Several flat parameters in one launch (every dense parameter of a model step: the
+// MLP's weights and biases, float-field embeddings, scalar biases — C4 ran them as six
+// launches): block b takes 1,024 consecutive elements of the parameter whose block
+// range holds b. The same adam_elem per element as every other K5 form.
+constexpr int kFlatMax = 16;
+struct FlatParams {
+  mirec_flat_param t[kFlatMax];
+  int64_t block_start[kFlatMax + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
+    const FlatParams fp, const float* __restrict__ consts, const int32_t* __restrict__ step_idx,
+    AdamConsts k) {
+  int q = 0;
+#pragma unroll
+  for (int t = 1; t < kFlatMax; ++t)
+    if (t < fp.n && (int64_t)blockIdx.x >= fp.block_start[t]) q = t;
+  const mirec_flat_param& P = fp.t[q];
+  const StepConsts sc = step_consts(consts, step_idx[0]);
+  const int64_t i0 = ((int64_t)blockIdx.x - fp.block_start[q]) * (4 * kAdamThreads);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = i0 + u * kAdamThreads + threadIdx.x;
+    if (i < P.n) {
+      float pp = P.p[i], mm = P.m[i], vv = P.v[i];
+      adam_elem(pp, mm, vv, P.g[i], sc, k);
+      P.p[i] = pp;
+      P.m[i] = mm;
+      P.v[i] = vv;
+    }
+  }
+}
+
 }  // namespace mirec
+
+extern "C" int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t n_params,
+                                         const float* step_consts_dev,
+                                         const int32_t* step_idx_dev, double beta1, double beta2,
+                                         double eps, double weight_decay, void* stream) {
+  if (n_params == 0) return 0;
+  if (!params || n_params < 0 || n_params > kFlatMax || !step_consts_dev || !step_idx_dev) {
+    set_error("mirec_adam_flat_multi_f32: bad arguments (at most %d parameters)", kFlatMax);
+    return -1;
+  }
+  FlatParams fp;
+  memset(&fp, 0, sizeof(fp));
+  fp.n = n_params;
+  int64_t blocks = 0;
+  for (int q = 0; q < n_params; ++q) {
+    const mirec_flat_param& t = params[q];
+    if (!t.p || !t.m || !t.v || !t.g || t.n < 0) {
+      set_error("mirec_adam_flat_multi_f32: bad parameter %d", q);
+      return -1;
+    }
+    fp.t[q] = t;
+    fp.block_start[q] = blocks;
+    blocks += (t.n + 4 * kAdamThreads - 1) / (4 * kAdamThreads);
+  }
+  for (int q = n_params; q <= kFlatMax; ++q) fp.block_start[q] = blocks;
+  if (blocks == 0) return 0;
+  AdamConsts k;
+  k.omb1 = (float)(1.0 - beta1);
+  k.omb1m1 = k.omb1 - 1.0f;
+  k.lerp_small = fabsf(k.omb1) < 0.5f;
+  k.b2 = (float)beta2;
+  k.omb2 = (float)(1.0 - beta2);
+  k.eps = (float)eps;
+  k.wd = (float)weight_decay;
+  hipLaunchKernelGGL(adam_flat_multi_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0,
+                     (hipStream_t)stream, fp, step_consts_dev, step_idx_dev, k);
+  return launch_status("mirec_adam_flat_multi_f32");
+}
 
 extern "C" int mirec_adam_flat_f32(float* p, float* m, float* v, int64_t n,
                                    const float* grad, const float* step_consts_dev,

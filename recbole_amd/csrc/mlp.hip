@@ -15,8 +15,10 @@
 //                was kept and h > 0); writes every g_z and the input gradient.
 //   weight grad  one block per 16x16 tile of every dW (plus, for the tiles of the
 //                first input column, the bias gradient): dW = g_z^T x over the batch,
-//                the four waves each take a quarter of the rows and their partial
+//                the eight waves each take an eighth of the rows and their partial
 //                tiles are added in wave order (fixed order, run to run identical).
+// Every loop issues the next group's loads before the current group's MFMAs (the
+// first version, one dependent load level per 16-wide slice, ran the forward at 83 µs).
 //
 // Dropout draws are counter-based (mirec_mlp_draw below; restated in numpy by
 // tests/mlp_spec.py): element e of layer l in the forward with counter value c is
@@ -28,7 +30,10 @@
 namespace mirec {
 
 constexpr int kMlpRows = 16;       // rows per forward / data-grad block
-constexpr int kMlpThreads = 256;   // four waves
+constexpr int kMlpThreads = 512;   // eight waves
+constexpr int kMlpWaves = kMlpThreads / 64;
+constexpr int kMlpU = 4;           // 16-wide slices per prefetch group (data grad)
+constexpr int kFwdU = 8;           // forward: 8 slices (32 MFMAs) per group
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -71,25 +76,46 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
   for (int l = 0; l < L; ++l) any_drop |= train && a.dropout[l];
   const uint64_t key = any_drop ? splitmix64(a.seed + (uint64_t)a.counter[0]) : 0ull;
 
-  // layer 0's input rows, after its dropout
+  // layer 0's input rows, after its dropout: the block's 16 rows are one contiguous
+  // range of x; every float4 of it is loaded before any is processed (stores to the
+  // saved buffers may alias x as far as the compiler knows, which would otherwise
+  // serialise one load per element)
   {
     const int K = a.dims[0];
     const bool drop = train && a.dropout[0];
-    for (int idx = tid; idx < kMlpRows * K; idx += kMlpThreads) {
-      const int i = idx / K, k = idx - i * K;
-      const int64_t row = r0 + i;
-      float v = 0.f;
-      if (row < B) {
-        const int64_t e = row * K + k;
-        v = x[e];
+    constexpr int kV = kMlpRows * 1024 / 4 / kMlpThreads;   // float4 per thread, K <= 1024
+    const int nv = kMlpRows * K / 4;
+    const int64_t lim = (B - r0) * K / 4;                   // float4 of valid rows
+    const float4* x4 = reinterpret_cast<const float4*>(x + r0 * K);
+    float4 xv[kV];
+#pragma unroll
+    for (int j = 0; j < kV; ++j) {
+      const int q = tid + j * kMlpThreads;
+      xv[j] = (q < nv && q < lim) ? x4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < kV; ++j) {
+      const int q = tid + j * kMlpThreads;
+      if (q >= nv) break;
+      const int e0 = 4 * q, i = e0 / K, k = e0 - i * K;
+      float4 v = xv[j];
+      if (q < lim) {
+        const int64_t e = r0 * K + e0;
         if (drop) {
-          const bool kp = mlp_keep(key, 0, (uint64_t)e, a.keep_threshold);
-          v = kp ? v * a.scale : 0.f;
-          a.mask0[e] = kp ? 1 : 0;
+          const bool k0 = mlp_keep(key, 0, (uint64_t)e, a.keep_threshold);
+          const bool k1 = mlp_keep(key, 0, (uint64_t)e + 1, a.keep_threshold);
+          const bool k2 = mlp_keep(key, 0, (uint64_t)e + 2, a.keep_threshold);
+          const bool k3 = mlp_keep(key, 0, (uint64_t)e + 3, a.keep_threshold);
+          v.x = k0 ? v.x * a.scale : 0.f;
+          v.y = k1 ? v.y * a.scale : 0.f;
+          v.z = k2 ? v.z * a.scale : 0.f;
+          v.w = k3 ? v.w * a.scale : 0.f;
+          *reinterpret_cast<uint32_t*>(a.mask0 + e) =
+              (k0 ? 1u : 0u) | (k1 ? 1u << 8 : 0u) | (k2 ? 1u << 16 : 0u) | (k3 ? 1u << 24 : 0u);
         }
-        if (a.xs[0] && a.xs[0] != x) a.xs[0][e] = v;
+        if (a.xs[0] && a.xs[0] != x) *reinterpret_cast<float4*>(a.xs[0] + e) = v;
       }
-      tA[i * ldA + k] = v;
+      *reinterpret_cast<float4*>(tA + i * ldA + k) = v;
     }
   }
   __syncthreads();
@@ -106,45 +132,50 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
     const bool relu = a.relu[l] != 0;
     float* __restrict__ save = last ? nullptr : a.xs[l + 1];
     const int ntile = (N + 15) / 16;
-    for (int t0 = wave; t0 < ntile; t0 += 8) {      // two column tiles per wave: t0, t0 + 4
-      const int t1 = t0 + 4;
-      const bool has1 = t1 < ntile;
-      const int c0 = t0 * 16 + li, c1 = t1 * 16 + li;
-      const float* w0 = W + (int64_t)(c0 < N ? c0 : N - 1) * K;
-      const float* w1 = W + (int64_t)(c1 < N ? c1 : N - 1) * K;
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      // k = k0 + 4*lk + s: the four MFMAs of a 16-wide slice cover it once each
-      for (int k0 = 0; k0 < K; k0 += 16) {
-        const int k = k0 + 4 * lk;
-        const bool kin = k < K;
-        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 av = kin ? *reinterpret_cast<const float4*>(cur + li * ld + k) : z4;
-        const float4 b0 = kin ? *reinterpret_cast<const float4*>(w0 + k) : z4;
-        const float4 b1 = (kin && has1) ? *reinterpret_cast<const float4*>(w1 + k) : z4;
-        acc0 = mfma4(av.x, b0.x, acc0);
-        acc0 = mfma4(av.y, b0.y, acc0);
-        acc0 = mfma4(av.z, b0.z, acc0);
-        acc0 = mfma4(av.w, b0.w, acc0);
-        if (has1) {
-          acc1 = mfma4(av.x, b1.x, acc1);
-          acc1 = mfma4(av.y, b1.y, acc1);
-          acc1 = mfma4(av.z, b1.z, acc1);
-          acc1 = mfma4(av.w, b1.w, acc1);
+    for (int t = wave; t < ntile; t += kMlpWaves) {     // one 16-column tile per wave
+      const int c = t * 16 + li;
+      const float* wr = W + (int64_t)(c < N ? c : N - 1) * K;
+      // k = k0 + 16u + 4*lk + s: the four MFMAs of a 16-wide slice cover it once each;
+      // the next group's loads are issued before this group's MFMAs (two accumulators)
+      float4 pa[kFwdU], pb[kFwdU];
+      // branch-free loads (addresses clamped into the row, out-of-range slices zeroed
+      // after the load): straight-line code lets the compiler wait on the older group
+      // only (vmcnt(N)) while the next group is in flight
+      auto load = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < kFwdU; ++u) {
+          const int k = k0 + 16 * u + 4 * lk;
+          const int kc = k < K ? k : K - 4;
+          pa[u] = *reinterpret_cast<const float4*>(cur + li * ld + kc);
+          pb[u] = *reinterpret_cast<const float4*>(wr + kc);
+          if (k >= K) pb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      };
+      floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
+      load(0);
+      for (int k0 = 0; k0 < K; k0 += 16 * kFwdU) {
+        float4 ca[kFwdU], cb[kFwdU];
+#pragma unroll
+        for (int u = 0; u < kFwdU; ++u) { ca[u] = pa[u]; cb[u] = pb[u]; }
+        if (k0 + 16 * kFwdU < K) load(k0 + 16 * kFwdU);
+#pragma unroll
+        for (int u = 0; u < kFwdU; ++u) {
+          floatx4& acc = (u & 1) ? accB : accA;
+          acc = mfma4(ca[u].x, cb[u].x, acc);
+          acc = mfma4(ca[u].y, cb[u].y, acc);
+          acc = mfma4(ca[u].z, cb[u].z, acc);
+          acc = mfma4(ca[u].w, cb[u].w, acc);
         }
       }
+      const floatx4 acc0 = accA + accB;
       // epilogue: lane holds rows 4*lk + r of column c
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !has1) break;
-        const int c = h ? c1 : c0;
-        if (c >= N) continue;
-        const floatx4 acc = h ? acc1 : acc0;
+      if (c < N) {
         const float bc = bias ? bias[c] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 4 * lk + r;
           const int64_t row = r0 + i;
-          float z = acc[r] + bc;
+          float z = acc0[r] + bc;
           if (relu) z = z < 0.f ? 0.f : z;           // NaN passes, as torch.relu
           if (last) {
             if (row < B) y[row * N + c] = z;
@@ -208,35 +239,68 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
     float* __restrict__ gz = l > 0 ? a.gz[l - 1] : nullptr;
     const float sc = (a.dropout[l] ? a.scale : 1.f);
     const int ntile = (K + 15) / 16;
-    for (int t0 = wave; t0 < ntile; t0 += 8) {
-      const int t1 = t0 + 4;
-      const bool has1 = t1 < ntile;
-      const int c0 = t0 * 16 + li, c1 = t1 * 16 + li;
-      const bool in0 = c0 < K, in1 = has1 && c1 < K;
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      for (int n0 = 0; n0 < N; n0 += 16) {
-        float av[4], b0[4], b1[4];
+    // this wave's (tile, group) sequence — tiles t = wave, wave + 8, ..., groups of
+    // kMlpU 16-wide slices of N — with the next item's loads (and, at a tile's first
+    // group, the tile's saved-input loads for its epilogue) issued before the current
+    // item's MFMAs, across tile boundaries too
+    const int ng = (N + 16 * kMlpU - 1) / (16 * kMlpU);
+    const int my_tiles = wave < ntile ? (ntile - wave + kMlpWaves - 1) / kMlpWaves : 0;
+    const int items = my_tiles * ng;
+    float pa[kMlpU][4], pb[kMlpU][4], px[4];
+    auto load = [&](int it) {         // branch-free, as in the forward
+      const int t = wave + (it / ng) * kMlpWaves, g0 = (it % ng) * 16 * kMlpU;
+      const int c = t * 16 + li;
+      const bool cin = c < K;
+      const int cc = cin ? c : K - 1;
+#pragma unroll
+      for (int u = 0; u < kMlpU; ++u) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int n = n0 + 4 * lk + s;
-          const bool nin = n < N;
-          av[s] = nin ? cur[li * ld + n] : 0.f;
-          b0[s] = (nin && in0) ? W[(int64_t)n * K + c0] : 0.f;
-          b1[s] = (nin && in1) ? W[(int64_t)n * K + c1] : 0.f;
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc0 = mfma4(av[s], b0[s], acc0);
-        if (has1) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc1 = mfma4(av[s], b1[s], acc1);
+          const int n = g0 + 16 * u + 4 * lk + s;
+          const int nc = n < N ? n : N - 1;
+          pa[u][s] = cur[li * ld + nc];
+          // a multiply by 0 / 1, not a select: the compiler sinks `cond ? load : 0` into
+          // a conditional load followed by a full vmcnt(0) wait, one load at a time
+          pb[u][s] = W[(int64_t)nc * K + cc] * ((n < N && cin) ? 1.f : 0.f);
         }
       }
+      if (it % ng == 0) {             // the tile's saved inputs / layer-0 keep flags
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !has1) break;
-        const int c = h ? c1 : c0;
-        if (c >= K) continue;
-        const floatx4 acc = h ? acc1 : acc0;
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = r0 + 4 * lk + r;
+          const int64_t e = (row < B ? row : B - 1) * K + cc;
+          px[r] = l > 0 ? xs[e] : (a.dropout[0] ? (float)a.mask0[e] : 1.f);
+        }
+      }
+    };
+    floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
+    float xv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (items > 0) load(0);
+    for (int it = 0; it < items; ++it) {
+      float ca[kMlpU][4], cb[kMlpU][4];
+#pragma unroll
+      for (int u = 0; u < kMlpU; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { ca[u][s] = pa[u][s]; cb[u][s] = pb[u][s]; }
+      if (it % ng == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xv[r] = px[r];
+      }
+      if (it + 1 < items) load(it + 1);
+#pragma unroll
+      for (int u = 0; u < kMlpU; ++u) {
+        floatx4& acc = (u & 1) ? accB : accA;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(ca[u][s], cb[u][s], acc);
+      }
+      if (it % ng != ng - 1) continue;
+      // the tile is complete: epilogue
+      const int t = wave + (it / ng) * kMlpWaves;
+      const int c = t * 16 + li;
+      const floatx4 acc = accA + accB;
+      accA = floatx4{0.f, 0.f, 0.f, 0.f};
+      accB = accA;
+      if (c < K) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 4 * lk + r;
@@ -244,12 +308,12 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
           float g = acc[r];
           if (l > 0) {
             // dropout backward (g * mask * scale) then ReLU backward ([h > 0])
-            const bool live = row < B && xs[row * K + c] > 0.f;
+            const bool live = row < B && xv[r] > 0.f;
             g = live ? g * sc : 0.f;
             if (row < B) gz[row * K + c] = g;
             nxt[i * ldn + c] = g;
           } else if (row < B) {
-            if (a.dropout[0]) g = a.mask0[row * K + c] ? g * sc : 0.f;
+            if (a.dropout[0]) g = xv[r] != 0.f ? g * sc : 0.f;
             gx0[row * K + c] = g;
           }
         }
@@ -264,8 +328,8 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
 __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_weight_kernel(mirec_mlp a, int64_t B,
                                                                      const float* __restrict__ x0,
                                                                      const float* __restrict__ dy) {
-  __shared__ float part[4][64][5];
-  __shared__ float bpart[4][16];
+  __shared__ float part[kMlpWaves][64][5];
+  __shared__ float bpart[kMlpWaves][16];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, lk = lane >> 4;
   int l = 0;
@@ -279,50 +343,65 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_weight_kernel(mirec_mlp a
   const int o = ot * 16 + li, i = it * 16 + li;
   const bool oin = o < N, iin = i < K;
   const bool with_bias = it == 0 && a.db[l];
-  // rows of this wave: a quarter of the batch (multiple of 4)
-  const int64_t q = ((B + 15) / 16) * 4;
+  // rows of this wave: an eighth of the batch (multiple of 4)
+  const int64_t q = ((B + 4 * kMlpWaves - 1) / (4 * kMlpWaves)) * 4;
   const int64_t b_lo = wave * q, b_hi = (b_lo + q < B) ? b_lo + q : B;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  int64_t b0 = b_lo;
-  for (; b0 + 16 <= b_hi; b0 += 16) {     // 16 rows: eight loads in flight, four MFMAs
-    float av[4], bv[4];
+  // groups of 64 rows: row b0 + 4s + lk (s < 16); the next group's 32 loads are issued
+  // before this group's sixteen MFMAs
+  constexpr int S = 16;
+  float pa[S], pb[S];
+  const int oc = oin ? o : N - 1, ic = iin ? i : K - 1;
+  auto load = [&](int64_t b0) {     // branch-free: clamped rows, zeroed after the load
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < S; ++s) {
       const int64_t b = b0 + 4 * s + lk;
-      av[s] = oin ? gz[b * N + o] : 0.f;
-      bv[s] = iin ? xs[b * K + i] : 0.f;
+      const bool bin = b < b_hi;
+      const int64_t bc = bin ? b : b_lo;
+      const float g = gz[bc * N + oc];
+      const float x = xs[bc * K + ic];
+      pa[s] = (oin && bin) ? g : 0.f;
+      pb[s] = (iin && bin) ? x : 0.f;
     }
+  };
+  if (b_lo < b_hi) load(b_lo);
+  for (int64_t b0 = b_lo; b0 < b_hi; b0 += 4 * S) {
+    float ca[S], cb[S];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc = mfma4(av[s], bv[s], acc);
-      bsum += av[s];
+    for (int s = 0; s < S; ++s) { ca[s] = pa[s]; cb[s] = pb[s]; }
+    if (b0 + 4 * S < b_hi) load(b0 + 4 * S);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      floatx4& acc = (s & 1) ? accB : accA;
+      acc = mfma4(ca[s], cb[s], acc);
+      bsum += ca[s];
     }
   }
-  for (; b0 < b_hi; b0 += 4) {
-    const int64_t b = b0 + lk;
-    const float av = (oin && b < b_hi) ? gz[b * N + o] : 0.f;
-    const float bv = (iin && b < b_hi) ? xs[b * K + i] : 0.f;
-    acc = mfma4(av, bv, acc);
-    bsum += av;
-  }
+  const floatx4 acc = accA + accB;
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[wave][lane][r] = acc[r];
   if (with_bias) {       // the four row phases of column o, in phase order
-    float s1 = __shfl(bsum, li + 16, 64), s2 = __shfl(bsum, li + 32, 64),
-          s3 = __shfl(bsum, li + 48, 64);
+    const float s1 = __shfl(bsum, li + 16, 64), s2 = __shfl(bsum, li + 32, 64),
+                s3 = __shfl(bsum, li + 48, 64);
     if (lk == 0) bpart[wave][li] = ((bsum + s1) + s2) + s3;
   }
   __syncthreads();
   if (wave == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = ((part[0][lane][r] + part[1][lane][r]) + part[2][lane][r]) + part[3][lane][r];
+      float v = part[0][lane][r];
+#pragma unroll
+      for (int w = 1; w < kMlpWaves; ++w) v += part[w][lane][r];
       const int oo = ot * 16 + 4 * lk + r;
       if (oo < N && iin) a.dW[l][(int64_t)oo * K + i] = v;
     }
-    if (with_bias && lk == 0 && oin)
-      a.db[l][o] = ((bpart[0][li] + bpart[1][li]) + bpart[2][li]) + bpart[3][li];
+    if (with_bias && lk == 0 && oin) {
+      float v = bpart[0][li];
+#pragma unroll
+      for (int w = 1; w < kMlpWaves; ++w) v += bpart[w][li];
+      a.db[l][o] = v;
+    }
   }
 }
 

@@ -470,13 +470,74 @@ def segment_reduce(rows: torch.Tensor, segs: Segments):
     check(rc, "mirec_segment_reduce_f32")
     ident = Segments.__new__(Segments)
     ident.n = n
-    ident.perm = torch.arange(max(n, 1), dtype=torch.int32, device=rows.device)
-    ident.seg = torch.arange(max(n, 1) + 1, dtype=torch.int32, device=rows.device)
+    iota = _iota(rows.device, max(n, 1) + 1)       # identity perm / seg: no launch per call
+    ident.perm = iota[:max(n, 1)]
+    ident.seg = iota[:max(n, 1) + 1]
     ident.uniq, ident.n_uniq, ident.ws = segs.uniq, segs.n_uniq, segs.ws
     return out, ident
 
 
+def segment_reduce2(rows: torch.Tensor, rows1: torch.Tensor, segs: Segments):
+    """segment_reduce of a [n, d] source (2 <= d <= 16) and a [n, 1] source grouped by
+    the same segments, in one pass: (compact, compact1, identity Segments), bit for bit
+    the two separate reductions."""
+    _dev(rows, torch.float32, "rows")
+    _dev(rows1, torch.float32, "rows1")
+    n, d = segs.n, rows.shape[1]
+    out = torch.empty(max(n, 1), d, dtype=torch.float32, device=rows.device)
+    out1 = torch.empty(max(n, 1), 1, dtype=torch.float32, device=rows.device)
+    ws = _scatter_ws(rows.device, lib().mirec_segment_scatter_add_workspace_size(n, d + 1))
+    rc = lib().mirec_segment_reduce2_f32(ptr(rows), d, ptr(rows1), ptr(segs.perm), ptr(segs.uniq),
+                                         ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out), ptr(out1),
+                                         ptr(ws), ws.numel(), stream_handle())
+    check(rc, "mirec_segment_reduce2_f32")
+    ident = Segments.__new__(Segments)
+    ident.n = n
+    iota = _iota(rows.device, max(n, 1) + 1)
+    ident.perm = iota[:max(n, 1)]
+    ident.seg = iota[:max(n, 1) + 1]
+    ident.uniq, ident.n_uniq, ident.ws = segs.uniq, segs.n_uniq, segs.ws
+    return out, out1, ident
+
+
+_IOTA = {}
+
+
+def _iota(device, n):
+    """0, 1, ..., n-1 as a persistent int32 device tensor (grown on demand; read only).
+    Allocated outside any graph capture the first time a size is needed."""
+    key = str(device)
+    t = _IOTA.get(key)
+    if t is None or t.numel() < n:
+        if torch.cuda.is_current_stream_capturing():   # graph-pool memory: not cached
+            return torch.arange(n, dtype=torch.int32, device=device)
+        t = _IOTA[key] = torch.arange(max(n, 1 << 16), dtype=torch.int32, device=device)
+    return t[:n]
+
+
 # ---------------------------------------------------------------- K5 Adam
+def adam_flat_multi(specs, step_consts, step_idx, beta1=0.9, beta2=0.999, eps=1e-8,
+                    weight_decay=0.0):
+    """Dense Adam steps of several parameters in one launch per 16 (specs: dicts with
+    p, m, v, g — contiguous float32 device tensors of one size each)."""
+    from recbole_amd._native import FlatParam
+    _dev(step_consts, torch.float32, "step_consts")
+    _dev(step_idx, torch.int32, "step_idx")
+    for i in range(0, len(specs), 16):
+        part = specs[i:i + 16]
+        arr = (FlatParam * len(part))()
+        for t, sp in zip(arr, part):
+            for n_ in ("p", "m", "v", "g"):
+                x = _dev(sp[n_], torch.float32, n_)
+                if not x.is_contiguous() or x.numel() != sp["p"].numel():
+                    raise ValueError(f"adam_flat_multi: {n_} must be contiguous, numel of p")
+            t.p, t.m, t.v, t.g, t.n = (ptr(sp["p"]), ptr(sp["m"]), ptr(sp["v"]), ptr(sp["g"]),
+                                       sp["p"].numel())
+        check(lib().mirec_adam_flat_multi_f32(arr, len(part), ptr(step_consts), ptr(step_idx),
+                                              beta1, beta2, eps, weight_decay, stream_handle()),
+              "mirec_adam_flat_multi_f32")
+
+
 def adam_step(p, m, v, step_consts, step_idx, rows=None, segs: Segments | None = None,
               dense_grad=None, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
     """One dense Adam step over every row of p (K5); the gradient is the grouped

@@ -165,6 +165,11 @@ class FusedBPRTrainStep(object):
     # row is touched, and its slowest wave sets the step time: measured on C2 (64
     # warm-up + 256 steps) 18.0 M positives/s at 64, 12.4 M at 256, 12.3 M at 1,024.
     FLUSH_EVERY = 64
+    # diagnostic: prepare a chunk the model side waits for at once (pipeline start / a
+    # timed region that holds its own preparation) on the model's stream instead of the
+    # prep streams. Measured slower on the C2 driver window (16.45 vs 17.06-17.16 M
+    # positives/s: the first launch started 218 µs after t0 instead of 72 µs)
+    MAIN_FIRST = False
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None, fused_step=None):
@@ -299,12 +304,16 @@ class FusedBPRTrainStep(object):
     def _sharded(self, Bc):
         return self.G > 1 and Bc == self.Bg
 
-    def _prepare(self, slot, chunk):
+    def _prepare(self, slot, chunk, on=None):
+        """Issue the walk half of a chunk's preparation on the prep stream, or — `on`, a
+        pipeline (re)start whose chunk the model side waits for at once — the whole
+        preparation on that stream (no cross-queue hand-off on the critical path; the
+        prep and group streams order their next launches after it)."""
         b0, nb, Bc = chunk
         T = self.times
         KI = (1 + T) * Bc
-        if slot.free_recorded:
-            self.prep_stream.wait_event(slot.free)
+        if slot.free_recorded and on is None and not slot.free.query():
+            self.prep_stream.wait_event(slot.free)     # (a completed event needs no wait)
         if not self._sharded(Bc):
             # keys, K4 walk, K2 groupings and look-ahead lists: one native call
             # (mirec_prepare_chunk) on the prep stream
@@ -316,11 +325,20 @@ class FusedBPRTrainStep(object):
                 thr, idx, cp.alias_seed, cp.alias_counter = samp.alias_args(
                     self.device, nb * Bc * T)
                 cp.alias_thr, cp.alias_idx, cp.n_alias = thr.data_ptr(), idx.data_ptr(), thr.numel()
-            check(lib().mirec_prepare_chunk_walk(ctypes.byref(cp), self.prep_stream.cuda_stream),
+            st = on if on is not None else self.prep_stream
+            check(lib().mirec_prepare_chunk_walk(ctypes.byref(cp), st.cuda_stream),
                   'mirec_prepare_chunk_walk')
-            slot.walked.record(self.prep_stream)
-            slot.group_pending = True          # the grouping half: _issue_groups
+            slot.walked.record(st)
             slot.chunk = chunk
+            if on is None:
+                slot.group_pending = True      # the grouping half: _issue_groups
+                return
+            self.prep_stream.wait_event(slot.walked)     # the next walks continue the walk
+            check(lib().mirec_prepare_chunk_group(ctypes.byref(cp), st.cuda_stream),
+                  'mirec_prepare_chunk_group')
+            slot.ready.record(st)
+            self.group_stream.wait_event(slot.ready)     # shared sort workspace
+            slot.group_pending = False
             return
         with torch.cuda.stream(self.prep_stream):
             s0 = b0 * self.Bg
@@ -695,13 +713,13 @@ class FusedBPRTrainStep(object):
         self._prep_limit = (len(self._plan) if upto is None
                             else self._chunk_of(max(int(upto) - 1, 0)) + 1)
 
-    def _issue_prep(self):
+    def _issue_prep(self, on=None):
         k = self._next_chunk
         if k >= min(len(self._plan), self._prep_limit):
             return
         slot = self.slots[k % len(self.slots)]
         slot.group_pending = False
-        self._prepare(slot, self._plan[k])
+        self._prepare(slot, self._plan[k], on)
         self._next_chunk += 1
 
     def _issue_groups(self, upto):
@@ -720,6 +738,9 @@ class FusedBPRTrainStep(object):
             prev = self.slots[self._cur % S]
             prev.free.record(stream)
             prev.free_recorded = True
+        if (self.MAIN_FIRST and self._next_chunk == k and k < min(len(self._plan), self._prep_limit)
+                and not self._sharded(self._plan[k][2])):
+            self._issue_prep(on=stream)        # pipeline (re)start: prepared on this stream
         while self._next_chunk <= k and self._next_chunk < min(len(self._plan),
                                                                self._prep_limit):
             self._issue_prep()

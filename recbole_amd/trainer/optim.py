@@ -118,6 +118,7 @@ class FusedAdam(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         deferred = getattr(self, '_deferred', {})
         params = [p for p in self._params() if p.grad is not None and p not in deferred]
+        self._pair_reduce(deferred)
         for p in deferred:
             self._deferred_step(p)
         if params:
@@ -180,10 +181,8 @@ class FusedAdam(torch.optim.Optimizer):
 
     def _dense_step(self, params, window=256):
         """One Adam step of parameters with dense gradients: the step constants come
-        from a window uploaded once per `window` steps, and parameters of one row width
-        share a launch (up to 4 tables per K5 launch; [numel/4, 4] views for the
-        rest, the flat kernel for numel % 4 != 0) — few launches and no per-step
-        host-to-device copy."""
+        from a window uploaded once per `window` steps and every parameter goes into
+        one flat K5 launch (up to 16 per launch) — no per-step host-to-device copy."""
         dev = params[0].device
         if self._g is not None:               # graph mode: the shared window, device index
             w = {'consts': self._g['consts'], 'zero': self._g['step'], 't0': self.n_steps,
@@ -199,28 +198,16 @@ class FusedAdam(torch.optim.Optimizer):
                 'idx': torch.arange(window, dtype=torch.int32, device=dev),
                 'zero': torch.zeros(1, dtype=torch.int32, device=dev)}
         r = self.n_steps - w['t0']
-        groups, flat = {}, []
+        # every dense parameter in one flat launch per 16 (the same per-element step as
+        # the row-table kernels: bit-identical; DeepFM ran six launches here)
+        specs = []
         for p in params:
             st = self._ensure_state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            if p.dim() == 2 and p.shape[1] in (16, 32, 64, 128, 256):
-                d, view = p.shape[1], (lambda t: t)
-            elif p.numel() % 4 == 0:
-                d, view = 4, (lambda t: t.view(-1, 4))
-            else:
-                flat.append((p, st, g))
-                continue
-            groups.setdefault(d, []).append({'p': view(p.data), 'm': view(st['exp_avg']),
-                                             'v': view(st['exp_avg_sq']),
-                                             'dense_grad': view(g)})
-        for d, specs in groups.items():
-            for i in range(0, len(specs), 4):
-                ops.adam_multi(ops.adam_tables(specs[i:i + 4]), d, w['consts'], w['zero'], r,
-                               schedule='streamed', **self._group_args())
-        for p, st, g in flat:
-            ops.adam_step(p.data, st['exp_avg'], st['exp_avg_sq'], w['consts'],
-                          w['idx'] if self._g is not None else w['idx'][r:r + 1], dense_grad=g,
-                          **self._group_args())
+            specs.append({'p': p.data, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'g': g})
+        ops.adam_flat_multi(specs, w['consts'],
+                            w['idx'] if self._g is not None else w['idx'][r:r + 1],
+                            **self._group_args())
 
     def advance(self, n: int):
         self.n_steps += n
@@ -333,6 +320,27 @@ class FusedAdam(torch.optim.Optimizer):
                 p.data.copy_(self._gather_shard(ds, ds['shard']['p'], p.shape[0]))
                 ds['shard']['synced'] = self.n_steps
 
+    def _pair_reduce(self, deferred):
+        """Tables stashed with the same single grouping — a [V, d] table (d <= 16) and a
+        [V, 1] one, DeepFM's token rows and first-order weights — are reduced in one pass
+        (ops.segment_reduce2, bit for bit the two reductions); the results wait in
+        ds['pre'] for _deferred_step."""
+        one = [(p, ds) for p, ds in deferred.items()
+               if len(ds['stash']) == 1 and ds['stash'][0][2] is not None and 'shard' not in ds
+               and p.grad is None]
+        wide = [(p, ds) for p, ds in one if 2 <= p.shape[1] <= 16]
+        narrow = [(p, ds) for p, ds in one if p.shape[1] == 1]
+        for p, ds in wide:
+            rows, keys, segs = ds['stash'][0]
+            for q, dq in narrow:
+                r1, k1, s1 = dq['stash'][0]
+                if s1 is segs and 'pre' not in dq and r1.shape[0] == rows.shape[0]:
+                    out, out1, ident = ops.segment_reduce2(rows.contiguous(),
+                                                           r1.contiguous().view(-1, 1), segs)
+                    ds['pre'] = (out, ident, ident.n)
+                    dq['pre'] = (out1, ident, ident.n)
+                    break
+
     def _combine_stash(self, p, stash):
         """One summed gradient row per touched table row. Each source (one autograd
         Function's contributions) is grouped and reduced on its own, in chunked
@@ -386,7 +394,10 @@ class FusedAdam(torch.optim.Optimizer):
             return
         ds = self._dstate(p)
         r = self.n_steps - ds['t0']
-        if stash:
+        pre = ds.pop('pre', None)
+        if pre is not None:                   # reduced together with its pair table
+            rows, segs, n_keys = pre
+        elif stash:
             rows, segs, n_keys = self._combine_stash(p, stash)
         graph = self._g is not None
         if p.grad is not None and 'shard' in ds:

@@ -745,11 +745,12 @@ def test_adam_fast_math_selftest(dev):
     assert sq_bad == 0 and dv_bad == 0, (sq_bad, dv_bad)
 
 
-@pytest.mark.parametrize('block_n,n_blocks,space', [(2048, 26, 1 << 25), (100, 7, 1000), (8192, 3, 1 << 20), (513, 4, 2100)])
+@pytest.mark.parametrize('block_n,n_blocks,space', [(2048, 26, 1 << 25), (100, 7, 1000), (8192, 3, 1 << 20), (513, 4, 2100),
+                                                   (4096, 5, 1 << 30), (64, 3, 64 * 3)])
 def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
     """mirec_segment_sort_blocks on keys in blocks of increasing key ranges (DeepFM's
     field-major token keys) gives exactly the device-wide segment_sort's outputs,
-    incl. a ragged last block."""
+    incl. a ragged last block (rank sort for 64 <= block_n <= 4096, LDS radix above)."""
     from recbole_amd import ops
     g = torch.Generator(device='cpu').manual_seed(block_n)
     edges = torch.linspace(0, space, n_blocks + 1).long()
@@ -767,3 +768,27 @@ def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
     assert torch.equal(a.perm[:n], b.perm[:n])
     assert torch.equal(a.uniq[:nu], b.uniq[:nu])
     assert torch.equal(a.seg[:nu + 1], b.seg[:nu + 1])
+
+
+@pytest.mark.parametrize('d', [4, 16])
+def test_segment_reduce2_equals_two_reductions(dev, d):
+    """mirec_segment_reduce2_f32 (the [V, d] token rows and the [V, 1] first-order rows
+    of DeepFM reduced in one pass) equals two segment_reduce calls bit for bit, incl.
+    hot rows cut into many pieces (fixup path) and one-piece rows."""
+    from recbole_amd import ops
+    g = torch.Generator().manual_seed(d)
+    n = 53_248
+    keys = torch.cat([torch.zeros(3000, dtype=torch.int64),                 # one very hot row
+                      torch.randint(1, 40, (10_000,), generator=g),         # hot rows
+                      torch.randint(40, 5_000_000, (n - 13_000,), generator=g)])
+    keys = keys[torch.randperm(n, generator=g)].to(dev)
+    rows = (torch.randn(n, d, generator=g)).to(dev)
+    rows1 = (torch.randn(n, 1, generator=g)).to(dev)
+    segs = ops.segment_sort(keys, 5_000_000)
+    a, sa = ops.segment_reduce(rows, segs)
+    a1, _ = ops.segment_reduce(rows1, segs)
+    b, b1, sb = ops.segment_reduce2(rows, rows1, segs)
+    nu = int(segs.n_uniq.item())
+    assert torch.equal(a[:nu], b[:nu])
+    assert torch.equal(a1[:nu], b1[:nu])
+    assert torch.equal(sa.perm, sb.perm) and torch.equal(sa.seg, sb.seg)

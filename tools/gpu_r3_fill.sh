@@ -1,22 +1,22 @@
 #!/bin/bash
-# Driver-window fill: parity tests of the step path, then short (--warmup 5 --steps 20)
-# benches with chunk-ramp variants, the default window, and one marked short trace.
+# C2 driver window (--warmup 5 --steps 20): the default vs variants of the pipeline start,
+# then the kernel timeline of the default.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r3fill2
+O=gpurun_out/fill
 mkdir -p $O
-T="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu"
-timeout -k 10 600 $T tests/test_gpu_step.py tests/test_gpu_e2e.py tests/test_gpu_chain.py > $O/tests.log 2>&1
-rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 10
-b() {  # tag, args...
-  local tag=$1; shift
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-eval --in-memory "$@" > $O/$tag 2>&1 || { tail -5 $O/$tag; exit 4; }
-  echo "$tag: $(grep -o '"value": [0-9.]*' $O/$tag | head -n1) $(grep -o '"kernels_us": {[^}]*}' $O/$tag | head -n1)"
+run() {  # name, extra args
+  local name=$1; shift
+  for rep in 1 2; do
+    timeout -k 10 200 python bench.py --warmup 5 --steps 20 --no-cpu-baseline --no-eval --in-memory "$@" > $O/$name.$rep.log 2>&1 || { tail -5 $O/$name.$rep.log; exit 3; }
+    python -c "import json,sys; d=json.loads([l for l in open('$O/$name.$rep.log') if l.startswith('{')][0]); print('$name', d['value'], d['ms_per_step'], d['config']['chunk_plan_timed'])"
+  done
 }
-S="--warmup 5 --steps 20"
-b base $S; b base2 $S
-b r4444 $S --ramp 4,4,4,4,8,16,32; b r2444 $S --ramp 2,4,4,4,8,16,32; b r468 $S --ramp 4,6,8,10,12,16,24,32
-b default; b default_r4444 --ramp 4,4,4,4,8,16,32
-BENCH_MARKERS=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o run -- \
-  python bench.py --no-cpu-baseline --no-eval --in-memory $S > $O/trace_bench.log 2>&1 || exit 5
+run default
+run side --no-main-first
+run r2 --ramp 2,4,8,16,32
+run r3 --ramp 3,6,12,24
+run r6 --ramp 6,8,16,32
+bash tools/trace_short.sh || exit 4
+head -60 gpurun_out/prof_short/tw.txt
 echo done
