@@ -15,8 +15,6 @@
 // counts, one block scan per pass). Larger batches: one large batch takes a
 // device-wide LSD radix sort (upsweep histograms, scan, stable downsweep), several
 // take one workgroup each over global ping-pong buffers (1-bit stable splits).
-#include <stdlib.h>
-
 #include "common.h"
 #include "ahead.h"
 
@@ -222,128 +220,6 @@ __global__ __launch_bounds__(256) void blocks_concat_kernel(
   if (b == n_blocks - 1 && threadIdx.x == 0) {
     seg[off + nu] = (int32_t)n;
     n_uniq[0] = off + nu;
-  }
-}
-
-// Rank sort of block-partitioned keys (round 3; mirec_segment_sort_blocks with
-// block_n <= 4096). The LDS radix sort costs a fixed ~4-5 µs per 4-bit pass and DeepFM's
-// 10 M-row field needs 6 passes, so its 26 field blocks took ~30 µs however few keys
-// they hold. Here every key finds its place directly: key i of a block is at rank
-// #{j : k_j < k_i} + #{j < i : k_j == k_i} (the stable order), counted against the
-// block's keys in LDS by one thread per key, 256-key slices of a block in separate
-// workgroups (the chip, not one CU per block, does the O(block_n^2) compares).
-// Pass 2 (one workgroup per block) marks the group heads of the sorted keys, scans
-// them, and writes the concatenated perm / uniq / seg — the same outputs as the radix
-// sort + blocks_concat.
-constexpr int kRankMax = 4096;
-
-__global__ __launch_bounds__(256) void rank_sort_kernel(const int64_t* __restrict__ keys,
-                                                        int64_t n, int block_n, int slices,
-                                                        int32_t* __restrict__ perm_t,
-                                                        int32_t* __restrict__ skey_t,
-                                                        int32_t* __restrict__ cnt) {
-  __shared__ int32_t ks[kRankMax];
-  __shared__ int wsum[4];
-  const int b = blockIdx.x / slices, s = blockIdx.x - b * slices;
-  const int64_t base = (int64_t)b * block_n;
-  const int nb = (int)min((int64_t)block_n, n - base);
-  // the block's keys into LDS, every thread's loads issued before any store (clamped
-  // addresses; padded to a multiple of 16 with INT32_MAX)
-  constexpr int kPer = kRankMax / 256;
-  int32_t kv[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int j = threadIdx.x + u * 256;
-    const int64_t v = keys[base + (j < nb ? j : nb - 1)];
-    kv[u] = j < nb ? (int32_t)v : INT32_MAX;
-  }
-  const int n16 = (nb + 15) & ~15;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int j = threadIdx.x + u * 256;
-    if (j < n16) ks[j] = kv[u];
-  }
-  __syncthreads();
-  const int i = s * 256 + threadIdx.x;
-  const bool valid = i < nb;
-  const int32_t ki = valid ? ks[i] : 0;
-  int lt = 0, eqb = 0;
-  const int4* k4 = reinterpret_cast<const int4*>(ks);
-  for (int j16 = 0; j16 < n16; j16 += 16) {    // sixteen keys per step: four LDS reads in flight
-    int4 q[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) q[t] = k4[(j16 >> 2) + t];     // broadcast reads
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = j16 + 4 * t;
-      lt += (q[t].x < ki) + (q[t].y < ki) + (q[t].z < ki) + (q[t].w < ki);
-      eqb += ((q[t].x == ki) & (j < i)) + ((q[t].y == ki) & (j + 1 < i)) +
-             ((q[t].z == ki) & (j + 2 < i)) + ((q[t].w == ki) & (j + 3 < i));
-    }
-  }
-  // padding keys (INT32_MAX) are never < ki; a real key equal to INT32_MAX cannot
-  // occur (key_space <= INT32_MAX), so they never count as equal either
-  if (valid) {
-    const int r = lt + eqb;
-    perm_t[base + r] = i;
-    skey_t[base + r] = ki;
-  }
-  // distinct keys of this slice: first occurrences (no equal key before)
-  const uint64_t bal = __ballot(valid && eqb == 0);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
-  __syncthreads();
-  if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
-
-__global__ __launch_bounds__(256) void rank_concat_kernel(const int32_t* __restrict__ perm_t,
-                                                          const int32_t* __restrict__ skey_t,
-                                                          const int32_t* __restrict__ cnt,
-                                                          int64_t n, int block_n, int slices,
-                                                          int n_blocks, int32_t* __restrict__ perm,
-                                                          int32_t* __restrict__ uniq,
-                                                          int32_t* __restrict__ seg,
-                                                          int32_t* __restrict__ n_uniq) {
-  __shared__ int scan_lds[256 / 64 + 1];
-  const int b = blockIdx.x;
-  int off = 0;
-  for (int c = 0; c < b * slices; ++c) off += cnt[c];
-  const int64_t base = (int64_t)b * block_n;
-  const int nb = (int)min((int64_t)block_n, n - base);
-  constexpr int kPer = kRankMax / 256;         // sorted positions per thread (contiguous)
-  const int p0 = threadIdx.x * kPer;
-  int heads = 0;
-  int32_t kv[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {           // clamped addresses: every load issued at once
-    const int p = p0 + u;
-    const int32_t v = skey_t[base + (p < nb ? p : nb - 1)];
-    kv[u] = p < nb ? v : 0;
-  }
-  const int32_t pv = skey_t[base + (p0 > 0 && p0 - 1 < nb ? p0 - 1 : 0)];
-  const int32_t prev0 = (p0 > 0 && p0 - 1 < nb) ? pv : 0;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int p = p0 + u;
-    const int32_t pk = u == 0 ? prev0 : kv[u - 1];
-    heads += (p < nb && (p == 0 || kv[u] != pk)) ? 1 : 0;
-  }
-  int total;
-  int h = block_exclusive_scan(heads, scan_lds, &total);
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int p = p0 + u;
-    if (p >= nb) break;
-    const int32_t pk = u == 0 ? prev0 : kv[u - 1];
-    if (p == 0 || kv[u] != pk) {
-      uniq[off + h] = kv[u];
-      seg[off + h] = (int32_t)(base + p);
-      ++h;
-    }
-    perm[base + p] = (int32_t)base + perm_t[base + p];
-  }
-  if (b == n_blocks - 1 && threadIdx.x == 0) {
-    seg[off + total] = (int32_t)n;
-    n_uniq[0] = off + total;
   }
 }
 
@@ -924,17 +800,6 @@ extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t
   int32_t* uniq_t = perm_t + nb * block_n;
   int32_t* seg_t = uniq_t + nb * block_n;
   int32_t* nu_t = seg_t + nb * (block_n + 1);
-  static const bool radix_only = getenv("MIREC_BLOCKS_RADIX") != nullptr;   // diagnostic A/B
-  if (block_n >= 64 && block_n <= kRankMax && !radix_only) {
-    // rank sort (the workspace of the radix path holds its perm / keys / counts)
-    const int slices = (int)((block_n + 255) / 256);
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(rank_sort_kernel, dim3((unsigned)(nb * slices)), dim3(256), 0, st, keys,
-                       n, (int)block_n, slices, perm_t, uniq_t, seg_t);
-    hipLaunchKernelGGL(rank_concat_kernel, dim3((unsigned)nb), dim3(256), 0, st, perm_t, uniq_t,
-                       seg_t, n, (int)block_n, slices, (int)nb, perm, uniq, seg, n_uniq_dev);
-    return launch_status("mirec_segment_sort_blocks");
-  }
   int nbits = 0;
   while (nbits < 31 && ((int64_t)1 << nbits) < key_space) ++nbits;
   hipStream_t st = (hipStream_t)stream;

@@ -707,11 +707,14 @@ class FusedBPRTrainStep(object):
 
     def release_prep(self, upto=None):
         """Let the chunks held by begin_epoch(hold_prep_from=...) be prepared; the
-        first is issued when run_batches enters it. upto: prepare only the chunks
+        first one's walk is issued at once (the rest as run_batches reaches them).
+        upto: prepare only the chunks
         that start before global batch `upto` (a later call releases the rest), so a
         timed region does not also run the sampler walk of the batches after it."""
         self._prep_limit = (len(self._plan) if upto is None
                             else self._chunk_of(max(int(upto) - 1, 0)) + 1)
+        if not self.MAIN_FIRST and self._next_chunk < min(len(self._plan), self._prep_limit):
+            self._issue_prep()                 # the first released walk starts right away
 
     def _issue_prep(self, on=None):
         k = self._next_chunk

@@ -750,7 +750,7 @@ def test_adam_fast_math_selftest(dev):
 def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
     """mirec_segment_sort_blocks on keys in blocks of increasing key ranges (DeepFM's
     field-major token keys) gives exactly the device-wide segment_sort's outputs,
-    incl. a ragged last block (rank sort for 64 <= block_n <= 4096, LDS radix above)."""
+    incl. a ragged last block."""
     from recbole_amd import ops
     g = torch.Generator(device='cpu').manual_seed(block_n)
     edges = torch.linspace(0, space, n_blocks + 1).long()
