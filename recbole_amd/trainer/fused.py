@@ -977,7 +977,7 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             recv.copy_(r)
 
     # ------------------------------------------------------------ data side
-    def _prepare(self, slot, chunk):
+    def _prepare(self, slot, chunk, on=None):     # on: the base class's diagnostic (unused)
         b0, nb, Bc = chunk
         T, G, r = self.times, self.G, self.rank
         KI = (1 + T) * Bc

@@ -22,7 +22,7 @@ if [ "${SMOKE:-1}" = "1" ]; then
 fi
 if [ "${TESTS:-1}" = "1" ]; then
   step gputests 1000 python -u -m pytest ${TEST_ARGS:-tests} -m gpu -v -p no:cacheprovider \
-    --timeout 300 --timeout-method thread
+    --timeout 170 --timeout-method thread
 fi
 if [ "${BENCH:-1}" = "1" ]; then
   step bench_short 300 python bench.py --warmup 5 --steps 20 ${BENCH_ARGS:-}
