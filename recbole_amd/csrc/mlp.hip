@@ -210,13 +210,17 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
                                                                    const float* __restrict__ dy,
                                                                    int64_t B,
                                                                    float* __restrict__ gx0,
-                                                                   int ldA, int ldB) {
+                                                                   int ldA, int ldB, int split) {
   extern __shared__ float lds[];
   float* const tA = lds;
   float* const tB = lds + kMlpRows * ldA;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, lk = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
+  // split = 2: two blocks per 16 rows; both run the narrow layers above layer 0 (block
+  // half 0 alone stores their g_z), and they share layer 0's wide output tiles (even /
+  // odd), which is where the time goes (C4: 39 tiles of 624 columns)
+  const int half = split > 1 ? (int)(blockIdx.x & 1) : 0;
+  const int64_t r0 = (int64_t)(blockIdx.x / split) * kMlpRows;
   const int L = a.n_layers;
   {
     const int N = a.dims[L];
@@ -244,11 +248,15 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
     // group, the tile's saved-input loads for its epilogue) issued before the current
     // item's MFMAs, across tile boundaries too
     const int ng = (N + 16 * kMlpU - 1) / (16 * kMlpU);
-    const int my_tiles = wave < ntile ? (ntile - wave + kMlpWaves - 1) / kMlpWaves : 0;
+    // tiles of this wave: t0, t0 + stride, ... (layer 0 split over the block pair)
+    const int t0 = l == 0 ? half + split * wave : wave;
+    const int tstride = l == 0 ? split * kMlpWaves : kMlpWaves;
+    const int my_tiles = t0 < ntile ? (ntile - t0 + tstride - 1) / tstride : 0;
+    const bool store_gz = half == 0;
     const int items = my_tiles * ng;
     float pa[kMlpU][4], pb[kMlpU][4], px[4];
     auto load = [&](int it) {         // branch-free, as in the forward
-      const int t = wave + (it / ng) * kMlpWaves, g0 = (it % ng) * 16 * kMlpU;
+      const int t = t0 + (it / ng) * tstride, g0 = (it % ng) * 16 * kMlpU;
       const int c = t * 16 + li;
       const bool cin = c < K;
       const int cc = cin ? c : K - 1;
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
       }
       if (it % ng != ng - 1) continue;
       // the tile is complete: epilogue
-      const int t = wave + (it / ng) * kMlpWaves;
+      const int t = t0 + (it / ng) * tstride;
       const int c = t * 16 + li;
       const floatx4 acc = accA + accB;
       accA = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
             // dropout backward (g * mask * scale) then ReLU backward ([h > 0])
             const bool live = row < B && xv[r] > 0.f;
             g = live ? g * sc : 0.f;
-            if (row < B) gz[row * K + c] = g;
+            if (row < B && store_gz) gz[row * K + c] = g;
             nxt[i * ldn + c] = g;
           } else if (row < B) {
             if (a.dropout[0]) g = xv[r] != 0.f ? g * sc : 0.f;
@@ -487,8 +495,12 @@ extern "C" int mirec_mlp_bwd_f32(const mirec_mlp* mlp, const float* x, const flo
   const size_t shm = (size_t)kMlpRows * (ldA + ldB) * sizeof(float);
   if (mlp_lds_limit(shm, "mirec_mlp_bwd_f32")) return -1;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(mlp_bwd_data_kernel, dim3((unsigned)((B + kMlpRows - 1) / kMlpRows)),
-                     dim3(kMlpThreads), shm, st, a, dy, B, gx, ldA, ldB);
+  // two blocks per 16 rows while that still fits one wave of blocks on the chip and
+  // layer 0 has tiles for both
+  const int64_t row_blocks = (B + kMlpRows - 1) / kMlpRows;
+  const int split = (row_blocks * 2 <= 256 && (a.dims[0] + 15) / 16 >= 2 * kMlpWaves) ? 2 : 1;
+  hipLaunchKernelGGL(mlp_bwd_data_kernel, dim3((unsigned)(row_blocks * split)),
+                     dim3(kMlpThreads), shm, st, a, dy, B, gx, ldA, ldB, split);
   int rc = launch_status("mirec_mlp_bwd_f32: data");
   if (rc) return rc;
   hipLaunchKernelGGL(mlp_bwd_weight_kernel, dim3((unsigned)tiles), dim3(kMlpThreads), 0, st, a, B,

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from recbole_amd import ops
 from recbole_amd._native import MLP_MAX_LAYERS, MlpDesc, check, lib, ptr, stream_handle
 
 
@@ -117,8 +118,10 @@ class _DeepFn(torch.autograd.Function):
                 keep += [x0, m0]
                 d.xs[0], d.mask0 = ptr(x0), ptr(m0)
         y = E(B, dims[L])
-        check(lib().mirec_mlp_fwd_f32(ctypes.byref(d), ptr(x), B, ptr(y), 1 if train else 0,
-                                      stream_handle()), 'mirec_mlp_fwd_f32')
+        with ops.timed_launch('mlp_fwd'):
+            rc = lib().mirec_mlp_fwd_f32(ctypes.byref(d), ptr(x), B, ptr(y), 1 if train else 0,
+                                         stream_handle())
+        check(rc, 'mirec_mlp_fwd_f32')
         ctx.desc, ctx.keep, ctx.dims, ctx.L = d, keep, dims, L
         ctx.has_bias = [b is not None for b in bs]
         ctx.save_for_backward(x, *Ws)
@@ -140,8 +143,10 @@ class _DeepFn(torch.autograd.Function):
             d.dW[l] = ptr(dW[l])
             d.db[l] = ptr(db[l])
         gx = E(B, dims[0])
-        check(lib().mirec_mlp_bwd_f32(ctypes.byref(d), ptr(x), ptr(gy), B, ptr(gx),
-                                      stream_handle()), 'mirec_mlp_bwd_f32')
+        with ops.timed_launch('mlp_bwd'):            # two launches: data, weight gradients
+            rc = lib().mirec_mlp_bwd_f32(ctypes.byref(d), ptr(x), ptr(gy), B, ptr(gx),
+                                         stream_handle())
+        check(rc, 'mirec_mlp_bwd_f32')
         ctx.keep = None
         out = [None, None, gx]
         for l in range(L):

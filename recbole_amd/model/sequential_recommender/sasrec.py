@@ -36,7 +36,9 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         dev = E.device
         seq = item_seq.contiguous()
         h = getattr(E, '_mirec_deferred', None)
-        ctx.segs = h.catch_up(E, seq.view(-1)) if h is not None else None
+        # item 0 is the padding_idx (reference sasrec.py: nn.Embedding(..., padding_idx=0)):
+        # no gradient, so its positions are left out of the grouping
+        ctx.segs = h.catch_up(E, seq.view(-1), drop_key=0) if h is not None else None
         ctx.deferred = h is not None
         out = torch.empty(B, L, d, dtype=torch.float32, device=dev)
         mean = torch.empty(B * L, dtype=torch.float32, device=dev)

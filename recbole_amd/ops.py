@@ -396,9 +396,10 @@ def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int) -> Seg
     _dev(keys, torch.int64, "keys")
     n = keys.numel()
     segs = Segments(n, keys.device, lib().mirec_segment_sort_blocks_workspace_size(n, block_n))
-    rc = lib().mirec_segment_sort_blocks(ptr(keys), n, block_n, key_space, ptr(segs.perm),
-                                         ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq),
-                                         ptr(segs.ws), segs.ws.numel(), stream_handle())
+    with timed_launch('k2_blocks'):              # two launches: the block sorts, the concat
+        rc = lib().mirec_segment_sort_blocks(ptr(keys), n, block_n, key_space, ptr(segs.perm),
+                                             ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq),
+                                             ptr(segs.ws), segs.ws.numel(), stream_handle())
     check(rc, "mirec_segment_sort_blocks")
     return segs
 

@@ -266,13 +266,27 @@ class FusedAdam(torch.optim.Optimizer):
         spec.update(kw)
         return ops.adam_tables([spec])
 
-    def catch_up(self, p, keys, segs=None, blocks=None):
+    def catch_up(self, p, keys, segs=None, blocks=None, drop_key=None):
         """Make the rows `keys` (int64, any order / duplicates) current before a
         forward pass reads them; returns their K2 grouping (`segs`: the grouping
         when the caller already has it, e.g. another table read by the same keys;
         `blocks`: the keys come in blocks of this size with increasing key ranges,
-        which K2 then sorts block by block in LDS)."""
-        if segs is None and blocks:
+        which K2 then sorts block by block in LDS). drop_key: a padding_idx row —
+        nn.Embedding gives it no gradient, so its contributions are left out of the
+        grouping (they sort last under a sentinel key and n_uniq excludes them): the row
+        stays untouched, which the deferred schedule makes bit-identical to a step with a
+        zero gradient, and the reduction skips what can be half of a padded sequence
+        batch's positions. Only with weight_decay 0: the row then never moves (a zero-
+        gradient step keeps m = v = 0 and p), so the forward may read it un-caught-up."""
+        if (segs is None and drop_key is not None and 'shard' not in self._deferred[p]
+                and self._group_args()['weight_decay'] == 0):
+            n_rows = p.shape[0]
+            k = keys.contiguous()
+            k = torch.where(k == int(drop_key), torch.full_like(k, n_rows), k)
+            segs = ops.segment_sort(k, n_rows + 1)
+            last = segs.uniq.gather(0, (segs.n_uniq.long() - 1).clamp(min=0))
+            segs.n_uniq.sub_((last == n_rows).to(torch.int32))
+        elif segs is None and blocks:
             segs = ops.segment_sort_blocks(keys.contiguous(), int(blocks), p.shape[0])
         elif segs is None:
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])

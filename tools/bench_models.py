@@ -33,6 +33,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+MFMA_F32_PEAK_TFLOPS = 157.3   # fp32 matrix peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # fp32 MFMA / vector peak
 CPU_BASELINE = True
@@ -220,10 +221,18 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
         opt.zero_grad()
         model.calculate_loss(b).backward()
         opt.step()
-    ev = _window_events(eager, ('ctx_fm_bwd', 'ctx_fm_fwd'))
+    ev = _window_events(eager, ('ctx_fm_bwd', 'ctx_fm_fwd', 'mlp_fwd', 'mlp_bwd', 'k2_blocks'))
     opt.flush()
     bwd_n, bwd_us = ev['ctx_fm_bwd']
     fwd_n, fwd_us = ev['ctx_fm_fwd']
+    # K10 (the MLP on fp32 MFMA): 2 FLOPs per multiply-add of every layer, per launch
+    dims = [39 * d, 128, 128, 128, 1]
+    mlp_flops = 2 * B * sum(a * b_ for a, b_ in zip(dims[:-1], dims[1:]))
+    mf_n, mf_us = ev['mlp_fwd']
+    mb_n, mb_us = ev['mlp_bwd']
+    k2_n, k2_us = ev['k2_blocks']
+    nk = 26 * B                                 # token keys of a step
+    k2_bytes = nk * (8 + 4 + 4 + 4)             # keys read; perm, uniq, seg written
     bwd_bytes = B * (2 * 39 * d * 4 + 4 + 39 * d * 4 + 39 * 4)
     fwd_bytes = B * (26 * (d * 4 + 4 + 8) + 13 * 4 + 39 * d * 4 + 4 + 26 * 8)
     traffic, tsrc = _pmc_traffic('ctx_fm_bwd_kernel')
@@ -242,6 +251,29 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                          f'restatement on torch CPU (DeepFMCPU + dense optim.Adam over every '
                          f'table; a bounded sample: one step moves the 2.1 GB tables several '
                          f'times), {sum(r[1] for r in runs):.1f} s timed in all'}
+    k10 = {'kernel': 'mlp_fwd_kernel (K10 forward: MLPLayers 624-128-128-128 + '
+                     'deep_predict_layer, dropout, ReLU)', 'bound': 'mfma',
+           'achieved': round(mlp_flops / (mf_us * 1e-6) / 1e12, 2),
+           'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+           'frac': round(mlp_flops / (mf_us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+           'traffic': _pmc_traffic('mlp_fwd_kernel')[0],
+           'traffic_source': _pmc_traffic('mlp_fwd_kernel')[1],
+           'flops_per_launch': mlp_flops, 'launch_us': round(mf_us, 2),
+           'launches_per_step': mf_n,
+           'timing': 'HIP events around each launch on its stream, 8 eager steps'}
+    k2 = {'kernel': 'segsort_lds_kernel + blocks_concat_kernel (K2 grouping of the 26 '
+                    'token fields, one event pair around both launches; latency-bound)',
+          'bound': 'hbm', 'achieved': round(k2_bytes / (k2_us * 1e-6) / 1e9, 1),
+          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+          'frac': round(k2_bytes / (k2_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+          'traffic': _pmc_traffic('segsort_lds_kernel')[0],
+          'traffic_source': _pmc_traffic('segsort_lds_kernel')[1],
+          'bytes_per_launch': k2_bytes, 'launch_us': round(k2_us, 2), 'launches_per_step': k2_n,
+          'timing': 'HIP events around each call on its stream, 8 eager steps'}
+    # the roofline of the timed step's dominant kernel (committed trace breakdown)
+    sb = _step_breakdown('C4')
+    dom = (sb or {}).get('dominant', {}).get('kernel', '') if sb else ''
+    roof = k2 if 'segsort' in dom else k10
     return {
         'cpu_baseline': cpu,
         'adam_mode': ADAM_MODE, 'graph_step': bool(GRAPH_STEP),
@@ -251,8 +283,16 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                     f'(incl. PADs), d={d}, MLP 624-128-128-128-1, dropout 0.2, BCE, dense Adam',
         'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) ids, log-normal floats, seeded)',
         'step_breakdown': _step_breakdown('C4'),
-        'roofline': {'kernel': 'ctx_fm_bwd_kernel<16> (K8 backward; the timed step\'s dominant '
-                               'kernel)', 'bound': 'hbm',
+        'roofline': roof,
+        'k10_fwd': k10,
+        'k2_grouping': k2,
+        'k10_bwd': {'kernel': 'mlp_bwd_data_kernel + mlp_bwd_weight_kernel (K10 backward, one '
+                              'event pair around both launches)', 'bound': 'mfma',
+                    'achieved': round(2 * mlp_flops / (mb_us * 1e-6) / 1e12, 2),
+                    'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                    'frac': round(2 * mlp_flops / (mb_us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+                    'flops_per_call': 2 * mlp_flops, 'call_us': round(mb_us, 2)},
+        'k8_bwd': {'kernel': 'ctx_fm_bwd_kernel<16> (K8 backward)', 'bound': 'hbm',
                      'achieved': round(bwd_bytes / (bwd_us * 1e-6) / 1e9, 1),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(bwd_bytes / (bwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
