@@ -8,6 +8,9 @@ set -u
 export TMPDIR=/tmp
 O=gpurun_out/r3f
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu \
+  tests/test_gpu_mlp.py tests/test_gpu_deepfm.py tests/test_gpu_graph_step.py > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit 10
 for c in C4 C3; do
   MODELS_MARKERS=1 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/tr_$c -o run -- \
     python tools/bench_models.py --configs $c --steps 32 --warmup 8 --no-cpu-baseline > $O/tr_$c.log 2>&1 || exit 7
