@@ -62,18 +62,6 @@ static void mlp_ld(const mirec_mlp& a, int* ldA, int* ldB) {
 }
 
 // -------------------------------------------------------------------------- forward
-// One prefetch group of a W row for the forward: slices k0 + 16u + 4*lk (float4),
-// clamped into the row and zeroed past its end.
-__device__ __forceinline__ void fwd_load_w(const float* __restrict__ wr, int K, int k0, int lk,
-                                           float4* __restrict__ pb) {
-#pragma unroll
-  for (int u = 0; u < kFwdU; ++u) {
-    const int k = k0 + 16 * u + 4 * lk;
-    pb[u] = *reinterpret_cast<const float4*>(wr + (k < K ? k : K - 4));
-    if (k >= K) pb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
 __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const float* __restrict__ x,
                                                               int64_t B, float* __restrict__ y,
                                                               int train, int ldA, int ldB) {
@@ -132,10 +120,6 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
   }
   __syncthreads();
 
-  // group 0 of the next layer's W for this wave's first tile, loaded before the layer
-  // barrier (W does not depend on the layer below): one L2 latency off each boundary
-  float4 wnext[kFwdU];
-  bool have_next = false;
   for (int l = 0; l < L; ++l) {
     const int K = a.dims[l], N = a.dims[l + 1];
     const float* cur = (l & 1) ? tB : tA;
@@ -157,25 +141,18 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
       // branch-free loads (addresses clamped into the row, out-of-range slices zeroed
       // after the load): straight-line code lets the compiler wait on the older group
       // only (vmcnt(N)) while the next group is in flight
-      auto loadA = [&](int k0) {
+      auto load = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < kFwdU; ++u) {
           const int k = k0 + 16 * u + 4 * lk;
-          pa[u] = *reinterpret_cast<const float4*>(cur + li * ld + (k < K ? k : K - 4));
+          const int kc = k < K ? k : K - 4;
+          pa[u] = *reinterpret_cast<const float4*>(cur + li * ld + kc);
+          pb[u] = *reinterpret_cast<const float4*>(wr + kc);
+          if (k >= K) pb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       };
-      auto load = [&](int k0) {
-        loadA(k0);
-        fwd_load_w(wr, K, k0, lk, pb);
-      };
       floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
-      if (t == wave && have_next) {          // group 0 of W came in before the barrier
-        loadA(0);
-#pragma unroll
-        for (int u = 0; u < kFwdU; ++u) pb[u] = wnext[u];
-      } else {
-        load(0);
-      }
+      load(0);
       for (int k0 = 0; k0 < K; k0 += 16 * kFwdU) {
         float4 ca[kFwdU], cb[kFwdU];
 #pragma unroll
@@ -213,13 +190,6 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
         }
       }
     }
-    have_next = false;
-    if (l + 1 < L && wave < (a.dims[l + 2] + 15) / 16) {
-      const int K2 = a.dims[l + 1], N2 = a.dims[l + 2];
-      const int c2 = wave * 16 + li;
-      fwd_load_w(a.W[l + 1] + (int64_t)(c2 < N2 ? c2 : N2 - 1) * K2, K2, 0, lk, wnext);
-      have_next = true;
-    }
     __syncthreads();
   }
 
@@ -236,35 +206,6 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
 }
 
 // ------------------------------------------------------------------------ data grad
-// Global loads of one data-gradient item of layer l: W[n][c] for the group's slices n
-// (times 0 / 1 past the ends: a select would be sunk into a conditional load) and, for a
-// tile's first group, the tile's saved inputs (layer 0: its keep flags) for the epilogue.
-__device__ __forceinline__ void bwd_load_wx(const mirec_mlp& a, int l, int t, int g0, int li,
-                                            int lk, int64_t r0, int64_t B,
-                                            float (&pb)[kMlpU][4], float (&px)[4], bool with_x) {
-  const int K = a.dims[l], N = a.dims[l + 1];
-  const float* __restrict__ W = a.W[l];
-  const int c = t * 16 + li;
-  const bool cin = c < K;
-  const int cc = cin ? c : K - 1;
-#pragma unroll
-  for (int u = 0; u < kMlpU; ++u)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int n = g0 + 16 * u + 4 * lk + s;
-      const int nc = n < N ? n : N - 1;
-      pb[u][s] = W[(int64_t)nc * K + cc] * ((n < N && cin) ? 1.f : 0.f);
-    }
-  if (with_x) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = r0 + 4 * lk + r;
-      const int64_t e = (row < B ? row : B - 1) * K + cc;
-      px[r] = l > 0 ? a.xs[l][e] : (a.dropout[0] ? (float)a.mask0[e] : 1.f);
-    }
-  }
-}
-
 __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
                                                                    const float* __restrict__ dy,
                                                                    int64_t B,
@@ -292,13 +233,13 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
     }
   }
   __syncthreads();
-  float wn[kMlpU][4], xn[4];
-  bool have_next = false;
   for (int l = L - 1; l >= 0; --l) {
     const int K = a.dims[l], N = a.dims[l + 1];     // g_x [16, K] = g_z [16, N] . W [N, K]
     const float* cur = ((l + 1) & 1) ? tB : tA;      // g_z: width dims[l + 1]
     float* nxt = (l & 1) ? tB : tA;                  // g_z of the layer below: width dims[l]
     const int ld = ((l + 1) & 1) ? ldB : ldA, ldn = (l & 1) ? ldB : ldA;
+    const float* __restrict__ W = a.W[l];
+    const float* __restrict__ xs = l > 0 ? a.xs[l] : nullptr;
     float* __restrict__ gz = l > 0 ? a.gz[l - 1] : nullptr;
     const float sc = (a.dropout[l] ? a.scale : 1.f);
     const int ntile = (K + 15) / 16;
@@ -316,31 +257,33 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
     float pa[kMlpU][4], pb[kMlpU][4], px[4];
     auto load = [&](int it) {         // branch-free, as in the forward
       const int t = t0 + (it / ng) * tstride, g0 = (it % ng) * 16 * kMlpU;
+      const int c = t * 16 + li;
+      const bool cin = c < K;
+      const int cc = cin ? c : K - 1;
 #pragma unroll
-      for (int u = 0; u < kMlpU; ++u)
+      for (int u = 0; u < kMlpU; ++u) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int n = g0 + 16 * u + 4 * lk + s;
-          pa[u][s] = cur[li * ld + (n < N ? n : N - 1)];
+          const int nc = n < N ? n : N - 1;
+          pa[u][s] = cur[li * ld + nc];
+          // a multiply by 0 / 1, not a select: the compiler sinks `cond ? load : 0` into
+          // a conditional load followed by a full vmcnt(0) wait, one load at a time
+          pb[u][s] = W[(int64_t)nc * K + cc] * ((n < N && cin) ? 1.f : 0.f);
         }
-      bwd_load_wx(a, l, t, g0, li, lk, r0, B, pb, px, it % ng == 0);
+      }
+      if (it % ng == 0) {             // the tile's saved inputs / layer-0 keep flags
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = r0 + 4 * lk + r;
+          const int64_t e = (row < B ? row : B - 1) * K + cc;
+          px[r] = l > 0 ? xs[e] : (a.dropout[0] ? (float)a.mask0[e] : 1.f);
+        }
+      }
     };
     floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
     float xv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (items > 0 && have_next) {      // item 0's global loads came in before the barrier
-#pragma unroll
-      for (int u = 0; u < kMlpU; ++u)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int n = 16 * u + 4 * lk + s;
-          pa[u][s] = cur[li * ld + (n < N ? n : N - 1)];
-          pb[u][s] = wn[u][s];
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) px[r] = xn[r];
-    } else if (items > 0) {
-      load(0);
-    }
+    if (items > 0) load(0);
     for (int it = 0; it < items; ++it) {
       float ca[kMlpU][4], cb[kMlpU][4];
 #pragma unroll
@@ -382,16 +325,6 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_bwd_data_kernel(mirec_mlp a,
             gx0[row * K + c] = g;
           }
         }
-      }
-    }
-    // item 0 of the layer below: its W rows and saved inputs do not depend on this
-    // layer's output, so they load before the barrier (one L2 latency off the boundary)
-    have_next = false;
-    if (l >= 1) {
-      const int tn = l - 1 == 0 ? half + split * wave : wave;
-      if (tn < (a.dims[l - 1] + 15) / 16) {
-        bwd_load_wx(a, l - 1, tn, 0, li, lk, r0, B, wn, xn, true);
-        have_next = true;
       }
     }
     __syncthreads();
