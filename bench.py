@@ -8,17 +8,23 @@ embedding_size 128, 4 uniform negatives per positive, train_batch_size 2,048
 rows -> 512 positives per step, Adam lr 1e-3 — built and trained through the
 product path (Dataset -> data_preparation -> BPR -> FusedBPRTrainStep).
 
-A step = one batch: K4 sampler walk -> K3 fused BPR fwd/bwd -> K2 grouping ->
-K5 dense Adam over every row of both tables -> loss bookkeeping. Inputs are
-resident in HBM before the timed region.
+A step = one batch: K4 sampler walk + K2 grouping + K35 step records (the data side,
+on two prep streams, one chunk of batches per launch) -> K35, one launch per step: BPR
+forward + backward + the touched rows' dense-Adam step (deferred schedule: every
+zero-gradient step of every row is applied, bit-identically, when the row is next read
+or at a flush) + the look-ahead replays of the rows the next step reads -> per-chunk
+loss bookkeeping; the timed region ends with the flush that makes every row current.
+Inputs are resident in HBM before the timed region; the walk and grouping of every
+timed step run inside it.
 
 Prints ONE JSON line (rank 0). With --gpus N>1 (torchrun, one rank per GPU) the
-step is data parallel: each optimizer step consumes a global batch of N x 512
-positives, rank g computes K3's forward on its 512, one RCCL all-gather over xGMI
-exchanges the per-row loss coefficients (10 KB per rank), every rank rebuilds the
-global batch's gradient rows, and applies the same dense Adam to its replica of
-the tables — bit-identical to one GPU running the global batch (weak scaling: the
-per-GPU batch is fixed; value = global positives / max-over-ranks time).
+tables are ROW-SHARDED (cyclic ownership; --dp-mode replicated keeps
+replicas): each optimizer step consumes a global batch of N x 512 positives, every
+rank walks and groups the global batch, owners send the rows each rank's slice reads
+and receive its gradient rows back (two RCCL all-to-alls over xGMI), and apply the
+deferred Adam step to their rows only — bit-identical to one GPU running the global
+batch (weak scaling: the per-GPU batch is fixed; value = global positives /
+max-over-ranks time).
 """
 from __future__ import annotations
 
@@ -58,7 +64,18 @@ def make_c2(seed=2020, n_users=138493, n_items=26744, target=20_000_263):
     return u[order], i[order], n_users + 1, n_items + 1
 
 
-C2_NAME = 'c2-synth'
+# the generator's version: bump it whenever make_c2 / write_c2_inter change what they write
+C2_GEN_VERSION = 1
+
+
+def c2_name(seed=2020):
+    """Dataset name (= directory and file stem) of the synthetic C2 atomic file: it carries
+    the seed and the generator version, so a cached file from other generator arguments is
+    never reused (build_workload regenerates when the name is absent)."""
+    return f'c2-synth-s{seed}-g{C2_GEN_VERSION}'
+
+
+C2_NAME = c2_name()
 
 
 def write_c2_inter(path, u, i, seed=2020):
@@ -98,7 +115,8 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     from recbole_amd.utils import init_seed
     info = {'source': source}
     root = os.environ.get('MIREC_BENCH_DATA', '/tmp/mirec_bench')
-    path = os.path.join(root, C2_NAME, f'{C2_NAME}.inter')
+    name = c2_name(seed)
+    path = os.path.join(root, name, f'{name}.inter')
     cd = {'data_path': root if source == 'file' else ROOT, 'embedding_size': d,
           'training_neg_sample_num': neg, 'train_batch_size': batch_rows,
           'eval_setting': 'RO_RS,full', 'use_gpu': True, 'state': 'ERROR',
@@ -115,7 +133,7 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     if source == 'file':
         info['file'] = path
         info['file_mb'] = round(os.path.getsize(path) / 2 ** 20, 1)
-    config = Config(model='BPR', dataset=C2_NAME if source == 'file' else 'synthetic-ml20m',
+    config = Config(model='BPR', dataset=name if source == 'file' else 'synthetic-ml20m',
                     config_dict=cd)
     config['device'] = dev
     init_seed(config['seed'], config['reproducibility'])
@@ -325,14 +343,23 @@ def cpu_baseline(train, step_obj, d, neg, steps, warmup=20, runs=3):
     items = train.dataset.inter_feat['item_id'].cpu().numpy()
     ptr, cols = train.sampler.used_csr['train']
     threads, how = cb.host_threads()
-    vals, dts = [], []
+    vals, dts, splits = [], [], []
     for r in range(runs):
+        sp = {}
         pps, dt, used = cb.time_bpr_steps(users, items, ptr, cols, train.sampler.random_list,
                                           step_obj.nU, step_obj.nI, d, step_obj.B, neg,
-                                          steps=steps, warmup=warmup, threads=threads, seed=r)
+                                          steps=steps, warmup=warmup, threads=threads, seed=r,
+                                          split=sp)
         vals.append(pps)
         dts.append(dt)
+        splits.append(sp)
+    med = int(np.argsort(vals)[len(vals) // 2])         # the median run's cost centres
+    sp = splits[med]
     return {'value': round(float(np.median(vals)), 1), 'unit': 'positives/s', 'cores': used,
+            # data pipeline (slice + sampler walk with the Python rejection
+            # loop + pairwise layout) vs model step (fwd + bwd + dense Adam), median run
+            'pipeline_s': round(sp['pipeline_s'], 3), 'model_s': round(sp['model_s'], 3),
+            'pipeline_frac': round(sp['pipeline_s'] / (sp['pipeline_s'] + sp['model_s']), 4),
             'kind': 'port', 'runs': [round(v, 1) for v in vals],
             'nproc': os.cpu_count(), 'cpu_model': _cpu_model(),
             'torch_threads': used, 'threads_derivation': how,

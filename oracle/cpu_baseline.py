@@ -68,8 +68,12 @@ def host_threads():
 
 
 def time_bpr_steps(users, items, used_ptr, used_cols, random_list, n_users, n_items, d, B, T,
-                   steps=20, warmup=3, lr=1e-3, threads=None, seed=0):
-    """Returns (positives_per_second, seconds_timed, threads_used)."""
+                   steps=20, warmup=3, lr=1e-3, threads=None, seed=0, split=None):
+    """Returns (positives_per_second, seconds_timed, threads_used). `split` (a dict, if
+    given) receives the timed seconds by cost centre: 'pipeline_s' = the
+    batch slice + the sampler walk with its Python rejection loop (sampler.py:144-153) +
+    the pairwise layout (general_dataloader.py:233-241), 'model_s' = zero_grad +
+    calculate_loss + backward + Adam step (trainer.py:160-173)."""
     if threads:
         torch.set_num_threads(threads)
     torch.manual_seed(seed)
@@ -79,22 +83,31 @@ def time_bpr_steps(users, items, used_ptr, used_cols, random_list, n_users, n_it
     users = torch.as_tensor(users)
     items = torch.as_tensor(items)
 
+    acc = [0.0, 0.0]
+
     def one(b):
+        ta = time.perf_counter()
         ub, ib = users[b * B:(b + 1) * B], items[b * B:(b + 1) * B]
         neg = torch.as_tensor(walk.sample_by_key_ids(ub.numpy(), T))
         ur, pr_, nr = cpu_ref.pairwise_rows(ub, ib, neg, T)
+        tb = time.perf_counter()
         opt.zero_grad()
         loss = model.calculate_loss(ur, pr_, nr)
         loss.item()
         loss.backward()
         opt.step()
+        acc[0] += tb - ta
+        acc[1] += time.perf_counter() - tb
 
     for b in range(warmup):
         one(b)
+    acc[0] = acc[1] = 0.0
     t0 = time.perf_counter()
     for b in range(warmup, warmup + steps):
         one(b)
     dt = time.perf_counter() - t0
+    if split is not None:
+        split['pipeline_s'], split['model_s'] = acc[0], acc[1]
     return steps * B / dt, dt, torch.get_num_threads()
 
 

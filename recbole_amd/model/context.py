@@ -189,6 +189,9 @@ class _CtxFMFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_concat, g_fm):
         concat, keys = ctx.saved_tensors
+        if ctx.keep is None:        # the descriptors point into buffers the first backward freed
+            raise RuntimeError('K8 context fields: backward through the same graph a second '
+                               'time is not supported (its saved buffers were released)')
         layout, tables, B, d = ctx.layout, ctx.tables, ctx.B, ctx.d
         dev = concat.device
         nt, ns, nf = len(layout.token_names), len(layout.seq_names), len(layout.float_names)

@@ -130,6 +130,11 @@ class _DeepFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, *Ws = ctx.saved_tensors
+        if ctx.keep is None:
+            # the descriptor's saved-activation pointers point into ctx.keep, released by
+            # the first backward: a second one (retain_graph=True) would read freed memory
+            raise RuntimeError('K10 MLP: backward through the same graph a second time is not '
+                               'supported (its saved activations were released)')
         d, dims, L = ctx.desc, ctx.dims, ctx.L
         dev, B = x.device, x.shape[0]
         gy = gy.contiguous()

@@ -21,6 +21,17 @@ def free_port():
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
+    config.addinivalue_line('markers', 'slow: full-scale CPU test (minutes, GBs of memory); '
+                                       'runs only with MIREC_SLOW_TESTS=1')
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get('MIREC_SLOW_TESTS') == '1':
+        return
+    skip = pytest.mark.skip(reason='full-scale test: set MIREC_SLOW_TESTS=1 to run it')
+    for item in items:
+        if 'slow' in item.keywords:
+            item.add_marker(skip)
 
 
 @pytest.fixture(scope='session')
