@@ -116,6 +116,28 @@ int64_t mirec_host_csr_build(const int64_t* keys, const int64_t* vals, int64_t n
 
 /* Used-id bitmap of a CSR (sampler.py:206-227 used_ids as bits):
  * bits[k * ceil(n_bits/32) + v/32] bit v%32 set iff v in used[k], v < n_bits. */
+/* K4s — the same walk (values, pointer, status: bit for bit mirec_sample_walk's) of
+ * n_batches fixed-size batches by speculation: every batch is walked at every start its
+ * window admits (R = refill draws of the batches before it, windows b*r_mean -+
+ * (4.5*r_sd*sqrt(b) + 3) from the caller's per-batch rejection statistics, b < 16) in one
+ * chip-wide launch, a second launch chains the exact starts and writes each batch from
+ * its chosen start; a batch outside its window and every batch after it are walked by the
+ * single-block walk. Two launches per 16 batches instead of one serial walk. keys =
+ * users (batch b at users + b*batch_keys); out / out_stride as mirec_sample_walk. With
+ * user_keys (and items, item_keys, key_stride >= batch_keys) it also copies each batch's
+ * keys to user_keys + b*batch_keys and its items to item_keys + b*key_stride (the chunk
+ * preparation's key rows). batch_keys <= 1024, batch_keys * num <= 4096. Workspace:
+ * mirec_sample_walk_spec_workspace_size(batch_keys, num, min(n_batches, 16), r_mean, r_sd). */
+size_t mirec_sample_walk_spec_workspace_size(int64_t batch_keys, int64_t num,
+                                             int64_t max_batches, double r_mean, double r_sd);
+int mirec_sample_walk_spec(const int32_t* random_list, int64_t L, int64_t* pr_dev,
+                           const int64_t* users, const int64_t* items, int64_t n_batches,
+                           int64_t batch_keys, int64_t num, const int64_t* used_ptr,
+                           const int32_t* used_cols, const uint32_t* used_bits, int64_t n_bits,
+                           int64_t n_key_space, int reject, double r_mean, double r_sd,
+                           int64_t* out, int64_t out_stride, int64_t* user_keys,
+                           int64_t* item_keys, int64_t key_stride, int32_t* status_dev, void* ws,
+                           size_t ws_bytes, void* stream);
 size_t mirec_used_bitmap_bytes(int64_t n_keys, int64_t n_bits);
 int mirec_used_bitmap_build(const int64_t* used_ptr, const int32_t* used_cols, int64_t n_keys,
                             int64_t n_bits, uint32_t* bits, void* stream);
@@ -263,6 +285,9 @@ typedef struct mirec_chunk_prep {
   uint64_t alias_seed, alias_counter;
   /* K35 records (u_rec != NULL): mirec_step_records after the groupings */
   int32_t *u_rec, *u_crec, *i_rec, *i_crec;
+  /* K4s (spec_ws != NULL, walk only): the chunk's walk and key rows by
+   * mirec_sample_walk_spec with the rejection statistics r_mean / r_sd */
+  void* spec_ws; size_t spec_ws_bytes; double r_mean, r_sd;
 } mirec_chunk_prep;
 int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
 /* The two halves of mirec_prepare_chunk, for two streams (the caller orders
@@ -271,6 +296,21 @@ int mirec_prepare_chunk(const mirec_chunk_prep* p, void* stream);
  * chunk c is grouped. */
 int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream);
 int mirec_prepare_chunk_group(const mirec_chunk_prep* p, void* stream);
+/* K36 — a prepared chunk's grouping side in ONE launch, one workgroup per (table,
+ * batch): the K2 groupings (perm / uniq / seg / n_uniq, identical to
+ * mirec_segment_sort_batched's), the K35 records (identical to mirec_step_records';
+ * u_rec.. NULL: none) and the look-ahead lists (identical to mirec_uniq_ahead_diff's;
+ * u_ahead.. NULL: none). Keys are clamped to [0, n) as the records clamp them.
+ * Returns 1 when done, 0 when the shapes are outside its one-workgroup form (Bc >
+ * 2,048, (1+T)*Bc > 4,096, key and position bits > 32, or look-ahead key spaces >
+ * 2^18 rows) — nothing was launched, the caller groups by the general path — and
+ * < 0 on bad arguments. mirec_prepare_chunk_group uses it when it applies. */
+int mirec_chunk_group(const int64_t* user_keys, const int64_t* item_keys, int64_t n_batches,
+                      int64_t Bc, int32_t T, int64_t n_users, int64_t n_items, int32_t* u_perm,
+                      int32_t* u_uniq, int32_t* u_seg, int32_t* u_nu, int32_t* i_perm,
+                      int32_t* i_uniq, int32_t* i_seg, int32_t* i_nu, int32_t* u_rec,
+                      int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, int32_t* u_ahead,
+                      int32_t* u_nah, int32_t* i_ahead, int32_t* i_nah, void* stream);
 
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of
@@ -409,6 +449,15 @@ int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32
                          const float* step_consts_dev, const int32_t* step_base_dev,
                          int32_t step_off, double beta1, double beta2, double eps,
                          double weight_decay, void* stream);
+/* The same flush (same results) for tables whose rows mostly need nothing (the zero
+ * state, or current): each wave owns rows_per_wave[q] (1..64, HOST array per table)
+ * consecutive rows of table q and completes those that lag one after another, so the
+ * grid has rows / (4 * R) workgroups instead of one per row (the workgroup dispatcher,
+ * not the replay, bounds a one-per-row flush of a mostly idle table). d >= 64. */
+int mirec_adam_flush_rows_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,
+                              const int32_t* rows_per_wave, const float* step_consts_dev,
+                              const int32_t* step_base_dev, int32_t step_off, double beta1,
+                              double beta2, double eps, double weight_decay, void* stream);
 /* K35 — one training step of the fused BPR path in ONE launch: BPR forward + backward
  * (mirec_bpr_fwd_bwd_f32's arithmetic) and the deferred Adam step
  * (mirec_adam_deferred_f32's arithmetic) of every touched row, and the look-ahead

@@ -82,7 +82,9 @@ class ChunkPrep(ctypes.Structure):
                 ('u_ahead', _P), ('u_nah', _P), ('i_ahead', _P), ('i_nah', _P),
                 ('alias_thr', _P), ('alias_idx', _P), ('n_alias', c_int64),
                 ('alias_seed', ctypes.c_uint64), ('alias_counter', ctypes.c_uint64),
-                ('u_rec', _P), ('u_crec', _P), ('i_rec', _P), ('i_crec', _P)]
+                ('u_rec', _P), ('u_crec', _P), ('i_rec', _P), ('i_crec', _P),
+                ('spec_ws', _P), ('spec_ws_bytes', c_size_t), ('r_mean', c_double),
+                ('r_sd', c_double)]
 
 
 # Every symbol include/mirec.h declares: name -> (restype, argtypes)
@@ -96,6 +98,11 @@ SIGNATURES = {
     "mirec_sample_walk_segments": (c_int, [_P, c_int64, _P, _P, _P, c_int64, c_int64, c_int64,
                                            _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
                                            c_size_t, _P]),
+    "mirec_sample_walk_spec_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_double,
+                                                         c_double]),
+    "mirec_sample_walk_spec": (c_int, [_P, c_int64, _P, _P, _P, c_int64, c_int64, c_int64, _P, _P,
+                                       _P, c_int64, c_int64, c_int, c_double, c_double, _P,
+                                       c_int64, _P, _P, c_int64, _P, _P, c_size_t, _P]),
     "mirec_used_bitmap_bytes": (c_size_t, [c_int64, c_int64]),
     "mirec_alias_build": (c_int, [_P, c_int64, _P, _P]),
     "mirec_host_counting_order": (c_int, [_P, c_int64, c_int64, _P]),
@@ -160,11 +167,16 @@ SIGNATURES = {
                                         _P]),
     "mirec_adam_flush_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
+    "mirec_adam_flush_rows_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
+                                          _P, c_int32, c_double, c_double, c_double, c_double,
+                                          _P]),
     "mirec_bpr_adam_step_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, c_int64,
                                         c_int32, ctypes.c_float, ctypes.c_float, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_double,
                                         c_double, c_double, c_double, _P]),
     "mirec_step_record_ints": (c_int64, [c_int64]),
+    "mirec_chunk_group": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64] + [_P] * 16
+                          + [_P]),
     "mirec_step_records": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64, _P, _P,
                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _P]),

@@ -256,6 +256,60 @@ __global__ __launch_bounds__(kFlushRowThreads) void adam_flush_row_kernel(
   if ((threadIdx.x & 63) == 0) T.last[r] = target;
 }
 
+// Flush for sparse activity (the first steps of an epoch: most rows are in the zero
+// state, which is current at every step). One wave per row would dispatch a workgroup
+// per table row, and the dispatcher hands out ~2-3 workgroups per ns: a C2 flush of
+// 165 K one-wave blocks takes ~55 µs whatever the work. Here each wave owns R
+// consecutive rows (R per table, host's choice): lanes 0..R-1 read `last`, one ballot
+// lists the rows that lag (or, at an odd target, are current in p_alt only), and the
+// wave completes them one after another with the one-row-per-wave body above (same
+// replay engine, same results). Blocks of four waves: R = 8 makes the grid 32x smaller.
+struct FlushRows {
+  int32_t r[kMaxTables];
+};
+
+template <int D>
+__global__ __launch_bounds__(kAdamThreads) void adam_flush_scan_kernel(
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k, FlushRows rows_per_wave) {
+  using V = typename FlushVec<D>::T;
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si];
+  const int R = rows_per_wave.r[si];
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 =
+      (((int64_t)blockIdx.x - tabs.block_start[si]) * (kAdamThreads / 64) + (threadIdx.x >> 6)) * R;
+  if (r0 >= T.n_rows) return;                          // wave-uniform
+  const int target = step_base[0] + step_off;
+  const bool par = T.p_alt != nullptr;
+  const bool odd = par && (target & 1);
+  int raw = kZeroState;
+  if (lane < R && r0 + lane < T.n_rows) raw = T.last[r0 + lane];
+  const bool need = min(raw, target) < target || (odd && raw != kZeroState);
+  uint64_t todo = __ballot(need);
+  while (todo) {                                       // wave-uniform loop over its rows
+    const int i = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int64_t r = r0 + i;
+    const int rraw = __shfl(raw, i, 64);
+    const int last = min(rraw, target);
+    const int64_t off = r * 64 + lane;
+    if (last >= target) {                              // current, in p_alt only: publish
+      reinterpret_cast<V*>(T.p)[off] = reinterpret_cast<const V*>(T.p_alt)[off];
+      continue;
+    }
+    V p = reinterpret_cast<const V*>((par && (last & 1)) ? T.p_alt : T.p)[off];
+    V m = reinterpret_cast<const V*>(T.m)[off];
+    V v = reinterpret_cast<const V*>(T.v)[off];
+    replay<V, true>(p, m, v, last, target, consts, k);
+    if (odd) reinterpret_cast<V*>(T.p_alt)[off] = p;
+    reinterpret_cast<V*>(T.p)[off] = p;
+    reinterpret_cast<V*>(T.m)[off] = m;
+    reinterpret_cast<V*>(T.v)[off] = v;
+    if (lane == 0) T.last[r] = target;
+  }
+}
+
 // Flush of a width-1 table (DeepFM's first-order [V, 1] weights): one row per
 // lane; the rows of a wave lag by different step counts, so the general replay
 // (wave-uniform step loop from the wave's smallest count, lanes active from their
@@ -296,7 +350,8 @@ enum class Sched { kStreamed, kDeferred, kFlush };
 int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                 const int64_t* n_max_uniq, int32_t d, const float* consts,
                 const int32_t* step_base, int32_t step_off, double beta1, double beta2,
-                double eps, double weight_decay, void* stream, const char* what) {
+                double eps, double weight_decay, void* stream, const char* what,
+                const int32_t* flush_rows = nullptr) {
   if (n_tables < 1 || n_tables > kMaxTables || !tables || !consts || !step_base) {
     set_error("%s: bad arguments (n_tables=%d)", what, n_tables);
     return -1;
@@ -311,6 +366,24 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     return -1;
   }
   const int VPR = d / 4;
+  // flush with R rows per wave (adam_flush_scan_kernel): d >= 64, R in [1, 64] per table
+  FlushRows fr;
+  bool scan = false;
+  for (int q = 0; q < kMaxTables; ++q) fr.r[q] = 1;
+  if (sched == Sched::kFlush && flush_rows) {
+    if (d < 64) {
+      set_error("%s: rows per wave need d >= 64", what);
+      return -1;
+    }
+    for (int q = 0; q < n_tables; ++q) {
+      if (flush_rows[q] < 1 || flush_rows[q] > 64) {
+        set_error("%s: rows per wave %d of table %d not in [1, 64]", what, flush_rows[q], q);
+        return -1;
+      }
+      fr.r[q] = flush_rows[q];
+    }
+    scan = true;
+  }
   AdamTables tabs;
   memset(&tabs, 0, sizeof(tabs));
   const bool deferred = sched == Sched::kDeferred;
@@ -352,6 +425,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     } else {
       tabs.block_start[q] = blocks;
       const int64_t rows_per_block = d == 1 ? kAdamThreads
+                                     : scan ? (int64_t)(kAdamThreads / 64) * fr.r[q]
                                      : (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64
                                                                            : kAdamRows;
       blocks += (t.n_rows + rows_per_block - 1) / rows_per_block;
@@ -380,6 +454,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                                     : adam_deferred_kernel<DD, float>),                      \
                          grd, dim3(deferred_block(DD / dvec)), 0, st, tabs, consts,          \
                          step_base, step_off, k);                                            \
+    else if (DD >= 64 && scan)                                                               \
+      hipLaunchKernelGGL(adam_flush_scan_kernel<(DD >= 64 ? DD : 64)>, grd, blk, 0, st, tabs,  \
+                         consts, step_base, step_off, k, fr);                                \
     else if (DD >= 64)                                                                       \
       hipLaunchKernelGGL(adam_flush_row_kernel<(DD >= 64 ? DD : 64)>, grd,                   \
                          dim3(kFlushRowThreads), 0, st, tabs,                                \
@@ -437,6 +514,21 @@ extern "C" int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_ta
   return launch_adam(Sched::kFlush, tables, n_tables, nullptr, d, step_consts_dev,
                      step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
                      "mirec_adam_flush_f32");
+}
+
+extern "C" int mirec_adam_flush_rows_f32(const mirec_adam_table* tables, int32_t n_tables,
+                                         int32_t d, const int32_t* rows_per_wave,
+                                         const float* step_consts_dev,
+                                         const int32_t* step_base_dev, int32_t step_off,
+                                         double beta1, double beta2, double eps,
+                                         double weight_decay, void* stream) {
+  if (!rows_per_wave) {
+    set_error("mirec_adam_flush_rows_f32: rows_per_wave is NULL");
+    return -1;
+  }
+  return launch_adam(Sched::kFlush, tables, n_tables, nullptr, d, step_consts_dev,
+                     step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
+                     "mirec_adam_flush_rows_f32", rows_per_wave);
 }
 
 extern "C" int mirec_adam_sparse_grad_f32(float* p, float* m, float* v, int64_t n_rows,

@@ -157,6 +157,13 @@ static bool prep_ok(const mirec_chunk_prep* p) {
 extern "C" int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream) {
   if (!prep_ok(p)) return -1;
   const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
+  if (p->spec_ws && !p->alias_thr)        // K4s: walk + key rows, no keys launch
+    return mirec_sample_walk_spec(p->random_list, p->L, p->pr_dev, p->users + p->s0,
+                                  p->items + p->s0, p->n_batches, p->Bc, p->T, p->used_ptr,
+                                  p->used_cols, p->used_bits, p->n_bits, p->n_users, p->reject,
+                                  p->r_mean, p->r_sd, p->item_keys + p->Bc, KI, p->user_keys,
+                                  p->item_keys, KI, p->status, p->spec_ws, p->spec_ws_bytes,
+                                  stream);
   const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
   hipLaunchKernelGGL(mirec::chunk_keys_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                      p->users, p->items, p->s0, n, p->Bc, KI, p->user_keys, p->item_keys);
@@ -176,6 +183,14 @@ extern "C" int mirec_prepare_chunk_walk(const mirec_chunk_prep* p, void* stream)
 extern "C" int mirec_prepare_chunk_group(const mirec_chunk_prep* p, void* stream) {
   if (!prep_ok(p)) return -1;
   const int64_t n = p->n_batches * p->Bc, KI = (1 + p->T) * p->Bc;
+  // K36: grouping + records + look-ahead lists in one launch where the shapes allow
+  const int g = mirec_chunk_group(p->user_keys, p->item_keys, p->n_batches, p->Bc,
+                                  (int32_t)p->T, p->n_users, p->n_items, p->u_perm, p->u_uniq,
+                                  p->u_seg, p->u_nu, p->i_perm, p->i_uniq, p->i_seg, p->i_nu,
+                                  p->u_rec, p->u_crec, p->i_rec, p->i_crec, p->u_ahead,
+                                  p->u_ahead ? p->u_nah : nullptr, p->i_ahead,
+                                  p->i_ahead ? p->i_nah : nullptr, stream);
+  if (g != 0) return g < 0 ? g : 0;
   // with K35 records the look-ahead lists come from the records launch (one launch
   // after the sort instead of two)
   const bool rec = p->u_rec != nullptr;

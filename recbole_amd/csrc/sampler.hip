@@ -158,26 +158,38 @@ __device__ __forceinline__ void walk_refill(const int32_t* __restrict__ rl, int6
   }
 }
 
-__global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
-    const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
-    const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
-    int64_t num, UsedSet used, int64_t key_space, int reject, int64_t* __restrict__ out,
-    int64_t out_stride, int32_t* __restrict__ status, int32_t* __restrict__ rejA_g,
-    int32_t* __restrict__ rejB_g, const int64_t* __restrict__ seg_ptr) {
-  __shared__ int scan_lds[2][kSampThreads / 64 + 1];
-  __shared__ int32_t listA[kListLds];
-  __shared__ int32_t listB[kListLds];
-  __shared__ int32_t key_lds[kKeyLds];
-  __shared__ int32_t wl[64];
-  __shared__ int64_t pr_lds;
-  int64_t pr = pr_dev[0] % L;
-  int bad_key = 0;
-  int livelock = 0;
+// Shared memory of the single-block walk (sample_walk_kernel, and the fallback block of
+// the speculative walk below).
+struct WalkLds {
+  int scan[2][kSampThreads / 64 + 1];
+  int32_t listA[kListLds];
+  int32_t listB[kListLds];
+  int32_t key_lds[kKeyLds];
+  int32_t wl[64];
+  int64_t pr;
+  uint64_t wsum[kSampThreads / 64];
+};
 
+// Walk batches [b_begin, b_end) in order from pointer `pr` (advanced in place), every
+// thread of the block taking part. bad_key / livelock are set (block-uniform for
+// livelock) as the batches go; a livelock stops the walk.
+__device__ void walk_serial(const int32_t* __restrict__ rl, int64_t L, int64_t& pr,
+                            const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys,
+                            int64_t b_begin, int64_t n_batches, int64_t num, const UsedSet& used,
+                            int64_t key_space, int reject, int64_t* __restrict__ out,
+                            int64_t out_stride, int32_t* __restrict__ rejA_g,
+                            int32_t* __restrict__ rejB_g, const int64_t* __restrict__ seg_ptr,
+                            WalkLds& S, int& bad_key, int& livelock) {
+  auto& scan_lds = S.scan;
+  int32_t* listA = S.listA;
+  int32_t* listB = S.listB;
+  int32_t* key_lds = S.key_lds;
+  int32_t* wl = S.wl;
+  int64_t& pr_lds = S.pr;
 #ifdef MIREC_WALK_PROF
   unsigned long long tp = __builtin_amdgcn_s_memtime();
 #endif
-  for (int64_t b = 0; b < n_batches && !livelock; ++b) {
+  for (int64_t b = b_begin; b < n_batches && !livelock; ++b) {
     // batch b = one sample_by_key_ids call: fixed-size batches, or the segments
     // [seg_ptr[b], seg_ptr[b+1]) of the key list (output packed at k0 * num)
     const int64_t k0 = seg_ptr ? seg_ptr[b] : b * batch_keys;
@@ -245,7 +257,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
         const uint64_t y = __shfl_up(incl, off, 64);
         if (lane >= off) incl += y;
       }
-      __shared__ uint64_t wsum[kSampThreads / 64];
+      uint64_t* wsum = S.wsum;
       if (lane == 63) wsum[wid] = incl;
       __syncthreads();
       uint64_t before = 0, tot = 0;
@@ -309,6 +321,20 @@ __global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
     __syncthreads();                          // LDS lists / keys reused by the next batch
     WALK_MARK(2, tp);                         // refill rounds
   }
+}
+
+__global__ __launch_bounds__(kSampThreads) void sample_walk_kernel(
+    const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
+    const int64_t* __restrict__ keys, int64_t n_keys, int64_t batch_keys, int64_t n_batches,
+    int64_t num, UsedSet used, int64_t key_space, int reject, int64_t* __restrict__ out,
+    int64_t out_stride, int32_t* __restrict__ status, int32_t* __restrict__ rejA_g,
+    int32_t* __restrict__ rejB_g, const int64_t* __restrict__ seg_ptr) {
+  __shared__ WalkLds S;
+  int64_t pr = pr_dev[0] % L;
+  int bad_key = 0;
+  int livelock = 0;
+  walk_serial(rl, L, pr, keys, n_keys, batch_keys, 0, n_batches, num, used, key_space, reject,
+              out, out_stride, rejA_g, rejB_g, seg_ptr, S, bad_key, livelock);
   if (bad_key) atomicExch(status, -2);
   if (livelock && threadIdx.x == 0) atomicExch(status, -3);
   __syncthreads();
@@ -421,6 +447,216 @@ __global__ __launch_bounds__(kSampThreads) void walk_refill_kernel(
     pr_dev[0] = pr;
     if (livelock) atomicExch(status, -3);
   }
+}
+
+// ---- K4s: the walk of a chunk by speculation, exact.
+// The walk is sequential only through its pointer: batch b of a chunk starts at
+// s_b = s_0 + b * total + R_b, R_b = the refill draws of the batches before it
+// (r_b = the values batch b takes beyond its total round-0 slots). Given its start, a
+// batch's walk is a pure function of it: r_b(s_b) and its values. So every batch is
+// walked at EVERY start it can plausibly have — R in [lo_b, lo_b + W_b), a window the
+// host sizes from the sampler's rejection statistics (mirec_sample_walk_spec) — one wave
+// per (batch, candidate) in ONE chip-wide launch (walk_spec_kernel: round 0 as 64-slot
+// ballots, the refill rounds in the wave, r and the final values of the slots round 0
+// rejected kept per candidate). A second launch (walk_commit_kernel) chains the exact
+// starts (R_{b+1} = R_b + r_b(R_b), a lookup per batch) and writes each batch's values
+// from its chosen candidate. A batch whose start falls outside its window (or whose
+// candidate could not be resolved in the wave: too many round-0 rejections, or more than
+// kSpecRounds refill rounds) and every batch after it are walked by the single-block
+// walk from that exact start — so the result is the serial walk's, bit for bit, always;
+// speculation only decides how fast. Up to kSpecMaxBatches batches per launch pair.
+constexpr int kSpecMaxBatches = 16;
+constexpr int kSpecWaves = 4;            // candidates (waves) per block
+constexpr int kSpecMaxTotal = 4096;      // slots per batch (uint16 pending lists)
+constexpr int kSpecMaxKeys = 1024;       // keys per batch (LDS)
+constexpr int kSpecFinCap = 256;         // round-0 rejections a candidate may resolve
+constexpr int kSpecRounds = 64;          // refill rounds a candidate may take
+constexpr int kSpecGroup = 16;           // round-0 words with their loads in flight
+
+struct SpecPlan {
+  int32_t nb;                            // batches
+  int32_t lo[kSpecMaxBatches];           // candidates of batch b: R = lo[b] + c, c < W[b]
+  int32_t W[kSpecMaxBatches];
+  int32_t cand0[kSpecMaxBatches + 1];    // first candidate index of batch b (prefix of W)
+  int32_t xblocks;                       // blocks per XCD slice of the grid
+};
+
+// block g of the spec grid -> (batch, first candidate): batch b's blocks sit on the
+// grid positions g = b % 8 (mod 8) — one XCD under the observed round-robin placement,
+// so a batch's bitmap rows stay in one L2 (speed only)
+__device__ __forceinline__ bool spec_block(const SpecPlan& P, int g, int& b, int& c0) {
+  const int x = g & 7;
+  int m = g >> 3;
+  for (int q = x; q < P.nb; q += 8) {
+    const int nbk = (P.W[q] + kSpecWaves - 1) / kSpecWaves;
+    if (m < nbk) {
+      b = q;
+      c0 = m * kSpecWaves;
+      return true;
+    }
+    m -= nbk;
+  }
+  return false;
+}
+
+__device__ __forceinline__ int64_t wrap_pos(int64_t p, int64_t L) { return p < L ? p : p % L; }
+
+__global__ __launch_bounds__(kSpecWaves * 64) void walk_spec_kernel(
+    const int32_t* __restrict__ rl, int64_t L, const int64_t* __restrict__ pr_dev,
+    const int64_t* __restrict__ keys, int32_t Kb, int32_t num, UsedSet used, int64_t key_space,
+    int reject, SpecPlan P, int32_t* __restrict__ rtab, int32_t* __restrict__ n0tab,
+    int2* __restrict__ fin, int64_t* __restrict__ s0_out) {
+  __shared__ int32_t K[kSpecMaxKeys];
+  __shared__ uint16_t lst[kSpecWaves][kSpecMaxTotal];
+  const int64_t s0 = pr_dev[0] % L;
+  if (blockIdx.x == 0 && threadIdx.x == 0) s0_out[0] = s0;   // the commit's start
+  int b, c0;
+  if (!spec_block(P, blockIdx.x, b, c0)) return;              // block-uniform
+  const int64_t* __restrict__ bkeys = keys + (int64_t)b * Kb;
+  for (int k = threadIdx.x; k < Kb; k += kSpecWaves * 64) {
+    const int64_t key = bkeys[k];
+    K[k] = (key < 0 || key >= key_space) ? -1 : (int32_t)key;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = c0 + wave;
+  if (c >= P.W[b]) return;                                    // wave-uniform, no barrier after
+  const int cand = P.cand0[b] + c;
+  const int total = Kb * num;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int64_t s = (s0 + (int64_t)b * total + P.lo[b] + c) % L;
+  uint16_t* __restrict__ l = lst[wave];
+  // round 0: kSpecGroup 64-slot words at a time, their value and membership loads in flight
+  int n0 = 0;
+  for (int w0 = 0; w0 * 64 < total; w0 += kSpecGroup) {
+    int32_t v[kSpecGroup];
+    int32_t key[kSpecGroup];
+#pragma unroll
+    for (int i = 0; i < kSpecGroup; ++i) {
+      const int t = (w0 + i) * 64 + lane;
+      v[i] = t < total ? rl[wrap_pos(s + t, L)] : 0;
+      key[i] = t < total ? K[t % Kb] : -1;
+    }
+    int rej[kSpecGroup];
+#pragma unroll
+    for (int i = 0; i < kSpecGroup; ++i)
+      rej[i] = (reject && key[i] >= 0 && is_used(used, key[i], v[i])) ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < kSpecGroup; ++i) {
+      const uint64_t m = __ballot(rej[i]);
+      if (rej[i] && n0 + __popcll(m & lt) < kSpecMaxTotal)
+        l[n0 + __popcll(m & lt)] = (uint16_t)((w0 + i) * 64 + lane);
+      n0 += __popcll(m);
+    }
+  }
+  n0tab[cand] = n0;
+  if (n0 > kSpecFinCap) {                                     // left to the serial walk
+    if (lane == 0) rtab[cand] = -1;
+    return;
+  }
+  // refill rounds: pending slot i (ascending) takes the i-th next value
+  int2* __restrict__ F = fin + (int64_t)cand * kSpecFinCap;
+  int n = n0, nfin = 0, rounds = 0;
+  int64_t p = wrap_pos(s + total, L);
+  int64_t r = 0;
+  bool ok = true;
+  while (n > 0) {
+    if (++rounds > kSpecRounds) { ok = false; break; }
+    int nn = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      int rj = 0, acc = 0, t = 0, v = 0;
+      if (i < n) {
+        t = l[i];
+        v = rl[wrap_pos(p + i, L)];
+        rj = is_used(used, K[t % Kb], v) ? 1 : 0;
+        acc = !rj;
+      }
+      const uint64_t mr = __ballot(rj), ma = __ballot(acc);
+      if (rj) l[nn + __popcll(mr & lt)] = (uint16_t)t;        // in place: nn <= i0
+      if (acc) F[nfin + __popcll(ma & lt)] = make_int2(t, v);
+      nn += __popcll(mr);
+      nfin += __popcll(ma);
+    }
+    r += n;
+    p = wrap_pos(p + n, L);
+    n = nn;
+  }
+  if (lane == 0) rtab[cand] = ok ? (int32_t)r : -1;
+}
+
+// Chains the starts, writes every resolved batch (plus the chunk's key rows), and —
+// block nb — walks the unresolved tail serially or publishes the next start.
+__global__ __launch_bounds__(kSampThreads) void walk_commit_kernel(
+    const int32_t* __restrict__ rl, int64_t L, int64_t* __restrict__ pr_dev,
+    const int64_t* __restrict__ s0_in, const int64_t* __restrict__ users,
+    const int64_t* __restrict__ items, int32_t Kb, int32_t num, UsedSet used, int64_t key_space,
+    int reject, SpecPlan P, const int32_t* __restrict__ rtab, const int32_t* __restrict__ n0tab,
+    const int2* __restrict__ fin, int64_t* __restrict__ out, int64_t out_stride,
+    int64_t* __restrict__ ukeys_dst, int64_t* __restrict__ ikeys_dst, int64_t key_stride,
+    int32_t* __restrict__ status, int32_t* __restrict__ rejA_g, int32_t* __restrict__ rejB_g) {
+  __shared__ WalkLds S;
+  __shared__ int32_t Rs[kSpecMaxBatches + 1];
+  __shared__ int s_fail;
+  const int b = blockIdx.x;
+  const int64_t total = (int64_t)Kb * num;
+  const int64_t s0 = s0_in[0];
+  // the chunk's key rows (users; positives at the head of each item row): do not depend
+  // on the walk
+  if (b < P.nb && ukeys_dst) {
+    for (int k = threadIdx.x; k < Kb; k += kSampThreads) {
+      ukeys_dst[(int64_t)b * Kb + k] = users[(int64_t)b * Kb + k];
+      ikeys_dst[(int64_t)b * key_stride + k] = items[(int64_t)b * Kb + k];
+    }
+  }
+  if (threadIdx.x == 0) {                     // chain the starts (a lookup per batch)
+    int32_t R = 0;
+    int f = P.nb;
+    for (int q = 0; q < P.nb; ++q) {
+      const int idx = R - P.lo[q];
+      const int32_t rq = (idx >= 0 && idx < P.W[q]) ? rtab[P.cand0[q] + idx] : -1;
+      Rs[q] = R;
+      if (rq < 0) { f = q; break; }
+      R += rq;
+    }
+    if (f == P.nb) Rs[P.nb] = R;
+    s_fail = f;
+  }
+  __syncthreads();
+  const int f = s_fail;
+  if (b < P.nb) {
+    if (b >= f) return;                       // the tail block walks it
+    const int64_t sb = (s0 + (int64_t)b * total + Rs[b]) % L;
+    const int cand = P.cand0[b] + (Rs[b] - P.lo[b]);
+    int64_t* __restrict__ bout = out + (int64_t)b * out_stride;
+    int bad = 0;
+    for (int64_t t = threadIdx.x; t < total; t += kSampThreads) {
+      bout[t] = rl[wrap_pos(sb + t, L)];
+      if (reject) {
+        const int64_t key = users[(int64_t)b * Kb + t % Kb];
+        bad |= (key < 0 || key >= key_space) ? 1 : 0;
+      }
+    }
+    if (bad) atomicExch(status, -2);
+    __syncthreads();                          // round-0 values before the refilled ones
+    const int n0 = n0tab[cand];
+    const int2* __restrict__ F = fin + (int64_t)cand * kSpecFinCap;
+    for (int i = threadIdx.x; i < n0; i += kSampThreads) bout[F[i].x] = F[i].y;
+    return;
+  }
+  // block nb: the unresolved tail, or the next start
+  if (f == P.nb) {
+    if (threadIdx.x == 0) pr_dev[0] = (s0 + (int64_t)P.nb * total + Rs[P.nb]) % L;
+    return;
+  }
+  int64_t pr = (s0 + (int64_t)f * total + Rs[f]) % L;
+  int bad_key = 0, livelock = 0;
+  walk_serial(rl, L, pr, users, (int64_t)P.nb * Kb, Kb, f, P.nb, num, used, key_space, reject,
+              out, out_stride, rejA_g, rejB_g, nullptr, S, bad_key, livelock);
+  if (bad_key) atomicExch(status, -2);
+  if (livelock && threadIdx.x == 0) atomicExch(status, -3);
+  __syncthreads();
+  if (threadIdx.x == 0) pr_dev[0] = pr;
 }
 
 // bits[key, v>>5] |= 1 << (v & 31) for every used id; one wave per key.
@@ -601,6 +837,133 @@ extern "C" int mirec_sample_walk(const int32_t* random_list, int64_t L, int64_t*
                        masks, status_dev, rejA, rejB);
   }
   return launch_status("mirec_sample_walk");
+}
+
+// ---- K4s host side
+namespace {
+struct SpecShape {
+  SpecPlan P;
+  int64_t cands;
+};
+
+// Windows of a sub-chunk of nb batches: R_b in b*mean -+ (z*sd*sqrt(b) + slack). The
+// statistics only size the windows (a miss costs speed, never exactness).
+SpecShape spec_plan(int nb, double mean, double sd) {
+  SpecShape sh;
+  memset(&sh, 0, sizeof(sh));
+  sh.P.nb = nb;
+  const double z = 4.5;
+  int64_t c = 0;
+  for (int b = 0; b < nb; ++b) {
+    int64_t lo = 0, hi = 0;
+    if (b > 0 && (mean > 0.0 || sd > 0.0)) {
+      const double half = z * sd * sqrt((double)b) + 3.0;
+      lo = (int64_t)floor(b * mean - half);
+      hi = (int64_t)ceil(b * mean + half);
+      if (lo < 0) lo = 0;
+      if (hi < lo) hi = lo;
+    }
+    sh.P.lo[b] = (int32_t)lo;
+    sh.P.W[b] = (int32_t)(hi - lo + 1);
+    sh.P.cand0[b] = (int32_t)c;
+    c += hi - lo + 1;
+  }
+  sh.P.cand0[nb] = (int32_t)c;
+  int xb = 0;
+  for (int x = 0; x < 8; ++x) {
+    int m = 0;
+    for (int q = x; q < nb; q += 8) m += (sh.P.W[q] + kSpecWaves - 1) / kSpecWaves;
+    xb = std::max(xb, m);
+  }
+  sh.P.xblocks = xb;
+  sh.cands = c;
+  return sh;
+}
+}  // namespace
+
+extern "C" size_t mirec_sample_walk_spec_workspace_size(int64_t batch_keys, int64_t num,
+                                                        int64_t max_batches, double r_mean,
+                                                        double r_sd) {
+  if (batch_keys <= 0 || num <= 0 || max_batches <= 0) return 256;
+  const int nb = (int)std::min<int64_t>(max_batches, kSpecMaxBatches);
+  const int64_t cands = spec_plan(nb, r_mean, r_sd).cands;
+  // serial-walk lists | s0 | rtab | n0tab | fin
+  return mirec_sample_walk_workspace_size(batch_keys, num) + 16 + (size_t)cands * 8 +
+         (size_t)cands * kSpecFinCap * sizeof(int2) + 256;
+}
+
+extern "C" int mirec_sample_walk_spec(const int32_t* random_list, int64_t L, int64_t* pr_dev,
+                                      const int64_t* users, const int64_t* items,
+                                      int64_t n_batches, int64_t batch_keys, int64_t num,
+                                      const int64_t* used_ptr, const int32_t* used_cols,
+                                      const uint32_t* used_bits, int64_t n_bits,
+                                      int64_t n_key_space, int reject, double r_mean,
+                                      double r_sd, int64_t* out, int64_t out_stride,
+                                      int64_t* user_keys, int64_t* item_keys, int64_t key_stride,
+                                      int32_t* status_dev, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  const char* what = "mirec_sample_walk_spec";
+  if (L <= 0 || !random_list || !pr_dev || !users || !out || !status_dev || n_batches < 0 ||
+      batch_keys <= 0 || num <= 0 || !(r_mean >= 0.0) || !(r_sd >= 0.0) ||
+      (!user_keys) != (!item_keys) || (user_keys && (!items || key_stride < batch_keys))) {
+    set_error("%s: bad arguments", what);
+    return -1;
+  }
+  if (n_batches == 0) return 0;
+  if (batch_keys > kSpecMaxKeys || batch_keys * num > kSpecMaxTotal) {
+    set_error("%s: batch of %lld keys x %lld exceeds the speculative walk's %d keys / %d slots",
+              what, (long long)batch_keys, (long long)num, kSpecMaxKeys, kSpecMaxTotal);
+    return -1;
+  }
+  if (reject && ((!used_ptr || !used_cols) && !used_bits)) {
+    set_error("%s: reject=1 needs the used-id CSR or bitmap", what);
+    return -1;
+  }
+  const int nbmax = (int)std::min<int64_t>(n_batches, kSpecMaxBatches);
+  const size_t need = mirec_sample_walk_spec_workspace_size(batch_keys, num, nbmax, r_mean, r_sd);
+  if (!ws || ws_bytes < need) {
+    set_error("%s: workspace %zu < %zu", what, ws_bytes, need);
+    return -1;
+  }
+  if (out_stride == 0) out_stride = batch_keys * num;
+  UsedSet u;
+  u.ptr = used_ptr;
+  u.cols = used_cols;
+  u.bits = used_bits;
+  u.nbits = n_bits;
+  u.words = used_bits ? (n_bits + 31) / 32 : 0;
+  const int64_t total = batch_keys * num;
+  int32_t* rejA = (int32_t*)ws;
+  int32_t* rejB = rejA + total;
+  char* q = (char*)ws + mirec_sample_walk_workspace_size(batch_keys, num);
+  q = (char*)(((uintptr_t)q + 15) & ~(uintptr_t)15);
+  int64_t* s0 = (int64_t*)q;
+  q += 16;
+  hipStream_t st = (hipStream_t)stream;
+  for (int64_t b0 = 0; b0 < n_batches; b0 += kSpecMaxBatches) {
+    const int nb = (int)std::min<int64_t>(kSpecMaxBatches, n_batches - b0);
+    const SpecShape sh = spec_plan(nb, r_mean, r_sd);
+    int32_t* rtab = (int32_t*)q;
+    int32_t* n0tab = rtab + sh.cands;
+    int2* fin = (int2*)(((uintptr_t)(n0tab + sh.cands) + 15) & ~(uintptr_t)15);
+    const int64_t* ub = users + b0 * batch_keys;
+    hipLaunchKernelGGL(walk_spec_kernel, dim3((unsigned)(8 * sh.P.xblocks)),
+                       dim3(kSpecWaves * 64), 0, st, random_list, L, pr_dev, ub,
+                       (int32_t)batch_keys, (int32_t)num, u, n_key_space, reject, sh.P, rtab,
+                       n0tab, fin, s0);
+    int rc = launch_status(what);
+    if (rc) return rc;
+    hipLaunchKernelGGL(walk_commit_kernel, dim3((unsigned)(nb + 1)), dim3(kSampThreads), 0, st,
+                       random_list, L, pr_dev, s0, ub, items ? items + b0 * batch_keys : nullptr,
+                       (int32_t)batch_keys, (int32_t)num, u, n_key_space, reject, sh.P, rtab,
+                       n0tab, fin, out + b0 * out_stride, out_stride,
+                       user_keys ? user_keys + b0 * batch_keys : nullptr,
+                       item_keys ? item_keys + b0 * key_stride : nullptr, key_stride, status_dev,
+                       rejA, rejB);
+    rc = launch_status(what);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 // Vose's alias method in exact integer arithmetic: column capacity W = sum(counts),

@@ -219,6 +219,261 @@ __global__ __launch_bounds__(kPrepThreads) void step_prep_kernel(
   if (threadIdx.x == 0) task[(int64_t)kSplitCap * kTaskRec] = min(dealt, kSplitCap);
 }
 
+// ---- K36: a chunk's whole grouping side in ONE launch (replaces the K2 LDS sort launch
+// and step_prep_kernel on the C2 path). One 512-lane workgroup per (table, batch):
+//  1. the batch's user and item keys into LDS (ids clamped as the records clamp them);
+//  2. a sort of the 32-bit composites key << pbits | position (the stable sort by key IS
+//     the sort of these distinct composites): bucket counts by the key's top 12 bits in
+//     LDS, one scan, a scatter, a rank inside each bucket — no per-digit passes;
+//  3. segment heads -> uniq / seg / perm (the K2 outputs, identical to the radix sort's);
+//  4. K35 row / share records and the contribution records from LDS (step_prep_kernel's
+//     roles 1 and 2, the same share dealing in 512-slot chunks: identical records);
+//  5. the look-ahead list of the PREVIOUS batch, uniq(b) \ uniq(b-1) in ascending order,
+//     from a bitmap of batch b-1's keys (step_prep_kernel's role 0 as a membership test).
+// The radix sort's latency was set by its fixed per-pass cost (C2: user / item sorts of
+// a batch 14.7 / 20.3 us), the records launch by three dependent global load levels.
+constexpr int kGrpThreads = 512;                    // = kPrepThreads: same share dealing
+constexpr int kGrpEpt = 8;                          // composites per lane
+constexpr int kGrpMax = kGrpThreads * kGrpEpt;      // keys per (table, batch)
+constexpr int kGrpUserMax = kGrpMax / 2;            // user keys per batch (T >= 1)
+constexpr int kGrpBitmapWords = 8192;               // look-ahead bitmap: key spaces <= 2^18
+constexpr int kGrpBucketBits = 12;                  // sort buckets: the key's top 12 bits
+constexpr int kGrpBuckets = 1 << kGrpBucketBits;
+static_assert(kGrpThreads == kPrepThreads, "share dealing must match step_prep_kernel");
+
+struct GroupJob {
+  int32_t *perm, *uniq, *seg, *nu;   // K2 grouping of the table's batches
+  int32_t *rec, *crec;               // K35 records (nullptr: none)
+  int32_t *ahead, *nah;              // look-ahead lists (nullptr: none)
+  int64_t space;                     // key space (table rows)
+  int pbits;                         // bits of a position (per - 1)
+};
+
+struct GroupLds {
+  uint32_t xa[kGrpMax], xb[kGrpMax];     // xa = the sorted composites, xb = by bucket
+  int32_t hist[kGrpBuckets], bstart[kGrpBuckets];
+  int32_t uk[kGrpUserMax], ik[kGrpMax];  // the batch's keys (clamped)
+  int32_t srow[kGrpMax], sseg[kGrpMax + 1];
+  uint32_t bits[kGrpBitmapWords];
+  int scan[kGrpThreads / 64 + 1];
+};
+static_assert(sizeof(GroupLds) <= 160 * 1024, "GroupLds exceeds the gfx950 LDS");
+
+// contrib_record from the LDS copies of the keys (ids already clamped)
+__device__ __forceinline__ void contrib_record_lds(int q, int tb, int Bc, int T,
+                                                   const int32_t* uk, const int32_t* ik,
+                                                   int32_t* __restrict__ out) {
+  int kk = q, jn = -1;
+  if (tb == 1 && q >= Bc) {
+    const int r = q - Bc;
+    jn = r / Bc;
+    kk = r - jn * Bc;
+  }
+  int32_t r[kRecInts];
+  r[0] = kk;
+  r[1] = jn;
+  r[2] = uk[kk];
+  r[3] = ik[kk];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int jj = jn >= 0 ? (j == 0 ? jn : -1) : (j < T ? j : -1);
+    r[4 + j] = jj >= 0 ? ik[Bc + jj * Bc + kk] : 0;
+  }
+  reinterpret_cast<int4*>(out)[0] = make_int4(r[0], r[1], r[2], r[3]);
+  reinterpret_cast<int4*>(out)[1] = make_int4(r[4], r[5], r[6], r[7]);
+}
+
+__global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
+    const int64_t* __restrict__ ukeys, const int64_t* __restrict__ ikeys, int n_batches, int Bc,
+    int T, GroupJob U, GroupJob I) {
+  __shared__ GroupLds L;
+  const int tb = blockIdx.x >= (unsigned)n_batches;
+  const int b = tb ? blockIdx.x - n_batches : blockIdx.x;
+  const GroupJob& J = tb ? I : U;
+  const int KI = (1 + T) * Bc;
+  const int per = tb ? KI : Bc;
+  const int tid = threadIdx.x;
+  const int64_t nU = U.space, nI = I.space;
+  // 1. keys (both tables: the records need the user and the item ids of every position)
+  const int64_t* __restrict__ user = ukeys + (int64_t)b * Bc;
+  const int64_t* __restrict__ items = ikeys + (int64_t)b * KI;
+  for (int i = tid; i < Bc; i += kGrpThreads) L.uk[i] = (int32_t)clamp_id(user[i], nU);
+  for (int i = tid; i < KI; i += kGrpThreads) L.ik[i] = (int32_t)clamp_id(items[i], nI);
+  const bool ahead = J.ahead != nullptr && b > 0;   // this block lists batch b-1's look-ahead
+  if (ahead) {
+    const int words = (int)((J.space + 31) >> 5);
+    for (int w = tid; w < words; w += kGrpThreads) L.bits[w] = 0u;
+  }
+  if (J.ahead != nullptr && b == 0 && tid == 0) J.nah[n_batches - 1] = 0;   // nothing after
+  __syncthreads();
+  if (ahead) {                                      // batch b-1's keys of this table
+    const int64_t* __restrict__ prev = tb ? ikeys + (int64_t)(b - 1) * KI
+                                          : ukeys + (int64_t)(b - 1) * Bc;
+    for (int i = tid; i < per; i += kGrpThreads) {
+      const int32_t k = (int32_t)clamp_id(prev[i], J.space);
+      atomicOr(&L.bits[k >> 5], 1u << (k & 31));
+    }
+  }
+  // 2. sort of the composites key << pbits | position (distinct values: stability comes
+  //    free). Bucket by the key's top bits (<= 4,096 buckets, LDS counters: atomics give
+  //    each element a slot in its bucket in any order), scan the counts, scatter, then
+  //    rank each element inside its bucket (its rank = the bucket's smaller composites;
+  //    a bucket holds one or a few keys — a Zipf head key's many positions among them).
+  const int pbits = J.pbits;
+  const int32_t* keys = tb ? L.ik : L.uk;
+  int kbits = 0;
+  while (kbits < 31 && ((int64_t)1 << kbits) < J.space) ++kbits;
+  const int shift = kbits > kGrpBucketBits ? kbits - kGrpBucketBits : 0;
+  const int nbk = (int)(((J.space - 1) >> shift) + 1);
+  for (int q = tid; q < nbk; q += kGrpThreads) L.hist[q] = 0;
+  __syncthreads();
+  uint32_t x[kGrpEpt];
+  int slot_in[kGrpEpt];
+#pragma unroll
+  for (int r = 0; r < kGrpEpt; ++r) {
+    const int e = tid + r * kGrpThreads;
+    x[r] = 0u;
+    slot_in[r] = 0;
+    if (e < per) {
+      x[r] = ((uint32_t)keys[e] << pbits) | (uint32_t)e;
+      slot_in[r] = atomicAdd(&L.hist[keys[e] >> shift], 1);
+    }
+  }
+  __syncthreads();
+  {                                               // exclusive scan of the bucket counts
+    constexpr int kPer = kGrpBuckets / kGrpThreads;
+    int c[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = tid * kPer + j;
+      c[j] = q < nbk ? L.hist[q] : 0;
+      sum += c[j];
+    }
+    int tot;
+    int run = block_exclusive_scan(sum, L.scan, &tot);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = tid * kPer + j;
+      if (q < nbk) L.bstart[q] = run;
+      run += c[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kGrpEpt; ++r) {
+    const int e = tid + r * kGrpThreads;
+    if (e < per) L.xb[L.bstart[keys[e] >> shift] + slot_in[r]] = x[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kGrpEpt; ++r) {
+    const int e = tid + r * kGrpThreads;
+    if (e < per) {
+      const int bk = keys[e] >> shift;
+      const int b0 = L.bstart[bk], n = L.hist[bk];
+      int rank = 0;
+      for (int f = 0; f < n; ++f) rank += L.xb[b0 + f] < x[r] ? 1 : 0;
+      L.xa[b0 + rank] = x[r];
+    }
+  }
+  __syncthreads();
+  // 3. segments: heads of equal-key runs, uniq / seg / perm
+  const uint32_t* S = L.xa;
+  int32_t* __restrict__ perm = J.perm + (int64_t)b * per;
+  int32_t* __restrict__ uniq = J.uniq + (int64_t)b * per;
+  int32_t* __restrict__ seg = J.seg + (int64_t)b * (per + 1);
+  int hm = 0, cnt = 0;
+#pragma unroll
+  for (int r = 0; r < kGrpEpt; ++r) {
+    const int e = kGrpEpt * tid + r;
+    if (e < per) {
+      const uint32_t k = S[e] >> pbits;
+      const int h = (e == 0 || (S[e - 1] >> pbits) != k) ? 1 : 0;
+      hm |= h << r;
+      cnt += h;
+      perm[e] = (int32_t)(S[e] & ((1u << pbits) - 1u));
+    }
+  }
+  int nu;
+  int slot = block_exclusive_scan(cnt, L.scan, &nu);
+#pragma unroll
+  for (int r = 0; r < kGrpEpt; ++r) {
+    if ((hm >> r) & 1) {
+      const int e = kGrpEpt * tid + r;
+      const int32_t k = (int32_t)(S[e] >> pbits);
+      L.srow[slot] = k;
+      L.sseg[slot] = e;
+      uniq[slot] = k;
+      seg[slot] = e;
+      ++slot;
+    }
+  }
+  if (tid == 0) {
+    L.sseg[nu] = per;
+    seg[nu] = per;
+    J.nu[b] = nu;
+  }
+  __syncthreads();
+  // 4. K35 records (step_prep_kernel roles 1 and 2, from LDS)
+  if (J.rec != nullptr) {
+    int32_t* __restrict__ rec = J.rec + (int64_t)b * rec_ints(per);
+    int32_t* __restrict__ task = rec + (int64_t)per * kRowRec;
+    const uint32_t pm = (1u << pbits) - 1u;
+    int dealt = 0;
+    for (int x0 = 0; x0 < nu; x0 += kGrpThreads) {
+      const int xs = x0 + tid;
+      int i0 = 0, nc = 0, row = 0;
+      if (xs < nu) {
+        i0 = L.sseg[xs];
+        nc = L.sseg[xs + 1] - i0;
+        row = L.srow[xs];
+      }
+      const int want = nc > kShare ? (nc + kShare - 1) / kShare - 1 : 0;
+      int total;
+      const int base = dealt + block_exclusive_scan(want, L.scan, &total);
+      dealt += total;
+      if (xs >= nu) continue;
+      const int got = max(0, min(want, kSplitCap - base));
+      const int nsh = 1 + got;
+      int32_t* r = rec + (int64_t)xs * kRowRec;
+      reinterpret_cast<int4*>(r)[0] = make_int4(row, i0, nc, nsh);
+      for (int c = 0; c < kRecInline && c < nc; ++c)
+        contrib_record_lds((int)(S[i0 + c] & pm), tb, Bc, T, L.uk, L.ik, r + 4 + c * kRecInts);
+      for (int jj = 1; jj <= got; ++jj) {
+        int32_t* tr = task + (int64_t)(base + jj - 1) * kTaskRec;
+        reinterpret_cast<int4*>(tr)[0] = make_int4(xs, jj, i0, nc);
+        reinterpret_cast<int4*>(tr)[1] = make_int4(row, nsh, 0, 0);
+        for (int c = 0; c < kShare && jj * kShare + c < nc; ++c)
+          contrib_record_lds((int)(S[i0 + jj * kShare + c] & pm), tb, Bc, T, L.uk, L.ik,
+                             tr + 8 + c * kRecInts);
+      }
+    }
+    if (tid == 0) task[(int64_t)kSplitCap * kTaskRec] = min(dealt, kSplitCap);
+    int32_t* __restrict__ crec = J.crec + (int64_t)b * per * kRecInts;
+    for (int e = tid; e < per; e += kGrpThreads)
+      contrib_record_lds((int)(S[e] & pm), tb, Bc, T, L.uk, L.ik, crec + (int64_t)e * kRecInts);
+  }
+  // 5. look-ahead list of batch b-1: this batch's rows that batch b-1 does not touch
+  if (ahead) {
+    int32_t* __restrict__ out = J.ahead + (int64_t)(b - 1) * per;
+    int base = 0;
+    for (int x0 = 0; x0 < nu; x0 += kGrpThreads) {
+      const int xs = x0 + tid;
+      int f = 0;
+      int32_t k = 0;
+      if (xs < nu) {
+        k = L.srow[xs];
+        f = ((L.bits[k >> 5] >> (k & 31)) & 1u) ? 0 : 1;
+      }
+      int tot;
+      const int ex = block_exclusive_scan(f, L.scan, &tot);
+      if (f) out[base + ex] = k;
+      base += tot;
+    }
+    if (tid == 0) J.nah[b - 1] = base;
+  }
+}
+
 // Hand-off of a split row's contribution vectors between the blocks of one launch
 // (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off form: write-through
 // agent-scope stores, every storing wave drained before one lane's agent-scope add, the
@@ -555,6 +810,49 @@ extern "C" int mirec_step_records(const int64_t* user_keys, const int64_t* item_
 }
 
 extern "C" int64_t mirec_step_record_ints(int64_t per) { return per < 0 ? -1 : rec_ints(per); }
+
+namespace mirec {
+static int bits_for(int64_t n) {        // bits of n - 1 (n >= 1)
+  int b = 0;
+  while (b < 40 && ((int64_t)1 << b) < n) ++b;
+  return b;
+}
+}  // namespace mirec
+
+// K36 on a prepared chunk (include/mirec.h): 1 = done, 0 = shapes outside the one-
+// workgroup form (the caller runs the K2 sort + mirec_step_records), < 0 = error.
+extern "C" int mirec_chunk_group(const int64_t* user_keys, const int64_t* item_keys,
+                                 int64_t n_batches, int64_t Bc, int32_t T, int64_t n_users,
+                                 int64_t n_items, int32_t* u_perm, int32_t* u_uniq,
+                                 int32_t* u_seg, int32_t* u_nu, int32_t* i_perm,
+                                 int32_t* i_uniq, int32_t* i_seg, int32_t* i_nu,
+                                 int32_t* u_rec, int32_t* u_crec, int32_t* i_rec,
+                                 int32_t* i_crec, int32_t* u_ahead, int32_t* u_nah,
+                                 int32_t* i_ahead, int32_t* i_nah, void* stream) {
+  if (n_batches < 0 || n_batches > 32767 || Bc < 0 || T < 1 || n_users <= 0 || n_items <= 0 ||
+      !user_keys || !item_keys || !u_perm || !u_uniq || !u_seg || !u_nu || !i_perm || !i_uniq ||
+      !i_seg || !i_nu || !u_rec != !u_crec || !u_rec != !i_rec || !i_rec != !i_crec ||
+      !u_ahead != !u_nah || !u_ahead != !i_ahead || !i_ahead != !i_nah) {
+    set_error("mirec_chunk_group: bad arguments");
+    return -1;
+  }
+  if (n_batches == 0 || Bc == 0) return 1;
+  const int64_t KI = (int64_t)(1 + T) * Bc;
+  const int pu = bits_for(Bc), pi = bits_for(KI);
+  const bool ahead = u_ahead != nullptr;
+  if (Bc > kGrpUserMax || KI > kGrpMax || bits_for(n_users) + pu > 32 ||
+      bits_for(n_items) + pi > 32 ||
+      (ahead && (n_users > 32 * (int64_t)kGrpBitmapWords ||
+                 n_items > 32 * (int64_t)kGrpBitmapWords)))
+    return 0;
+  GroupJob U = {u_perm, u_uniq, u_seg, u_nu, u_rec, u_crec, u_ahead, u_nah, n_users, pu};
+  GroupJob I = {i_perm, i_uniq, i_seg, i_nu, i_rec, i_crec, i_ahead, i_nah, n_items, pi};
+  hipLaunchKernelGGL(chunk_group_kernel, dim3((unsigned)(2 * n_batches)), dim3(kGrpThreads), 0,
+                     (hipStream_t)stream, user_keys, item_keys, (int)n_batches, (int)Bc, T, U, I);
+  const int rc = launch_status("mirec_chunk_group");
+  return rc ? rc : 1;
+}
+
 
 extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
                                        const int64_t* n_max_uniq, int32_t d,

@@ -95,6 +95,38 @@ def sample_walk(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Ten
     return out
 
 
+def sample_walk_spec(random_list: torch.Tensor, pr_dev: torch.Tensor, users: torch.Tensor,
+                     batch_keys: int, n_batches: int, num: int, used_ptr, used_cols,
+                     n_key_space: int, reject: bool, r_mean: float, r_sd: float,
+                     out: torch.Tensor | None = None, out_stride: int = 0, status=None,
+                     used_bits=None, n_bits: int = 0, items=None, user_keys=None,
+                     item_keys=None, key_stride: int = 0) -> torch.Tensor:
+    """K4s (mirec_sample_walk_spec): the walk of n_batches batches of batch_keys keys
+    (users[b*batch_keys:]) by speculation — the same values, pointer and status as
+    sample_walk, bit for bit; r_mean / r_sd size the windows (Sampler.walk_stats)."""
+    _dev(random_list, torch.int32, "random_list")
+    _dev(pr_dev, torch.int64, "pr_dev")
+    _dev(users, torch.int64, "users")
+    dev = users.device
+    if out is None:
+        out = torch.empty(n_batches * batch_keys * num, dtype=torch.int64, device=dev)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+    bits = reject and used_bits is not None
+    wsz = lib().mirec_sample_walk_spec_workspace_size(batch_keys, num, min(n_batches, 16),
+                                                      r_mean, r_sd)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    rc = lib().mirec_sample_walk_spec(
+        ptr(random_list), random_list.numel(), ptr(pr_dev), ptr(users), ptr(items), n_batches,
+        batch_keys, num, ptr(used_ptr) if reject and not bits else None,
+        ptr(used_cols) if reject and not bits else None, ptr(used_bits) if bits else None,
+        n_bits if bits else 0, n_key_space, 1 if reject else 0, float(r_mean), float(r_sd),
+        ptr(out), out_stride, ptr(user_keys), ptr(item_keys), key_stride, ptr(status), ptr(ws),
+        ws.numel(), stream_handle())
+    check(rc, "mirec_sample_walk_spec")
+    return out
+
+
 def sample_walk_segments(random_list: torch.Tensor, pr_dev: torch.Tensor, keys: torch.Tensor,
                          seg_ptr: torch.Tensor, max_seg_keys: int, num: int,
                          used_ptr: torch.Tensor | None, used_cols: torch.Tensor | None,
@@ -629,16 +661,18 @@ def adam_tables(specs):
 
 
 def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_users: int,
-                 n_items: int, gu, gi):
+                 n_items: int, gu, gi, out=None):
     """K35 records (mirec_step_records) of n_batches batches from their K2 groupings
     gu / gi (Segments or any object with perm, uniq, seg, n_uniq; per-batch strides Bc
-    and (1+T)*Bc): (u_rec, u_crec, i_rec, i_crec) int32 device tensors."""
+    and (1+T)*Bc): (u_rec, u_crec, i_rec, i_crec) int32 device tensors (`out`: the
+    caller's four buffers)."""
     for n_, t_ in (("user_keys", user_keys), ("item_keys", item_keys)):
         _dev(t_, torch.int64, n_)
     dev = user_keys.device
     KI = (1 + times) * Bc
-    out = [torch.empty(n_batches * n, dtype=torch.int32, device=dev)
-           for n in (step_record_ints(Bc), Bc * 8, step_record_ints(KI), KI * 8)]
+    if out is None:
+        out = [torch.empty(n_batches * n, dtype=torch.int32, device=dev)
+               for n in (step_record_ints(Bc), Bc * 8, step_record_ints(KI), KI * 8)]
     rc = lib().mirec_step_records(ptr(user_keys), ptr(item_keys), n_batches, Bc, times, n_users,
                                   n_items, ptr(gu.perm), ptr(gu.uniq), ptr(gu.seg),
                                   ptr(gu.n_uniq), ptr(gi.perm), ptr(gi.uniq), ptr(gi.seg),
@@ -646,6 +680,28 @@ def step_records(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_us
                                   stream_handle())
     check(rc, "mirec_step_records")
     return out
+
+
+def chunk_group(user_keys, item_keys, n_batches: int, Bc: int, times: int, n_users: int,
+                n_items: int, outs: dict, records: bool = True, ahead: bool = True):
+    """K36 (mirec_chunk_group): the groupings, K35 records and look-ahead lists of a
+    chunk in one launch, into the int32 device tensors of `outs` (keys u_perm, u_uniq,
+    u_seg, u_nu, i_perm, i_uniq, i_seg, i_nu, and u_rec, u_crec, i_rec, i_crec /
+    u_ahead, u_nah, i_ahead, i_nah when asked for). Returns False (nothing launched)
+    when the shapes are outside its one-workgroup form."""
+    for n_, t_ in (("user_keys", user_keys), ("item_keys", item_keys)):
+        _dev(t_, torch.int64, n_)
+    names = ["u_perm", "u_uniq", "u_seg", "u_nu", "i_perm", "i_uniq", "i_seg", "i_nu"]
+    rec = ["u_rec", "u_crec", "i_rec", "i_crec"]
+    ah = ["u_ahead", "u_nah", "i_ahead", "i_nah"]
+    args = [ptr(outs[k]) for k in names]
+    args += [ptr(outs[k]) for k in rec] if records else [None] * 4
+    args += [ptr(outs[k]) for k in ah] if ahead else [None] * 4
+    rc = lib().mirec_chunk_group(ptr(user_keys), ptr(item_keys), n_batches, Bc, times, n_users,
+                                 n_items, *args, stream_handle())
+    if rc < 0:
+        check(rc, "mirec_chunk_group")
+    return rc == 1
 
 
 def step_record_ints(per: int) -> int:
@@ -688,9 +744,11 @@ def bpr_adam_step(tables, n_max_uniq, d: int, items, Bc: int, times: int, grad_s
 
 def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
                schedule: str = "streamed", n_max_uniq=None, beta1=0.9, beta2=0.999, eps=1e-8,
-               weight_decay=0.0):
+               weight_decay=0.0, flush_rows=None):
     """K5 over several tables in one launch: schedule 'streamed' (every row),
-    'deferred' (touched rows, replaying skipped zero-gradient steps) or 'flush'."""
+    'deferred' (touched rows, replaying skipped zero-gradient steps) or 'flush'
+    (flush_rows: rows per wave per table, mirec_adam_flush_rows_f32; None = one wave
+    per row)."""
     import ctypes
     _dev(step_consts, torch.float32, "step_consts")
     _dev(step_base, torch.int32, "step_base")
@@ -701,6 +759,9 @@ def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
     elif schedule == "deferred":
         nm = (ctypes.c_int64 * len(tables))(*n_max_uniq)
         rc = lib().mirec_adam_deferred_f32(tables, len(tables), nm, d, *args)
+    elif schedule == "flush" and flush_rows is not None:
+        rpw = (ctypes.c_int32 * len(tables))(*flush_rows)
+        rc = lib().mirec_adam_flush_rows_f32(tables, len(tables), d, rpw, *args)
     elif schedule == "flush":
         rc = lib().mirec_adam_flush_f32(tables, len(tables), d, *args)
     else:

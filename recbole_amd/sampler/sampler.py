@@ -220,6 +220,42 @@ class AbstractSampler(object):
         bits, n_bits = self._used_bits()
         return self._rl_dev, self._pr_dev, up, uc, bits, n_bits, up is not None, self._status
 
+    def walk_stats(self, key_counts, batch_keys, num):
+        """(mean, sd) of the refill draws one walk batch of `batch_keys` keys x `num`
+        takes beyond its round-0 slots, when its keys are drawn like `key_counts` (host
+        per-key weights, e.g. the train users' interaction counts): a key u rejects a
+        draw with p_u = (occurrences in random_list of u's used ids) / L, so a slot takes
+        Geometric(1 - p_u) - 1 extra draws (mean p/(1-p), variance p/(1-p)^2) and the
+        num slots of a key share its p_u. Sizes the speculative walk's windows
+        (mirec_sample_walk_spec) — a statistic, never a parity assumption."""
+        key = (self.phase, int(batch_keys), int(num))
+        cache = self.__dict__.setdefault('_walk_stats', {})
+        if key in cache:
+            return cache[key]
+        try:
+            reject = self._used_dev()[0] is not None       # RepeatableSampler: no rejection
+        except ValueError:                                  # no phase set
+            reject = False
+        if not reject or self.random_list_length == 0:
+            cache[key] = (0.0, 0.0)
+            return cache[key]
+        ptr, cols = self.used_csr[self.phase]
+        rl = np.asarray(self.random_list, dtype=np.int64)
+        mult = np.bincount(rl, minlength=int(max(self.n_items, rl.max() + 1 if len(rl) else 1)))
+        cs = np.concatenate([[0], np.cumsum(mult[np.asarray(cols, dtype=np.int64)])])
+        ptr = np.asarray(ptr, dtype=np.int64)
+        p = np.minimum((cs[ptr[1:]] - cs[ptr[:-1]]) / float(len(rl)), 0.999)
+        w = np.asarray(key_counts, dtype=np.float64)[:len(p)]
+        w = np.pad(w, (0, len(p) - len(w)))
+        w = w / max(w.sum(), 1.0)
+        q = p / (1.0 - p)
+        eq, eq2 = float((w * q).sum()), float((w * q / (1.0 - p)).sum())
+        var_q = max(float((w * q * q).sum()) - eq * eq, 0.0)
+        mean = batch_keys * num * eq
+        var = batch_keys * num * eq2 + batch_keys * num * num * var_q
+        cache[key] = (mean, float(np.sqrt(var)))
+        return cache[key]
+
     def launch_segments(self, keys_dev, seg_ptr_dev, max_seg_keys, num):
         """Successive sample_by_key_ids calls (call s over keys_dev[seg_ptr[s]:
         seg_ptr[s+1]]) in ONE launch, the walk continuing from call to call; call

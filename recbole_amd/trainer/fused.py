@@ -42,6 +42,7 @@ from __future__ import annotations
 import ctypes
 import logging
 import math
+import os
 
 import numpy as np
 import torch
@@ -286,7 +287,9 @@ class FusedBPRTrainStep(object):
         when the next chunk would take the count past 1.5 x FLUSH_EVERY (the ramp's
         4 + 8 + 16 + 32 steps flush before the first 64-step chunk instead of after it),
         and before a ragged batch / the end; a chunk after one that did not flush starts
-        with an entry catch-up of the rows its first batch reads."""
+        with an entry catch-up of the rows its first batch reads. `flush` is False or
+        the flush's rows per wave per table (_flush_rows: a tuple, part of the chunk
+        graph's key)."""
         flags, since = [], 0
         at = getattr(self, '_flush_at', set())
         for i, (b0, nb, Bc) in enumerate(plan):
@@ -298,8 +301,30 @@ class FusedBPRTrainStep(object):
                      or not nxt_full or b0 + nb in at)
             if flush:
                 since = 0
-            flags.append((entry, flush))
+            flags.append((entry, self._flush_rows(b0 + nb) if flush else False))
         return flags
+
+    # a flush of a table whose rows are mostly current (zero state) runs R rows per wave
+    # (mirec_adam_flush_rows_f32) when about one row per R would lag
+    FLUSH_SPARSE_MAX_ROWS = 8
+
+    def _flush_rows(self, b_end):
+        """Rows per wave of the flush after global batch b_end - 1, per table: an upper
+        bound on the rows that can lag = the rows outside the zero state at the epoch
+        start + every row the steps since then touched (B users, (1+T)B item slots per
+        step); R = the largest power of two <= FLUSH_SPARSE_MAX_ROWS with R x that
+        fraction <= 1 (one wave per row, R = 1, where most rows lag)."""
+        if self.adam_mode != 'deferred' or self.d < 64:
+            return (1, 1)
+        out = []
+        for q, per in enumerate((self.Bg, (1 + self.times) * self.Bg)):
+            n_rows, busy0 = self._tables[q].n_rows, self._busy0[q]   # (a shard when sharded)
+            frac = min(1.0, (busy0 + b_end * per) / max(n_rows, 1))
+            r = 1
+            while r * 2 <= self.FLUSH_SPARSE_MAX_ROWS and r * 2 * frac <= 1.0:
+                r *= 2
+            out.append(r)
+        return tuple(out)
 
     def _sharded(self, Bc):
         return self.G > 1 and Bc == self.Bg
@@ -407,8 +432,33 @@ class FusedBPRTrainStep(object):
                 setattr(cp, f'{tag}_nah', getattr(slot, f'{tag}_nah').data_ptr())
         if slot.records is not None:
             cp.u_rec, cp.u_crec, cp.i_rec, cp.i_crec = (r.data_ptr() for r in slot.records)
+        spec = self._spec_ws()
+        if spec is not None:                        # K4s: the speculative walk
+            cp.spec_ws, cp.spec_ws_bytes = spec.data_ptr(), spec.numel()
+            cp.r_mean, cp.r_sd = self._spec_stats
         slot.prep = cp
         return cp
+
+    # K4s (mirec_sample_walk_spec): the chunk's walk by speculation (exact; two launches
+    # per 16 batches instead of a serial walk of ~10 us per batch)
+    SPEC_WALK = os.environ.get('MIREC_SPEC_WALK', '1') != '0'
+
+    def _spec_ws(self):
+        """Workspace of the speculative walk (shared by the slots: the walks run in
+        order on the walk stream), or None where it does not apply."""
+        if not self.SPEC_WALK or self.data.sampler.alias is not None:
+            return None
+        T, Bc = self.times, self.Bg
+        if Bc > 1024 or Bc * T > 4096:
+            return None
+        ws = getattr(self, '_spec_buf', None)
+        if ws is None:
+            counts = np.bincount(self._users.cpu().numpy(), minlength=self.nU)
+            self._spec_stats = self.data.sampler.walk_stats(counts, Bc, T)
+            n = lib().mirec_sample_walk_spec_workspace_size(Bc, T, min(self.C, 16),
+                                                            *self._spec_stats)
+            ws = self._spec_buf = torch.empty(n, dtype=torch.uint8, device=self.device)
+        return ws
 
     # ------------------------------------------------------------------ model side
     def _rec_ints(self, Bc):
@@ -570,15 +620,25 @@ class FusedBPRTrainStep(object):
                                       self.ticket.data_ptr(), stream.cuda_stream)
         check(rc, 'mirec_chunk_finish')
 
-    def _flush(self, stream):
-        """Deferred schedule: bring every row to step_idx applied steps."""
+    def _flush(self, stream, rows=None):
+        """Deferred schedule: bring every row to step_idx applied steps. rows: rows per
+        wave per table (_flush_rows), or None / all ones for one wave per row."""
         if self.adam_mode != 'deferred':
             return
+        if rows is not None and any(r > 1 for r in rows):
+            rpw = (ctypes.c_int32 * 2)(*rows)
 
-        def flush():
-            check(lib().mirec_adam_flush_f32(self._tables, 2, self.d, self.consts.data_ptr(),
-                                             self.step_idx.data_ptr(), 0, *self._adam_args,
-                                             stream.cuda_stream), 'mirec_adam_flush_f32')
+            def flush():
+                check(lib().mirec_adam_flush_rows_f32(self._tables, 2, self.d, rpw,
+                                                      self.consts.data_ptr(),
+                                                      self.step_idx.data_ptr(), 0,
+                                                      *self._adam_args, stream.cuda_stream),
+                      'mirec_adam_flush_rows_f32')
+        else:
+            def flush():
+                check(lib().mirec_adam_flush_f32(self._tables, 2, self.d, self.consts.data_ptr(),
+                                                 self.step_idx.data_ptr(), 0, *self._adam_args,
+                                                 stream.cuda_stream), 'mirec_adam_flush_f32')
         self._record('flush', stream, flush)
 
     def _entry_lists(self, slot):
@@ -632,7 +692,7 @@ class FusedBPRTrainStep(object):
                     self._step(slot, c, self.Bg, cap, c, c + 1 < nb)
                 self._finish(0, nb, self.Bg, cap)
                 if flush:
-                    self._flush(cap)
+                    self._flush(cap, flush)
             torch.cuda.current_stream(self.device).wait_stream(cap)
             slot.graphs[key] = g
         return g
@@ -680,9 +740,15 @@ class FusedBPRTrainStep(object):
         self.consts[:table.size].copy_(torch.from_numpy(table))
         self.loss_hist.zero_()
         self.step_idx.zero_()
+        self._busy0 = [t.n_rows for t in self._tables]   # rows that may lag (flush rows per wave)
+        self._batches_enqueued = 0
         if self.adam_mode == 'deferred':       # rows are all flushed: epoch-relative counts
+            busy = []
             for m, v, last in self._adam_state():   # zero-state rows: marked (adam.hip)
                 ops.zero_state_marks(m, v, last, self._adam_args[3])
+                busy.append((last != ops.ADAM_ZERO_STATE).sum())
+            # one host read per epoch (outside any timed step)
+            self._busy0 = [int(x) for x in torch.stack(busy).cpu()]
         if self.fused_step:                    # parity buffers: state 0 (and every
             self.pU_alt.copy_(self.pU.data)    # zero-state row) valid in both
             self.pI_alt.copy_(self.pI.data)
@@ -787,10 +853,11 @@ class FusedBPRTrainStep(object):
                     self._finish(c, 1, Bc, stream)
                 self._current = False
                 if c1 == nb and flush:
-                    self._flush(stream)
+                    self._flush(stream, flush)
                     self._current = True
             self._issue_groups(k + len(self.slots))   # later chunks' groupings, behind
             b = b0 + c1
+            self._batches_enqueued = b
 
     def _top_up_prep(self, k):
         """Prepare chunks up to k + SLOTS - 1 (their slots are free once the chunks
@@ -813,7 +880,8 @@ class FusedBPRTrainStep(object):
         """Make the parameters current (deferred schedule: flush every row, unless
         the last enqueued work was a chunk's closing flush)."""
         if not self._current:
-            self._flush(torch.cuda.current_stream(self.device))
+            self._flush(torch.cuda.current_stream(self.device),
+                        self._flush_rows(self._batches_enqueued))
             self._current = True
 
     def end_epoch(self, n_done=None):

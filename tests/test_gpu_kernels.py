@@ -452,6 +452,48 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide, marks):
             assert torch.equal(a, b), (a - b).abs().max()
 
 
+@pytest.mark.parametrize('d', [64, 128, 256])
+@pytest.mark.parametrize('rows', [(8, 1), (2, 64), (5, 3)])
+@pytest.mark.parametrize('target', [24, 25])        # even / odd: parity-buffer publishing
+def test_adam_flush_rows_equals_flush(dev, d, rows, target):
+    """mirec_adam_flush_rows_f32 (R rows per wave) leaves every buffer bit-identical to
+    the one-wave-per-row flush: rows in the zero state, rows current at the target
+    (held in p_alt at an odd target), rows lagging by 1..target steps with their state
+    in either parity buffer, and table sizes that are not multiples of 4R."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(d + target)
+    sizes = (1037, 301)
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(1))], lr=1e-2)
+    consts = torch.from_numpy(opt.step_constants(1, 64).reshape(-1)).to(dev)
+    base = torch.full((1,), target, dtype=torch.int32, device=dev)
+    state = []
+    for n in sizes:
+        P = torch.randn(n, d, generator=g) * 0.1
+        A = torch.randn(n, d, generator=g) * 0.1
+        M = torch.randn(n, d, generator=g) * 1e-3
+        V = torch.rand(n, d, generator=g) * 1e-6
+        last = torch.randint(0, target + 1, (n,), generator=g, dtype=torch.int32)
+        kind = torch.randint(0, 4, (n,), generator=g)
+        last[kind == 0] = ops.ADAM_ZERO_STATE           # zero state: identical buffers
+        zs = kind == 0
+        M[zs] = 0
+        V[zs] = 0
+        A[zs] = P[zs]
+        last[kind == 1] = target                         # current
+        state.append((P, A, M, V, last))
+
+    def run(flush_rows):
+        bufs = [[x.clone().to(dev) for x in st] for st in state]
+        tabs = ops.adam_tables([dict(p=P, p_alt=A, m=M, v=V, last=L) for P, A, M, V, L in bufs])
+        ops.adam_multi(tabs, d, consts, base, 0, 'flush', flush_rows=flush_rows)
+        return [x.cpu() for b in bufs for x in b]
+
+    ref, got = run(None), run(rows)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+
+
 @pytest.mark.parametrize('lr', [1e-3, 3e-2])
 @pytest.mark.parametrize('wide', [False, True])
 def test_adam_deferred_long_idle_rows_bitwise(dev, lr, wide):
