@@ -49,6 +49,7 @@ struct StepLaunch {
                                // slot at join_ahead (zero between launches)
   int64_t join_ahead[2];
   int64_t block_start[7];      // segments: shares U, I, look-ahead U, I, touched U, I, end
+  int32_t seg_rows[6];         // rows each segment is sized for (the buffers' bound)
 };
 
 // rows of one contribution of the positive k: u = EU[user[k]], p = EI[items[k]],
@@ -74,7 +75,8 @@ __device__ unsigned long long g_step_stamps[kStampBlocks * 4];
     unsigned long long t_;                                                                 \
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");           \
     __builtin_amdgcn_sched_barrier(0);                                                     \
-    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) g_step_stamps[blockIdx.x * 4 + (slot)] = t_; \
+    const int sb_ = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);              \
+    if ((threadIdx.x & 63) == 0 && sb_ < kStampBlocks) g_step_stamps[sb_ * 4 + (slot)] = t_; \
   } while (0)
 #else
 #define MIREC_STAMP(slot) \
@@ -501,19 +503,49 @@ template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
 template <typename V> struct AheadVec { using T = float; };
 
+// Rows per workgroup: a row of D <= 128 is one wave, and RPB of them share a workgroup
+// (each wave works alone: wave-level synchronisation only), so the dispatcher hands out
+// RPB times fewer workgroups (it deals ~2-3 per ns: ~10 K one-row workgroups were ~3 us
+// of a launch). D = 256 rows span two waves: one row per workgroup.
+#ifndef MIREC_STEP_RPB
+#define MIREC_STEP_RPB 4
+#endif
+template <int D> struct StepRows { static constexpr int n = D <= 128 ? MIREC_STEP_RPB : 1; };
+#ifndef MIREC_STEP_WAVES
+#define MIREC_STEP_WAVES 6               // waves per SIMD the register budget allows
+#endif
+
 template <int D>
-__global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_adam_step_kernel(
+__global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n * StepRows<D>::n,
+                             MIREC_STEP_WAVES)
+void bpr_adam_step_kernel(
     const StepLaunch L, const int64_t* __restrict__ items, int Bc, int T, float gamma,
     float grad_scale, float* __restrict__ loss_k, const float* __restrict__ consts,
     const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
   using V = typename StepVec<D>::T;
   constexpr int EPT = Lanes<V>::n;         // elements per thread
-  constexpr int TPB = D / EPT;             // threads per block (one row)
+  constexpr int TPB = D / EPT;             // threads per row
+  constexpr int RPB = StepRows<D>::n;      // rows per workgroup
+  static_assert(RPB == 1 || TPB == 64, "several rows per workgroup need one wave per row");
   constexpr int LPR = D / 4;               // lanes per contribution (float4 each, K3's layout)
-  constexpr int NG = TPB / LPR;            // contributions in flight per block
-  constexpr int kAheadHalves = EPT;        // look-ahead blocks per row (one element per thread)
-  __shared__ float cont[NG][D];
-  __shared__ int s_last;
+  constexpr int NG = TPB / LPR;            // contributions in flight per row
+  constexpr int kAheadHalves = EPT;        // look-ahead rows per table row (one element per thread)
+  __shared__ float cont_all[RPB][NG][D];
+  __shared__ int s_last_all[RPB];
+  // the row of this wave: wave-uniform, so the row's indices stay in scalar registers
+  const int wv = RPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / TPB)) : 0;
+  auto& cont = cont_all[wv];
+  int& s_last = s_last_all[wv];
+  // the row's threads in step: a workgroup barrier for a two-wave row, else the wave
+  auto row_sync = [&]() {
+    if (RPB == 1) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  };
   MIREC_STAMP(0);
   int si = 0;
 #pragma unroll
@@ -523,8 +555,9 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
   const bool ahead = kind == 1;
   const int tb = si & 1;                   // 0 users, 1 items
   const mirec_adam_table& T_ = L.t[tb];
-  const int u = (int)((int64_t)blockIdx.x - L.block_start[si]);
-  const int t = threadIdx.x;
+  const int u = (int)(((int64_t)blockIdx.x - L.block_start[si]) * RPB) + wv;
+  if (u >= L.seg_rows[si]) return;         // past the segment's bound (wave-uniform)
+  const int t = threadIdx.x - wv * TPB;
   const int grp = t / LPR;
   const int l = t - grp * LPR;
   // first load level, all independent of each other: the count and the row id (look-
@@ -562,7 +595,7 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
     }
   }
   const int st = step_base[0] + step_off;
-  if (u >= n) return;                      // block-uniform
+  if (u >= n) return;                      // wave-uniform (row-uniform)
 #if defined(MIREC_STEP_PROBE_NO_AHEAD)     // timing probes only (tools/build_variant.sh)
   if (ahead) return;
 #endif
@@ -596,11 +629,13 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
     reinterpret_cast<H*>(T_.m)[offh] = m;
     reinterpret_cast<H*>(T_.v)[offh] = v;
     if (kAheadHalves == 1) {
-      __syncthreads();                             // every thread read `last`
+      row_sync();                                  // every thread read `last`
       if (t == 0) T_.last[row] = st + 1;
     } else {
-      // both halves read `last` before the first one counts in (its replay used it)
-      __syncthreads();
+      // both halves read `last` before the first one counts in (its replay used it). No
+      // data passes between the halves: the counter only elects the one that marks the
+      // row, after both have read its old mark (a relaxed add suffices)
+      row_sync();
       if (t == 0) {
         int32_t* j = L.join[tb] + L.join_ahead[tb] + u / kAheadHalves;
         if (__hip_atomic_fetch_add(j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
@@ -644,14 +679,15 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
   V g;
   memset(&g, 0, sizeof(V));
   // records of contributions kRecInline.. into LDS (one level, beside round 0's rows)
-  __shared__ int4 xrec[kStepExtraCap][2];
-  if (cnt > kRecInline) {                          // block-uniform (own block only)
+  __shared__ int4 xrec_all[RPB][kStepExtraCap][2];
+  auto& xrec = xrec_all[wv];
+  if (cnt > kRecInline) {                          // row-uniform (own row only)
     const int32_t* __restrict__ C = L.crec[tb] + (int64_t)(i0 + cskip) * kRecInts;
     for (int c = kRecInline + t; c < min(cnt, kRecInline + kStepExtraCap); c += TPB) {
       xrec[c - kRecInline][0] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[0];
       xrec[c - kRecInline][1] = reinterpret_cast<const int4*>(C + (int64_t)c * kRecInts)[1];
     }
-    __syncthreads();
+    row_sync();
   }
   for (int base = 0; base < cnt; base += NG) {
     const int i = base + grp;
@@ -717,7 +753,7 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
       }
     }
     if (!split) {
-      __syncthreads();
+      row_sync();
 #pragma unroll
       for (int h = 0; h < NG; ++h)
         if (base + h < cnt) {
@@ -725,23 +761,33 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
 #pragma unroll
           for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv, e);
         }
-      __syncthreads();                               // cont is rewritten next round
+      row_sync();                                    // cont is rewritten next round
     }
   }
   if (split) {
-    // every storing wave drained, then one lane counts the block in; the last of the
-    // row's nsh participants sums all nc vectors in grouping order and steps the row
+    // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility). Producer: the vectors
+    // went out as 8-byte agent-scope atomic (write-through) stores; every storing wave
+    // drains them (vmcnt(0)) before the row's threads meet, then ONE lane counts the row
+    // in on join[x] with an agent-scope add. The add that returns nsh - 1 is the last:
+    // its lane takes an agent-scope acquire (this CU's L1 invalidated) and waits for it
+    // before the row's threads load the vectors with agent-scope loads — the consumer
+    // form the memory model asks for, whatever the placement or the load.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    row_sync();
     if (t == 0) {
       const int arrived =
           __hip_atomic_fetch_add(L.join[tb] + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = arrived == nsh - 1;
-      if (s_last)                                    // every participant has counted in
+      if (s_last) {                                  // every participant has counted in
         __hip_atomic_store(L.join[tb] + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if !defined(MIREC_STEP_NO_ACQUIRE)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      }
     }
-    __syncthreads();
-    if (!s_last) return;                             // block-uniform
+    row_sync();
+    if (!s_last) return;                             // row-uniform
     const float* __restrict__ pe = part + EPT * t;
     int c = 0;
     for (; c + 8 <= nc; c += 8) {
@@ -769,7 +815,7 @@ __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n, 6) void bpr_a
   replay<V, true>(p, m, v, last, st, consts, k);
   const bool fresh = last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
-  __syncthreads();
+  row_sync();
   if (!fresh) return;
   reinterpret_cast<V*>(Pw)[off] = p;
   reinterpret_cast<V*>(T_.m)[off] = m;
@@ -901,20 +947,18 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   // segments: the shares of split rows first (their row's step waits for them), then
   // the look-ahead rows (their replays are long chains), then the touched rows
   if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
+  const int halves = d >= 128 ? 2 : 1;            // look-ahead rows per table row
+  const int64_t rows[6] = {kSplitCap, kSplitCap,
+                           L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0,
+                           L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0,
+                           n_max_uniq[0], n_max_uniq[1]};
+  const int rpb = d <= 128 ? MIREC_STEP_RPB : 1;  // StepRows<d>
   int64_t b = 0;
-  L.block_start[0] = b;
-  b += kSplitCap;
-  L.block_start[1] = b;
-  b += kSplitCap;
-  L.block_start[2] = b;
-  const int halves = d >= 128 ? 2 : 1;            // look-ahead blocks per row
-  b += L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0;
-  L.block_start[3] = b;
-  b += L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0;
-  L.block_start[4] = b;
-  b += n_max_uniq[0];
-  L.block_start[5] = b;
-  b += n_max_uniq[1];
+  for (int q = 0; q < 6; ++q) {
+    L.block_start[q] = b;
+    L.seg_rows[q] = (int32_t)rows[q];
+    b += (rows[q] + rpb - 1) / rpb;
+  }
   L.block_start[6] = b;
   AdamConsts k;
   k.omb1 = (float)(1.0 - beta1);
@@ -929,7 +973,8 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
 #define MIREC_STEP_CASE(DD)                                                                  \
   case DD:                                                                                   \
     hipLaunchKernelGGL(bpr_adam_step_kernel<DD>, grd,                                        \
-                       dim3(DD / Lanes<typename StepVec<DD>::T>::n), 0, st, L, items,        \
+                       dim3(DD / Lanes<typename StepVec<DD>::T>::n * StepRows<DD>::n), 0, st,\
+                       L, items,                                                             \
                        (int)Bc, T, gamma, grad_scale, loss_k, step_consts_dev, step_base_dev,\
                        step_off, k);                                                         \
     break;

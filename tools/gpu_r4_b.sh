@@ -9,3 +9,5 @@ timeout -k 10 400 $PT tests/test_gpu_group.py tests/test_gpu_spec_walk.py > $O/t
 rc=$?; tail -5 $O/tests.log; [ $rc -eq 0 ] || exit 10
 timeout -k 10 300 python tools/probe_prep.py > $O/probe.log 2>&1 || { tail $O/probe.log; exit 4; }
 grep '^{' $O/probe.log
+timeout -k 10 300 python tools/host_timeline.py --reps 3 > $O/host.log 2>&1 || { tail $O/host.log; exit 5; }
+tail -45 $O/host.log

@@ -36,9 +36,9 @@ def main():
     # wrap the host entry points of the timed region
     orig_prepare, orig_step = step._prepare, step._step
 
-    def prepare(slot, chunk):
+    def prepare(slot, chunk, *a):
         mark(f'prepare{chunk[:2]} in')
-        orig_prepare(slot, chunk)
+        orig_prepare(slot, chunk, *a)
         mark('prepare out')
     step._prepare = prepare
 
