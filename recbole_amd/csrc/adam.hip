@@ -249,6 +249,7 @@ __global__ __launch_bounds__(kFlushRowThreads) void adam_flush_row_kernel(
   V m = reinterpret_cast<const V*>(T.m)[off];
   V v = reinterpret_cast<const V*>(T.v)[off];
   replay<V, true>(p, m, v, last, target, consts, k);
+  MIREC_WORK(10, 1);
   if (odd) reinterpret_cast<V*>(T.p_alt)[off] = p;
   reinterpret_cast<V*>(T.p)[off] = p;
   reinterpret_cast<V*>(T.m)[off] = m;
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_scan_kernel(
     V m = reinterpret_cast<const V*>(T.m)[off];
     V v = reinterpret_cast<const V*>(T.v)[off];
     replay<V, true>(p, m, v, last, target, consts, k);
+    MIREC_WORK(10, 1);
     if (odd) reinterpret_cast<V*>(T.p_alt)[off] = p;
     reinterpret_cast<V*>(T.p)[off] = p;
     reinterpret_cast<V*>(T.m)[off] = m;
@@ -515,6 +517,18 @@ extern "C" int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_ta
                      step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
                      "mirec_adam_flush_f32");
 }
+
+#if defined(MIREC_STEP_COUNT)
+// diagnostic build only: this unit's executed-work counters (the flush's replays)
+extern "C" int mirec_work_counters_adam(unsigned long long* dst, int clear) {
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_work), sizeof(g_work)) != hipSuccess) return -1;
+  if (clear) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_work), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" int mirec_adam_flush_rows_f32(const mirec_adam_table* tables, int32_t n_tables,
                                          int32_t d, const int32_t* rows_per_wave,

@@ -12,6 +12,28 @@
 
 namespace mirec {
 
+// Executed-work counters (diagnostic build only: tools/build_variant.sh work
+// -DMIREC_STEP_COUNT; tools/probe_step_work.py). Element-steps actually executed, by
+// kind, so a roofline can be put on the work done rather than on the dense formula:
+// [0] zero-gradient steps with the p update, [1] vanishing steps (m, v only), [2]
+// gradient steps, [3] the look-ahead's own zero-gradient step, [4] touched rows stepped,
+// [5] look-ahead row halves replayed, [6..8] contributions formed (user row / item as
+// positive / item as negative), [9] split-row participants, [10] flush rows replayed.
+// Each translation unit has its own copy (read by its mirec_work_counters*).
+#if defined(MIREC_STEP_COUNT)
+static __device__ unsigned long long g_work[16];
+#define MIREC_WORK(i, n)                                                                  \
+  do {                                                                                    \
+    const uint64_t act_ = __ballot(1);                                                    \
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)act_) - 1)                 \
+      atomicAdd(&g_work[(i)], (unsigned long long)(n));                                   \
+  } while (0)
+#define MIREC_WORK_LANES() ((unsigned long long)__popcll(__ballot(1)))
+#else
+#define MIREC_WORK(i, n) do {} while (0)
+#define MIREC_WORK_LANES() 0ull
+#endif
+
 constexpr int kAdamThreads = 256;
 constexpr int kAdamRows = 64;  // table rows per block (streamed / flush)
 constexpr int kMaxTables = 4;
@@ -320,6 +342,7 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
       vanish = __all(mine);
       if (vanish) enter_skip();
     }
+    MIREC_WORK(vanish ? 1 : 0, N * MIREC_WORK_LANES());
     if (!vanish) {
       float q[N];
       incr(me, ve, sc, q);
@@ -354,6 +377,7 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
 #pragma unroll
         for (int i = 0; i < N; ++i) mine = mine && fixed_p_vanish(me[j][i], ve[j][i], sc[j], i);
       group_done = __all(mine);                 // four skipped steps
+      if (group_done) MIREC_WORK(1, G * N * MIREC_WORK_LANES());
     } else {
       bool mine = true;
 #pragma unroll
@@ -362,6 +386,7 @@ __device__ __forceinline__ void adam_replay_row(V& p, V& m, V& v, int s0, int s1
       if (!__all(mine)) {                       // four full steps, increments side by side
         float q[G][N];
         incr_steps<G, N>(me, ve, sc, k, q);
+        MIREC_WORK(0, G * N * MIREC_WORK_LANES());
 #pragma unroll
         for (int j = 0; j < G; ++j)
 #pragma unroll

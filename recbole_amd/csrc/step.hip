@@ -625,6 +625,8 @@ void bpr_adam_step_kernel(
     H z;
     memset(&z, 0, sizeof(H));
     adam_vec(p, m, v, z, step_consts(consts, st), k);   // step st: zero gradient
+    MIREC_WORK(3, Lanes<H>::n * MIREC_WORK_LANES());
+    MIREC_WORK(5, 1);
     reinterpret_cast<H*>(Pw)[offh] = p;
     reinterpret_cast<H*>(T_.m)[offh] = m;
     reinterpret_cast<H*>(T_.v)[offh] = v;
@@ -704,6 +706,9 @@ void bpr_adam_step_kernel(
         }
       }
       const int kk = r0.x, jn = r0.y;
+      if (l == 0) {
+        if (jn >= 0) { MIREC_WORK(8, 1); } else if (tb == 0) { MIREC_WORK(6, 1); } else { MIREC_WORK(7, 1); }
+      }
       const float4 uv = reinterpret_cast<const float4*>(EU + (int64_t)r0.z * D)[l];
       const float4 pv = reinterpret_cast<const float4*>(EI + (int64_t)r0.w * D)[l];
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -764,6 +769,7 @@ void bpr_adam_step_kernel(
       row_sync();                                    // cont is rewritten next round
     }
   }
+  if (split) MIREC_WORK(9, 1);
   if (split) {
     // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility). Producer: the vectors
     // went out as 8-byte agent-scope atomic (write-through) stores; every storing wave
@@ -815,6 +821,10 @@ void bpr_adam_step_kernel(
   replay<V, true>(p, m, v, last, st, consts, k);
   const bool fresh = last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
+  if (fresh) {
+    MIREC_WORK(2, EPT * MIREC_WORK_LANES());
+    MIREC_WORK(4, 1);
+  }
   row_sync();
   if (!fresh) return;
   reinterpret_cast<V*>(Pw)[off] = p;
@@ -856,6 +866,18 @@ extern "C" int mirec_step_records(const int64_t* user_keys, const int64_t* item_
 }
 
 extern "C" int64_t mirec_step_record_ints(int64_t per) { return per < 0 ? -1 : rec_ints(per); }
+
+#if defined(MIREC_STEP_COUNT)
+// diagnostic build only: copy (and clear) this unit's executed-work counters (16 x u64)
+extern "C" int mirec_work_counters(unsigned long long* dst, int clear) {
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_work), sizeof(g_work)) != hipSuccess) return -1;
+  if (clear) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_work), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 namespace mirec {
 static int bits_for(int64_t n) {        // bits of n - 1 (n >= 1)

@@ -1118,7 +1118,8 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         if not new:
             return
         slot = self.slots[k % len(self.slots)]
-        slot.planned.synchronize()
+        if not slot.planned.query():          # the plan status reaches pinned memory
+            slot.planned.synchronize()
         over, most = (int(x) for x in slot.plan_status_host)
         if over == -4:
             self._grow_cap(most)
