@@ -197,6 +197,120 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
                     blockIdx.x, L);
 }
 
+// Bucket-rank form of the per-block LDS sort, for blocks of <= kBktMax keys whatever the
+// key space (DeepFM's field blocks: 2,048 keys of up to 10 M ids, which took six
+// barrier-bound 4-bit radix passes): the block's key range is cut into <= 4,096 buckets
+// by the top bits of (key - min); LDS counters give every key a slot in its bucket (in
+// any order), one scan places the buckets, and each key's final position is its
+// bucket's start + the number of (key, position) pairs of its bucket below its own — the
+// stable sort's order, the same perm / uniq / seg / n_uniq as segsort_lds_batch.
+constexpr int kBktThreads = 512;
+constexpr int kBktEpt = 8;
+constexpr int kBktMax = kBktThreads * kBktEpt;
+constexpr int kBktBits = 12;
+struct BucketLds {
+  int32_t hist[1 << kBktBits], bstart[1 << kBktBits];
+  int32_t bk[kBktMax], bp[kBktMax];      // (key, position) in bucket order
+  int32_t sk[kBktMax];                   // keys in sorted order
+  int scan[kBktThreads / 64 + 1];
+  int32_t kmin, kmax;
+};
+
+__global__ __launch_bounds__(kBktThreads) void segsort_bucket_kernel(
+    const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n,
+    int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all) {
+  __shared__ BucketLds L;
+  const int64_t b = blockIdx.x;
+  const int n = (int)min((int64_t)batch_n, n_total - b * batch_n);
+  const int64_t* __restrict__ keys = keys_all + b * batch_n;
+  const int tid = threadIdx.x;
+  int32_t k[kBktEpt];
+  int lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+  for (int r = 0; r < kBktEpt; ++r) {
+    const int e = tid + r * kBktThreads;
+    k[r] = e < n ? (int32_t)keys[e] : 0;
+    if (e < n) {
+      lo = min(lo, k[r]);
+      hi = max(hi, k[r]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, __shfl_xor(lo, off, 64));
+    hi = max(hi, __shfl_xor(hi, off, 64));
+  }
+  if (tid == 0) {
+    L.kmin = INT32_MAX;
+    L.kmax = INT32_MIN;
+  }
+  for (int q = tid; q < (1 << kBktBits); q += kBktThreads) L.hist[q] = 0;
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    atomicMin(&L.kmin, lo);
+    atomicMax(&L.kmax, hi);
+  }
+  __syncthreads();
+  const int32_t kmin = L.kmin;
+  const uint32_t span = (uint32_t)(L.kmax - kmin);
+  int shift = 0;
+  while (shift < 32 && (span >> shift) >= (1u << kBktBits)) ++shift;
+  int slot[kBktEpt];
+#pragma unroll
+  for (int r = 0; r < kBktEpt; ++r) {
+    const int e = tid + r * kBktThreads;
+    slot[r] = e < n ? atomicAdd(&L.hist[(uint32_t)(k[r] - kmin) >> shift], 1) : 0;
+  }
+  __syncthreads();
+  {
+    constexpr int kPer = (1 << kBktBits) / kBktThreads;
+    int c[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      c[j] = L.hist[tid * kPer + j];
+      sum += c[j];
+    }
+    int tot;
+    int run = block_exclusive_scan(sum, L.scan, &tot);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      L.bstart[tid * kPer + j] = run;
+      run += c[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kBktEpt; ++r) {
+    const int e = tid + r * kBktThreads;
+    if (e < n) {
+      const int q = L.bstart[(uint32_t)(k[r] - kmin) >> shift] + slot[r];
+      L.bk[q] = k[r];
+      L.bp[q] = e;
+    }
+  }
+  __syncthreads();
+  int32_t* __restrict__ perm = perm_all + b * batch_n;
+#pragma unroll
+  for (int r = 0; r < kBktEpt; ++r) {
+    const int e = tid + r * kBktThreads;
+    if (e < n) {
+      const int bi = (uint32_t)(k[r] - kmin) >> shift;
+      const int b0 = L.bstart[bi], c = L.hist[bi];
+      int rank = 0;
+      for (int f = 0; f < c; ++f) {
+        const int32_t kf = L.bk[b0 + f];
+        rank += (kf < k[r] || (kf == k[r] && L.bp[b0 + f] < e)) ? 1 : 0;
+      }
+      L.sk[b0 + rank] = k[r];
+      perm[b0 + rank] = e;
+    }
+  }
+  __syncthreads();
+  emit_segments(L.sk, n, uniq_all + b * batch_n, seg_all + b * (batch_n + 1), n_uniq_all + b,
+                L.scan);
+}
+
 // Block-partitioned sort (keys in n_blocks blocks of block_n, every key of block b
 // below every key of block b+1 — DeepFM's token keys, one block per field at its
 // table offset): each block sorted in LDS by its own workgroup, then concatenated —
@@ -803,8 +917,12 @@ extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t
   int nbits = 0;
   while (nbits < 31 && ((int64_t)1 << nbits) < key_space) ++nbits;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys, n,
-                     (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
+  if (block_n <= kBktMax)      // bucket-rank sort: no per-digit passes
+    hipLaunchKernelGGL(segsort_bucket_kernel, dim3((unsigned)nb), dim3(kBktThreads), 0, st, keys,
+                       n, (int)block_n, perm_t, uniq_t, seg_t, nu_t);
+  else
+    hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys,
+                       n, (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
   hipLaunchKernelGGL(blocks_concat_kernel, dim3((unsigned)nb), dim3(256), 0, st, perm_t, uniq_t,
                      seg_t, nu_t, n, (int)block_n, (int)nb, perm, uniq, seg, n_uniq_dev);
   return launch_status("mirec_segment_sort_blocks");
