@@ -188,6 +188,15 @@ int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* EI, int64_t 
  * mirec_bpr_fwd_bwd_f32 (loss_k as there) plus coef[times*B], coef[r] = dloss/dx_r
  * of row r = j*B + k — the ONLY per-row quantity the backward needs besides the
  * rows themselves. Ranks exchange these (4 B per row instead of a d-float row). */
+/* K3 on a row-sharded step's received rows (csrc/shard.hip): E holds the rows every slot
+ * reads (users and items alike), ids index E, and each slot's gradient row is written at
+ * grad + id * d — the message position it returns in — instead of at its slot: K3 and the
+ * backward gather (mirec_gather_rows_i32idx) in one launch. The ids of a batch's slots
+ * must be distinct. Arithmetic: mirec_bpr_fwd_bwd_f32's, bit for bit. */
+int mirec_bpr_fwd_bwd_at_ids_f32(const float* E, int64_t nE, int32_t d, const int64_t* user,
+                                 const int64_t* pos, const int64_t* neg, int64_t B,
+                                 int32_t times, float gamma, float grad_scale, float* loss_k,
+                                 float* grad, void* stream);
 int mirec_bpr_fwd_coef_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,
                            int32_t d, const int64_t* user, const int64_t* pos,
                            const int64_t* neg, int64_t B, int32_t times,

@@ -56,7 +56,11 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, int lane, co
 // negatives are gathered NB at a time with all their loads issued before the
 // first reduction, so a positive costs ~2 dependent memory round trips instead
 // of one per negative.
-template <int D>
+// AT_IDS: the gradient row of every slot is written at its row id (gU + id*D for the
+// user, gI + id*D for the items) instead of at its slot — the row-sharded step, whose
+// ids are positions in the received message buffer and whose gradient rows go back in
+// the same positions (csrc/shard.hip): K3 and the backward gather in one launch.
+template <int D, bool AT_IDS = false>
 __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     const float* __restrict__ EU, int64_t nU, const float* __restrict__ EI, int64_t nI,
     const int64_t* __restrict__ user, const int64_t* __restrict__ pos,
@@ -83,6 +87,16 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     int64_t id = q < times ? neg[(int64_t)q * B + k] : 0;
     nid[q] = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
   }
+  int64_t wid[NB];                    // AT_IDS: this group's negative ids (the next load early)
+#pragma unroll
+  for (int q = 0; q < NB; ++q) wid[q] = nid[q];
+  // the first group's negative rows in flight with u and p: all the rows of a positive
+  // with T <= NB in one dependent level after the ids
+  float4 nf[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q)
+    nf[q] = q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
   const float sp = group_sum<LPR>(dot4(u, p));
   float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gp = gu;
   float lsum = 0.f;
@@ -91,9 +105,12 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
     float4 n[NB];
 #pragma unroll
     for (int q = 0; q < NB; ++q)
-      n[q] = j0 + q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      n[q] = j0 == 0 ? nf[q]
+                     : (j0 + q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
+                                       : make_float4(0.f, 0.f, 0.f, 0.f));
     // ids of the next group in flight under this group's arithmetic
+#pragma unroll
+    for (int q = 0; q < NB; ++q) wid[q] = nid[q];
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int j = j0 + NB + q;
@@ -113,7 +130,7 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
         float4 gn;
         pair_contrib(gu, gp, gn, dx, u, p, n[q]);
         const int64_t r = (int64_t)j * B + k;
-        if (gI) reinterpret_cast<float4*>(gI + (B + r) * D)[l] = gn;
+        if (gI) reinterpret_cast<float4*>(gI + (AT_IDS ? wid[q] : B + r) * D)[l] = gn;
         if (l == 0) {
           if (neg_score) neg_score[r] = sn[q];
           if (coef) coef[r] = dx;
@@ -121,8 +138,8 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
       }
     }
   }
-  if (gU) reinterpret_cast<float4*>(gU + k * D)[l] = gu;
-  if (gI) reinterpret_cast<float4*>(gI + k * D)[l] = gp;
+  if (gU) reinterpret_cast<float4*>(gU + (AT_IDS ? uid : k) * D)[l] = gu;
+  if (gI) reinterpret_cast<float4*>(gI + (AT_IDS ? pid : k) * D)[l] = gp;
   if (l == 0) {
     if (loss_k) loss_k[k] = lsum;
     if (pos_score) pos_score[k] = sp;
@@ -241,7 +258,7 @@ int launch_bpr(const float* EU, int64_t nU, const float* EI, int64_t nI, int32_t
                const int64_t* user, const int64_t* pos, const int64_t* neg, int64_t B,
                int32_t times, float gamma, float grad_scale, float* loss_k, float* pos_score,
                float* neg_score, float* gU, float* gI, float* coef, void* stream,
-               const char* what) {
+               const char* what, bool at_ids = false) {
   if (B == 0) return 0;
   if (!EU || !EI || !user || !pos || (times > 0 && !neg) || B < 0 || times < 0 || nU <= 0 ||
       nI <= 0) {
@@ -252,7 +269,8 @@ int launch_bpr(const float* EU, int64_t nU, const float* EI, int64_t nI, int32_t
   hipStream_t st = (hipStream_t)stream;
 #define MIREC_BPR_CASE(DD)                                                                    \
   case DD:                                                                                    \
-    hipLaunchKernelGGL(bpr_fwd_bwd_kernel<DD>,                                                \
+    hipLaunchKernelGGL((at_ids ? bpr_fwd_bwd_kernel<DD, true>                         \
+                                 : bpr_fwd_bwd_kernel<DD, false>),                        \
                        dim3((unsigned)((B + 4 * (256 / DD) - 1) / (4 * (256 / DD)))), blk, 0, \
                        st, EU, nU, EI, nI, user, pos,                                         \
                        neg, B, times, gamma, grad_scale, loss_k, pos_score, neg_score, gU, gI, \
@@ -280,6 +298,24 @@ extern "C" int mirec_bpr_fwd_bwd_f32(const float* EU, int64_t nU, const float* E
                                      float* neg_score, float* gU, float* gI, void* stream) {
   return launch_bpr(EU, nU, EI, nI, d, user, pos, neg, B, times, gamma, grad_scale, loss_k,
                     pos_score, neg_score, gU, gI, nullptr, stream, "mirec_bpr_fwd_bwd_f32");
+}
+
+// K3 with every gradient row written at its row id (the row-sharded step: ids are message
+// positions, gradient rows return in the same positions) — grad may be the same buffer
+// for both tables; the ids of one batch must be distinct slots (they are: one message
+// position per slot).
+extern "C" int mirec_bpr_fwd_bwd_at_ids_f32(const float* E, int64_t nE, int32_t d,
+                                           const int64_t* user, const int64_t* pos,
+                                           const int64_t* neg, int64_t B, int32_t times,
+                                           float gamma, float grad_scale, float* loss_k,
+                                           float* grad, void* stream) {
+  if (B > 0 && !grad) {
+    set_error("mirec_bpr_fwd_bwd_at_ids_f32: grad is required");
+    return -1;
+  }
+  return launch_bpr(E, nE, E, nE, d, user, pos, neg, B, times, gamma, grad_scale, loss_k,
+                    nullptr, nullptr, grad, grad, nullptr, stream,
+                    "mirec_bpr_fwd_bwd_at_ids_f32", true);
 }
 
 extern "C" int mirec_bpr_fwd_coef_f32(const float* EU, int64_t nU, const float* EI, int64_t nI,

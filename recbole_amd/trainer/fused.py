@@ -957,7 +957,6 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         self.lastU = torch.zeros(self.SU, dtype=torch.int32, device=dev)
         self.lastI = torch.zeros(self.SI, dtype=torch.int32, device=dev)
         self._solo = dist is None            # one rank, no process group: no collectives
-        self.xloc = torch.empty((2 + T) * B, d, device=dev)
         self.loss_g = torch.empty(G * self.C * B, dtype=torch.float32, device=dev)
         self.loss_mine = torch.zeros(self.C * B, dtype=torch.float32, device=dev)
         self.status = torch.zeros(2, dtype=torch.int32, device=dev)    # epoch backstop
@@ -1187,22 +1186,19 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         self._record('exchange', stream, lambda: self._all_to_all(self.recvF, self.sendF))
         loss_p = self.loss_mine.data_ptr() + 4 * c * B
         pos_p = slot.pos.data_ptr() + 8 * c * (2 + T) * B
-        x0 = self.xloc.data_ptr()
 
         def bpr():
+            # K3 reading the received rows; each slot's gradient row goes straight into
+            # its backward message position (the position its row came in): no separate
+            # backward gather (sendB's padding rows are never read by the owners)
             if n == 0:
                 return
-            check(L.mirec_bpr_fwd_bwd_f32(self.recvF.data_ptr(), M, self.recvF.data_ptr(), M, d,
-                                          pos_p, pos_p + 8 * n, pos_p + 16 * n, n, T, 1e-10,
-                                          self._grad_scale(Bc), loss_p, None, None, x0,
-                                          x0 + 4 * n * d, st), 'mirec_bpr_fwd_bwd_f32')
+            check(L.mirec_bpr_fwd_bwd_at_ids_f32(self.recvF.data_ptr(), M, d, pos_p,
+                                                 pos_p + 8 * n, pos_p + 16 * n, n, T, 1e-10,
+                                                 self._grad_scale(Bc), loss_p,
+                                                 self.sendB.data_ptr(), st),
+                  'mirec_bpr_fwd_bwd_at_ids_f32')
         self._record('bpr', stream, bpr)
-
-        def bwd_gather():
-            check(L.mirec_gather_rows_i32idx(self.xloc.data_ptr(), self.xloc.shape[0], 4 * d,
-                                             slot.bwd_src.data_ptr() + 4 * c * M, M,
-                                             self.sendB.data_ptr(), st), 'mirec_gather_rows_i32idx')
-        self._record('gather_bwd', stream, bwd_gather)
         self._record('exchange_bwd', stream, lambda: self._all_to_all(self.recvB, self.sendB))
         t = self._tables
         for q, (tag, per) in enumerate((('u', Bc), ('i', KI))):

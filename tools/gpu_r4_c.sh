@@ -8,7 +8,7 @@ O=gpurun_out/r4c
 mkdir -p $O
 PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
 timeout -k 10 600 $PT tests/test_gpu_group.py tests/test_gpu_spec_walk.py tests/test_gpu_step.py \
-  tests/test_gpu_e2e.py tests/test_gpu_chain.py tests/test_gpu_kernels.py > $O/tests.log 2>&1
+  tests/test_gpu_e2e.py tests/test_gpu_chain.py tests/test_gpu_kernels.py tests/test_gpu_shard.py > $O/tests.log 2>&1
 rc=$?; tail -4 $O/tests.log; [ $rc -eq 0 ] || exit 10
 MIREC_LIB=recbole_amd/_lib/alt/work.so timeout -k 10 300 python tools/probe_step_work.py --out $O/k35_work.json > $O/work.log 2>&1 || { tail $O/work.log; exit 3; }
 python -c "import json; d=json.load(open('$O/k35_work.json')); print(json.dumps(d['timed_region'])[:600]); print(json.dumps(d['measurement_window']['per_launch']))"
