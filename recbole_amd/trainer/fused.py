@@ -766,6 +766,8 @@ class FusedBPRTrainStep(object):
         self._cur = None                       # chunk index being consumed
         for s in self.slots:
             s.free_recorded = False
+            if not self._sharded(self.Bg):     # the native preparation's descriptors now,
+                self._chunk_prep(s)            # not on a timed region's first launch
         for _ in range(len(self.slots)):
             self._issue_prep()
         self._issue_groups(len(self.slots))
