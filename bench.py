@@ -173,6 +173,21 @@ def pmc_bytes(substr):
     return None, None
 
 
+def executed_work(W, K):
+    """K35's executed work in bench's measurement window after --warmup W --steps K, from
+    the newest committed counter run of the same window (profiles/r*_k35_work*.json,
+    tools/probe_step_work.py on the diagnostic build: element-steps actually executed —
+    zero-state rows and rows already current never run, vanishing steps count as the m / v
+    work they do), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_k35_work*.json')))[::-1]:
+        d = json.load(open(path))
+        c = d.get('config', {})
+        if c.get('warmup') == W and c.get('steps') == K:
+            return d, os.path.basename(path)
+    return None, None
+
+
 def pmc_valu_insts(substr):
     """(VALU, transcendental f32) wave-instructions per launch of the kernel whose
     name contains `substr` (SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32 pass of
@@ -198,7 +213,7 @@ ADAM_FLOPS = 13      # IEEE fp32 ops per element per Adam step in torch's formul
 VALU_PEAK_TFLOPS = 157.3   # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 
 
-def roofline(step, events, uniq, d, M):
+def roofline(step, events, uniq, d, M, W=None, K=None):
     """Rooflines from the per-launch HIP events of an eager window of M steps
     that starts right after a flush and ends with one (every row of both tables
     is advanced exactly M Adam steps by the window's K5 launches).
@@ -282,6 +297,38 @@ def roofline(step, events, uniq, d, M):
                          'traffic_note': 'PMC FETCH_SIZE x2 + WRITE_SIZE per launch x launches; '
                                          'streamed dense Adam moves 6*(nU+nI)*d*4 = %d per step'
                                          % (6 * (step.nU + step.nI) * R)})
+    work, wsrc = executed_work(W, K) if fused else (None, None)
+    if work is not None:
+        # the roofline on the work the kernels execute (counter run of this same window):
+        # the formula above credits every element-step of the dense update; here zero-state
+        # rows, current rows and vanishing steps count only what they run
+        mw = work['measurement_window']
+        ex = mw['window_total']
+        tf_ex = ex['flops'] / t_adam / 1e12
+        t_step = kernels_us['step'] * 1e-6
+        pl = mw['per_launch']
+        alg_gbs = pl['algorithmic_bytes'] / t_step / 1e9
+        tb_step, tsrc = pmc_bytes(per_k)
+        adam.update({
+            'dense_formula': {'achieved': adam['achieved'], 'frac': adam['frac'],
+                              'flops_per_window': adam['flops_per_window']},
+            'achieved': round(tf_ex, 3), 'frac': round(tf_ex / VALU_PEAK_TFLOPS, 4),
+            'flops_per_window': int(ex['flops']), 'flops_source': wsrc,
+            'flops_formula': 'executed (counters): 13 per gradient element-step, 9 per '
+                             'zero-gradient step with its p update, 3 per vanishing step, BPR '
+                             'dots + contribution vectors per contribution formed',
+            'k35_per_launch': {
+                'executed_flops': int(pl['flops']),
+                'algorithmic_bytes': int(pl['algorithmic_bytes']),
+                'algorithmic_bytes_formula': '(touched rows + look-ahead rows) x (p, m, v) x '
+                                             'd x 4 B, read and written',
+                'gathered_bytes': int(pl['gathered_bytes']),
+                'avg_launch_us': kernels_us['step'],
+                'hbm_frac_algorithmic': round(alg_gbs / HBM_PEAK_GBS, 4),
+                'pmc_bytes_per_launch': tb_step, 'pmc_source': tsrc,
+                'rows': {k: mw['per_launch_mean'][k] for k in
+                         ('touched_rows', 'ahead_halves', 'contrib_user', 'contrib_pos',
+                          'contrib_neg', 'split_parts')}}})
     if step.adam_mode == 'streamed':           # memory-bound: HBM view is the binding one
         by = 6 * (step.nU + step.nI) * R * M
         gbs = by / t_adam / 1e9
@@ -291,36 +338,55 @@ def roofline(step, events, uniq, d, M):
     return adam, bpr, kernels_us
 
 
-def gather_throughput(step, d, neg, B=65536, reps=20):
+def gather_throughput(step, d, neg, B=65536, reps=20, big_rows=2_000_000):
     """north_star's gather roofline at the throughput setting of SURVEY.md §8d
-    (B = 65,536 positives, C2 tables): K3 alone — (2+T) row gathers per positive
-    and the per-contribution gradient rows written — HIP events per launch.
+    (B = 65,536 positives, 4 negatives): K3 alone — (2+T) row gathers per positive and
+    the per-contribution gradient rows written — HIP events per launch, median of reps.
     Bytes per launch = 2*(B + (1+T)B)*d*4 (rows read + gradient rows written)
-    + 8*(B + (1+T)B) (ids) + 4*B (losses)."""
+    + 8*(B + (1+T)B) (ids) + 4*B (losses).
+    The HBM figure ('frac') is taken on tables past the 256 MiB Infinity Cache (big_rows
+    users + big_rows items, uniform ids: almost every row gather misses the LLC); the
+    C2-table figure is reported beside it as LLC-resident (84.6 MB of tables)."""
     from recbole_amd import ops
     dev = step.device
-    g = torch.Generator(device='cpu').manual_seed(7)
-    user = torch.randint(0, step.nU, (B,), generator=g).to(dev)
-    pos = torch.randint(1, step.nI, (B,), generator=g).to(dev)
-    negs = torch.randint(1, step.nI, (neg * B,), generator=g).to(dev)
-    out = {}
-    ops.bpr_fwd_bwd(step.pU.detach(), step.pI.detach(), user, pos, negs, neg, out=out)
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        ops.bpr_fwd_bwd(step.pU.detach(), step.pI.detach(), user, pos, negs, neg, out=out)
-        b.record()
-        torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b) * 1e-3)
-    t = float(np.median(ts))
+
+    def one(EU, EI, nU, nI):
+        g = torch.Generator(device='cpu').manual_seed(7)
+        user = torch.randint(0, nU, (B,), generator=g).to(dev)
+        pos = torch.randint(1, nI, (B,), generator=g).to(dev)
+        negs = torch.randint(1, nI, (neg * B,), generator=g).to(dev)
+        out = {}
+        ops.bpr_fwd_bwd(EU, EI, user, pos, negs, neg, out=out)
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            ops.bpr_fwd_bwd(EU, EI, user, pos, negs, neg, out=out)
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) * 1e-3)
+        return float(np.median(ts))
+
     rows = B + (1 + neg) * B
     nbytes = 2 * rows * d * 4 + rows * 8 + B * 4
+    t_llc = one(step.pU.detach(), step.pI.detach(), step.nU, step.nI)
+    g = torch.Generator(device=dev).manual_seed(11)
+    EU = torch.randn(big_rows, d, device=dev, generator=g) * 0.1
+    EI = torch.randn(big_rows, d, device=dev, generator=g) * 0.1
+    t = one(EU, EI, big_rows, big_rows)
+    del EU, EI
+    traffic, tsrc = pmc_bytes('gather_big')
     gbs = nbytes / t / 1e9
-    return {'kernel': f'K3 bpr_fwd_bwd<{d}> at B={B} positives', 'bound': 'hbm',
-            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+    return {'kernel': f'K3 bpr_fwd_bwd<{d}> at B={B} positives, tables {big_rows:,} + '
+                      f'{big_rows:,} rows ({2 * big_rows * d * 4 / 2**30:.2f} GiB: past the LLC)',
+            'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes,
-            'launch_us': round(t * 1e6, 1), 'positives_per_s': round(B / t, 1)}
+            'traffic': traffic, 'traffic_source': tsrc,
+            'launch_us': round(t * 1e6, 1), 'positives_per_s': round(B / t, 1),
+            'llc_resident': {'tables': 'C2 (84.6 MB, fits the 256 MiB Infinity Cache)',
+                             'achieved': round(nbytes / t_llc / 1e9, 1),
+                             'frac': round(nbytes / t_llc / 1e9 / HBM_PEAK_GBS, 4),
+                             'launch_us': round(t_llc * 1e6, 1)}}
 
 
 def _cpu_model():
@@ -510,7 +576,7 @@ def main():
     step.kernel_events = None
     losses = step.end_epoch(W + K + M)
     assert all(np.isfinite(losses)), 'non-finite loss'
-    roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M)
+    roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M, W, K)
     mine = {'rank': rank, 'timed_s': round(local_elapsed, 6), 'kernels_us': kernels_us,
             'k5_us_per_step': roof['us_per_step'],
             'table_rows': int(getattr(step, 'SU', step.nU) + getattr(step, 'SI', step.nI))}
