@@ -128,7 +128,7 @@ def time_deepfm_steps(batches, tok, tok_dims, flt, d, hidden, steps=3, warmup=1,
         torch.set_num_threads(threads)
     model = cpu_ref.DeepFMCPU(tok, tok_dims, [], [], flt, d, hidden, dropout)
     opt = torch.optim.Adam(model.parameters(), lr=lr)
-    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]
+    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]   # cycled when fewer
 
     def one(b):
         opt.zero_grad()
@@ -137,11 +137,11 @@ def time_deepfm_steps(batches, tok, tok_dims, flt, d, hidden, steps=3, warmup=1,
         loss.backward()
         opt.step()
 
-    for b in cb[:warmup]:
-        one(b)
+    for i in range(warmup):
+        one(cb[i % len(cb)])
     t0 = time.perf_counter()
-    for b in cb[warmup:warmup + steps]:
-        one(b)
+    for i in range(warmup, warmup + steps):
+        one(cb[i % len(cb)])
     dt = time.perf_counter() - t0
     B = len(cb[0]['label'])
     return steps * B / dt, dt, torch.get_num_threads()
@@ -156,7 +156,7 @@ def time_sasrec_steps(batches, random_list, n_items, L, d, n_neg, steps=3, warmu
     model = cpu_ref.SASRecCPU(n_items, L, d, 2, 2, 256, 1e-12)
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     walk = cpu_ref.NumpyWalk(random_list, _EmptySets())     # RepeatableSampler: no rejection
-    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]
+    cb = [_cpu_batch(b) for b in batches[:steps + warmup]]   # cycled when fewer
 
     def one(b):
         neg = torch.as_tensor(walk.sample_by_key_ids(b['user_id'].numpy(), n_neg))
@@ -167,11 +167,11 @@ def time_sasrec_steps(batches, random_list, n_items, L, d, n_neg, steps=3, warmu
         loss.backward()
         opt.step()
 
-    for b in cb[:warmup]:
-        one(b)
+    for i in range(warmup):
+        one(cb[i % len(cb)])
     t0 = time.perf_counter()
-    for b in cb[warmup:warmup + steps]:
-        one(b)
+    for i in range(warmup, warmup + steps):
+        one(cb[i % len(cb)])
     dt = time.perf_counter() - t0
     return steps * len(cb[0]['item_id']) / dt, dt, torch.get_num_threads()
 

@@ -499,6 +499,27 @@ __device__ __forceinline__ void part_load(const float* p, float2& a) {
   a = make_float2(__uint_as_float((unsigned)w), __uint_as_float((unsigned)(w >> 32)));
 }
 
+// Row-state stores of K35. MIREC_STEP_WT (probe build): write-through (agent-scope)
+// stores, so the launch leaves no dirty lines for the kernel boundary's L2 write-back.
+template <typename V>
+__device__ __forceinline__ void state_store(V* p, const V& x) {
+#if defined(MIREC_STEP_WT)
+  if constexpr (sizeof(V) == 8) {
+    auto q = (__attribute__((address_space(1))) unsigned long long*)(p);
+    unsigned long long w;
+    memcpy(&w, &x, 8);
+    __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    auto q = (__attribute__((address_space(1))) unsigned int*)(p);
+    unsigned int w;
+    memcpy(&w, &x, 4);
+    __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#else
+  *p = x;
+#endif
+}
+
 template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
 template <typename V> struct AheadVec { using T = float; };
@@ -627,9 +648,9 @@ void bpr_adam_step_kernel(
     adam_vec(p, m, v, z, step_consts(consts, st), k);   // step st: zero gradient
     MIREC_WORK(3, Lanes<H>::n * MIREC_WORK_LANES());
     MIREC_WORK(5, 1);
-    reinterpret_cast<H*>(Pw)[offh] = p;
-    reinterpret_cast<H*>(T_.m)[offh] = m;
-    reinterpret_cast<H*>(T_.v)[offh] = v;
+    state_store(reinterpret_cast<H*>(Pw) + offh, p);
+    state_store(reinterpret_cast<H*>(T_.m) + offh, m);
+    state_store(reinterpret_cast<H*>(T_.v) + offh, v);
     if (kAheadHalves == 1) {
       row_sync();                                  // every thread read `last`
       if (t == 0) T_.last[row] = st + 1;
@@ -827,9 +848,9 @@ void bpr_adam_step_kernel(
   }
   row_sync();
   if (!fresh) return;
-  reinterpret_cast<V*>(Pw)[off] = p;
-  reinterpret_cast<V*>(T_.m)[off] = m;
-  reinterpret_cast<V*>(T_.v)[off] = v;
+  state_store(reinterpret_cast<V*>(Pw) + off, p);
+  state_store(reinterpret_cast<V*>(T_.m) + off, m);
+  state_store(reinterpret_cast<V*>(T_.v) + off, v);
   if (t == 0) T_.last[row] = st + 1;
   MIREC_STAMP(3);
 }

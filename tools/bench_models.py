@@ -243,14 +243,17 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
         runs = [cb.time_deepfm_steps(batches, [f'C{j}' for j in range(26)],
                                      [nums[f'C{j}'] for j in range(26)],
                                      [f'I{j}' for j in range(13)], d, [128, 128, 128],
-                                     steps=5, threads=thr) for _ in range(3)]
+                                     steps=20, warmup=2, threads=thr) for _ in range(3)]
         sps, used = float(np.median([r[0] for r in runs])), runs[0][2]
+        vals = np.array([r[0] for r in runs])
         cpu = {'value': round(sps, 1), 'unit': 'samples/s', 'cores': used, 'kind': 'port',
                'threads_derivation': how, 'runs': [round(r[0], 1) for r in runs],
-               'sample': f'median of 3 runs of 1 warm-up + 5 timed C4 steps of the oracle '
+               'cv': round(float(vals.std() / vals.mean()), 4),
+               'sample': f'median of 3 runs of 2 warm-up + 20 timed C4 steps of the oracle '
                          f'restatement on torch CPU (DeepFMCPU + dense optim.Adam over every '
-                         f'table; a bounded sample: one step moves the 2.1 GB tables several '
-                         f'times), {sum(r[1] for r in runs):.1f} s timed in all'}
+                         f'table), {sum(r[1] for r in runs):.1f} s timed in all; bounded below '
+                         f'the 20 + 200 of SURVEY.md 8d: a CPU step moves the 2.1 GB tables '
+                         f'several times (~1 s), and the run-to-run spread (cv) is reported'}
     k10 = {'kernel': 'mlp_fwd_kernel (K10 forward: MLPLayers 624-128-128-128 + '
                      'deep_predict_layer, dropout, ReLU)', 'bound': 'mfma',
            'achieved': round(mlp_flops / (mf_us * 1e-6) / 1e12, 2),
@@ -392,14 +395,18 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
         from oracle import cpu_baseline as cb
         thr, how = cb.host_threads()
         runs = [cb.time_sasrec_steps(batches, random_list.cpu().numpy(), n_items, L, d, n_neg,
-                                     steps=2, threads=thr) for _ in range(3)]
+                                     steps=8, warmup=1, threads=thr) for _ in range(3)]
         sps, used = float(np.median([r[0] for r in runs])), runs[0][2]
+        vals = np.array([r[0] for r in runs])
         cpu = {'value': round(sps, 1), 'unit': 'sequences/s', 'cores': used, 'kind': 'port',
                'threads_derivation': how, 'runs': [round(r[0], 1) for r in runs],
-               'sample': f'median of 3 runs of 1 warm-up + 2 timed C3 steps of the oracle '
+               'cv': round(float(vals.std() / vals.mean()), 4),
+               'sample': f'median of 3 runs of 1 warm-up + 8 timed C3 steps of the oracle '
                          f'restatement on torch CPU (numpy walk, SASRecCPU + sampled softmax, '
-                         f'dense optim.Adam over the 1.5 GB item table; a bounded sample), '
-                         f'{sum(r[1] for r in runs):.1f} s timed in all'}
+                         f'dense optim.Adam over the 1.5 GB item table), '
+                         f'{sum(r[1] for r in runs):.1f} s timed in all; bounded below the '
+                         f'20 + 200 of SURVEY.md 8d (~3 s per CPU step), the run-to-run spread '
+                         f'(cv) is reported'}
     return {
         'cpu_baseline': cpu,
         'adam_mode': ADAM_MODE,

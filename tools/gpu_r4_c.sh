@@ -31,5 +31,6 @@ run nospec "MIREC_SPEC_WALK=0" || exit 6
 run rpb1 "MIREC_LIB=recbole_amd/_lib/alt/k35_rpb1.so" || exit 6
 run w5 "MIREC_LIB=recbole_amd/_lib/alt/k35_w5.so" || exit 6
 run noacq "MIREC_LIB=recbole_amd/_lib/alt/k35_noacq.so" || exit 6
+run wt "MIREC_LIB=recbole_amd/_lib/alt/k35_wt.so" || exit 6
 bash tools/trace_short.sh || exit 7
 cat gpurun_out/prof_short/tw.txt | head -80
