@@ -316,6 +316,9 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
       atomicOr(&L.bits[k >> 5], 1u << (k & 31));
     }
   }
+#if defined(MIREC_GRP_STOP)          // timing probes only (tools/build_variant.sh)
+  if (MIREC_GRP_STOP == 1) return;
+#endif
   // 2. sort of the composites key << pbits | position (distinct values: stability comes
   //    free). Bucket by the key's top bits (<= 4,096 buckets, LDS counters: atomics give
   //    each element a slot in its bucket in any order), scan the counts, scatter, then
@@ -379,6 +382,9 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     }
   }
   __syncthreads();
+#if defined(MIREC_GRP_STOP)
+  if (MIREC_GRP_STOP == 2) return;
+#endif
   // 3. segments: heads of equal-key runs, uniq / seg / perm
   const uint32_t* S = L.xa;
   int32_t* __restrict__ perm = J.perm + (int64_t)b * per;
@@ -416,6 +422,9 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     J.nu[b] = nu;
   }
   __syncthreads();
+#if defined(MIREC_GRP_STOP)
+  if (MIREC_GRP_STOP == 3) return;
+#endif
   // 4. K35 records (step_prep_kernel roles 1 and 2, from LDS)
   if (J.rec != nullptr) {
     int32_t* __restrict__ rec = J.rec + (int64_t)b * rec_ints(per);
@@ -455,6 +464,9 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     for (int e = tid; e < per; e += kGrpThreads)
       contrib_record_lds((int)(S[e] & pm), tb, Bc, T, L.uk, L.ik, crec + (int64_t)e * kRecInts);
   }
+#if defined(MIREC_GRP_STOP)
+  if (MIREC_GRP_STOP == 4) return;
+#endif
   // 5. look-ahead list of batch b-1: this batch's rows that batch b-1 does not touch
   if (ahead) {
     int32_t* __restrict__ out = J.ahead + (int64_t)(b - 1) * per;
