@@ -472,13 +472,15 @@ constexpr int kSpecMaxKeys = 1024;       // keys per batch (LDS)
 constexpr int kSpecFinCap = 256;         // round-0 rejections a candidate may resolve
 constexpr int kSpecRounds = 64;          // refill rounds a candidate may take
 constexpr int kSpecGroup = 16;           // round-0 words with their loads in flight
+constexpr int kSpecCommitLds = 6144;     // resolve results the commit stages in LDS
 
 struct SpecPlan {
   int32_t nb;                            // batches
   int32_t lo[kSpecMaxBatches];           // candidates of batch b: R = lo[b] + c, c < W[b]
   int32_t W[kSpecMaxBatches];
   int32_t cand0[kSpecMaxBatches + 1];    // first candidate index of batch b (prefix of W)
-  int32_t xblocks;                       // blocks per XCD slice of the grid
+  int32_t xblocks;                       // blocks per XCD slice of the resolve grid
+  int64_t mbase[kSpecMaxBatches + 1];    // batch b's rejection masks: words from mbase[b]
 };
 
 // block g of the spec grid -> (batch, first candidate): batch b's blocks sit on the
@@ -501,15 +503,71 @@ __device__ __forceinline__ bool spec_block(const SpecPlan& P, int g, int& b, int
 
 __device__ __forceinline__ int64_t wrap_pos(int64_t p, int64_t L) { return p < L ? p : p % L; }
 
-__global__ __launch_bounds__(kSpecWaves * 64) void walk_spec_kernel(
+// Round 0 of every candidate, key-major (walk_mask_kernel): candidate c of batch b tests
+// slot t = j*Kb + k against value rl[s_b + lo_b + c + t] — for a fixed slot the
+// candidates read CONSECUTIVE values and one key's used-id row. So one wave per
+// (batch, key) runs its num slots with the candidates across its lanes: the value loads
+// are coalesced, the membership loads stay inside one bitmap row (a few cache lines),
+// and a ballot per 64 candidates writes the slot's rejection bits M[b][t][c / 64].
+// (One wave per candidate made 2,048 random row loads per wave: 183 candidates of a
+// 4-batch chunk took 34 us.)
+__global__ __launch_bounds__(kSpecWaves * 64) void walk_mask_kernel(
     const int32_t* __restrict__ rl, int64_t L, const int64_t* __restrict__ pr_dev,
     const int64_t* __restrict__ keys, int32_t Kb, int32_t num, UsedSet used, int64_t key_space,
-    int reject, SpecPlan P, int32_t* __restrict__ rtab, int32_t* __restrict__ n0tab,
-    int2* __restrict__ fin, int64_t* __restrict__ s0_out) {
+    int reject, SpecPlan P, uint64_t* __restrict__ M, int64_t* __restrict__ s0_out) {
+  const int64_t s0 = pr_dev[0] % L;
+  if (blockIdx.x == 0 && threadIdx.x == 0) s0_out[0] = s0;   // the later launches' start
+  const int64_t gw = (int64_t)blockIdx.x * kSpecWaves + (threadIdx.x >> 6);
+  const int b = (int)(gw / Kb);
+  const int k = (int)(gw - (int64_t)b * Kb);
+  if (b >= P.nb) return;                                      // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int64_t key = keys[(int64_t)b * Kb + k];
+  const bool valid = reject && key >= 0 && key < key_space;
+  const int total = Kb * num;
+  const int W = P.W[b];
+  const int nW = (W + 63) >> 6;
+  const int64_t sb = (s0 + (int64_t)b * total + P.lo[b]) % L;
+  uint64_t* __restrict__ Mb = M + P.mbase[b];
+  // the (j, c) words of this key, kMaskGroup at a time: every value load of the group,
+  // then every membership load, then the ballots
+  constexpr int kMaskGroup = 16;
+  const int nwords = num * nW;
+  for (int q0 = 0; q0 < nwords; q0 += kMaskGroup) {
+    int32_t v[kMaskGroup];
+    bool act[kMaskGroup];
+#pragma unroll
+    for (int i = 0; i < kMaskGroup; ++i) {
+      const int q = q0 + i;
+      const int j = q / nW, c = q - j * nW;
+      const int d = c * 64 + lane;
+      act[i] = valid && q < nwords && d < W;
+      v[i] = act[i] ? rl[wrap_pos(sb + j * Kb + k + d, L)] : 0;
+    }
+    int rej[kMaskGroup];
+#pragma unroll
+    for (int i = 0; i < kMaskGroup; ++i) rej[i] = act[i] && is_used(used, key, v[i]) ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < kMaskGroup; ++i) {
+      const int q = q0 + i;
+      const uint64_t m = __ballot(rej[i]);
+      if (lane == 0 && q < nwords) {
+        const int j = q / nW, c = q - j * nW;
+        Mb[(int64_t)(j * Kb + k) * nW + c] = m;
+      }
+    }
+  }
+}
+
+// Per candidate (one wave): its round-0 rejections from the masks, then its refill rounds.
+__global__ __launch_bounds__(kSpecWaves * 64) void walk_spec_kernel(
+    const int32_t* __restrict__ rl, int64_t L, const int64_t* __restrict__ s0_in,
+    const int64_t* __restrict__ keys, int32_t Kb, int32_t num, UsedSet used, int64_t key_space,
+    int reject, SpecPlan P, const uint64_t* __restrict__ M, int32_t* __restrict__ rtab,
+    int32_t* __restrict__ n0tab, int2* __restrict__ fin) {
   __shared__ int32_t K[kSpecMaxKeys];
   __shared__ uint16_t lst[kSpecWaves][kSpecMaxTotal];
-  const int64_t s0 = pr_dev[0] % L;
-  if (blockIdx.x == 0 && threadIdx.x == 0) s0_out[0] = s0;   // the commit's start
+  const int64_t s0 = s0_in[0];
   int b, c0;
   if (!spec_block(P, blockIdx.x, b, c0)) return;              // block-uniform
   const int64_t* __restrict__ bkeys = keys + (int64_t)b * Kb;
@@ -526,26 +584,23 @@ __global__ __launch_bounds__(kSpecWaves * 64) void walk_spec_kernel(
   const uint64_t lt = (1ull << lane) - 1ull;
   const int64_t s = (s0 + (int64_t)b * total + P.lo[b] + c) % L;
   uint16_t* __restrict__ l = lst[wave];
-  // round 0: kSpecGroup 64-slot words at a time, their value and membership loads in flight
+  const int nW = (P.W[b] + 63) >> 6;
+  const uint64_t* __restrict__ Mb = M + P.mbase[b] + (c >> 6);
+  const int cb = c & 63;
+  // round 0: the candidate's bit of every slot's mask, kSpecGroup words in flight
   int n0 = 0;
   for (int w0 = 0; w0 * 64 < total; w0 += kSpecGroup) {
-    int32_t v[kSpecGroup];
-    int32_t key[kSpecGroup];
+    uint64_t mw[kSpecGroup];
 #pragma unroll
     for (int i = 0; i < kSpecGroup; ++i) {
       const int t = (w0 + i) * 64 + lane;
-      v[i] = t < total ? rl[wrap_pos(s + t, L)] : 0;
-      key[i] = t < total ? K[t % Kb] : -1;
+      mw[i] = t < total ? Mb[(int64_t)t * nW] : 0ull;
     }
-    int rej[kSpecGroup];
-#pragma unroll
-    for (int i = 0; i < kSpecGroup; ++i)
-      rej[i] = (reject && key[i] >= 0 && is_used(used, key[i], v[i])) ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < kSpecGroup; ++i) {
-      const uint64_t m = __ballot(rej[i]);
-      if (rej[i] && n0 + __popcll(m & lt) < kSpecMaxTotal)
-        l[n0 + __popcll(m & lt)] = (uint16_t)((w0 + i) * 64 + lane);
+      const int rej = (int)((mw[i] >> cb) & 1ull);
+      const uint64_t m = __ballot(rej);
+      if (rej) l[n0 + __popcll(m & lt)] = (uint16_t)((w0 + i) * 64 + lane);
       n0 += __popcll(m);
     }
   }
@@ -598,6 +653,7 @@ __global__ __launch_bounds__(kSampThreads) void walk_commit_kernel(
   __shared__ WalkLds S;
   __shared__ int32_t Rs[kSpecMaxBatches + 1];
   __shared__ int s_fail;
+  __shared__ int32_t rt[kSpecCommitLds];      // the resolve results (one load level)
   const int b = blockIdx.x;
   const int64_t total = (int64_t)Kb * num;
   const int64_t s0 = s0_in[0];
@@ -609,12 +665,18 @@ __global__ __launch_bounds__(kSampThreads) void walk_commit_kernel(
       ikeys_dst[(int64_t)b * key_stride + k] = items[(int64_t)b * Kb + k];
     }
   }
+  const int ncand = P.cand0[P.nb];
+  const bool lds_rt = ncand <= kSpecCommitLds;
+  if (lds_rt)
+    for (int i = threadIdx.x; i < ncand; i += kSampThreads) rt[i] = rtab[i];
+  __syncthreads();
   if (threadIdx.x == 0) {                     // chain the starts (a lookup per batch)
     int32_t R = 0;
     int f = P.nb;
     for (int q = 0; q < P.nb; ++q) {
       const int idx = R - P.lo[q];
-      const int32_t rq = (idx >= 0 && idx < P.W[q]) ? rtab[P.cand0[q] + idx] : -1;
+      const int32_t rq = (idx >= 0 && idx < P.W[q])
+                             ? (lds_rt ? rt[P.cand0[q] + idx] : rtab[P.cand0[q] + idx]) : -1;
       Rs[q] = R;
       if (rq < 0) { f = q; break; }
       R += rq;
@@ -879,6 +941,17 @@ SpecShape spec_plan(int nb, double mean, double sd) {
   sh.cands = c;
   return sh;
 }
+
+// rejection-mask words of a plan (walk_mask_kernel), and each batch's base
+int64_t spec_masks(SpecPlan& P, int64_t total) {
+  int64_t w = 0;
+  for (int b = 0; b < P.nb; ++b) {
+    P.mbase[b] = w;
+    w += total * ((P.W[b] + 63) / 64);
+  }
+  P.mbase[P.nb] = w;
+  return w;
+}
 }  // namespace
 
 extern "C" size_t mirec_sample_walk_spec_workspace_size(int64_t batch_keys, int64_t num,
@@ -886,10 +959,11 @@ extern "C" size_t mirec_sample_walk_spec_workspace_size(int64_t batch_keys, int6
                                                         double r_sd) {
   if (batch_keys <= 0 || num <= 0 || max_batches <= 0) return 256;
   const int nb = (int)std::min<int64_t>(max_batches, kSpecMaxBatches);
-  const int64_t cands = spec_plan(nb, r_mean, r_sd).cands;
-  // serial-walk lists | s0 | rtab | n0tab | fin
-  return mirec_sample_walk_workspace_size(batch_keys, num) + 16 + (size_t)cands * 8 +
-         (size_t)cands * kSpecFinCap * sizeof(int2) + 256;
+  SpecShape sh = spec_plan(nb, r_mean, r_sd);
+  const int64_t masks = spec_masks(sh.P, batch_keys * num);
+  // serial-walk lists | s0 | rtab | n0tab | fin | masks
+  return mirec_sample_walk_workspace_size(batch_keys, num) + 16 + (size_t)sh.cands * 8 +
+         (size_t)sh.cands * kSpecFinCap * sizeof(int2) + (size_t)masks * 8 + 512;
 }
 
 extern "C" int mirec_sample_walk_spec(const int32_t* random_list, int64_t L, int64_t* pr_dev,
@@ -942,16 +1016,25 @@ extern "C" int mirec_sample_walk_spec(const int32_t* random_list, int64_t L, int
   hipStream_t st = (hipStream_t)stream;
   for (int64_t b0 = 0; b0 < n_batches; b0 += kSpecMaxBatches) {
     const int nb = (int)std::min<int64_t>(kSpecMaxBatches, n_batches - b0);
-    const SpecShape sh = spec_plan(nb, r_mean, r_sd);
+    SpecShape sh = spec_plan(nb, r_mean, r_sd);
+    spec_masks(sh.P, total);
     int32_t* rtab = (int32_t*)q;
     int32_t* n0tab = rtab + sh.cands;
     int2* fin = (int2*)(((uintptr_t)(n0tab + sh.cands) + 15) & ~(uintptr_t)15);
+    uint64_t* masks = (uint64_t*)(fin + sh.cands * kSpecFinCap);
     const int64_t* ub = users + b0 * batch_keys;
-    hipLaunchKernelGGL(walk_spec_kernel, dim3((unsigned)(8 * sh.P.xblocks)),
+    const int64_t mwaves = (int64_t)nb * batch_keys;
+    hipLaunchKernelGGL(walk_mask_kernel, dim3((unsigned)((mwaves + kSpecWaves - 1) / kSpecWaves)),
                        dim3(kSpecWaves * 64), 0, st, random_list, L, pr_dev, ub,
-                       (int32_t)batch_keys, (int32_t)num, u, n_key_space, reject, sh.P, rtab,
-                       n0tab, fin, s0);
+                       (int32_t)batch_keys, (int32_t)num, u, n_key_space, reject, sh.P, masks,
+                       s0);
     int rc = launch_status(what);
+    if (rc) return rc;
+    hipLaunchKernelGGL(walk_spec_kernel, dim3((unsigned)(8 * sh.P.xblocks)),
+                       dim3(kSpecWaves * 64), 0, st, random_list, L, s0, ub,
+                       (int32_t)batch_keys, (int32_t)num, u, n_key_space, reject, sh.P, masks,
+                       rtab, n0tab, fin);
+    rc = launch_status(what);
     if (rc) return rc;
     hipLaunchKernelGGL(walk_commit_kernel, dim3((unsigned)(nb + 1)), dim3(kSampThreads), 0, st,
                        random_list, L, pr_dev, s0, ub, items ? items + b0 * batch_keys : nullptr,

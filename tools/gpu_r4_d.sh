@@ -5,6 +5,11 @@ set -u
 export TMPDIR=/tmp
 O=gpurun_out/r4d
 mkdir -p $O
+PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
+timeout -k 10 400 $PT tests/test_gpu_spec_walk.py tests/test_gpu_chain.py > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 10
+timeout -k 10 200 python tools/probe_prep.py --reps 30 > $O/probe.log 2>&1 || { tail $O/probe.log; exit 3; }
+grep '^{' $O/probe.log
 for v in 1 2 3 4; do
   MIREC_LIB=recbole_amd/_lib/alt/grp$v.so timeout -k 10 200 python tools/probe_prep.py --reps 30 > $O/grp$v.log 2>&1 || { tail $O/grp$v.log; exit 3; }
   echo "grp$v $(grep '"batches": 4' $O/grp$v.log)"
