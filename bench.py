@@ -375,7 +375,13 @@ def gather_throughput(step, d, neg, B=65536, reps=20, big_rows=2_000_000):
     EI = torch.randn(big_rows, d, device=dev, generator=g) * 0.1
     t = one(EU, EI, big_rows, big_rows)
     del EU, EI
-    traffic, tsrc = pmc_bytes('gather_big')
+    traffic, tsrc = None, None        # PMC HBM bytes of the same launch (tools/gather_pmc.py)
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_gather.json')))[::-1]:
+        big = [e for e in json.load(open(path)) if e.get('tables') == 'big']
+        if big and big[0].get('table_rows') == [big_rows, big_rows]:
+            traffic, tsrc = big[0].get('traffic'), os.path.basename(path)
+            break
     gbs = nbytes / t / 1e9
     return {'kernel': f'K3 bpr_fwd_bwd<{d}> at B={B} positives, tables {big_rows:,} + '
                       f'{big_rows:,} rows ({2 * big_rows * d * 4 / 2**30:.2f} GiB: past the LLC)',
