@@ -26,5 +26,6 @@ run r20 "" --ramp 20 || exit 6
 run r16 "" --ramp 16 || exit 6
 run r12 "" --ramp 12 || exit 6
 run r8 "" --ramp 8 || exit 6
+run r20mf "" --ramp 20 --main-first || exit 6
 run w5 "MIREC_LIB=recbole_amd/_lib/alt/k35_w5.so" || exit 6
 run w5r20 "MIREC_LIB=recbole_amd/_lib/alt/k35_w5.so" --ramp 20 || exit 6
