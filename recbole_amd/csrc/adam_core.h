@@ -235,13 +235,56 @@ __device__ __forceinline__ float div_bc2s_finite(float x, const StepConsts& sc) 
 // checks it) and so |num| and den (bc2s non-decreasing) never increase, and every
 // operation involved is monotone, so the bounds at the two ends hold for the
 // steps between them.
+// The fast-path increments two at a time on gfx950's packed fp32 pipe (v_pk_fma_f32 /
+// v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 operations per lane and instruction, each
+// rounded as its scalar form), for G*N independent (step, element) pairs. Same operations,
+// same roundings, same order per value as sqrt_rn_normal / div_bc2s_finite / div_rn_normal.
+typedef float mirec_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ mirec_f2 pk_fma(mirec_f2 a, mirec_f2 b, mirec_f2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+
+// q = RN(RN(-ss*me) / den), den = RN(RN(RN(sqrt(ve)) / bc2s) + eps), for two pairs at once
+// (each pair with its own step constants)
+__device__ __forceinline__ mirec_f2 incr_pair(mirec_f2 me, mirec_f2 ve, mirec_f2 ss,
+                                              mirec_f2 bc2s, mirec_f2 rbc, float eps) {
+  // sqrt_rn_normal, component-wise selects
+  const mirec_f2 s = {__builtin_amdgcn_sqrtf(ve.x), __builtin_amdgcn_sqrtf(ve.y)};
+  const mirec_f2 sd = {__uint_as_float(__float_as_uint(s.x) - 1u),
+                       __uint_as_float(__float_as_uint(s.y) - 1u)};
+  const mirec_f2 su = {__uint_as_float(__float_as_uint(s.x) + 1u),
+                       __uint_as_float(__float_as_uint(s.y) + 1u)};
+  const mirec_f2 rd = pk_fma(-sd, s, ve);
+  const mirec_f2 ru = pk_fma(-su, s, ve);
+  mirec_f2 sq;
+  sq.x = ru.x > 0.f ? su.x : (rd.x <= 0.f ? sd.x : s.x);
+  sq.y = ru.y > 0.f ? su.y : (rd.y <= 0.f ? sd.y : s.y);
+  // div_bc2s_finite + eps
+  const mirec_f2 q = sq * rbc;
+  const mirec_f2 den = pk_fma(pk_fma(-q, bc2s, sq), rbc, q) + (mirec_f2){eps, eps};
+  // div_rn_normal(-ss * me, den)
+  const mirec_f2 a = (-ss) * me;
+  const mirec_f2 y0 = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  const mirec_f2 one = {1.0f, 1.0f};
+  const mirec_f2 e = pk_fma(-den, y0, one);
+  const mirec_f2 y = pk_fma(e, y0, y0);
+  const mirec_f2 q0 = a * y;
+  const mirec_f2 r0 = pk_fma(-den, q0, a);
+  const mirec_f2 q1 = pk_fma(r0, y, q0);
+  const mirec_f2 r1 = pk_fma(-den, q1, a);
+  return pk_fma(r1, y, q1);
+}
+
 template <int G, int N>
 __device__ __forceinline__ void incr_steps(const float (*me)[N], const float (*ve)[N],
                                            const StepConsts* sc, const AdamConsts& k,
                                            float (*q)[N]) {
   float num[G][N], den[G][N];
+  // range conditions at the group's first and last step (see below); the values they
+  // test are recomputed in the paired path exactly as here
 #pragma unroll
-  for (int j = 0; j < G; ++j)
+  for (int j = 0; j < G; j += (G > 1 ? G - 1 : 1))
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       den[j][i] = div_bc2s_finite(sqrt_rn_normal(ve[j][i]), sc[j]) + k.eps;
@@ -254,16 +297,38 @@ __device__ __forceinline__ void incr_steps(const float (*me)[N], const float (*v
           (int)(fabsf(num[0][i]) <= 0x1p40f) & (int)(fabsf(num[G - 1][i]) >= 0x1p-60f) &
           (int)(den[0][i] <= 0x1p40f) & (int)(den[G - 1][i] >= 0x1p-40f);
   if (__all(ok)) {
+    constexpr int NE = G * N;
+#if defined(MIREC_NO_PK)                        // probe build: the scalar form
 #pragma unroll
-    for (int j = 0; j < G; ++j)
+    for (int e = 0; e < NE; ++e) {
+      const int j = e / N, i = e % N;
+      q[j][i] = div_rn_normal((-sc[j].ss) * me[j][i],
+                              div_bc2s_finite(sqrt_rn_normal(ve[j][i]), sc[j]) + k.eps);
+    }
+    return;
+#endif
 #pragma unroll
-      for (int i = 0; i < N; ++i) q[j][i] = div_rn_normal(num[j][i], den[j][i]);
+    for (int e = 0; e + 1 < NE; e += 2) {
+      const int ja = e / N, ia = e % N, jb = (e + 1) / N, ib = (e + 1) % N;
+      const mirec_f2 r = incr_pair((mirec_f2){me[ja][ia], me[jb][ib]},
+                                   (mirec_f2){ve[ja][ia], ve[jb][ib]},
+                                   (mirec_f2){sc[ja].ss, sc[jb].ss},
+                                   (mirec_f2){sc[ja].bc2s, sc[jb].bc2s},
+                                   (mirec_f2){sc[ja].rbc, sc[jb].rbc}, k.eps);
+      q[ja][ia] = r.x;
+      q[jb][ib] = r.y;
+    }
+    if (NE & 1) {                               // an odd count: the last one alone
+      constexpr int jl = (NE - 1) / N, il = (NE - 1) % N;
+      const float dl = div_bc2s_finite(sqrt_rn_normal(ve[jl][il]), sc[jl]) + k.eps;
+      q[jl][il] = div_rn_normal((-sc[jl].ss) * me[jl][il], dl);
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < G; ++j)
 #pragma unroll
       for (int i = 0; i < N; ++i)
-        q[j][i] = num[j][i] / (div_bc2s(sqrtf(ve[j][i]), sc[j]) + k.eps);
+        q[j][i] = ((-sc[j].ss) * me[j][i]) / (div_bc2s(sqrtf(ve[j][i]), sc[j]) + k.eps);
   }
 }
 

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r4d
 mkdir -p $O
 PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
-timeout -k 10 400 $PT tests/test_gpu_spec_walk.py tests/test_gpu_chain.py > $O/tests.log 2>&1
+timeout -k 10 500 $PT tests/test_gpu_spec_walk.py tests/test_gpu_chain.py tests/test_gpu_kernels.py -k "adam or flush or spec or chain" > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit 10
 timeout -k 10 200 python tools/probe_prep.py --reps 30 > $O/probe.log 2>&1 || { tail $O/probe.log; exit 3; }
 grep '^{' $O/probe.log
@@ -22,6 +22,7 @@ run() {   # name "env assignments" bench-args...
   done
 }
 run default "" || exit 6
+run nopk "MIREC_LIB=recbole_amd/_lib/alt/nopk.so" || exit 6
 run r20 "" --ramp 20 || exit 6
 run r16 "" --ramp 16 || exit 6
 run r12 "" --ramp 12 || exit 6
