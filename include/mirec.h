@@ -711,6 +711,16 @@ int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* l
 
 /* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
 int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);
+/* Several column sums in ONE launch (up to 4 jobs: out[q][j] = sum_i x[q][i*m[q] + j],
+ * x[q] of n[q] rows): each job summed exactly as mirec_colsum_f32 sums it (same tile, same
+ * order), the three of a DeepFM backward (float fields, their first-order terms, the bias)
+ * in one launch. HOST arrays of device pointers and sizes. */
+int mirec_colsum_multi_f32(const float* const* x, const int64_t* n, const int64_t* m,
+                           float* const* out, int32_t n_jobs, void* stream);
+/* keys[f*B + i] = cols[f][i] + offsets[f] for n_fields <= 64 int64 id columns (HOST array of
+ * device pointers; HOST offsets): DeepFM's token keys in the shared table, one launch. */
+int mirec_offset_keys(const int64_t* const* cols, const int64_t* offsets, int32_t n_fields,
+                      int64_t B, int64_t* out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K10  DeepFM's deep part (recbole/model/layers.py:30-86 MLPLayers: Dropout -> Linear

@@ -175,6 +175,8 @@ SIGNATURES = {
                                         _P, _P, _P, _P, _P, _P, _P, _P, c_int32, c_double,
                                         c_double, c_double, c_double, _P]),
     "mirec_step_record_ints": (c_int64, [c_int64]),
+    "mirec_colsum_multi_f32": (c_int, [_P, _P, _P, _P, c_int32, _P]),
+    "mirec_offset_keys": (c_int, [_P, _P, c_int32, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_at_ids_f32": (c_int, [_P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
                                              ctypes.c_float, ctypes.c_float, _P, _P, _P]),
     "mirec_chunk_group": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64] + [_P] * 16

@@ -233,6 +233,79 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   }
 }
 
+// Several column sums in ONE launch (DeepFM's float-field [B, nf*d] and [B, nf] gradients
+// and the bias [B, 1]: three launches before): block b takes the job whose block range holds
+// it and runs colsum_kernel's body with that job's column tile — the same tile choice as
+// mirec_colsum_f32 for its width, so every sum is the one-launch form's bit for bit.
+constexpr int kColsumJobs = 4;
+struct ColsumJobs {
+  const float* x[kColsumJobs];
+  float* out[kColsumJobs];
+  int64_t n[kColsumJobs], m[kColsumJobs];
+  int32_t cb[kColsumJobs];
+  int64_t block_start[kColsumJobs + 1];
+  int n_jobs;
+};
+
+template <int CB>
+__device__ __forceinline__ void colsum_tile(const float* __restrict__ x, int64_t n, int64_t m,
+                                            float* __restrict__ out, int64_t tile,
+                                            float* part) {     // [RG][CB + 1]
+  constexpr int RG = 1024 / CB;
+  const int c = threadIdx.x % CB, r = threadIdx.x / CB;
+  const int64_t j = tile * CB + c;
+  float s = 0.f;
+  if (j < m) {
+    constexpr int U = 8;
+    int64_t i = r;
+    for (; i + (U - 1) * RG < n; i += U * RG) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = x[(i + u * RG) * m + j];
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += v[u];
+    }
+    for (; i < n; i += RG) s += x[i * m + j];
+  }
+  part[r * (CB + 1) + c] = s;
+  __syncthreads();
+  if (r == 0 && j < m) {
+    float t = 0.f;
+    for (int q = 0; q < RG; ++q) t += part[q * (CB + 1) + c];
+    out[j] = t;
+  }
+}
+
+__global__ __launch_bounds__(1024) void colsum_multi_kernel(const ColsumJobs J) {
+  __shared__ float part[2048];         // [RG][CB + 1] of the largest form (CB = 1: 1024 x 2)
+  int q = 0;
+#pragma unroll
+  for (int t = 1; t < kColsumJobs; ++t)
+    if (t < J.n_jobs && (int64_t)blockIdx.x >= J.block_start[t]) q = t;
+  const int64_t tile = (int64_t)blockIdx.x - J.block_start[q];
+  if (J.cb[q] == 64)
+    colsum_tile<64>(J.x[q], J.n[q], J.m[q], J.out[q], tile, part);
+  else if (J.cb[q] == 8)
+    colsum_tile<8>(J.x[q], J.n[q], J.m[q], J.out[q], tile, part);
+  else
+    colsum_tile<1>(J.x[q], J.n[q], J.m[q], J.out[q], tile, part);
+}
+
+// keys[f * B + i] = cols[f][i] + offsets[f]: DeepFM's token keys (every token field's ids at
+// its offset in the shared table) in one launch (a stack + add in torch: two)
+constexpr int kKeyFields = 64;
+struct KeyFields {
+  const int64_t* col[kKeyFields];
+  int64_t off[kKeyFields];
+};
+
+__global__ __launch_bounds__(256) void offset_keys_kernel(const KeyFields F, int n_fields,
+                                                          int64_t B, int64_t* __restrict__ out) {
+  const int f = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256)
+    out[(int64_t)f * B + i] = F.col[f][i] + F.off[f];
+}
+
 static unsigned ctx_grid(int64_t B, int lps) {
   const int64_t spb = (kCtxThreads / 64) * (64 / lps);
   return (unsigned)((B + spb - 1) / spb);
@@ -314,6 +387,64 @@ extern "C" int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, con
   hipLaunchKernelGGL(sigmoid_bce_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, y_fm, y_deep, label, B, grad_scale, prob, loss, dz);
   return launch_status("mirec_sigmoid_bce_f32");
+}
+
+extern "C" int mirec_colsum_multi_f32(const float* const* x, const int64_t* n, const int64_t* m,
+                                      float* const* out, int32_t n_jobs, void* stream) {
+  if (n_jobs < 0 || n_jobs > kColsumJobs || (n_jobs > 0 && (!x || !n || !m || !out))) {
+    set_error("mirec_colsum_multi_f32: bad arguments (at most %d jobs)", kColsumJobs);
+    return -1;
+  }
+  ColsumJobs J;
+  memset(&J, 0, sizeof(J));
+  int64_t blocks = 0;
+  int k = 0;
+  for (int q = 0; q < n_jobs; ++q) {
+    if (m[q] == 0) continue;
+    if (!x[q] || !out[q] || n[q] < 0 || m[q] < 0) {
+      set_error("mirec_colsum_multi_f32: bad job %d", q);
+      return -1;
+    }
+    const int cb = m[q] >= 64 ? 64 : (m[q] >= 8 ? 8 : 1);   // mirec_colsum_f32's tile
+    J.x[k] = x[q];
+    J.out[k] = out[q];
+    J.n[k] = n[q];
+    J.m[k] = m[q];
+    J.cb[k] = cb;
+    J.block_start[k] = blocks;
+    blocks += (m[q] + cb - 1) / cb;
+    ++k;
+  }
+  J.n_jobs = k;
+  for (int q = k; q <= kColsumJobs; ++q) J.block_start[q] = blocks;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3((unsigned)blocks), dim3(1024), 0,
+                     (hipStream_t)stream, J);
+  return launch_status("mirec_colsum_multi_f32");
+}
+
+extern "C" int mirec_offset_keys(const int64_t* const* cols, const int64_t* offsets,
+                                 int32_t n_fields, int64_t B, int64_t* out, void* stream) {
+  if (n_fields < 0 || n_fields > kKeyFields || B < 0 || (n_fields > 0 && B > 0 &&
+      (!cols || !offsets || !out))) {
+    set_error("mirec_offset_keys: bad arguments (at most %d fields)", kKeyFields);
+    return -1;
+  }
+  if (n_fields == 0 || B == 0) return 0;
+  KeyFields F;
+  memset(&F, 0, sizeof(F));
+  for (int f = 0; f < n_fields; ++f) {
+    if (!cols[f]) {
+      set_error("mirec_offset_keys: field %d has no column", f);
+      return -1;
+    }
+    F.col[f] = cols[f];
+    F.off[f] = offsets[f];
+  }
+  const unsigned gx = (unsigned)std::min<int64_t>((B + 255) / 256, 64);
+  hipLaunchKernelGGL(offset_keys_kernel, dim3(gx, (unsigned)n_fields), dim3(256), 0,
+                     (hipStream_t)stream, F, n_fields, B, out);
+  return launch_status("mirec_offset_keys");
 }
 
 extern "C" int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream) {

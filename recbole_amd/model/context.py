@@ -159,10 +159,13 @@ class _CtxFMFn(torch.autograd.Function):
         keys = torch.empty(len(layout.token_names) * B, dtype=torch.int64, device=bias.device)
         h = getattr(T, '_mirec_deferred', None) if T is not None else None
         if h is not None:                     # deferred Adam: complete the rows read
-            off = layout.offsets_on(bias.device)
-            keys.view(len(layout.token_names), B).copy_(
-                torch.stack([_col(interaction, n, torch.int64) for n in layout.token_names])
-                + off.unsqueeze(1))
+            # keys[f*B + i] = id + the field's table offset, every field in one launch
+            cols = [_col(interaction, n, torch.int64) for n in layout.token_names]
+            nt = len(cols)
+            cptr = (ctypes.c_void_p * nt)(*[ptr(x) for x in cols])
+            offs = (ctypes.c_int64 * nt)(*layout.token_offsets)
+            check(lib().mirec_offset_keys(cptr, offs, nt, B, ptr(keys), stream_handle()),
+                  'mirec_offset_keys')
             # one key block per field (ranges increase with the field offsets): K2
             # sorts each field's B keys in LDS instead of a device-wide radix sort
             blocks = B if (layout.blocks_ok and 0 < B <= 8192 and len(layout.token_names) > 1) \
@@ -218,16 +221,19 @@ class _CtxFMFn(torch.autograd.Function):
                 ctx.deferred_T1._mirec_deferred.stash(ctx.deferred_T1, grads['T1'], keys, segs)
             else:
                 dT1 = ops.segment_scatter_add(grads['T1'], segs, torch.zeros_like(tables['T1']))
+        # the float-field, first-order float and bias gradients: column sums, one launch
+        dbias = torch.empty(1, dtype=torch.float32, device=dev)
+        jobs = [(g_fm, 1, dbias)]
         if nf:
             dEf = torch.empty_like(tables['Ef'])
-            check(lib().mirec_colsum_f32(ptr(grads['Ef']), B, nf * d, ptr(dEf), stream_handle()),
-                  "mirec_colsum_f32")
             dEf1 = torch.empty_like(tables['Ef1'])
-            check(lib().mirec_colsum_f32(ptr(grads['Ef1']), B, nf, ptr(dEf1), stream_handle()),
-                  "mirec_colsum_f32")
-        dbias = torch.empty(1, dtype=torch.float32, device=dev)
-        check(lib().mirec_colsum_f32(ptr(g_fm), B, 1, ptr(dbias), stream_handle()),
-              "mirec_colsum_f32")
+            jobs = [(grads['Ef'], nf * d, dEf), (grads['Ef1'], nf, dEf1)] + jobs
+        nj = len(jobs)
+        check(lib().mirec_colsum_multi_f32((ctypes.c_void_p * nj)(*[ptr(j[0]) for j in jobs]),
+                                           (ctypes.c_int64 * nj)(*[B] * nj),
+                                           (ctypes.c_int64 * nj)(*[j[1] for j in jobs]),
+                                           (ctypes.c_void_p * nj)(*[ptr(j[2]) for j in jobs]),
+                                           nj, stream_handle()), "mirec_colsum_multi_f32")
         dseq, dseq1 = [], []
         for i, ids in enumerate(seq_ids):
             segs = ops.segment_sort(ids.view(-1), tables['seq'][i].shape[0])
