@@ -545,8 +545,8 @@ template <typename V> struct AheadVec { using T = float; };
 #endif
 template <int D> struct StepRows { static constexpr int n = D <= 128 ? MIREC_STEP_RPB : 1; };
 #ifndef MIREC_STEP_WAVES
-#define MIREC_STEP_WAVES 6               // waves per SIMD the register budget allows
-#endif
+#define MIREC_STEP_WAVES 5               // waves per SIMD the register budget allows (6: 80
+#endif                                   // VGPRs, 28 B/lane spilled; 5: 86, no spill)
 
 template <int D>
 __global__ __launch_bounds__(D / Lanes<typename StepVec<D>::T>::n * StepRows<D>::n,

@@ -158,7 +158,12 @@ class FusedBPRTrainStep(object):
 
     CHUNK = 64
     SLOTS = 3                     # chunk buffers in flight (walk, grouping, model)
-    RAMP = (4, 8, 16, 32)         # chunk sizes after a (re)start of the prep pipeline
+    # chunk sizes after a (re)start of the prep pipeline. With the speculative walk and K36 a
+    # chunk's preparation is ~45 us for 8 batches, and a preparation issued beside the model's
+    # K35 steps mostly waits for CUs (K35 fills the chip): the C2 driver window (warm-up 5,
+    # 20 timed steps) measured 21.7-21.9 M positives/s with chunks of 8 then 12 against
+    # 20.8-21.2 M with 4, 8, 8 and 21.0-21.5 M with one chunk of 20
+    RAMP = (8, 16, 32)
     # deferred schedule: steps between full-table flushes (every row complete;
     # parameters are also complete at every epoch end / sync_params()). Rarer
     # flushes let idle rows reach the cheap replay regime (adam.hip
