@@ -258,6 +258,18 @@ size_t mirec_segment_sort_blocks_workspace_size(int64_t n, int64_t block_n);
 int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t block_n, int64_t key_space,
                               int32_t* perm, int32_t* uniq, int32_t* seg, int32_t* n_uniq_dev,
                               void* ws, size_t ws_bytes, void* stream);
+/* The same in ONE launch for block_n <= 4,096 and at most 256 blocks: each block sorts
+ * in LDS (8-bit digits over its own key span) and writes straight into the
+ * concatenated outputs after summing the unique counts of the blocks before it.
+ * status: int32[n_status >= n_blocks + 1], all zero before the first call; every call
+ * leaves it zero again (reuse one buffer per stream; two calls in flight at once need
+ * two buffers). The grouping of the token-field embedding gradient rows of
+ * reference recbole/model/layers.py:121-141 (FMEmbedding, called from
+ * abstract_recommender.py:260 embed_token_fields) before the deferred Adam. */
+int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n, int64_t block_n,
+                                      int64_t key_space, int32_t* perm, int32_t* uniq,
+                                      int32_t* seg, int32_t* n_uniq_dev, int32_t* status,
+                                      int64_t n_status, void* stream);
 
 /* Look-ahead lists of the deferred Adam: for b < n_batches-1,
  * out[b*stride ..) = uniq(b+1) \ uniq(b) ascending, n_out[b] its length, where

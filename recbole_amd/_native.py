@@ -136,6 +136,8 @@ SIGNATURES = {
     "mirec_segment_sort_blocks_workspace_size": (c_size_t, [c_int64, c_int64]),
     "mirec_segment_sort_blocks": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                           c_size_t, _P]),
+    "mirec_segment_sort_blocks_chained": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P,
+                                                  _P, c_int64, _P]),
     "mirec_prepare_chunk": (c_int, [_P, _P]),
     "mirec_prepare_chunk_walk": (c_int, [_P, _P]),
     "mirec_prepare_chunk_group": (c_int, [_P, _P]),

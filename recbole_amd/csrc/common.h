@@ -36,6 +36,22 @@ __device__ __forceinline__ int wave_sum_i(int x) {
   return x;
 }
 
+// Inclusive scan over the 64 lanes of a wave (every lane active): Hillis-Steele inside
+// each 16-lane row with DPP row shifts (a lane whose source falls outside its row keeps
+// 0), then the row totals (lanes 15, 31, 47) carried across rows with readlane. Four
+// DPP adds and three readlanes — no LDS round trip (a __shfl_up is a ds_bpermute).
+__device__ __forceinline__ int wave_inclusive_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(v, 15);
+  const int r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = (int)(threadIdx.x & 63) >> 4;
+  return v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+}
+
 // Block-wide exclusive scan of one int per thread (blockDim.x <= 1024,
 // multiple of 64). `lds` needs blockDim.x/64 + 1 ints. Returns the exclusive
 // prefix; *total gets the block sum. Contains __syncthreads(). Every lane reads
@@ -45,13 +61,7 @@ __device__ __forceinline__ int block_exclusive_scan(int x, int* lds, int* total)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
-  // inclusive scan within the wave
-  int v = x;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(v, off, 64);
-    if (lane >= off) v += y;
-  }
+  const int v = wave_inclusive_scan(x);
   if (lane == 63) lds[wid] = v;
   __syncthreads();
   int pre = 0, tot = 0;

@@ -197,44 +197,67 @@ __global__ __launch_bounds__(kSortThreads) void segsort_lds_kernel(
                     blockIdx.x, L);
 }
 
-// Bucket-rank form of the per-block LDS sort, for blocks of <= kBktMax keys whatever the
-// key space (DeepFM's field blocks: 2,048 keys of up to 10 M ids, which took six
-// barrier-bound 4-bit radix passes): the block's key range is cut into <= 4,096 buckets
-// by the top bits of (key - min); LDS counters give every key a slot in its bucket (in
-// any order), one scan places the buckets, and each key's final position is its
-// bucket's start + the number of (key, position) pairs of its bucket below its own — the
-// stable sort's order, the same perm / uniq / seg / n_uniq as segsort_lds_batch.
-constexpr int kBktThreads = 512;
-constexpr int kBktEpt = 8;
-constexpr int kBktMax = kBktThreads * kBktEpt;
-constexpr int kBktBits = 12;
-struct BucketLds {
-  int32_t hist[1 << kBktBits], bstart[1 << kBktBits];
-  int32_t bk[kBktMax], bp[kBktMax];      // (key, position) in bucket order
-  int32_t sk[kBktMax];                   // keys in sorted order
-  int scan[kBktThreads / 64 + 1];
-  int32_t kmin, kmax;
+// Per-block stable sort for blocks of <= kR8Max keys whatever the key space or the
+// duplicates (DeepFM's field blocks: 2,048 ids of up to 10 M rows, Zipf heads and
+// small-vocabulary fields alike): LSD passes of 8-bit digits over (key - the block's
+// minimum) — ceil(bits of the block's key span / 8) passes instead of 4-bit passes over
+// the table's id width. Wave w owns a contiguous run of 64-key chunks; in each chunk the
+// 8 digit-bit ballots intersect to every lane's set of same-digit lanes, so a key's rank
+// is (its digit's count in the wave's earlier chunks, an LDS counter [digit][wave] the
+// digit's leader lane advances) + (same-digit lanes below it). One block scan of the
+// 256 x 8 counters (digit-major) gives every (digit, wave) its output offset — stable,
+// no atomics. Same perm / uniq / seg / n_uniq as segsort_lds_batch.
+constexpr int kR8Threads = 512;
+constexpr int kR8Waves = kR8Threads / 64;
+constexpr int kR8Max = 4096;
+constexpr int kChainMaxBlocks = 256;       // chained look-back: at most 4 loads per lane
+struct R8Lds {
+  uint32_t k[2][kR8Max];                   // the block's keys (int32 bit patterns)
+  uint16_t v[2][kR8Max];                   // their positions in the block
+  uint16_t rank[kR8Max];                   // a key's rank among its digit in its wave
+  int hist[256 * kR8Waves];                // [digit][wave] counts, then their offsets
+  int scan[kR8Waves + 1];
+  int32_t kmin, kmax, base, last;
 };
 
-__global__ __launch_bounds__(kBktThreads) void segsort_bucket_kernel(
+#ifdef MIREC_R8_PROBE
+__device__ uint64_t g_r8_probe[16];
+#define R8T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_r8_probe[k] = wall_clock64(); } while (0)
+#define R8C(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_r8_probe[k] = clock64(); } while (0)
+extern "C" int mirec_r8_probe_read(uint64_t* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_r8_probe), sizeof(g_r8_probe)) == hipSuccess ? 0 : -1;
+}
+#else
+#define R8T(k) do {} while (0)
+#define R8C(k) do {} while (0)
+#endif
+// status == nullptr: block b writes its own perm / uniq / seg / n_uniq at b's offsets in
+// the outputs (block-local positions; blocks_concat_kernel joins them). status != nullptr
+// (chained, one launch): block b publishes its unique count in status[b] (count + 1,
+// release), sums the counts of blocks < b (acquire; every one of them was dispatched
+// before b and publishes without waiting, so the wait ends) and writes straight into the
+// concatenated outputs; the block that takes the last ticket in status[nblocks] zeroes
+// status again for the next launch.
+__global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
     const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n,
     int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
-    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all) {
-  __shared__ BucketLds L;
+    int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all,
+    int32_t* __restrict__ status) {
+  __shared__ R8Lds L;
+  R8T(0);
+  R8C(12);
   const int64_t b = blockIdx.x;
   const int n = (int)min((int64_t)batch_n, n_total - b * batch_n);
   const int64_t* __restrict__ keys = keys_all + b * batch_n;
-  const int tid = threadIdx.x;
-  int32_t k[kBktEpt];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   int lo = INT32_MAX, hi = INT32_MIN;
-#pragma unroll
-  for (int r = 0; r < kBktEpt; ++r) {
-    const int e = tid + r * kBktThreads;
-    k[r] = e < n ? (int32_t)keys[e] : 0;
-    if (e < n) {
-      lo = min(lo, k[r]);
-      hi = max(hi, k[r]);
-    }
+  for (int i = tid; i < n; i += kR8Threads) {
+    const int32_t kv = (int32_t)keys[i];
+    L.k[0][i] = (uint32_t)kv;
+    L.v[0][i] = (uint16_t)i;
+    lo = min(lo, kv);
+    hi = max(hi, kv);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -245,70 +268,148 @@ __global__ __launch_bounds__(kBktThreads) void segsort_bucket_kernel(
     L.kmin = INT32_MAX;
     L.kmax = INT32_MIN;
   }
-  for (int q = tid; q < (1 << kBktBits); q += kBktThreads) L.hist[q] = 0;
   __syncthreads();
-  if ((tid & 63) == 0) {
+  if (lane == 0) {
     atomicMin(&L.kmin, lo);
     atomicMax(&L.kmax, hi);
   }
   __syncthreads();
-  const int32_t kmin = L.kmin;
-  const uint32_t span = (uint32_t)(L.kmax - kmin);
-  int shift = 0;
-  while (shift < 32 && (span >> shift) >= (1u << kBktBits)) ++shift;
-  int slot[kBktEpt];
+  R8T(1);
+  const uint32_t kmin = (uint32_t)L.kmin;
+  const uint32_t span = n > 0 ? (uint32_t)L.kmax - kmin : 0u;
+  int bits = 0;
+  while (bits < 32 && (span >> bits) != 0u) ++bits;
+  const int nch = (n + 63) >> 6;
+  const int cpw = (nch + kR8Waves - 1) / kR8Waves;   // chunks of this wave: [wid*cpw, +cpw)
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int cur = 0;
+  for (int shift = 0; shift < bits; shift += 8) {
+    for (int q = tid; q < 256 * kR8Waves; q += kR8Threads) L.hist[q] = 0;
+    __syncthreads();                             // keys of the pass in place, counters zeroed
+#pragma unroll 1
+    for (int cc = 0; cc < cpw; ++cc) {           // rolled: a short code path (one pass of
+      const int i = (wid * cpw + cc) * 64 + lane;  // one block runs cold in the I-cache)
+      const bool valid = i < n;
+      const uint32_t dd = valid ? ((L.k[cur][i] - kmin) >> shift) & 255u : 0u;
+      uint64_t m = __ballot(valid);
 #pragma unroll
-  for (int r = 0; r < kBktEpt; ++r) {
-    const int e = tid + r * kBktThreads;
-    slot[r] = e < n ? atomicAdd(&L.hist[(uint32_t)(k[r] - kmin) >> shift], 1) : 0;
-  }
-  __syncthreads();
-  {
-    constexpr int kPer = (1 << kBktBits) / kBktThreads;
-    int c[kPer], sum = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      c[j] = L.hist[tid * kPer + j];
-      sum += c[j];
-    }
-    int tot;
-    int run = block_exclusive_scan(sum, L.scan, &tot);
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      L.bstart[tid * kPer + j] = run;
-      run += c[j];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kBktEpt; ++r) {
-    const int e = tid + r * kBktThreads;
-    if (e < n) {
-      const int q = L.bstart[(uint32_t)(k[r] - kmin) >> shift] + slot[r];
-      L.bk[q] = k[r];
-      L.bp[q] = e;
-    }
-  }
-  __syncthreads();
-  int32_t* __restrict__ perm = perm_all + b * batch_n;
-#pragma unroll
-  for (int r = 0; r < kBktEpt; ++r) {
-    const int e = tid + r * kBktThreads;
-    if (e < n) {
-      const int bi = (uint32_t)(k[r] - kmin) >> shift;
-      const int b0 = L.bstart[bi], c = L.hist[bi];
-      int rank = 0;
-      for (int f = 0; f < c; ++f) {
-        const int32_t kf = L.bk[b0 + f];
-        rank += (kf < k[r] || (kf == k[r] && L.bp[b0 + f] < e)) ? 1 : 0;
+      for (int bb = 0; bb < 8; ++bb) {           // same-digit lanes: AND of xnor(ballot, bit)
+        const int32_t sb = __builtin_amdgcn_sbfe((int32_t)dd, bb, 1);
+        const uint64_t bl = __ballot(sb != 0);
+        const uint64_t s64 = (uint64_t)(int64_t)sb;
+        m &= ~(bl ^ s64);
       }
-      L.sk[b0 + rank] = k[r];
-      perm[b0 + rank] = e;
+      const int r = __popcll(m & lt);
+      int* h = &L.hist[(int)dd * kR8Waves + wid];
+      const int before = valid ? *h : 0;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && r == 0) *h = before + __popcll(m);
+      __builtin_amdgcn_wave_barrier();
+      if (valid) L.rank[i] = (uint16_t)(before + r);
+    }
+    if (shift == 8) R8T(8);
+    __syncthreads();
+    {                                            // exclusive scan of the counters, digit-major
+      constexpr int per = 256 * kR8Waves / kR8Threads;
+      int c[per], sum = 0;
+#pragma unroll
+      for (int q = 0; q < per; ++q) {
+        c[q] = L.hist[tid * per + q];
+        sum += c[q];
+      }
+      int tot;
+      int run = block_exclusive_scan(sum, L.scan, &tot);
+#pragma unroll
+      for (int q = 0; q < per; ++q) {
+        L.hist[tid * per + q] = run;
+        run += c[q];
+      }
+    }
+    __syncthreads();
+    if (shift == 8) R8T(9);
+#pragma unroll 1
+    for (int cc = 0; cc < cpw; ++cc) {
+      const int i = (wid * cpw + cc) * 64 + lane;
+      if (i < n) {
+        const uint32_t kv = L.k[cur][i];
+        const int dst = L.hist[(int)(((kv - kmin) >> shift) & 255u) * kR8Waves + wid] + L.rank[i];
+        L.k[cur ^ 1][dst] = kv;
+        L.v[cur ^ 1][dst] = L.v[cur][i];
+      }
+    }
+    cur ^= 1;
+    if (shift == 8) R8T(10);
+    __syncthreads();                             // offsets read before the next zeroing
+    R8T(2 + shift / 8);
+  }
+  R8T(6);
+  const uint32_t* __restrict__ ks = L.k[cur];
+  const int per = (n + kR8Threads - 1) / kR8Threads;  // uniq / seg: one scan over runs of
+  const int i0 = min(n, tid * per), i1 = min(n, i0 + per);   // per keys a thread
+  int f = 0;
+  for (int i = i0; i < i1; ++i) f += (i == 0 || ks[i - 1] != ks[i]) ? 1 : 0;
+  int nu;
+  int o = block_exclusive_scan(f, L.scan, &nu);
+  const int64_t pos0 = b * (int64_t)batch_n;
+  int32_t *perm, *uniq, *seg;
+  int32_t voff;                                  // added to block-local positions
+  if (status) {
+    if (tid == 0) __hip_atomic_store(&status[b], nu + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (wid == 0) {
+      int acc = 0;
+      for (int64_t j0 = 0; j0 < b; j0 += 64) {
+        const int64_t j = j0 + lane;
+        int c = 0;
+        if (j < b) {
+          while ((c = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE,
+                                        __HIP_MEMORY_SCOPE_AGENT)) == 0)
+            __builtin_amdgcn_s_sleep(1);
+          c -= 1;
+        }
+        acc += wave_sum_i(c);
+      }
+      if (lane == 0) L.base = acc;
+    }
+    __syncthreads();
+    perm = perm_all + pos0;
+    uniq = uniq_all + L.base;
+    seg = seg_all + L.base;
+    voff = (int32_t)pos0;
+  } else {
+    perm = perm_all + pos0;
+    uniq = uniq_all + pos0;
+    seg = seg_all + b * (int64_t)(batch_n + 1);
+    voff = 0;
+  }
+  for (int i = tid; i < n; i += kR8Threads) perm[i] = voff + L.v[cur][i];
+  for (int i = i0; i < i1; ++i) {
+    if (i == 0 || ks[i - 1] != ks[i]) {
+      uniq[o] = (int32_t)ks[i];
+      seg[o] = voff + i;
+      ++o;
     }
   }
-  __syncthreads();
-  emit_segments(L.sk, n, uniq_all + b * batch_n, seg_all + b * (batch_n + 1), n_uniq_all + b,
-                L.scan);
+  if (!status) {
+    if (tid == 0) {
+      seg[nu] = n;
+      n_uniq_all[b] = nu;
+    }
+  } else {
+    const int nblocks = (int)gridDim.x;
+    if (tid == 0) {
+      if (b == nblocks - 1) {
+        seg[nu] = (int32_t)n_total;
+        n_uniq_all[0] = L.base + nu;
+      }
+      L.last = __hip_atomic_fetch_add(&status[nblocks], 1, __ATOMIC_ACQ_REL,
+                                      __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
+    }
+    __syncthreads();
+    if (L.last)                                  // every block is past its look-back
+      for (int q = tid; q <= nblocks; q += kR8Threads) status[q] = 0;
+  }
+  R8T(7);
+  R8C(13);
 }
 
 // Block-partitioned sort (keys in n_blocks blocks of block_n, every key of block b
@@ -917,15 +1018,37 @@ extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t
   int nbits = 0;
   while (nbits < 31 && ((int64_t)1 << nbits) < key_space) ++nbits;
   hipStream_t st = (hipStream_t)stream;
-  if (block_n <= kBktMax)      // bucket-rank sort: no per-digit passes
-    hipLaunchKernelGGL(segsort_bucket_kernel, dim3((unsigned)nb), dim3(kBktThreads), 0, st, keys,
-                       n, (int)block_n, perm_t, uniq_t, seg_t, nu_t);
+  if (block_n <= kR8Max)       // 8-bit digits over the block's key span
+    hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0, st, keys,
+                       n, (int)block_n, perm_t, uniq_t, seg_t, nu_t, (int32_t*)nullptr);
   else
     hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys,
                        n, (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
   hipLaunchKernelGGL(blocks_concat_kernel, dim3((unsigned)nb), dim3(256), 0, st, perm_t, uniq_t,
                      seg_t, nu_t, n, (int)block_n, (int)nb, perm, uniq, seg, n_uniq_dev);
   return launch_status("mirec_segment_sort_blocks");
+}
+
+extern "C" int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n,
+                                                 int64_t block_n, int64_t key_space,
+                                                 int32_t* perm, int32_t* uniq, int32_t* seg,
+                                                 int32_t* n_uniq_dev, int32_t* status,
+                                                 int64_t n_status, void* stream) {
+  if (n <= 0 || block_n <= 0 || block_n > kR8Max || key_space <= 0 || key_space > INT32_MAX ||
+      n > INT32_MAX || !keys || !perm || !uniq || !seg || !n_uniq_dev || !status) {
+    set_error("mirec_segment_sort_blocks_chained: bad arguments (0 < block_n <= %d)", kR8Max);
+    return -1;
+  }
+  const int64_t nb = (n + block_n - 1) / block_n;
+  if (nb > kChainMaxBlocks || n_status < nb + 1) {
+    set_error("mirec_segment_sort_blocks_chained: %lld blocks need status[%lld] (at most %d "
+              "blocks)", (long long)nb, (long long)(nb + 1), kChainMaxBlocks);
+    return -1;
+  }
+  hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0,
+                     (hipStream_t)stream, keys, n, (int)block_n, perm, uniq, seg, n_uniq_dev,
+                     status);
+  return launch_status("mirec_segment_sort_blocks_chained");
 }
 
 extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,

@@ -10,65 +10,70 @@ from recbole_amd.data.dataloader.abstract_dataloader import AbstractDataLoader
 from recbole_amd.utils import DataLoaderType, EvaluatorType, FeatureSource, FeatureType, InputType
 
 
+def _hook(name):
+    """An abstract hook of the reference's mixins: raises until a loader supplies it."""
+    def missing(self, *args):
+        raise NotImplementedError(f'Method [{name}] should be implemented.')
+    return missing
+
+
 class NegSampleMixin(AbstractDataLoader):
     dl_type = DataLoaderType.NEGSAMPLE
+    _STRATEGIES = ('by', 'full')
 
     def __init__(self, config, dataset, sampler, neg_sample_args, batch_size=1,
                  dl_format=InputType.POINTWISE, shuffle=False):
-        if neg_sample_args['strategy'] not in ['by', 'full']:
-            raise ValueError(f"Neg_sample strategy [{neg_sample_args['strategy']}] has not been implemented.")
-        self.sampler = sampler
-        self.neg_sample_args = neg_sample_args
+        strategy = neg_sample_args['strategy']
+        if strategy not in self._STRATEGIES:
+            raise ValueError(f"Neg_sample strategy [{strategy}] has not been implemented.")
+        self.sampler, self.neg_sample_args = sampler, neg_sample_args
         super().__init__(config, dataset, batch_size=batch_size, dl_format=dl_format,
                          shuffle=shuffle)
 
     def setup(self):
         self._batch_size_adaptation()
 
-    def _batch_size_adaptation(self):
-        raise NotImplementedError('Method [batch_size_adaptation] should be implemented.')
-
-    def _neg_sampling(self, inter_feat):
-        raise NotImplementedError('Method [neg_sampling] should be implemented.')
-
-    def get_pos_len_list(self):
-        raise NotImplementedError('Method [get_pos_len_list] should be implemented.')
-
-    def get_user_len_list(self):
-        raise NotImplementedError('Method [get_user_len_list] should be implemented.')
+    _batch_size_adaptation = _hook('batch_size_adaptation')
+    _neg_sampling = _hook('neg_sampling')
+    get_pos_len_list = _hook('get_pos_len_list')
+    get_user_len_list = _hook('get_user_len_list')
 
 
 class NegSampleByMixin(NegSampleMixin):
+    """`by`-N sampling: the batch layout (times, label or neg_ fields) per dl_format."""
 
     def __init__(self, config, dataset, sampler, neg_sample_args, batch_size=1,
                  dl_format=InputType.POINTWISE, shuffle=False):
         if neg_sample_args['strategy'] != 'by':
             raise ValueError('neg_sample strategy in GeneralInteractionBasedDataLoader() should be `by`')
-        self.user_inter_in_one_batch = (sampler.phase != 'train') and (
-            config['eval_type'] != EvaluatorType.INDIVIDUAL)
+        evaluating = sampler.phase != 'train'
+        self.user_inter_in_one_batch = evaluating and config['eval_type'] != EvaluatorType.INDIVIDUAL
         self.neg_sample_by = neg_sample_args['by']
-        if dl_format == InputType.POINTWISE:
-            self.times = 1 + self.neg_sample_by
-            self.sampling_func = self._neg_sample_by_point_wise_sampling
-            self.label_field = config['LABEL_FIELD']
-            dataset.set_field_property(self.label_field, FeatureType.FLOAT,
-                                       FeatureSource.INTERACTION, 1)
-        elif dl_format == InputType.PAIRWISE:
-            self.times = self.neg_sample_by
-            self.sampling_func = self._neg_sample_by_pair_wise_sampling
-            self.neg_prefix = config['NEG_PREFIX']
-            iid_field = config['ITEM_ID_FIELD']
-            self.neg_item_id = self.neg_prefix + iid_field
-            cols = [iid_field] if dataset.item_feat is None else dataset.item_feat.columns
-            for c in cols:
-                dataset.copy_field_property(self.neg_prefix + c, c)
-        else:
+        layouts = {InputType.POINTWISE: self._layout_point_wise,
+                   InputType.PAIRWISE: self._layout_pair_wise}
+        if dl_format not in layouts:
             raise ValueError(f'`neg sampling by` with dl_format [{dl_format}] not been implemented.')
+        layouts[dl_format](config, dataset)
         super().__init__(config, dataset, sampler, neg_sample_args, batch_size=batch_size,
                          dl_format=dl_format, shuffle=shuffle)
 
-    def _neg_sample_by_pair_wise_sampling(self, *args):
-        raise NotImplementedError('Method [neg_sample_by_pair_wise_sampling] should be implemented.')
+    def _layout_point_wise(self, config, dataset):
+        # the positive row and N negative rows, told apart by a float label field
+        self.times = self.neg_sample_by + 1
+        self.sampling_func = self._neg_sample_by_point_wise_sampling
+        self.label_field = config['LABEL_FIELD']
+        dataset.set_field_property(self.label_field, FeatureType.FLOAT, FeatureSource.INTERACTION, 1)
 
-    def _neg_sample_by_point_wise_sampling(self, *args):
-        raise NotImplementedError('Method [neg_sample_by_point_wise_sampling] should be implemented.')
+    def _layout_pair_wise(self, config, dataset):
+        # one row per (positive, negative): every item feature again under the neg_ prefix
+        self.times = self.neg_sample_by
+        self.sampling_func = self._neg_sample_by_pair_wise_sampling
+        self.neg_prefix = config['NEG_PREFIX']
+        iid = config['ITEM_ID_FIELD']
+        self.neg_item_id = self.neg_prefix + iid
+        item_cols = [iid] if dataset.item_feat is None else list(dataset.item_feat.columns)
+        for c in item_cols:
+            dataset.copy_field_property(self.neg_prefix + c, c)
+
+    _neg_sample_by_pair_wise_sampling = _hook('neg_sample_by_pair_wise_sampling')
+    _neg_sample_by_point_wise_sampling = _hook('neg_sample_by_point_wise_sampling')

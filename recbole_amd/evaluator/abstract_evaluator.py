@@ -9,7 +9,6 @@ for the loss metrics and refuses full ranking, as the reference does.
 """
 import numpy as np
 import torch
-from torch.nn.utils.rnn import pad_sequence
 
 
 class BaseEvaluator(object):
@@ -33,14 +32,17 @@ class GroupedEvaluator(BaseEvaluator):
     """Metrics computed per user, then averaged (top-K). Subclasses set `self.topk`."""
 
     def sample_collect(self, scores_tensor, user_len_list):
-        rows = torch.split(scores_tensor, list(user_len_list), dim=0)
-        mat = pad_sequence(rows, batch_first=True, padding_value=-np.inf)
-        width = max(self.topk)
-        if mat.shape[1] < width:
-            wide = torch.full((mat.shape[0], width), -np.inf, device=mat.device)
-            wide[:, :mat.shape[1]] = mat
-            mat = wide
-        return mat
+        # one scatter into a -inf matrix: user u's j-th score lands at (u, j); the width
+        # covers the longest user and at least max(topk) columns
+        lens = torch.as_tensor(list(user_len_list), dtype=torch.long,
+                               device=scores_tensor.device)
+        width = max(int(lens.max()) if lens.numel() else 0, max(self.topk))
+        out = scores_tensor.new_full((lens.numel(), width), -np.inf)
+        owner = torch.repeat_interleave(torch.arange(lens.numel(), device=lens.device), lens)
+        first = torch.cumsum(lens, 0) - lens
+        col = torch.arange(owner.numel(), device=lens.device) - first[owner]
+        out[owner, col] = scores_tensor.reshape(-1)
+        return out
 
     def full_sort_collect(self, scores_tensor, user_len_list):
         return scores_tensor.view(len(user_len_list), -1)

@@ -404,7 +404,7 @@ class Segments:
         self.perm = torch.empty(cap, dtype=torch.int32, device=device)
         self.uniq = torch.empty(cap, dtype=torch.int32, device=device)
         self.seg = torch.empty(cap + 1, dtype=torch.int32, device=device)
-        self.n_uniq = torch.zeros(1, dtype=torch.int32, device=device)
+        self.n_uniq = torch.empty(1, dtype=torch.int32, device=device)   # every sort writes it
         self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
 
 
@@ -421,12 +421,29 @@ def segment_sort(keys: torch.Tensor, key_space: int, segs: Segments | None = Non
     return segs
 
 
-def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int) -> Segments:
+CHAIN_MAX_BLOCK_N, CHAIN_MAX_BLOCKS = 4096, 256
+
+
+def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int,
+                        status: torch.Tensor | None = None) -> Segments:
     """segment_sort for keys in blocks of block_n whose key ranges increase block to
     block (every key of block b below every key of block b+1): same outputs, each
-    block sorted in LDS (mirec_segment_sort_blocks)."""
+    block sorted in LDS. With `status` (int32, zero, >= n_blocks + 1 entries; left
+    zero) and block_n <= 4,096, <= 256 blocks: one launch (mirec_segment_sort_blocks_
+    chained); otherwise the sort + concatenation pair (mirec_segment_sort_blocks)."""
     _dev(keys, torch.int64, "keys")
     n = keys.numel()
+    nb = -(-n // max(block_n, 1))
+    if (status is not None and n > 0 and block_n <= CHAIN_MAX_BLOCK_N
+            and nb <= CHAIN_MAX_BLOCKS):
+        _dev(status, torch.int32, "status")
+        segs = Segments(n, keys.device)
+        with timed_launch('k2_blocks'):
+            rc = lib().mirec_segment_sort_blocks_chained(
+                ptr(keys), n, block_n, key_space, ptr(segs.perm), ptr(segs.uniq), ptr(segs.seg),
+                ptr(segs.n_uniq), ptr(status), status.numel(), stream_handle())
+        check(rc, "mirec_segment_sort_blocks_chained")
+        return segs
     segs = Segments(n, keys.device, lib().mirec_segment_sort_blocks_workspace_size(n, block_n))
     with timed_launch('k2_blocks'):              # two launches: the block sorts, the concat
         rc = lib().mirec_segment_sort_blocks(ptr(keys), n, block_n, key_space, ptr(segs.perm),

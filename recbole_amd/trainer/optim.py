@@ -233,6 +233,10 @@ class FusedAdam(torch.optim.Optimizer):
             self._zero_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
             self._dummy_i32 = torch.zeros(2, dtype=torch.int32, device=dev)
             self._dummy_f32 = torch.zeros(4, dtype=torch.float32, device=dev)
+            # the chained block sort's hand-off words (zero between calls; the optimizer
+            # issues its sorts one after another on one stream)
+            self._sort_status = torch.zeros(ops.CHAIN_MAX_BLOCKS + 1, dtype=torch.int32,
+                                            device=dev)
         for p in params:
             if p.dim() != 2 or p.shape[1] not in (1, 4, 16, 32, 64, 128, 256) or not p.is_cuda:
                 continue
@@ -287,7 +291,8 @@ class FusedAdam(torch.optim.Optimizer):
             last = segs.uniq.gather(0, (segs.n_uniq.long() - 1).clamp(min=0))
             segs.n_uniq.sub_((last == n_rows).to(torch.int32))
         elif segs is None and blocks:
-            segs = ops.segment_sort_blocks(keys.contiguous(), int(blocks), p.shape[0])
+            segs = ops.segment_sort_blocks(keys.contiguous(), int(blocks), p.shape[0],
+                                           status=self._sort_status)
         elif segs is None:
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])
         if 'shard' in self._deferred[p]:

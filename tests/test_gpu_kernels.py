@@ -789,10 +789,12 @@ def test_adam_fast_math_selftest(dev):
 
 @pytest.mark.parametrize('block_n,n_blocks,space', [(2048, 26, 1 << 25), (100, 7, 1000), (8192, 3, 1 << 20), (513, 4, 2100),
                                                    (4096, 5, 1 << 30), (64, 3, 64 * 3)])
-def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
+@pytest.mark.parametrize('chained', [False, True])
+def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space, chained):
     """mirec_segment_sort_blocks on keys in blocks of increasing key ranges (DeepFM's
     field-major token keys) gives exactly the device-wide segment_sort's outputs,
-    incl. a ragged last block."""
+    incl. a ragged last block; chained (one launch, block_n <= 4,096): the same, and
+    the status words are zero again after each of two calls."""
     from recbole_amd import ops
     g = torch.Generator(device='cpu').manual_seed(block_n)
     edges = torch.linspace(0, space, n_blocks + 1).long()
@@ -804,12 +806,45 @@ def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space):
         parts.append(lo + torch.randint(0, max(1, min(hi - lo, 50 + b * 997)), (m,), generator=g))
     keys = torch.cat(parts).to(dev)
     a = ops.segment_sort(keys, space)
-    b = ops.segment_sort_blocks(keys, block_n, space)
+    status = torch.zeros(300, dtype=torch.int32, device=dev) if chained else None
+    for _ in range(2 if chained else 1):
+        b = ops.segment_sort_blocks(keys, block_n, space, status=status)
+        if chained:
+            assert int(status.abs().sum().item()) == 0
     nu = int(a.n_uniq.item())
     assert int(b.n_uniq.item()) == nu
     assert torch.equal(a.perm[:n], b.perm[:n])
     assert torch.equal(a.uniq[:nu], b.uniq[:nu])
     assert torch.equal(a.seg[:nu + 1], b.seg[:nu + 1])
+
+
+def test_segment_sort_blocks_spans(dev):
+    """Block sort across key spans: a constant block (no digit pass), a two-key block,
+    a Zipf-headed block and blocks spanning 20 and 30 bits (3 and 4 digit passes), ragged
+    last block — equal to the device-wide sort."""
+    from recbole_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(7)
+    bn, space = 4096, (1 << 31) - 1
+    base = [0, 1 << 26, 1 << 27, 1 << 28, 1 << 29, 1 << 30]
+    parts = [torch.full((bn,), base[0] + 5, dtype=torch.int64),
+             base[1] + 3 * torch.randint(0, 2, (bn,), generator=g),
+             base[2] + torch.minimum(torch.distributions.Geometric(0.05).sample((bn,)).long(),
+                                     torch.tensor(999)),
+             base[3] + torch.randint(0, 1 << 20, (bn,), generator=g),
+             base[4] + torch.randint(0, 1 << 29, (bn,), generator=g),
+             base[5] + torch.randint(0, (1 << 30) - 1, (bn - 1000,), generator=g)]
+    keys = torch.cat(parts).to(dev)
+    n = keys.numel()
+    a = ops.segment_sort(keys, space)
+    nu = int(a.n_uniq.item())
+    status = torch.zeros(8, dtype=torch.int32, device=dev)
+    for st in (None, status, status):
+        b = ops.segment_sort_blocks(keys, bn, space, status=st)
+        assert int(b.n_uniq.item()) == nu
+        assert torch.equal(a.perm[:n], b.perm[:n])
+        assert torch.equal(a.uniq[:nu], b.uniq[:nu])
+        assert torch.equal(a.seg[:nu + 1], b.seg[:nu + 1])
+    assert int(status.abs().sum().item()) == 0
 
 
 @pytest.mark.parametrize('d', [4, 16])

@@ -112,6 +112,23 @@ def test_abstract_protocols_raise():
         IndividualEvaluator(cfg, ['auc'])
 
 
+def test_grouped_sample_collect_pads():
+    """GroupedEvaluator.sample_collect: per-user rows padded with -inf to the longest
+    user and at least max(topk) columns (abstract_evaluator.py:58-76 of the reference)."""
+    import numpy as np
+    import torch
+    from recbole.evaluator.abstract_evaluator import GroupedEvaluator
+    ev = GroupedEvaluator({'eval_setting': 'RO_RS,uni100', 'metric_decimal_place': 4}, ['hit'])
+    ev.topk = [3, 5]
+    sc = torch.arange(1, 12, dtype=torch.float32)
+    m = ev.sample_collect(sc, [3, 1, 7])
+    assert m.shape == (3, 7)
+    assert m[0, :3].tolist() == [1, 2, 3] and m[1, 0] == 4 and m[2].tolist() == list(range(5, 12))
+    assert torch.isinf(m[0, 3:]).all() and torch.isinf(m[1, 1:]).all()
+    assert ev.sample_collect(sc[:2], [1, 1]).shape == (2, 5)
+    assert np.isneginf(ev.sample_collect(sc[:2], [1, 1])[:, 1:].numpy()).all()
+
+
 def test_cli_flags():
     """run_recbole.py keeps the reference's flags (run_recbole.py:18-21)."""
     import os
