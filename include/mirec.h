@@ -263,13 +263,15 @@ int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t block_n, i
  * concatenated outputs after summing the unique counts of the blocks before it.
  * status: int32[n_status >= n_blocks + 1], all zero before the first call; every call
  * leaves it zero again (reuse one buffer per stream; two calls in flight at once need
- * two buffers). The grouping of the token-field embedding gradient rows of
+ * two buffers). pos_seg (nullable, int32[n]): pos_seg[p] = the segment of sorted
+ * position p (seg[pos_seg[p]] <= p < seg[pos_seg[p] + 1]) for the *_pos_seg reductions.
+ * The grouping of the token-field embedding gradient rows of
  * reference recbole/model/layers.py:121-141 (FMEmbedding, called from
  * abstract_recommender.py:260 embed_token_fields) before the deferred Adam. */
 int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n, int64_t block_n,
                                       int64_t key_space, int32_t* perm, int32_t* uniq,
                                       int32_t* seg, int32_t* n_uniq_dev, int32_t* status,
-                                      int64_t n_status, void* stream);
+                                      int64_t n_status, int32_t* pos_seg, void* stream);
 
 /* Look-ahead lists of the deferred Adam: for b < n_batches-1,
  * out[b*stride ..) = uniq(b+1) \ uniq(b) ascending, n_out[b] its length, where
@@ -358,6 +360,14 @@ int mirec_segment_reduce2_f32(const float* rows, int32_t d, const float* rows1,
                               const int32_t* perm, const int32_t* uniq, const int32_t* seg,
                               const int32_t* n_uniq_dev, int64_t n, float* out, float* out1,
                               void* ws, size_t ws_bytes, void* stream);
+/* mirec_segment_reduce2_f32 with pos_seg[n] (the segment of every sorted position, from
+ * mirec_segment_sort_blocks_chained): the same outputs bit for bit, without a search per
+ * chunk of positions. */
+int mirec_segment_reduce2_pos_seg_f32(const float* rows, int32_t d, const float* rows1,
+                                      const int32_t* perm, const int32_t* pos_seg,
+                                      const int32_t* uniq, const int32_t* seg,
+                                      const int32_t* n_uniq_dev, int64_t n, float* out,
+                                      float* out1, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K5  Dense Adam over every row, with the gradient supplied in compact form.

@@ -137,7 +137,7 @@ SIGNATURES = {
     "mirec_segment_sort_blocks": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                           c_size_t, _P]),
     "mirec_segment_sort_blocks_chained": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P,
-                                                  _P, c_int64, _P]),
+                                                  _P, c_int64, _P, _P]),
     "mirec_prepare_chunk": (c_int, [_P, _P]),
     "mirec_prepare_chunk_walk": (c_int, [_P, _P]),
     "mirec_prepare_chunk_group": (c_int, [_P, _P]),
@@ -152,6 +152,8 @@ SIGNATURES = {
                                          _P]),
     "mirec_segment_reduce2_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P,
                                           c_size_t, _P]),
+    "mirec_segment_reduce2_pos_seg_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, _P, c_int64,
+                                                  _P, _P, _P, c_size_t, _P]),
     "mirec_segment_scatter_add_workspace_size": (c_size_t, [c_int64, c_int32]),
     "mirec_segment_scatter_add_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P,
                                               c_int64, _P, c_size_t, _P]),

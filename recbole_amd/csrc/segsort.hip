@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
     const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n,
     int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
     int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, int32_t* __restrict__ pu_all) {
   __shared__ R8Lds L;
   R8T(0);
   R8C(12);
@@ -382,12 +382,15 @@ __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
     voff = 0;
   }
   for (int i = tid; i < n; i += kR8Threads) perm[i] = voff + L.v[cur][i];
+  int32_t* __restrict__ pu = pu_all ? pu_all + pos0 : nullptr;   // chained only
+  const int ubase = status ? L.base : 0;
   for (int i = i0; i < i1; ++i) {
     if (i == 0 || ks[i - 1] != ks[i]) {
       uniq[o] = (int32_t)ks[i];
       seg[o] = voff + i;
       ++o;
     }
+    if (pu) pu[i] = ubase + o - 1;               // the segment of sorted position i
   }
   if (!status) {
     if (tid == 0) {
@@ -887,18 +890,25 @@ __global__ __launch_bounds__(256) void scatter_chunks_kernel(
   if (l == 0) tail_seg[c] = ts;            // the fixup's owner list: no search there
 }
 
-// One 256-thread block per boundary b; its owner is the multi-piece segment that
-// starts in chunk b - 1 (tail_seg, written by the chunk kernel), which it sums with
-// KL = 256 / CW lanes per column (k = kl, kl + KL, ...), combined in kl order:
-// deterministic.
-__global__ __launch_bounds__(256) void scatter_fixup_kernel(
+// Fixup of the multi-piece segments: the owner of boundary b is the segment that starts
+// in chunk b - 1 and continues (tail_seg, written by the chunk kernel). Its sum is
+// defined by 256 partial sums per column block of CW = d rounded up to a power of two
+// columns: "thread" i (column cb + i % CW, kl = i / CW, KL = 256 / CW) sums
+// [tail[b-1] if kl = 0] + head[b + kl] + head[b + kl + KL] + ..., and the column's sum
+// is t = s_0 + s_1 + ... + s_{KL-1} in kl order — deterministic. One wave per boundary
+// forms the 256 partial sums (four per lane, their loads in flight together), stages
+// them in its LDS slice and folds them; four boundaries per workgroup. The one-column
+// source of a pair uses the same rule with CW = 1 (KL = 256).
+constexpr int kFixWaves = 4;
+__global__ __launch_bounds__(64 * kFixWaves) void scatter_fixup_kernel(
     int d, const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ tail_seg, float* __restrict__ dense, int64_t n_rows,
     const float* __restrict__ head, const float* __restrict__ tail, int n_chunks, int compact,
     float* __restrict__ dense1 = nullptr, const float* __restrict__ head1 = nullptr,
     const float* __restrict__ tail1 = nullptr) {
-  __shared__ float red[256];
-  const int b = blockIdx.x + 1;   // boundary
+  __shared__ float red[kFixWaves][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = 1 + (int)blockIdx.x * kFixWaves + w;           // this wave's boundary
   if (b >= n_chunks) return;
   const int u = tail_seg[b - 1];
   if (u < 0) return;
@@ -907,35 +917,157 @@ __global__ __launch_bounds__(256) void scatter_fixup_kernel(
   const int kend = b - 2 + (e - s0 + CH - 1) / CH;     // chunk holding its last piece's start
   const int64_t row = compact ? (int64_t)u : (int64_t)uniq[u];
   if (row < 0 || row >= n_rows) return;
+  float* R = red[w];
+  // partial sums of "threads" i = lane + 64 j over src (ld columns, CW, KL), into R
+  auto partials = [&](const float* __restrict__ hs, const float* __restrict__ ts, int ld, int cb,
+                      int CW, int KL) {
+    float acc[4];
+    int col[4], kl[4];
+    // loads are unconditional (clamped to a valid address) and the term is selected
+    // afterwards: loads under per-lane branches wait for each other
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = lane + 64 * j;
+      col[j] = cb + i % CW;
+      kl[j] = i / CW;
+      const float tv = ts[(int64_t)(b - 1) * ld + min(col[j], ld - 1)];
+      acc[j] = (kl[j] == 0 && col[j] < ld) ? tv : 0.f;
+    }
+    for (int r = 0; b + r * KL <= kend; ++r) {
+      float hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = min(b + kl[j] + r * KL, kend);
+        hv[j] = hs[(int64_t)k * ld + min(col[j], ld - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (col[j] < ld && b + kl[j] + r * KL <= kend) acc[j] += hv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R[lane + 64 * j] = acc[j];
+  };
   int cw = 1;
   while (cw < d && cw < 256) cw <<= 1;
   const int KL = 256 / cw;
-  const int col0 = threadIdx.x % cw, kl = threadIdx.x / cw;
   for (int cb = 0; cb < d; cb += cw) {
-    const int col = cb + col0;
-    float s = 0.f;
-    if (col < d) {
-      if (kl == 0) s = tail[(int64_t)(b - 1) * d + col];
-      for (int k = b + kl; k <= kend; k += KL) s += head[(int64_t)k * d + col];
+    partials(head, tail, d, cb, cw, KL);
+    __builtin_amdgcn_wave_barrier();                // one wave: its LDS ops stay in order
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = lane + 64 * j;
+      if (i < cw && cb + i < d) {
+        float t = R[i];
+        for (int z = 1; z < KL; ++z) t += R[z * cw + i];
+        if (compact) dense[row * d + cb + i] = t; else dense[row * d + cb + i] += t;
+      }
     }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (kl == 0 && col < d) {
-      float t = red[col0];
-      for (int z = 1; z < KL; ++z) t += red[z * cw + col0];
-      if (compact) dense[row * d + col] = t; else dense[row * d + col] += t;
-    }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
   if (dense1) {          // PAIR: the one-column source, as the d = 1 fixup sums it
-    float s = threadIdx.x == 0 ? tail1[b - 1] : 0.f;
-    for (int k = b + (int)threadIdx.x; k <= kend; k += 256) s += head1[k];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float t = red[0];
-      for (int z = 1; z < 256; ++z) t += red[z];
+    partials(head1, tail1, 1, 0, 1, 256);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      // partial sums without a term are +0: adding them in order only turns a -0 running
+      // sum into +0, which one add of +0 does as well
+      const int m = min(256, kend - b + 1);
+      float t = R[0];
+      for (int z = 1; z < m; ++z) t += R[z];
+      if (m < 256) t += 0.f;
       dense1[row] = t;
+    }
+  }
+}
+
+static inline unsigned fixup_blocks(int n_chunks) {
+  return (unsigned)((n_chunks - 1 + kFixWaves - 1) / kFixWaves);
+}
+
+// Narrow rows (2 <= d <= 16) with pos_seg (the segment of every sorted position, from
+// the chained block sort): chunk c of CH = 8 sorted positions owns the same pieces as
+// in scatter_chunks_kernel (pieces counted from each segment's first position) — those
+// whose start lies in [p0, p1) — and sums them in the same order, so the outputs are
+// bit for bit the same. No search and no serial walk over segments: the 16 lanes of a
+// group each resolve one position of the window [p0, p0 + 2 CH) (its perm, segment,
+// piece, whether the chunk owns it, piece start / end), every lane then loads its
+// column of the 16 window rows at once and folds them in order.
+constexpr int kWinKindFinal = 0, kWinKindTail = 1, kWinKindHead = 2;
+template <bool PAIR>
+__global__ __launch_bounds__(256) void scatter_window_kernel(
+    const float* __restrict__ rows, int d, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ pos_seg, const int32_t* __restrict__ uniq,
+    const int32_t* __restrict__ seg, const int32_t* __restrict__ n_uniq_dev,
+    float* __restrict__ dense, int64_t n_rows, float* __restrict__ head,
+    float* __restrict__ tail, int32_t* __restrict__ tail_seg, int n_chunks, int compact,
+    const float* __restrict__ rows1, float* __restrict__ dense1, float* __restrict__ head1,
+    float* __restrict__ tail1) {
+  constexpr int G = 16, CH = 8, W = 2 * CH;
+  const int nu = n_uniq_dev[0];
+  const int n = seg[nu];
+  const int lane = threadIdx.x & 63, gb = lane & ~(G - 1), l = lane & (G - 1);
+  const int c = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  if (c >= n_chunks) return;
+  const int p0 = c * CH;
+  if (nu == 0 || p0 >= n) {
+    if (l == 0) tail_seg[c] = -1;
+    return;
+  }
+  const int p1 = min(n, p0 + CH);
+  // lane l resolves window position q = p0 + l
+  const int q = p0 + l;
+  int pq = 0, info = 0, dst = 0;      // info: 1 owned | 2 piece start | 4 piece end | kind << 3
+  if (q < n) {
+    pq = perm[q];
+    const int u = pos_seg[q];
+    const int s0 = seg[u], e = seg[u + 1];
+    const int ps = s0 + (q - s0) / CH * CH;
+    if (ps >= p0 && ps < p1) {
+      const int pe = min(e, ps + CH);
+      const int kind = ps != s0 ? kWinKindHead : (e - s0 <= CH ? kWinKindFinal : kWinKindTail);
+      info = 1 | (q == ps ? 2 : 0) | (q == pe - 1 ? 4 : 0) | (kind << 3);
+      dst = kind == kWinKindFinal ? (compact ? u : uniq[u]) : u;
+    }
+  }
+  // the multi-piece segment starting here (its first piece is a tail piece), if any
+  const uint64_t tb = __ballot((info & 2) && (info >> 3) == kWinKindTail);
+  const uint64_t gm = tb & (0xFFFFull << gb);
+  const int tl = gm ? __builtin_ctzll(gm) : gb;
+  const int tsu = __shfl(dst, tl, 64);
+  if (l == 0) tail_seg[c] = gm ? tsu : -1;
+  int pt[W], it[W], dt[W];
+#pragma unroll
+  for (int t = 0; t < W; ++t) {
+    pt[t] = __shfl(pq, gb + t, 64);
+    it[t] = __shfl(info, gb + t, 64);
+    dt[t] = __shfl(dst, gb + t, 64);
+  }
+  // every lane loads all W rows (unowned positions read row pt = 0 of a valid position;
+  // their terms are skipped below): loads under per-lane branches wait for each other
+  float v[W], v1[W];
+  const int lc = min(l, d - 1);
+#pragma unroll
+  for (int t = 0; t < W; ++t) {
+    v[t] = rows[(int64_t)pt[t] * d + lc];
+    if (PAIR) v1[t] = rows1[pt[t]];
+  }
+  float acc = 0.f, acc1 = 0.f;
+#pragma unroll
+  for (int t = 0; t < W; ++t) {
+    if (!(it[t] & 1)) continue;
+    acc = ((it[t] & 2) ? 0.f : acc) + v[t];
+    if (PAIR) acc1 = ((it[t] & 2) ? 0.f : acc1) + v1[t];
+    if (!(it[t] & 4)) continue;
+    const int kind = it[t] >> 3;
+    if (kind == kWinKindFinal) {
+      const int64_t row = dt[t];
+      if (l < d && row >= 0 && row < n_rows) {
+        if (compact) dense[row * d + l] = acc; else dense[row * d + l] += acc;
+      }
+      if (PAIR && l == 0) dense1[dt[t]] = acc1;
+    } else {
+      float* out = (kind == kWinKindTail ? tail : head) + (int64_t)c * d;
+      if (l < d) out[l] = acc;
+      if (PAIR && l == 0) (kind == kWinKindTail ? tail1 : head1)[c] = acc1;
     }
   }
 }
@@ -1020,7 +1152,8 @@ extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t
   hipStream_t st = (hipStream_t)stream;
   if (block_n <= kR8Max)       // 8-bit digits over the block's key span
     hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0, st, keys,
-                       n, (int)block_n, perm_t, uniq_t, seg_t, nu_t, (int32_t*)nullptr);
+                       n, (int)block_n, perm_t, uniq_t, seg_t, nu_t, (int32_t*)nullptr,
+                       (int32_t*)nullptr);
   else
     hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys,
                        n, (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
@@ -1033,7 +1166,8 @@ extern "C" int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n,
                                                  int64_t block_n, int64_t key_space,
                                                  int32_t* perm, int32_t* uniq, int32_t* seg,
                                                  int32_t* n_uniq_dev, int32_t* status,
-                                                 int64_t n_status, void* stream) {
+                                                 int64_t n_status, int32_t* pos_seg,
+                                                 void* stream) {
   if (n <= 0 || block_n <= 0 || block_n > kR8Max || key_space <= 0 || key_space > INT32_MAX ||
       n > INT32_MAX || !keys || !perm || !uniq || !seg || !n_uniq_dev || !status) {
     set_error("mirec_segment_sort_blocks_chained: bad arguments (0 < block_n <= %d)", kR8Max);
@@ -1047,7 +1181,7 @@ extern "C" int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n,
   }
   hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0,
                      (hipStream_t)stream, keys, n, (int)block_n, perm, uniq, seg, n_uniq_dev,
-                     status);
+                     status, pos_seg);
   return launch_status("mirec_segment_sort_blocks_chained");
 }
 
@@ -1098,9 +1232,9 @@ static int scatter_impl(const float* rows, int32_t d, const int32_t* perm, const
   else MIREC_SCAT(64, 256)
 #undef MIREC_SCAT
   if (chunks > 1)
-    hipLaunchKernelGGL(scatter_fixup_kernel, dim3((unsigned)(chunks - 1)), dim3(256),
-                       0, st, d, uniq, seg, tail_seg, dense, n_rows, head, tail, chunks,
-                       compact);
+    hipLaunchKernelGGL(scatter_fixup_kernel, dim3(fixup_blocks(chunks)), dim3(64 * kFixWaves), 0,
+                       st, d,
+                       uniq, seg, tail_seg, dense, n_rows, head, tail, chunks, compact);
   return launch_status("mirec_segment_scatter_add_f32");
 }
 
@@ -1113,11 +1247,10 @@ extern "C" int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const
                       stream);
 }
 
-extern "C" int mirec_segment_reduce2_f32(const float* rows, int32_t d, const float* rows1,
-                                         const int32_t* perm, const int32_t* uniq,
-                                         const int32_t* seg, const int32_t* n_uniq_dev, int64_t n,
-                                         float* out, float* out1, void* ws, size_t ws_bytes,
-                                         void* stream) {
+static int reduce2_impl(const float* rows, int32_t d, const float* rows1, const int32_t* perm,
+                        const int32_t* pos_seg, const int32_t* uniq, const int32_t* seg,
+                        const int32_t* n_uniq_dev, int64_t n, float* out, float* out1, void* ws,
+                        size_t ws_bytes, void* stream) {
   if (n == 0) return 0;
   if (!rows || !rows1 || !perm || !uniq || !seg || !n_uniq_dev || !out || !out1 || d < 2 ||
       d > 16 || n < 0 || n > INT32_MAX) {
@@ -1137,7 +1270,11 @@ extern "C" int mirec_segment_reduce2_f32(const float* rows, int32_t d, const flo
   int32_t* tail_seg = (int32_t*)(tail1 + chunks);
   hipStream_t st = (hipStream_t)stream;
   const int64_t gpb = 4 * (64 / 16);
-  if (d <= 4)
+  if (pos_seg)
+    hipLaunchKernelGGL((scatter_window_kernel<true>), dim3((unsigned)((chunks + gpb - 1) / gpb)),
+                       dim3(256), 0, st, rows, d, perm, pos_seg, uniq, seg, n_uniq_dev, out, n,
+                       head, tail, tail_seg, chunks, 1, rows1, out1, head1, tail1);
+  else if (d <= 4)
     hipLaunchKernelGGL((scatter_chunks_kernel<4, 4, true>),
                        dim3((unsigned)((chunks + 4 * 16 - 1) / (4 * 16))), dim3(256), 0, st, rows,
                        d, perm, uniq, seg, n_uniq_dev, out, n, head, tail, tail_seg, chunks, 1,
@@ -1148,9 +1285,33 @@ extern "C" int mirec_segment_reduce2_f32(const float* rows, int32_t d, const flo
                        perm, uniq, seg, n_uniq_dev, out, n, head, tail, tail_seg, chunks, 1,
                        rows1, out1, head1, tail1);
   if (chunks > 1)
-    hipLaunchKernelGGL(scatter_fixup_kernel, dim3((unsigned)(chunks - 1)), dim3(256), 0, st, d,
+    hipLaunchKernelGGL(scatter_fixup_kernel, dim3(fixup_blocks(chunks)), dim3(64 * kFixWaves), 0,
+                       st, d,
                        uniq, seg, tail_seg, out, n, head, tail, chunks, 1, out1, head1, tail1);
   return launch_status("mirec_segment_reduce2_f32");
+}
+
+extern "C" int mirec_segment_reduce2_f32(const float* rows, int32_t d, const float* rows1,
+                                         const int32_t* perm, const int32_t* uniq,
+                                         const int32_t* seg, const int32_t* n_uniq_dev, int64_t n,
+                                         float* out, float* out1, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  return reduce2_impl(rows, d, rows1, perm, nullptr, uniq, seg, n_uniq_dev, n, out, out1, ws,
+                      ws_bytes, stream);
+}
+
+extern "C" int mirec_segment_reduce2_pos_seg_f32(const float* rows, int32_t d,
+                                                 const float* rows1, const int32_t* perm,
+                                                 const int32_t* pos_seg, const int32_t* uniq,
+                                                 const int32_t* seg, const int32_t* n_uniq_dev,
+                                                 int64_t n, float* out, float* out1, void* ws,
+                                                 size_t ws_bytes, void* stream) {
+  if (!pos_seg) {
+    set_error("mirec_segment_reduce2_pos_seg_f32: pos_seg is null");
+    return -1;
+  }
+  return reduce2_impl(rows, d, rows1, perm, pos_seg, uniq, seg, n_uniq_dev, n, out, out1, ws,
+                      ws_bytes, stream);
 }
 
 extern "C" int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,

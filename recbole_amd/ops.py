@@ -396,11 +396,12 @@ def fixed_sum(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
 class Segments:
     """Grouping of contribution rows by table row (output of K2)."""
 
-    __slots__ = ("perm", "uniq", "seg", "n_uniq", "n", "ws")
+    __slots__ = ("perm", "uniq", "seg", "n_uniq", "n", "ws", "pos_seg")
 
     def __init__(self, n: int, device, ws_bytes: int = 0):
         cap = max(n, 1)
         self.n = n
+        self.pos_seg = None      # int32[n]: the segment of each sorted position, if the sort gave it
         self.perm = torch.empty(cap, dtype=torch.int32, device=device)
         self.uniq = torch.empty(cap, dtype=torch.int32, device=device)
         self.seg = torch.empty(cap + 1, dtype=torch.int32, device=device)
@@ -438,10 +439,12 @@ def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int,
             and nb <= CHAIN_MAX_BLOCKS):
         _dev(status, torch.int32, "status")
         segs = Segments(n, keys.device)
+        segs.pos_seg = torch.empty(n, dtype=torch.int32, device=keys.device)
         with timed_launch('k2_blocks'):
             rc = lib().mirec_segment_sort_blocks_chained(
                 ptr(keys), n, block_n, key_space, ptr(segs.perm), ptr(segs.uniq), ptr(segs.seg),
-                ptr(segs.n_uniq), ptr(status), status.numel(), stream_handle())
+                ptr(segs.n_uniq), ptr(status), status.numel(), ptr(segs.pos_seg),
+                stream_handle())
         check(rc, "mirec_segment_sort_blocks_chained")
         return segs
     segs = Segments(n, keys.device, lib().mirec_segment_sort_blocks_workspace_size(n, block_n))
@@ -524,6 +527,7 @@ def segment_reduce(rows: torch.Tensor, segs: Segments):
     ident.perm = iota[:max(n, 1)]
     ident.seg = iota[:max(n, 1) + 1]
     ident.uniq, ident.n_uniq, ident.ws = segs.uniq, segs.n_uniq, segs.ws
+    ident.pos_seg = ident.perm
     return out, ident
 
 
@@ -537,9 +541,16 @@ def segment_reduce2(rows: torch.Tensor, rows1: torch.Tensor, segs: Segments):
     out = torch.empty(max(n, 1), d, dtype=torch.float32, device=rows.device)
     out1 = torch.empty(max(n, 1), 1, dtype=torch.float32, device=rows.device)
     ws = _scatter_ws(rows.device, lib().mirec_segment_scatter_add_workspace_size(n, d + 1))
-    rc = lib().mirec_segment_reduce2_f32(ptr(rows), d, ptr(rows1), ptr(segs.perm), ptr(segs.uniq),
-                                         ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out), ptr(out1),
-                                         ptr(ws), ws.numel(), stream_handle())
+    if getattr(segs, 'pos_seg', None) is not None:     # the chained sort's position -> segment
+        rc = lib().mirec_segment_reduce2_pos_seg_f32(
+            ptr(rows), d, ptr(rows1), ptr(segs.perm), ptr(segs.pos_seg), ptr(segs.uniq),
+            ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out), ptr(out1), ptr(ws), ws.numel(),
+            stream_handle())
+    else:
+        rc = lib().mirec_segment_reduce2_f32(ptr(rows), d, ptr(rows1), ptr(segs.perm),
+                                             ptr(segs.uniq), ptr(segs.seg), ptr(segs.n_uniq), n,
+                                             ptr(out), ptr(out1), ptr(ws), ws.numel(),
+                                             stream_handle())
     check(rc, "mirec_segment_reduce2_f32")
     ident = Segments.__new__(Segments)
     ident.n = n
@@ -547,6 +558,7 @@ def segment_reduce2(rows: torch.Tensor, rows1: torch.Tensor, segs: Segments):
     ident.perm = iota[:max(n, 1)]
     ident.seg = iota[:max(n, 1) + 1]
     ident.uniq, ident.n_uniq, ident.ws = segs.uniq, segs.n_uniq, segs.ws
+    ident.pos_seg = ident.perm
     return out, out1, ident
 
 

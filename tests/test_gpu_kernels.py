@@ -869,3 +869,44 @@ def test_segment_reduce2_equals_two_reductions(dev, d):
     assert torch.equal(a[:nu], b[:nu])
     assert torch.equal(a1[:nu], b1[:nu])
     assert torch.equal(sa.perm, sb.perm) and torch.equal(sa.seg, sb.seg)
+
+
+@pytest.mark.parametrize('d', [4, 16])
+def test_segment_reduce2_pos_seg_equals_search(dev, d):
+    """C4's grouping: 26 field blocks of 2,048 Zipf ids sorted by the chained block sort,
+    which also gives each sorted position's segment (pos_seg). The window reduction that
+    reads pos_seg (no search) equals the searching one and two single reductions bit for
+    bit — one-piece rows, hot rows of hundreds of pieces (fixup), -0.0 contributions —
+    and pos_seg agrees with seg."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(d)
+    B, F = 2048, 26
+    vocab = [10_000_000 // (j + 1) + 3 for j in range(F)]
+    off = np.concatenate([[0], np.cumsum(vocab)[:-1]])
+    keys = np.concatenate([off[j] + np.minimum(rng.zipf(1.1, B), vocab[j] - 1) for j in range(F)])
+    kd = torch.as_tensor(keys.astype(np.int64), device=dev)
+    n = kd.numel()
+    g = torch.Generator().manual_seed(d)
+    rows = torch.randn(n, d, generator=g)
+    rows[::7] = -0.0
+    rows1 = torch.randn(n, 1, generator=g)
+    rows1[::5] = -0.0
+    rows, rows1 = rows.to(dev), rows1.to(dev)
+    status = torch.zeros(F + 1, dtype=torch.int32, device=dev)
+    sc = ops.segment_sort_blocks(kd, B, int(sum(vocab)), status=status)
+    assert sc.pos_seg is not None
+    nu = int(sc.n_uniq.item())
+    seg = sc.seg[:nu + 1].cpu().numpy()
+    assert np.array_equal(sc.pos_seg.cpu().numpy(), np.repeat(np.arange(nu), np.diff(seg)))
+    plain = ops.Segments(n, dev)
+    for f in ('perm', 'uniq', 'seg', 'n_uniq'):
+        setattr(plain, f, getattr(sc, f))
+    a, a1, _ = ops.segment_reduce2(rows, rows1, plain)          # searching kernel
+    b, b1, _ = ops.segment_reduce2(rows, rows1, sc)             # pos_seg window kernel
+    c, _ = ops.segment_reduce(rows, plain)
+    c1, _ = ops.segment_reduce(rows1, plain)
+    for x, y in ((a, b), (a1, b1), (a, c), (a1, c1)):
+        assert torch.equal(x[:nu].view(torch.int32), y[:nu].view(torch.int32))
+    exp = torch.zeros(nu, d, dtype=torch.float64).index_add_(
+        0, sc.pos_seg.cpu().long(), rows.cpu().double()[sc.perm[:n].cpu().long()])
+    torch.testing.assert_close(b[:nu].cpu().double(), exp, rtol=1e-5, atol=1e-4)
