@@ -19,11 +19,26 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
 
-// sum over the LPR lanes of a lane group (xor butterfly: every lane gets the sum)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+
+// Sum over the LPR lanes of an aligned lane group; every lane gets the same bits. A
+// butterfly pairing lanes i, i^1, then i^2, ... : xor 1 and 2 are DPP quad permutations,
+// xor 4 and 8 the DPP half-row / row mirrors (after the quad steps every lane of a quad
+// holds the quad sum, so pairing i with 7 - i, then with 15 - i, adds the same values as
+// i^4, i^8), xor 16 a swizzle inside 32 lanes and xor 32 one bpermute: four VALU-latency
+// steps instead of ds_bpermute round trips. a + b = b + a exactly, so both partners agree.
 template <int LPR>
 __device__ __forceinline__ float group_sum(float x) {
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  static_assert(LPR >= 1 && LPR <= 64 && (LPR & (LPR - 1)) == 0, "LPR: a power of two <= 64");
+  if (LPR >= 2) x += dpp_f32<0xB1>(x);     // quad_perm [1,0,3,2]
+  if (LPR >= 4) x += dpp_f32<0x4E>(x);     // quad_perm [2,3,0,1]
+  if (LPR >= 8) x += dpp_f32<0x141>(x);    // row_half_mirror
+  if (LPR >= 16) x += dpp_f32<0x140>(x);   // row_mirror
+  if (LPR >= 32) x += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x401F));
+  if (LPR >= 64) x += __shfl_xor(x, 32, 64);
   return x;
 }
 

@@ -706,8 +706,10 @@ class FusedBPRTrainStep(object):
         """Capture the model-side graph of every (slot, size, entry, flush) variant the
         epoch's chunk plan uses."""
         S = len(self.slots)
+        # flush flags are False, True or a tuple of row counts: sort by their repr
         variants = sorted({(k % S, n, e, f) for k, ((_, n, Bc), (e, f)) in
-                           enumerate(zip(self._plan, self._flags)) if Bc == self.Bg})
+                           enumerate(zip(self._plan, self._flags)) if Bc == self.Bg},
+                          key=lambda v: (v[0], v[1], v[2], repr(v[3])))
         for k, n, e, f in variants:
             self._graph_for(self.slots[k], n, e, f)
 
