@@ -60,8 +60,30 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, int lane, co
 // user, gI + id*D for the items) instead of at its slot — the row-sharded step, whose
 // ids are positions in the received message buffer and whose gradient rows go back in
 // the same positions (csrc/shard.hip): K3 and the backward gather in one launch.
+// Register budget: 6 waves per SIMD for rows of d <= 128 (80 VGPRs; the compiler keeps
+// 88 B per lane in scratch, which costs less than the waves it buys: the past-LLC gather
+// at B = 65,536 reads + writes 4.94 TB/s against 4.57 at 4 waves, tools/gather_probe.py).
+#ifndef MIREC_K3_WAVES
+#define MIREC_K3_WAVES 6
+#endif
+template <int D> struct K3Waves { static constexpr int n = D <= 128 ? MIREC_K3_WAVES : 1; };
+// Gradient-row stores are non-temporal: each row is written once and read by a later
+// launch, so it should not displace the gathered rows in the caches (4.35 -> 4.57 TB/s).
+#ifndef MIREC_K3_TEMPORAL
+#define MIREC_K3_NT 1
+#endif
+__device__ __forceinline__ void grad_store(float* p, const float4& x) {
+#if defined(MIREC_K3_NT)
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = x;
+#endif
+}
+
 template <int D, bool AT_IDS = false>
-__global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
+__global__ __launch_bounds__(256, K3Waves<D>::n) void bpr_fwd_bwd_kernel(
     const float* __restrict__ EU, int64_t nU, const float* __restrict__ EI, int64_t nI,
     const int64_t* __restrict__ user, const int64_t* __restrict__ pos,
     const int64_t* __restrict__ neg, int64_t B, int times, float gamma, float grad_scale,
@@ -76,18 +98,20 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
   const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
   if (k >= B) return;  // whole lane group exits together (shuffles stay in the group)
 
-  int64_t uid = user[k], pid = pos[k];
-  uid = uid < 0 ? 0 : (uid >= nU ? nU - 1 : uid);
-  pid = pid < 0 ? 0 : (pid >= nI ? nI - 1 : pid);
-  const float4 u = reinterpret_cast<const float4*>(EU + uid * D)[l];
-  const float4 p = reinterpret_cast<const float4*>(EI + pid * D)[l];
-  int64_t nid[NB];
+  // row ids clamped as int32 (tables hold < 2^31 rows; the host checks): half the
+  // registers of int64 ids, which buys the occupancy the gather needs
+  const int64_t u64 = user[k], p64 = pos[k];
+  const int uid = (int)(u64 < 0 ? 0 : (u64 >= nU ? nU - 1 : u64));
+  const int pid = (int)(p64 < 0 ? 0 : (p64 >= nI ? nI - 1 : p64));
+  const float4 u = reinterpret_cast<const float4*>(EU + (int64_t)uid * D)[l];
+  const float4 p = reinterpret_cast<const float4*>(EI + (int64_t)pid * D)[l];
+  int nid[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    int64_t id = q < times ? neg[(int64_t)q * B + k] : 0;
-    nid[q] = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
+    const int64_t id = q < times ? neg[(int64_t)q * B + k] : 0;
+    nid[q] = (int)(id < 0 ? 0 : (id >= nI ? nI - 1 : id));
   }
-  int64_t wid[NB];                    // AT_IDS: this group's negative ids (the next load early)
+  int wid[NB];                        // AT_IDS: this group's negative ids (the next load early)
 #pragma unroll
   for (int q = 0; q < NB; ++q) wid[q] = nid[q];
   // the first group's negative rows in flight with u and p: all the rows of a positive
@@ -95,7 +119,7 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
   float4 nf[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q)
-    nf[q] = q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
+    nf[q] = q < times ? reinterpret_cast<const float4*>(EI + (int64_t)nid[q] * D)[l]
                       : make_float4(0.f, 0.f, 0.f, 0.f);
   const float sp = group_sum<LPR>(dot4(u, p));
   float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gp = gu;
@@ -106,7 +130,7 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < NB; ++q)
       n[q] = j0 == 0 ? nf[q]
-                     : (j0 + q < times ? reinterpret_cast<const float4*>(EI + nid[q] * D)[l]
+                     : (j0 + q < times ? reinterpret_cast<const float4*>(EI + (int64_t)nid[q] * D)[l]
                                        : make_float4(0.f, 0.f, 0.f, 0.f));
     // ids of the next group in flight under this group's arithmetic
 #pragma unroll
@@ -114,8 +138,8 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int j = j0 + NB + q;
-      int64_t id = j < times ? neg[(int64_t)j * B + k] : 0;
-      nid[q] = id < 0 ? 0 : (id >= nI ? nI - 1 : id);
+      const int64_t id = j < times ? neg[(int64_t)j * B + k] : 0;
+      nid[q] = (int)(id < 0 ? 0 : (id >= nI ? nI - 1 : id));
     }
     float sn[NB];
 #pragma unroll
@@ -130,7 +154,7 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
         float4 gn;
         pair_contrib(gu, gp, gn, dx, u, p, n[q]);
         const int64_t r = (int64_t)j * B + k;
-        if (gI) reinterpret_cast<float4*>(gI + (AT_IDS ? wid[q] : B + r) * D)[l] = gn;
+        if (gI) grad_store(gI + (AT_IDS ? (int64_t)wid[q] : B + r) * D + 4 * l, gn);
         if (l == 0) {
           if (neg_score) neg_score[r] = sn[q];
           if (coef) coef[r] = dx;
@@ -138,8 +162,8 @@ __global__ __launch_bounds__(256) void bpr_fwd_bwd_kernel(
       }
     }
   }
-  if (gU) reinterpret_cast<float4*>(gU + (AT_IDS ? uid : k) * D)[l] = gu;
-  if (gI) reinterpret_cast<float4*>(gI + (AT_IDS ? pid : k) * D)[l] = gp;
+  if (gU) grad_store(gU + (AT_IDS ? (int64_t)uid : k) * D + 4 * l, gu);
+  if (gI) grad_store(gI + (AT_IDS ? (int64_t)pid : k) * D + 4 * l, gp);
   if (l == 0) {
     if (loss_k) loss_k[k] = lsum;
     if (pos_score) pos_score[k] = sp;
@@ -261,7 +285,7 @@ int launch_bpr(const float* EU, int64_t nU, const float* EI, int64_t nI, int32_t
                const char* what, bool at_ids = false) {
   if (B == 0) return 0;
   if (!EU || !EI || !user || !pos || (times > 0 && !neg) || B < 0 || times < 0 || nU <= 0 ||
-      nI <= 0) {
+      nI <= 0 || nU > INT32_MAX || nI > INT32_MAX) {
     set_error("%s: bad arguments", what);
     return -1;
   }
