@@ -42,9 +42,13 @@ def main():
     torch.cuda.synchronize()
     nU_max, nI_max = step._n_max[0], step._n_max[1]
     cap = 256                                        # shares per (table, batch): step.hip kSplitCap
-    starts = [0, cap, 2 * cap]                       # segments: shares U, I, ahead U, I, touched U, I
-    for n in (nU_max, nI_max, nU_max, nI_max):
-        starts.append(starts[-1] + n)
+    rpb = 4                                          # rows (waves) per workgroup: MIREC_STEP_RPB
+    halves = 2 if step.d >= 128 else 1               # look-ahead slots per row
+    # segments (stamps per wave, each segment padded to whole workgroups): shares U, I,
+    # look-ahead U, I (halves x rows), touched U, I
+    starts = [0]
+    for n in (cap, cap, halves * nU_max, halves * nI_max, nU_max, nI_max):
+        starts.append(starts[-1] + -(-n // rpb) * rpb)
     buf = np.zeros(32768 * 4, dtype=np.uint64)
     out = []
     for b in range(args.warmup, args.warmup + args.steps):
