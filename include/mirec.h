@@ -417,6 +417,14 @@ int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t n_params,
                               const float* step_consts_dev, const int32_t* step_idx_dev,
                               double beta1, double beta2, double eps, double weight_decay,
                               void* stream);
+/* The same with step_idx_dev = step_counter_dev, which the launch then advances by one
+ * after every block has read it (graph mode's device step; ticket_dev: one int32, zero
+ * before the first call, left zero) — the optimizer step's last launch, no separate
+ * increment. */
+int mirec_adam_flat_multi_advance_f32(const mirec_flat_param* params, int32_t n_params,
+                                      const float* step_consts_dev, int32_t* step_counter_dev,
+                                      int32_t* ticket_dev, double beta1, double beta2,
+                                      double eps, double weight_decay, void* stream);
 
 /* Several tables in ONE launch (e.g. the user and the item embedding of BPR),
  * same arithmetic per table. `tables` is a HOST array of n_tables <= 4
@@ -730,6 +738,12 @@ int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n_fields, in
  * label may be NULL when only prob is requested. */
 int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* label, int64_t B,
                           float grad_scale, float* prob, float* loss, float* dz, void* stream);
+/* The training loss of DeepFM in one launch: dz as mirec_sigmoid_bce_f32, loss_b
+ * (nullable) the per-sample terms, loss_mean[0] = their fixed-order sum (mirec_sum_f32's
+ * order) / B — nn.BCELoss's mean (reference deepfm.py:66-73). 0 < B <= 2^24. */
+int mirec_sigmoid_bce_mean_f32(const float* y_fm, const float* y_deep, const float* label,
+                               int64_t B, float grad_scale, float* loss_b, float* loss_mean,
+                               float* dz, void* stream);
 
 /* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
 int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);

@@ -162,6 +162,8 @@ SIGNATURES = {
                                            c_double, _P]),
     "mirec_adam_flat_multi_f32": (c_int, [ctypes.POINTER(FlatParam), c_int32, _P, _P, c_double,
                                           c_double, c_double, c_double, _P]),
+    "mirec_adam_flat_multi_advance_f32": (c_int, [ctypes.POINTER(FlatParam), c_int32, _P, _P, _P,
+                                                  c_double, c_double, c_double, c_double, _P]),
     "mirec_adam_flat_f32": (c_int, [_P, _P, _P, c_int64, _P, _P, _P, c_double, c_double,
                                     c_double, c_double, _P]),
     "mirec_adam_multi_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
@@ -203,6 +205,7 @@ SIGNATURES = {
     "mirec_ctx_fm_work_floats": (c_size_t, [c_int64, c_int32, c_int32]),
     "mirec_ctx_fm_fwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P, _P]),
     "mirec_ctx_fm_bwd_f32": (c_int, [_P, c_int32, c_int64, c_int32, _P, _P, _P, _P, _P]),
+    "mirec_sigmoid_bce_mean_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
     "mirec_sigmoid_bce_f32": (c_int, [_P, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
     "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
     "mirec_mlp_fwd_f32": (c_int, [_P, _P, c_int64, _P, c_int32, _P]),

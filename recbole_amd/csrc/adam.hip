@@ -594,9 +594,12 @@ struct FlatParams {
   int n;
 };
 
+// advance != nullptr: the step counter the launch read is advanced once every block has
+// read it — the block that takes the last ticket (agent-scope counter, zero between
+// launches) adds 1 and zeroes the ticket (graph mode's `step += 1` without a launch).
 __global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
     const FlatParams fp, const float* __restrict__ consts, const int32_t* __restrict__ step_idx,
-    AdamConsts k) {
+    AdamConsts k, int32_t* __restrict__ advance, int32_t* __restrict__ ticket) {
   int q = 0;
 #pragma unroll
   for (int t = 1; t < kFlatMax; ++t)
@@ -615,14 +618,23 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
       P.v[i] = vv;
     }
   }
+  if (advance) {
+    __syncthreads();                       // every lane's read of step_idx is done
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            (int)gridDim.x - 1) {
+      advance[0] = advance[0] + 1;
+      ticket[0] = 0;
+    }
+  }
 }
 
 }  // namespace mirec
 
-extern "C" int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t n_params,
-                                         const float* step_consts_dev,
-                                         const int32_t* step_idx_dev, double beta1, double beta2,
-                                         double eps, double weight_decay, void* stream) {
+static int flat_multi_impl(const mirec_flat_param* params, int32_t n_params,
+                           const float* step_consts_dev, const int32_t* step_idx_dev,
+                           double beta1, double beta2, double eps, double weight_decay,
+                           int32_t* advance, int32_t* ticket, void* stream) {
   if (n_params == 0) return 0;
   if (!params || n_params < 0 || n_params > kFlatMax || !step_consts_dev || !step_idx_dev) {
     set_error("mirec_adam_flat_multi_f32: bad arguments (at most %d parameters)", kFlatMax);
@@ -653,8 +665,36 @@ extern "C" int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t
   k.eps = (float)eps;
   k.wd = (float)weight_decay;
   hipLaunchKernelGGL(adam_flat_multi_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0,
-                     (hipStream_t)stream, fp, step_consts_dev, step_idx_dev, k);
+                     (hipStream_t)stream, fp, step_consts_dev, step_idx_dev, k, advance, ticket);
   return launch_status("mirec_adam_flat_multi_f32");
+}
+
+extern "C" int mirec_adam_flat_multi_f32(const mirec_flat_param* params, int32_t n_params,
+                                         const float* step_consts_dev,
+                                         const int32_t* step_idx_dev, double beta1, double beta2,
+                                         double eps, double weight_decay, void* stream) {
+  return flat_multi_impl(params, n_params, step_consts_dev, step_idx_dev, beta1, beta2, eps,
+                         weight_decay, nullptr, nullptr, stream);
+}
+
+extern "C" int mirec_adam_flat_multi_advance_f32(const mirec_flat_param* params,
+                                                 int32_t n_params, const float* step_consts_dev,
+                                                 int32_t* step_counter_dev, int32_t* ticket_dev,
+                                                 double beta1, double beta2, double eps,
+                                                 double weight_decay, void* stream) {
+  if (!step_counter_dev || !ticket_dev || n_params <= 0) {
+    set_error("mirec_adam_flat_multi_advance_f32: bad arguments");
+    return -1;
+  }
+  int64_t blocks = 0;
+  for (int q = 0; q < n_params && q < kFlatMax; ++q)
+    blocks += (params[q].n + 4 * kAdamThreads - 1) / (4 * kAdamThreads);
+  if (blocks == 0) {
+    set_error("mirec_adam_flat_multi_advance_f32: no elements (the counter would not advance)");
+    return -1;
+  }
+  return flat_multi_impl(params, n_params, step_consts_dev, step_counter_dev, beta1, beta2, eps,
+                         weight_decay, step_counter_dev, ticket_dev, stream);
 }
 
 extern "C" int mirec_adam_flat_f32(float* p, float* m, float* v, int64_t n,

@@ -374,6 +374,51 @@ extern "C" int mirec_ctx_fm_bwd_f32(const mirec_ctx_field* fields_dev, int32_t n
   return launch_status("mirec_ctx_fm_bwd_f32");
 }
 
+// The loss and its gradient in one launch for the training step: one 1024-lane block,
+// lane t computes samples t, t + 1024, ... (loss terms and dz as sigmoid_bce_kernel) and
+// sums its loss terms in that order, then a fixed binary tree over the 1024 partials
+// (capi.hip block_fixed_sum's order) and the mean = sum / B — what mirec_sigmoid_bce_f32 +
+// mirec_sum_f32 + a division gave, bit for bit, in one launch instead of three.
+__global__ __launch_bounds__(1024) void sigmoid_bce_mean_kernel(
+    const float* __restrict__ y_fm, const float* __restrict__ y_deep,
+    const float* __restrict__ label, int64_t B, float grad_scale, float* __restrict__ loss_b,
+    float* __restrict__ loss_mean, float* __restrict__ dz) {
+  __shared__ float lds[1024];
+  float acc = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 1024) {
+    const float z = y_fm[b] + (y_deep ? y_deep[b] : 0.f);
+    const float p = 1.f / (1.f + expf(-z));
+    const float t = label[b];
+    const float lp = fmaxf(logf(p), -100.f);
+    const float l1p = fmaxf(logf(1.f - p), -100.f);
+    const float lb = (t - 1.f) * l1p - t * lp;
+    if (loss_b) loss_b[b] = lb;
+    acc += lb;
+    const float gp = grad_scale * (p - t) / fmaxf((1.f - p) * p, 1e-12f);
+    dz[b] = gp * (1.f - p) * p;
+  }
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) lds[threadIdx.x] += lds[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss_mean[0] = lds[0] / (float)B;
+}
+
+extern "C" int mirec_sigmoid_bce_mean_f32(const float* y_fm, const float* y_deep,
+                                          const float* label, int64_t B, float grad_scale,
+                                          float* loss_b, float* loss_mean, float* dz,
+                                          void* stream) {
+  if (!y_fm || !label || !loss_mean || !dz || B <= 0 || B > (1 << 24)) {
+    set_error("mirec_sigmoid_bce_mean_f32: bad arguments (0 < B <= 2^24)");
+    return -1;
+  }
+  hipLaunchKernelGGL(sigmoid_bce_mean_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, y_fm,
+                     y_deep, label, B, grad_scale, loss_b, loss_mean, dz);
+  return launch_status("mirec_sigmoid_bce_mean_f32");
+}
+
 extern "C" int mirec_sigmoid_bce_f32(const float* y_fm, const float* y_deep, const float* label,
                                      int64_t B, float grad_scale, float* prob, float* loss,
                                      float* dz, void* stream) {

@@ -245,28 +245,44 @@ class _CtxFMFn(torch.autograd.Function):
         return (None, None, dT, dT1, dEf, dEf1, dbias, *dseq, *dseq1)
 
 
+_UNIT = {}
+
+
+def unit_grad(device):
+    """A persistent 0-dim 1.0 per device. backward() seeded with it hands this very tensor
+    to the loss Function at the root (autograd passes the seed object through sums), which
+    then skips multiplying its gradient by the seed (x * 1 = x exactly): one launch fewer
+    per step. Allocate it outside any graph capture."""
+    key = str(device)
+    if key not in _UNIT:
+        _UNIT[key] = torch.ones((), dtype=torch.float32, device=device)
+    return _UNIT[key]
+
+
 class _SigmoidBCEFn(torch.autograd.Function):
-    """nn.BCELoss()(sigmoid(y_fm + y_deep), label) (deepfm.py:45, 66-73)."""
+    """nn.BCELoss()(sigmoid(y_fm + y_deep), label) (deepfm.py:45, 66-73): loss terms, their
+    fixed-order mean and the logit gradient in one launch (mirec_sigmoid_bce_mean_f32)."""
 
     @staticmethod
     def forward(ctx, y_fm, y_deep, label):
         B = y_fm.numel()
         yd = y_deep.detach().reshape(-1).contiguous()
         lab = label.detach().to(torch.float32).contiguous()
-        loss_b = torch.empty(B, dtype=torch.float32, device=y_fm.device)
+        loss = torch.empty((), dtype=torch.float32, device=y_fm.device)
         dz = torch.empty(B, dtype=torch.float32, device=y_fm.device)
         gs = float(np.float32(1.0) / np.float32(B))
-        rc = lib().mirec_sigmoid_bce_f32(ptr(y_fm.detach().contiguous()), ptr(yd), ptr(lab), B, gs,
-                                         None, ptr(loss_b), ptr(dz), stream_handle())
-        check(rc, "mirec_sigmoid_bce_f32")
+        rc = lib().mirec_sigmoid_bce_mean_f32(ptr(y_fm.detach().contiguous()), ptr(yd), ptr(lab),
+                                              B, gs, None, ptr(loss), ptr(dz), stream_handle())
+        check(rc, "mirec_sigmoid_bce_mean_f32")
         ctx.save_for_backward(dz)
         ctx.deep_shape = y_deep.shape
-        return ops.fixed_sum(loss_b).view(()) / B
+        return loss
 
     @staticmethod
     def backward(ctx, g):
         (dz,) = ctx.saved_tensors
-        dz = dz * g
+        if g is not _UNIT.get(str(g.device)):      # the unit seed: dz * 1 = dz
+            dz = dz * g
         return dz, dz.view(ctx.deep_shape), None
 
 

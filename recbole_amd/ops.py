@@ -579,9 +579,11 @@ def _iota(device, n):
 
 # ---------------------------------------------------------------- K5 Adam
 def adam_flat_multi(specs, step_consts, step_idx, beta1=0.9, beta2=0.999, eps=1e-8,
-                    weight_decay=0.0):
+                    weight_decay=0.0, advance_ticket=None):
     """Dense Adam steps of several parameters in one launch per 16 (specs: dicts with
-    p, m, v, g — contiguous float32 device tensors of one size each)."""
+    p, m, v, g — contiguous float32 device tensors of one size each). advance_ticket (an
+    int32 [1] device tensor, zero between calls): step_idx is the device step counter and
+    the last launch advances it by one after reading it."""
     from recbole_amd._native import FlatParam
     _dev(step_consts, torch.float32, "step_consts")
     _dev(step_idx, torch.int32, "step_idx")
@@ -595,6 +597,12 @@ def adam_flat_multi(specs, step_consts, step_idx, beta1=0.9, beta2=0.999, eps=1e
                     raise ValueError(f"adam_flat_multi: {n_} must be contiguous, numel of p")
             t.p, t.m, t.v, t.g, t.n = (ptr(sp["p"]), ptr(sp["m"]), ptr(sp["v"]), ptr(sp["g"]),
                                        sp["p"].numel())
+        if advance_ticket is not None and i + 16 >= len(specs):
+            _dev(advance_ticket, torch.int32, "advance_ticket")
+            check(lib().mirec_adam_flat_multi_advance_f32(
+                arr, len(part), ptr(step_consts), ptr(step_idx), ptr(advance_ticket), beta1,
+                beta2, eps, weight_decay, stream_handle()), "mirec_adam_flat_multi_advance_f32")
+            continue
         check(lib().mirec_adam_flat_multi_f32(arr, len(part), ptr(step_consts), ptr(step_idx),
                                               beta1, beta2, eps, weight_decay, stream_handle()),
               "mirec_adam_flat_multi_f32")

@@ -121,10 +121,11 @@ class FusedAdam(torch.optim.Optimizer):
         self._pair_reduce(deferred)
         for p in deferred:
             self._deferred_step(p)
+        advanced = False
         if params:
-            self._dense_step(params)
+            advanced = self._dense_step(params)
         if params or deferred:
-            if self._g is not None:
+            if self._g is not None and not advanced:
                 self._g['step'].add_(1)       # the device step counter of graph mode
             self.n_steps += 1
         return loss
@@ -145,7 +146,9 @@ class FusedAdam(torch.optim.Optimizer):
             ds['window'] = window
         self._g = {'W': window, 't0': None,
                    'consts': torch.zeros(window * 4, dtype=torch.float32, device=device),
-                   'step': torch.zeros(1, dtype=torch.int32, device=device)}
+                   'step': torch.zeros(1, dtype=torch.int32, device=device),
+                   # the flat launch's ticket when it advances 'step' (zero between steps)
+                   'ticket': torch.zeros(1, dtype=torch.int32, device=device)}
         self._graph_open_window()
 
     def _graph_open_window(self):
@@ -205,9 +208,12 @@ class FusedAdam(torch.optim.Optimizer):
             st = self._ensure_state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             specs.append({'p': p.data, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'g': g})
+        # graph mode: the step's last launch also advances the device step counter
         ops.adam_flat_multi(specs, w['consts'],
                             w['idx'] if self._g is not None else w['idx'][r:r + 1],
+                            advance_ticket=self._g['ticket'] if self._g is not None else None,
                             **self._group_args())
+        return self._g is not None
 
     def advance(self, n: int):
         self.n_steps += n
