@@ -534,7 +534,13 @@ __device__ __forceinline__ void state_store(V* p, const V& x) {
 
 template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
+// Look-ahead rows: one element per thread over two half-row slots (default), or whole
+// rows in one slot (MIREC_STEP_AHEAD_WHOLE, probe: half the look-ahead waves).
+#if defined(MIREC_STEP_AHEAD_WHOLE)
+template <typename V> struct AheadVec { using T = V; };
+#else
 template <typename V> struct AheadVec { using T = float; };
+#endif
 
 // Rows per workgroup: a row of D <= 128 is one wave, and RPB of them share a workgroup
 // (each wave works alone: wave-level synchronisation only), so the dispatcher hands out
@@ -562,7 +568,7 @@ void bpr_adam_step_kernel(
   static_assert(RPB == 1 || TPB == 64, "several rows per workgroup need one wave per row");
   constexpr int LPR = D / 4;               // lanes per contribution (float4 each, K3's layout)
   constexpr int NG = TPB / LPR;            // contributions in flight per row
-  constexpr int kAheadHalves = EPT;        // look-ahead rows per table row (one element per thread)
+  constexpr int kAheadHalves = EPT / Lanes<typename AheadVec<V>::T>::n;   // slots per look-ahead row
   __shared__ float cont_all[RPB][NG][D];
   __shared__ int s_last_all[RPB];
   // the row of this wave: wave-uniform, so the row's indices stay in scalar registers
@@ -1002,7 +1008,11 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   // segments: the shares of split rows first (their row's step waits for them), then
   // the look-ahead rows (their replays are long chains), then the touched rows
   if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
-  const int halves = d >= 128 ? 2 : 1;            // look-ahead rows per table row
+#if defined(MIREC_STEP_AHEAD_WHOLE)
+  const int halves = 1;
+#else
+  const int halves = d >= 128 ? 2 : 1;            // look-ahead slots per table row
+#endif
   const int64_t rows[6] = {kSplitCap, kSplitCap,
                            L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0,
                            L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0,
