@@ -249,6 +249,21 @@ int mirec_segment_sort_batched(const int64_t* keys, int64_t n, int64_t batch_n,
                                int64_t key_space, int32_t* perm, int32_t* uniq, int32_t* seg,
                                int32_t* n_uniq_dev, void* ws, size_t ws_bytes, void* stream);
 
+/* The single sort of mirec_segment_sort for n > 8,192 keys in 2 + ceil(bits / 8)
+ * launches (global digit histograms; per 8-bit pass a stable LDS ranking of 2,048-key
+ * tiles whose digit offsets come from a decoupled look-back; the segments by a look-back
+ * scan). Same perm / uniq / seg / n_uniq; pos_seg (nullable, int32[n]) = the segment of
+ * each sorted position. ws: >= 16 * n bytes. status: int32[n_status >=
+ * mirec_segment_sort_onesweep_status_words(n)], zero before the first call, left zero
+ * (one buffer per stream). 0 < n < 2^30. The grouping K2 of every gradient reduction
+ * (reference: torch's embedding backward in recbole/model/sequential_recommender/
+ * sasrec.py:107-141 and abstract_recommender.py's embedding lookups). */
+int64_t mirec_segment_sort_onesweep_status_words(int64_t n);
+int mirec_segment_sort_onesweep(const int64_t* keys, int64_t n, int64_t key_space,
+                                int32_t* perm, int32_t* uniq, int32_t* seg, int32_t* n_uniq_dev,
+                                int32_t* pos_seg, void* ws, size_t ws_bytes, int32_t* status,
+                                int64_t n_status, void* stream);
+
 /* The same single sort (mirec_segment_sort outputs) for keys that come in blocks of
  * block_n (<= 8,192) with every key of block b below every key of block b+1 (e.g.
  * DeepFM's token keys, field-major at increasing table offsets): each block sorted
@@ -352,6 +367,13 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
 int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,
                              const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq_dev,
                              int64_t n, float* out, void* ws, size_t ws_bytes, void* stream);
+/* mirec_segment_reduce_f32 with pos_seg[n] (the segment of every sorted position, from
+ * mirec_segment_sort_onesweep / _blocks_chained): the same outputs bit for bit (same
+ * pieces, same order), without a search per chunk of positions. 1 <= d <= 256. */
+int mirec_segment_reduce_pos_seg_f32(const float* rows, int32_t d, const int32_t* perm,
+                                     const int32_t* pos_seg, const int32_t* uniq,
+                                     const int32_t* seg, const int32_t* n_uniq_dev, int64_t n,
+                                     float* out, void* ws, size_t ws_bytes, void* stream);
 /* Two sources grouped by the same segments in one pass (DeepFM's [V, d] token rows and
  * [V, 1] first-order weights): out = mirec_segment_reduce_f32(rows, d, ...) and out1 =
  * the same for rows1 with d = 1, bit for bit. 2 <= d <= 16; ws: at least

@@ -134,6 +134,9 @@ SIGNATURES = {
                                            c_size_t, _P]),
     "mirec_uniq_ahead_diff": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P]),
     "mirec_segment_sort_blocks_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "mirec_segment_sort_onesweep_status_words": (c_int64, [c_int64]),
+    "mirec_segment_sort_onesweep": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, _P,
+                                            c_size_t, _P, c_int64, _P]),
     "mirec_segment_sort_blocks": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                           c_size_t, _P]),
     "mirec_segment_sort_blocks_chained": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P,
@@ -150,6 +153,8 @@ SIGNATURES = {
     "mirec_selftest_adam_math": (c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P, _P]),
     "mirec_segment_reduce_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, c_int64, _P, _P, c_size_t,
                                          _P]),
+    "mirec_segment_reduce_pos_seg_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P,
+                                                 _P, c_size_t, _P]),
     "mirec_segment_reduce2_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P,
                                           c_size_t, _P]),
     "mirec_segment_reduce2_pos_seg_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, _P, c_int64,

@@ -746,6 +746,268 @@ static int radix_segment_sort(const int64_t* keys, int n, int nbits, int32_t* pe
 }
 
 // ---------------------------------------------------------------------------
+// Device-wide sort in few launches ("onesweep" form): one launch builds every pass's
+// global digit histogram (8-bit digits: ceil(bits / 8) passes, 3 for a 3 M-row table
+// instead of 5 five-bit passes of upsweep + scan + downsweep), one launch per pass ranks
+// a 2,048-key tile stably in LDS (the ballot ranking of segsort_radix8_kernel) and finds
+// its digit offsets among the tiles by decoupled look-back, and one launch emits the
+// segments (with pos_seg) by a look-back scan of the run heads. 2 + passes launches,
+// against 5 x 3 + 5. Same perm / uniq / seg / n_uniq (stable sort: unique).
+//
+// status (int32, zero before the first call, left zero: the last block of each launch
+// zeroes what that launch used): hist [kOsMaxPasses][256] | look-back words [passes]
+// [tiles][256] | segment look-back words [tiles] | tickets [kOsMaxPasses + 1]. A look-back
+// word holds 1 << 30 | the tile's own count; a tile sums its predecessors' words.
+constexpr int kOsThreads = 512;
+constexpr int kOsWaves = kOsThreads / 64;
+constexpr int kOsTile = 2048;
+constexpr int kOsIpt = kOsTile / kOsThreads;       // keys per thread (loads)
+constexpr int kOsChunks = kOsTile / 64 / kOsWaves;  // 64-key chunks per wave
+constexpr int kOsMaxPasses = 4;
+constexpr uint32_t kOsFlagA = 1u << 30, kOsVal = (1u << 30) - 1;
+
+__host__ __device__ inline int64_t os_tiles(int64_t n) { return (n + kOsTile - 1) / kOsTile; }
+__host__ __device__ inline int64_t os_status_words(int64_t n) {
+  const int64_t t = os_tiles(n);
+  return (int64_t)kOsMaxPasses * 256 + (int64_t)kOsMaxPasses * t * 256 + t + kOsMaxPasses + 1;
+}
+
+// The look-back words carry only their own count (flag 1 << 30 | count): no data is
+// published through them, so relaxed agent-scope loads and stores suffice, and the loads
+// of many predecessors can be in flight together (an acquire load waits for itself).
+__device__ __forceinline__ uint32_t os_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void os_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of the counts of tiles h, h + H, h + 2H, ... < tile in column `words` (stride per
+// tile): every tile publishes its count before it sums, so no wait chains through
+// predecessors — 16 loads in flight per batch, a word not yet published is re-read
+__device__ __forceinline__ uint32_t os_sum_before(const uint32_t* words, int64_t tile,
+                                                  int64_t stride, int h, int H) {
+  uint32_t s = 0;
+  for (int64_t t0 = h; t0 < tile; t0 += 16 * (int64_t)H) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t t = t0 + j * (int64_t)H;
+      w[j] = t < tile ? os_load(words + t * stride) : kOsFlagA;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t t = t0 + j * (int64_t)H;
+      while ((w[j] >> 30) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        w[j] = os_load(words + t * stride);
+      }
+      s += t < tile ? (w[j] & kOsVal) : 0u;
+    }
+  }
+  return s;
+}
+
+// the last of the launch's blocks (ticket) zeroes `words` [0, n_words)
+__device__ __forceinline__ void os_cleanup(uint32_t* ticket, uint32_t* words, int64_t n_words,
+                                           int* flag_lds) {
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag_lds = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                gridDim.x - 1;
+  __syncthreads();
+  if (*flag_lds) {
+    for (int64_t q = threadIdx.x; q < n_words; q += blockDim.x) words[q] = 0u;
+    if (threadIdx.x == 0) *ticket = 0u;
+  }
+}
+
+__global__ __launch_bounds__(kOsThreads) void os_hist_kernel(
+    const int64_t* __restrict__ keys, int n, int passes, int32_t* __restrict__ k32,
+    int32_t* __restrict__ v32, uint32_t* __restrict__ hist) {
+  __shared__ int h[kOsMaxPasses][256];
+  for (int q = threadIdx.x; q < kOsMaxPasses * 256; q += kOsThreads) (&h[0][0])[q] = 0;
+  __syncthreads();
+  const int base = blockIdx.x * kOsTile;
+#pragma unroll
+  for (int j = 0; j < kOsIpt; ++j) {
+    const int i = base + j * kOsThreads + threadIdx.x;
+    if (i < n) {
+      const uint32_t kv = (uint32_t)keys[i];
+      k32[i] = (int32_t)kv;
+      v32[i] = i;
+      for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(kv >> (8 * p)) & 255u], 1);
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < passes * 256; q += kOsThreads) {
+    const int c = (&h[0][0])[q];
+    if (c) __hip_atomic_fetch_add(hist + q, (uint32_t)c, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+struct OsPassLds {
+  uint32_t k[kOsTile];
+  int32_t v[kOsTile];
+  int cnt[256 * kOsWaves];           // [digit][wave] counts, then their offsets in the tile
+  uint16_t rank[kOsTile];
+  int gbase[256];                    // global start of each digit (this pass)
+  int tstart[257];                   // start of each digit inside the tile
+  int scan[kOsWaves + 1];
+  uint32_t half[256];
+  int last;
+};
+
+__global__ __launch_bounds__(kOsThreads) void os_pass_kernel(
+    const int32_t* __restrict__ kin, const int32_t* __restrict__ vin, int n, int shift,
+    int64_t tiles, uint32_t* __restrict__ hist_p, uint32_t* __restrict__ look_p,
+    uint32_t* __restrict__ ticket_p, int32_t* __restrict__ kout, int32_t* __restrict__ vout) {
+  __shared__ OsPassLds L;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t tile = blockIdx.x;
+  const int base = (int)(tile * kOsTile);
+  const int tn = min(kOsTile, n - base);
+#pragma unroll
+  for (int j = 0; j < kOsIpt; ++j) {
+    const int i = j * kOsThreads + tid;
+    if (i < tn) {
+      L.k[i] = (uint32_t)kin[base + i];
+      L.v[i] = vin[base + i];
+    }
+  }
+  for (int q = tid; q < 256 * kOsWaves; q += kOsThreads) L.cnt[q] = 0;
+  // the pass's global digit starts: an exclusive scan of its histogram
+  {
+    const int c = tid < 256 ? (int)hist_p[tid] : 0;
+    int tot;
+    const int ex = block_exclusive_scan(c, L.scan, &tot);
+    if (tid < 256) L.gbase[tid] = ex;
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int cc = 0; cc < kOsChunks; ++cc) {       // wave wid owns chunks [wid * kOsChunks, ..)
+    const int i = (wid * kOsChunks + cc) * 64 + lane;
+    const bool valid = i < tn;
+    const uint32_t dd = valid ? (L.k[i] >> shift) & 255u : 0u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      const int32_t sb = __builtin_amdgcn_sbfe((int32_t)dd, bb, 1);
+      const uint64_t bl = __ballot(sb != 0);
+      m &= ~(bl ^ (uint64_t)(int64_t)sb);
+    }
+    const int r = __popcll(m & lt);
+    int* h = &L.cnt[(int)dd * kOsWaves + wid];
+    const int before = valid ? *h : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && r == 0) *h = before + __popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (valid) L.rank[i] = (uint16_t)(before + r);
+  }
+  __syncthreads();
+  {                                              // digit-major offsets inside the tile
+    constexpr int per = 256 * kOsWaves / kOsThreads;
+    int c[per], sum = 0;
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+      c[q] = L.cnt[tid * per + q];
+      sum += c[q];
+    }
+    int tot;
+    int run = block_exclusive_scan(sum, L.scan, &tot);
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+      L.cnt[tid * per + q] = run;
+      run += c[q];
+    }
+  }
+  __syncthreads();
+  if (tid < 256) L.tstart[tid] = L.cnt[tid * kOsWaves];
+  if (tid == 0) L.tstart[256] = tn;
+  __syncthreads();
+  if (tid < 256)                                 // digit tid: this tile's count
+    os_store(look_p + tile * 256 + tid,
+             kOsFlagA | (uint32_t)(L.tstart[tid + 1] - L.tstart[tid]));
+  {                                              // the counts of the tiles before: thread
+    const int dg = tid & 255, h = tid >> 8;      // (digit, half) sums every other tile
+    const uint32_t part = os_sum_before(look_p + dg, tile, 256, h, kOsThreads / 256);
+    if (h == 1) L.half[dg] = part;
+    __syncthreads();
+    if (h == 0)                                  // + the key's offset inside the tile
+      L.gbase[dg] += (int)(part + L.half[dg]) - L.tstart[dg];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int cc = 0; cc < kOsChunks; ++cc) {
+    const int i = (wid * kOsChunks + cc) * 64 + lane;
+    if (i < tn) {
+      const uint32_t kv = L.k[i];
+      const int dd = (int)((kv >> shift) & 255u);
+      const int dst = L.gbase[dd] + L.cnt[dd * kOsWaves + wid] + L.rank[i];
+      kout[dst] = (int32_t)kv;
+      vout[dst] = L.v[i];
+    }
+  }
+  // this pass's histogram and look-back words, zeroed by its last block
+  os_cleanup(ticket_p, look_p, tiles * 256, &L.last);
+  if (L.last)
+    for (int q = tid; q < 256; q += kOsThreads) hist_p[q] = 0u;
+}
+
+__global__ __launch_bounds__(kOsThreads) void os_seg_kernel(
+    const int32_t* __restrict__ k, int n, int64_t tiles, uint32_t* __restrict__ look,
+    uint32_t* __restrict__ ticket, int32_t* __restrict__ uniq, int32_t* __restrict__ seg,
+    int32_t* __restrict__ n_uniq, int32_t* __restrict__ pos_seg) {
+  __shared__ int scan[kOsWaves + 1];
+  __shared__ int prefix;
+  __shared__ int last;
+  const int64_t tile = blockIdx.x;
+  const int base = (int)(tile * kOsTile);
+  const int i0 = base + threadIdx.x * kOsIpt;      // blocked: kOsIpt consecutive keys
+  int32_t kk[kOsIpt];
+  int f = 0;
+#pragma unroll
+  for (int j = 0; j < kOsIpt; ++j) {
+    const int i = i0 + j;
+    kk[j] = i < n ? k[i] : 0;
+    if (i < n) f += (i == 0 || k[i - 1] != kk[j]) ? 1 : 0;
+  }
+  int tot;
+  const int ex = block_exclusive_scan(f, scan, &tot);
+  if (threadIdx.x == 0) os_store(look + tile, kOsFlagA | (uint32_t)tot);
+  {                                              // run heads of the tiles before this one
+    const uint32_t part = os_sum_before(look, tile, 1, threadIdx.x, kOsThreads);
+    int all;
+    (void)block_exclusive_scan((int)part, scan, &all);
+    if (threadIdx.x == 0) {
+      prefix = all;
+      if (tile == tiles - 1) {
+        seg[all + tot] = n;
+        n_uniq[0] = (int32_t)(all + tot);
+      }
+    }
+  }
+  __syncthreads();
+  int o = prefix + ex;
+#pragma unroll
+  for (int j = 0; j < kOsIpt; ++j) {
+    const int i = i0 + j;
+    if (i < n) {
+      if (i == 0 || k[i - 1] != kk[j]) {
+        uniq[o] = kk[j];
+        seg[o] = i;
+        ++o;
+      }
+      if (pos_seg) pos_seg[i] = o - 1;
+    }
+  }
+  os_cleanup(ticket, look, tiles, &last);
+}
+
+// ---------------------------------------------------------------------------
 // Chunked segmented scatter-add (hot rows: a Zipf head row may own 10^4..10^5
 // contributions, far too many for one wave to sum serially). Every segment is cut
 // into pieces of CH = scat_chunk(d) positions counted from ITS OWN start, so a row's
@@ -1072,6 +1334,101 @@ __global__ __launch_bounds__(256) void scatter_window_kernel(
   }
 }
 
+// Wide rows (16 < d <= 256) with pos_seg: chunk c of CH = 32 sorted positions owns the
+// same pieces as scatter_chunks_kernel and sums them in the same order (bit for bit).
+// One wave per chunk: lane l resolves window position p0 + l of [p0, p0 + 64) (perm,
+// segment, piece, ownership); then the wave walks the window in order, eight positions'
+// row loads in flight at a time — position t's perm and flags come from lane t by
+// readlane, so the walk is uniform (scalar branches) and every row read is one coalesced
+// access of the lanes' columns (l, l + 64, ...).
+template <int MAXC>
+__global__ __launch_bounds__(256) void scatter_wide_window_kernel(
+    const float* __restrict__ rows, int d, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ pos_seg, const int32_t* __restrict__ uniq,
+    const int32_t* __restrict__ seg, const int32_t* __restrict__ n_uniq_dev,
+    float* __restrict__ dense, int64_t n_rows, float* __restrict__ head,
+    float* __restrict__ tail, int32_t* __restrict__ tail_seg, int n_chunks, int compact) {
+  constexpr int CH = 32, W = 64;
+  const int nu = n_uniq_dev[0];
+  const int n = seg[nu];
+  const int lane = threadIdx.x & 63;
+  const int c = __builtin_amdgcn_readfirstlane(
+      (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  if (c >= n_chunks) return;
+  const int p0 = c * CH;
+  if (nu == 0 || p0 >= n) {
+    if (lane == 0) tail_seg[c] = -1;
+    return;
+  }
+  const int p1 = min(n, p0 + CH);
+  const int q = p0 + lane;
+  int pq = 0, info = 0, dst = 0;      // info: 1 owned | 2 piece start | 4 piece end | kind << 3
+  if (q < n) {
+    pq = perm[q];
+    const int u = pos_seg[q];
+    const int s0 = seg[u], e = seg[u + 1];
+    const int ps = s0 + (q - s0) / CH * CH;
+    if (ps >= p0 && ps < p1) {
+      const int pe = min(e, ps + CH);
+      const int kind = ps != s0 ? kWinKindHead : (e - s0 <= CH ? kWinKindFinal : kWinKindTail);
+      info = 1 | (q == ps ? 2 : 0) | (q == pe - 1 ? 4 : 0) | (kind << 3);
+      dst = kind == kWinKindFinal ? (compact ? u : uniq[u]) : u;
+    }
+  }
+  const uint64_t tb = __ballot((info & 2) && (info >> 3) == kWinKindTail);
+  const int tsu = tb ? __builtin_amdgcn_readlane(dst, __builtin_ctzll(tb)) : -1;
+  if (lane == 0) tail_seg[c] = tsu;
+  int col[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) col[j] = min(lane + 64 * j, d - 1);
+  float acc[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) acc[j] = 0.f;
+  for (int t0 = 0; t0 < W; t0 += 8) {
+    int it[8], pt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      it[j] = __builtin_amdgcn_readlane(info, t0 + j);
+      pt[j] = __builtin_amdgcn_readlane(pq, t0 + j);
+    }
+    float v[8][MAXC];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int cc = 0; cc < MAXC; ++cc)
+        v[j][cc] = (it[j] & 1) ? rows[(int64_t)pt[j] * d + col[cc]] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!(it[j] & 1)) continue;
+#pragma unroll
+      for (int cc = 0; cc < MAXC; ++cc) acc[cc] = ((it[j] & 2) ? 0.f : acc[cc]) + v[j][cc];
+      if (!(it[j] & 4)) continue;
+      const int kind = it[j] >> 3;
+      const int dt = __builtin_amdgcn_readlane(dst, t0 + j);
+      if (kind == kWinKindFinal) {
+        const int64_t row = dt;
+        if (row >= 0 && row < n_rows) {
+#pragma unroll
+          for (int cc = 0; cc < MAXC; ++cc) {
+            const int cl = lane + 64 * cc;
+            if (cl < d) {
+              if (compact) dense[row * d + cl] = acc[cc]; else dense[row * d + cl] += acc[cc];
+            }
+          }
+        }
+      } else {
+        float* out = (kind == kWinKindTail ? tail : head) + (int64_t)c * d;
+#pragma unroll
+        for (int cc = 0; cc < MAXC; ++cc) {
+          const int cl = lane + 64 * cc;
+          if (cl < d) out[cl] = acc[cc];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -1183,6 +1540,53 @@ extern "C" int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n,
                      (hipStream_t)stream, keys, n, (int)block_n, perm, uniq, seg, n_uniq_dev,
                      status, pos_seg);
   return launch_status("mirec_segment_sort_blocks_chained");
+}
+
+extern "C" int64_t mirec_segment_sort_onesweep_status_words(int64_t n) {
+  return n > 0 ? os_status_words(n) : 0;
+}
+
+extern "C" int mirec_segment_sort_onesweep(const int64_t* keys, int64_t n, int64_t key_space,
+                                           int32_t* perm, int32_t* uniq, int32_t* seg,
+                                           int32_t* n_uniq_dev, int32_t* pos_seg, void* ws,
+                                           size_t ws_bytes, int32_t* status, int64_t n_status,
+                                           void* stream) {
+  if (n <= 0 || n > (int64_t)kOsVal || key_space <= 0 || key_space > INT32_MAX || !keys ||
+      !perm || !uniq || !seg || !n_uniq_dev || !status) {
+    set_error("mirec_segment_sort_onesweep: bad arguments (0 < n < 2^30)");
+    return -1;
+  }
+  if (n_status < os_status_words(n) || !ws || ws_bytes < (size_t)4 * (size_t)n * 4) {
+    set_error("mirec_segment_sort_onesweep: status (%lld words) or workspace too small",
+              (long long)os_status_words(n));
+    return -1;
+  }
+  int nbits = 0;
+  while (nbits < 31 && ((int64_t)1 << nbits) < key_space) ++nbits;
+  const int passes = nbits == 0 ? 1 : (nbits + 7) / 8;
+  const int64_t tiles = os_tiles(n);
+  uint32_t* hist = (uint32_t*)status;
+  uint32_t* look = hist + kOsMaxPasses * 256;
+  uint32_t* slook = look + (int64_t)kOsMaxPasses * tiles * 256;
+  uint32_t* tickets = slook + tiles;
+  int32_t* kA = (int32_t*)ws;
+  int32_t* vA = kA + n;
+  int32_t* kB = vA + n;
+  int32_t* vB = kB + n;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(os_hist_kernel, dim3((unsigned)tiles), dim3(kOsThreads), 0, st, keys,
+                     (int)n, passes, kA, vA, hist);
+  for (int p = 0; p < passes; ++p) {
+    int32_t* vo = p == passes - 1 ? perm : vB;     // the last pass writes perm itself
+    hipLaunchKernelGGL(os_pass_kernel, dim3((unsigned)tiles), dim3(kOsThreads), 0, st, kA, vA,
+                       (int)n, 8 * p, tiles, hist + p * 256, look + (int64_t)p * tiles * 256,
+                       tickets + p, kB, vo);
+    int32_t* t = kA; kA = kB; kB = t;
+    t = vA; vA = vB; vB = t;
+  }
+  hipLaunchKernelGGL(os_seg_kernel, dim3((unsigned)tiles), dim3(kOsThreads), 0, st, kA, (int)n,
+                     tiles, slook, tickets + kOsMaxPasses, uniq, seg, n_uniq_dev, pos_seg);
+  return launch_status("mirec_segment_sort_onesweep");
 }
 
 extern "C" int mirec_segment_sort(const int64_t* keys, int64_t n, int64_t key_space,
@@ -1312,6 +1716,45 @@ extern "C" int mirec_segment_reduce2_pos_seg_f32(const float* rows, int32_t d,
   }
   return reduce2_impl(rows, d, rows1, perm, pos_seg, uniq, seg, n_uniq_dev, n, out, out1, ws,
                       ws_bytes, stream);
+}
+
+extern "C" int mirec_segment_reduce_pos_seg_f32(const float* rows, int32_t d,
+                                                const int32_t* perm, const int32_t* pos_seg,
+                                                const int32_t* uniq, const int32_t* seg,
+                                                const int32_t* n_uniq_dev, int64_t n, float* out,
+                                                void* ws, size_t ws_bytes, void* stream) {
+  if (n == 0) return 0;
+  if (!rows || !perm || !pos_seg || !uniq || !seg || !n_uniq_dev || !out || d <= 0 ||
+      d > 256 || n < 0 || n > INT32_MAX) {
+    set_error("mirec_segment_reduce_pos_seg_f32: bad arguments (1 <= d <= 256)");
+    return -1;
+  }
+  if (!ws || ws_bytes < mirec_segment_scatter_add_workspace_size(n, d)) {
+    set_error("mirec_segment_reduce_pos_seg_f32: workspace too small");
+    return -1;
+  }
+  const int chunks = (int)((n + scat_chunk(d) - 1) / scat_chunk(d));
+  float* head = (float*)ws;
+  float* tail = head + (int64_t)chunks * d;
+  int32_t* tail_seg = (int32_t*)(tail + (int64_t)chunks * d);
+  hipStream_t st = (hipStream_t)stream;
+  if (d <= 16) {
+    const int64_t gpb = 4 * (64 / 16);
+    hipLaunchKernelGGL((scatter_window_kernel<false>), dim3((unsigned)((chunks + gpb - 1) / gpb)),
+                       dim3(256), 0, st, rows, d, perm, pos_seg, uniq, seg, n_uniq_dev, out, n,
+                       head, tail, tail_seg, chunks, 1, nullptr, nullptr, nullptr, nullptr);
+  } else {
+    const dim3 grd((unsigned)((chunks + 3) / 4));   // four waves (chunks) per workgroup
+#define MIREC_WIDE(MC)                                                                         hipLaunchKernelGGL((scatter_wide_window_kernel<MC>), grd, dim3(256), 0, st, rows, d, perm,                        pos_seg, uniq, seg, n_uniq_dev, out, n, head, tail, tail_seg, chunks, 1)
+    if (d <= 64) MIREC_WIDE(1);
+    else if (d <= 128) MIREC_WIDE(2);
+    else MIREC_WIDE(4);
+#undef MIREC_WIDE
+  }
+  if (chunks > 1)
+    hipLaunchKernelGGL(scatter_fixup_kernel, dim3(fixup_blocks(chunks)), dim3(64 * kFixWaves), 0,
+                       st, d, uniq, seg, tail_seg, out, n, head, tail, chunks, 1);
+  return launch_status("mirec_segment_reduce_pos_seg_f32");
 }
 
 extern "C" int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,

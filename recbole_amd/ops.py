@@ -409,12 +409,45 @@ class Segments:
         self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
 
 
+ONESWEEP_MIN = 8193          # above the single-workgroup LDS sort
+_SORT_STATUS = {}
+
+
+def _sort_status(device, words):
+    """Zeroed look-back / histogram words of the onesweep sort, one buffer per device —
+    every call leaves it zero; calls are stream-ordered (the model's stream; a graph's
+    warm-up and capture streams wait for each other), as for _scatter_ws. None while a
+    graph capture is running and the buffer does not exist yet or is too small (the
+    caller then takes the radix path)."""
+    key = str(device)
+    buf = _SORT_STATUS.get(key)
+    if buf is None or buf.numel() < words:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        buf = torch.zeros(max(words, 1 << 16), dtype=torch.int32, device=device)
+        _SORT_STATUS[key] = buf
+    return buf
+
+
 def segment_sort(keys: torch.Tensor, key_space: int, segs: Segments | None = None) -> Segments:
     _dev(keys, torch.int64, "keys")
     n = keys.numel()
     wsz = lib().mirec_segment_sort_workspace_size(n, key_space)
     if segs is None or segs.n < n or segs.ws.numel() < wsz:
         segs = Segments(n, keys.device, wsz)
+    status = None
+    if ONESWEEP_MIN <= n < (1 << 30):
+        status = _sort_status(keys.device, lib().mirec_segment_sort_onesweep_status_words(n))
+    if status is not None:
+        if segs.pos_seg is None or segs.pos_seg.numel() < n:
+            segs.pos_seg = torch.empty(n, dtype=torch.int32, device=keys.device)
+        rc = lib().mirec_segment_sort_onesweep(
+            ptr(keys), n, key_space, ptr(segs.perm), ptr(segs.uniq), ptr(segs.seg),
+            ptr(segs.n_uniq), ptr(segs.pos_seg), ptr(segs.ws), segs.ws.numel(), ptr(status),
+            status.numel(), stream_handle())
+        check(rc, "mirec_segment_sort_onesweep")
+        return segs
+    segs.pos_seg = None
     rc = lib().mirec_segment_sort(ptr(keys), n, key_space, ptr(segs.perm), ptr(segs.uniq),
                                   ptr(segs.seg), ptr(segs.n_uniq), ptr(segs.ws), segs.ws.numel(),
                                   stream_handle())
@@ -517,9 +550,16 @@ def segment_reduce(rows: torch.Tensor, segs: Segments):
     n, d = segs.n, rows.shape[1]
     out = torch.empty(max(n, 1), d, dtype=torch.float32, device=rows.device)
     ws = _scatter_ws(rows.device, lib().mirec_segment_scatter_add_workspace_size(n, d))
-    rc = lib().mirec_segment_reduce_f32(ptr(rows), d, ptr(segs.perm), ptr(segs.uniq),
-                                        ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out), ptr(ws),
-                                        ws.numel(), stream_handle())
+    pos_seg = getattr(segs, 'pos_seg', None)
+    if pos_seg is not None and pos_seg is not getattr(segs, 'perm', None):
+        rc = lib().mirec_segment_reduce_pos_seg_f32(ptr(rows), d, ptr(segs.perm), ptr(pos_seg),
+                                                    ptr(segs.uniq), ptr(segs.seg),
+                                                    ptr(segs.n_uniq), n, ptr(out), ptr(ws),
+                                                    ws.numel(), stream_handle())
+    else:
+        rc = lib().mirec_segment_reduce_f32(ptr(rows), d, ptr(segs.perm), ptr(segs.uniq),
+                                            ptr(segs.seg), ptr(segs.n_uniq), n, ptr(out),
+                                            ptr(ws), ws.numel(), stream_handle())
     check(rc, "mirec_segment_reduce_f32")
     ident = Segments.__new__(Segments)
     ident.n = n

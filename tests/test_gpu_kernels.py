@@ -734,12 +734,75 @@ def test_large_segment_sort_and_hot_row_scatter(dev, n, key_space, d):
     assert np.array_equal(segs.perm[:n].cpu().numpy(), order)
     assert np.array_equal(segs.uniq[:nu].cpu().numpy(), u)
     assert np.array_equal(segs.seg[:nu + 1].cpu().numpy(), np.r_[first, n])
+    if segs.pos_seg is not None:
+        assert np.array_equal(segs.pos_seg[:n].cpu().numpy(), np.repeat(np.arange(nu),
+                                                                     np.diff(np.r_[first, n])))
     rows = torch.randn(n, d, generator=torch.Generator().manual_seed(1))
     n_rows = int(keys.max()) + 1
     exp = torch.zeros(n_rows, d, dtype=torch.float64).index_add_(
         0, torch.as_tensor(keys), rows.double())
     got = ops.segment_scatter_add(rows.to(dev), segs, torch.zeros(n_rows, d, device=dev))
     torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize('n,key_space,kind', [(8193, 1, 'zero'), (8193, 2, 'bits'),
+                                               (2048 * 7, 3_000_001, 'zipf'),
+                                               (309_248, 3_000_001, 'zipf'),
+                                               (100_001, (1 << 30) + 5, 'uniform'),
+                                               (50_000, 300, 'uniform')])
+def test_onesweep_sort_exact(dev, n, key_space, kind):
+    """The device-wide onesweep sort (8-bit passes, look-back offsets, look-back segment
+    scan) equals numpy's stable argsort for every pass count (0-4 digit bits over 1 to
+    31-bit key spaces), exact tile multiples and a ragged last tile, Zipf heads; pos_seg
+    is each sorted position's segment; its status words are zero after every call."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(n + key_space)
+    if kind == 'zero':
+        keys = np.zeros(n, np.int64)
+    elif kind == 'zipf':
+        keys = (np.minimum(rng.zipf(1.1, n), key_space) - 1).astype(np.int64)
+    else:
+        keys = rng.integers(0, key_space, n).astype(np.int64)
+    kd = torch.as_tensor(keys, device=dev)
+    order = np.argsort(keys, kind='stable')
+    u, first = np.unique(keys[order], return_index=True)
+    for _ in range(2):                                  # the status buffer is reused
+        segs = ops.segment_sort(kd, key_space)
+        assert segs.pos_seg is not None
+        nu = int(segs.n_uniq.item())
+        assert nu == len(u)
+        assert np.array_equal(segs.perm[:n].cpu().numpy(), order)
+        assert np.array_equal(segs.uniq[:nu].cpu().numpy(), u)
+        assert np.array_equal(segs.seg[:nu + 1].cpu().numpy(), np.r_[first, n])
+        assert np.array_equal(segs.pos_seg[:n].cpu().numpy(),
+                              np.repeat(np.arange(nu), np.diff(np.r_[first, n])))
+    torch.cuda.synchronize()
+    for buf in ops._SORT_STATUS.values():
+        assert int(buf.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize('d', [1, 4, 16, 64, 100, 128, 256])
+def test_segment_reduce_pos_seg_equals_search(dev, d):
+    """segment_reduce over the onesweep grouping, which gives pos_seg (window kernels, no
+    search) equals the searching chunk kernel bit for bit: Zipf-hot rows of thousands of
+    contributions (fixup), one-piece rows, -0.0 terms, d not a multiple of 64."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(d)
+    n = 60_000
+    keys = (np.minimum(rng.zipf(1.1, n), 3_000_000) - 1).astype(np.int64)
+    kd = torch.as_tensor(keys, device=dev)
+    rows = torch.randn(n, d, generator=torch.Generator().manual_seed(d))
+    rows[::11] = -0.0
+    rows = rows.to(dev)
+    sg = ops.segment_sort(kd, 3_000_000)
+    assert sg.pos_seg is not None
+    plain = ops.Segments(n, dev)
+    for f in ('perm', 'uniq', 'seg', 'n_uniq'):
+        setattr(plain, f, getattr(sg, f))
+    a, _ = ops.segment_reduce(rows, plain)
+    b, _ = ops.segment_reduce(rows, sg)
+    nu = int(sg.n_uniq.item())
+    assert torch.equal(a[:nu].view(torch.int32), b[:nu].view(torch.int32))
 
 
 @pytest.mark.parametrize('d', [1, 16, 128])

@@ -2,7 +2,7 @@
 # Round-4: C3 step trace and line.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r4r
+O=${O3:-gpurun_out/r4r}
 mkdir -p $O
 MODELS_MARKERS=1 timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d $O/tr_C3 -o run -- \
   python tools/bench_models.py --configs C3 --steps 8 --warmup 3 --no-cpu-baseline > $O/tr_C3.log 2>&1 || exit 7
