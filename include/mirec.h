@@ -361,6 +361,18 @@ int mirec_segment_scatter_add_f32(const float* rows, int32_t d, const int32_t* p
                                   const int32_t* uniq, const int32_t* seg,
                                   const int32_t* n_uniq_dev, int64_t n, float* dense,
                                   int64_t n_rows, void* ws, size_t ws_bytes, void* stream);
+/* The deferred optimizer's second level for two reduced sources of one table: A =
+ * (uA[0..*nA_dev) ascending distinct, rowsA [capA, d]), B likewise. uniq_out / rows_out
+ * get the union rows ascending, *n_out_dev their count, and each row the sum the
+ * second-level mirec_segment_reduce_f32 of [A; B] gives ((0 + a) + b, 0 + a, 0 + b; with
+ * a_pre = 1, a already carries its 0 +: a previous merge's output) — bit for bit,
+ * without sorting the concatenated keys. ws: >= 8 * (capA + capB) bytes; status:
+ * >= (capA + capB) / 512 + 2 int32, zero before the call, left zero. Two launches. */
+int mirec_segment_merge2_f32(const int32_t* uA, const int32_t* nA_dev, int64_t capA,
+                             const float* rowsA, const int32_t* uB, const int32_t* nB_dev,
+                             int64_t capB, const float* rowsB, int32_t d, int32_t a_pre,
+                             int32_t* uniq_out, int32_t* n_out_dev, float* rows_out, void* ws,
+                             size_t ws_bytes, int32_t* status, int64_t n_status, void* stream);
 /* Compact form: out[u, :] = sum of segment u's contributions (u < n_uniq), the same
  * chunked fixed-order summation; out needs n rows. Lets K5 take each touched row's
  * gradient as one row (hot Zipf rows would otherwise be summed serially in K5). */

@@ -155,6 +155,8 @@ SIGNATURES = {
                                          _P]),
     "mirec_segment_reduce_pos_seg_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P,
                                                  _P, c_size_t, _P]),
+    "mirec_segment_merge2_f32": (c_int, [_P, _P, c_int64, _P, _P, _P, c_int64, _P, c_int32,
+                                         c_int32, _P, _P, _P, _P, c_size_t, _P, c_int64, _P]),
     "mirec_segment_reduce2_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P, _P,
                                           c_size_t, _P]),
     "mirec_segment_reduce2_pos_seg_f32": (c_int, [_P, c_int32, _P, _P, _P, _P, _P, _P, c_int64,

@@ -1429,6 +1429,159 @@ __global__ __launch_bounds__(256) void scatter_wide_window_kernel(
   }
 }
 
+// Union of two reduced gradients (the deferred optimizer's second level, one table read
+// by two autograd Functions): A = (uA[0..nA), rowsA), B = (uB[0..nB), rowsB), each
+// ascending and distinct. Output: the union rows ascending, each row's sum formed as the
+// second-level segment_reduce of [A's rows; B's rows] formed it — (0 + a) + b, 0 + a,
+// 0 + b — where a_pre = 1 takes a as already carrying its leading 0 + (a previous
+// merge's output): the same bits, with no sort of the concatenated keys and no reduce.
+// Two launches: a stable merge of the key lists (A before B on equal keys) into the
+// merged order, then the run heads (tile counts summed over the tiles before, as in
+// os_seg_kernel) with each head's one or two rows summed by a wave.
+__device__ __forceinline__ int merge_lower(const int32_t* __restrict__ a, int n, int32_t key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int merge_upper(const int32_t* __restrict__ a, int n, int32_t key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void merge_place_kernel(
+    const int32_t* __restrict__ uA, const int32_t* __restrict__ nA_dev, int capA,
+    const int32_t* __restrict__ uB, const int32_t* __restrict__ nB_dev, int capB,
+    int32_t* __restrict__ mk, int32_t* __restrict__ ref) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nA = nA_dev[0], nB = nB_dev[0];
+  if (i < capA) {
+    if (i >= nA) return;
+    const int32_t key = uA[i];
+    const int pos = (int)i + merge_lower(uB, nB, key);
+    mk[pos] = key;
+    ref[pos] = (int32_t)i;
+  } else if (i < (int64_t)capA + capB) {
+    const int j = (int)(i - capA);
+    if (j >= nB) return;
+    const int32_t key = uB[j];
+    const int pos = j + merge_upper(uA, nA, key);
+    mk[pos] = key;
+    ref[pos] = (int32_t)(0x80000000u | (uint32_t)j);
+  }
+}
+
+constexpr int kMergeThreads = 256;
+constexpr int kMergeIpt = 2;
+constexpr int kMergeTile = kMergeThreads * kMergeIpt;   // merged positions per workgroup
+
+// one output row's (up to two) source rows folded, V floats at column c
+template <int V>
+__device__ __forceinline__ void merge_fold(const float* __restrict__ s0,
+                                           const float* __restrict__ s1, bool pre0, bool two,
+                                           float* __restrict__ dst) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    float v = s0[e];
+    if (!pre0) v = 0.f + v;
+    if (two) v = v + s1[e];
+    dst[e] = v;
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kMergeThreads) void merge_compact_kernel(
+    const int32_t* __restrict__ mk, const int32_t* __restrict__ ref,
+    const int32_t* __restrict__ nA_dev, const int32_t* __restrict__ nB_dev,
+    const float* __restrict__ rowsA, const float* __restrict__ rowsB, int d, int a_pre,
+    int32_t* __restrict__ uniq_out, int32_t* __restrict__ n_out, float* __restrict__ rows_out,
+    uint32_t* __restrict__ look, uint32_t* __restrict__ ticket) {
+  __shared__ int scan[kMergeThreads / 64 + 1];
+  __shared__ int hp[kMergeTile];                  // merged position of each run head
+  __shared__ int h0[kMergeTile], h1[kMergeTile];  // each head's source rows
+  __shared__ int prefix, n_heads, last;
+  const int m = nA_dev[0] + nB_dev[0];
+  const int64_t tile = blockIdx.x;
+  const int base = (int)(tile * kMergeTile);
+  const int i0 = base + threadIdx.x * kMergeIpt;
+  int f = 0;
+#pragma unroll
+  for (int j = 0; j < kMergeIpt; ++j) {
+    const int p = i0 + j;
+    if (p < m) f += (p == 0 || mk[p - 1] != mk[p]) ? 1 : 0;
+  }
+  int tot;
+  const int ex = block_exclusive_scan(f, scan, &tot);
+  if (threadIdx.x == 0) os_store(look + tile, kOsFlagA | (uint32_t)tot);
+  {
+    const uint32_t part = os_sum_before(look, tile, 1, threadIdx.x, kMergeThreads);
+    int all;
+    (void)block_exclusive_scan((int)part, scan, &all);
+    if (threadIdx.x == 0) {
+      prefix = all;
+      n_heads = tot;
+      if (tile == gridDim.x - 1) n_out[0] = all + tot;
+    }
+  }
+  int o = ex;
+#pragma unroll
+  for (int j = 0; j < kMergeIpt; ++j) {
+    const int p = i0 + j;
+    if (p < m && (p == 0 || mk[p - 1] != mk[p])) hp[o++] = p;
+  }
+  __syncthreads();
+  // per head: its one or two source rows, resolved once (LDS), uniq written
+  for (int h = threadIdx.x; h < n_heads; h += kMergeThreads) {
+    const int p = hp[h];
+    const int32_t key = mk[p];
+    const int r0 = ref[p];
+    const bool two = p + 1 < m && mk[p + 1] == key;
+    h0[h] = r0;                                    // A row, or B row | 0x80000000
+    h1[h] = two ? (ref[p + 1] & 0x7fffffff) : -1;  // the B row of a row in both
+    uniq_out[prefix + h] = key;
+  }
+  __syncthreads();
+  // (head, column group) items over the block's lanes, eight items' loads in flight
+  const int dv = d / V;
+  const int items = n_heads * dv;
+  for (int it0 = threadIdx.x; it0 < items; it0 += 8 * kMergeThreads) {
+    float a[8][V], b[8][V];
+    int hh[8], cc[8];
+    bool tw[8], pre[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int it = min(it0 + j * kMergeThreads, items - 1);
+      const int h = it / dv;
+      cc[j] = (it - h * dv) * V;
+      hh[j] = h;
+      const int r0 = h0[h], r1 = h1[h];
+      tw[j] = r1 >= 0;
+      const bool fromA = r0 >= 0;
+      pre[j] = fromA && a_pre;
+      const float* s0 = (fromA ? rowsA + (int64_t)r0 * d
+                               : rowsB + (int64_t)(r0 & 0x7fffffff) * d) + cc[j];
+      const float* s1 = rowsB + (int64_t)(tw[j] ? r1 : 0) * d + cc[j];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        a[j][e] = s0[e];
+        b[j][e] = s1[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (it0 + j * kMergeThreads >= items) continue;
+      merge_fold<V>(a[j], b[j], pre[j], tw[j], rows_out + (int64_t)(prefix + hh[j]) * d + cc[j]);
+    }
+  }
+  os_cleanup(ticket, look, gridDim.x, &last);
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -1755,6 +1908,42 @@ extern "C" int mirec_segment_reduce_pos_seg_f32(const float* rows, int32_t d,
     hipLaunchKernelGGL(scatter_fixup_kernel, dim3(fixup_blocks(chunks)), dim3(64 * kFixWaves), 0,
                        st, d, uniq, seg, tail_seg, out, n, head, tail, chunks, 1);
   return launch_status("mirec_segment_reduce_pos_seg_f32");
+}
+
+extern "C" int mirec_segment_merge2_f32(const int32_t* uA, const int32_t* nA_dev, int64_t capA,
+                                        const float* rowsA, const int32_t* uB,
+                                        const int32_t* nB_dev, int64_t capB, const float* rowsB,
+                                        int32_t d, int32_t a_pre, int32_t* uniq_out,
+                                        int32_t* n_out_dev, float* rows_out, void* ws,
+                                        size_t ws_bytes, int32_t* status, int64_t n_status,
+                                        void* stream) {
+  const int64_t cap = capA + capB;
+  if (!uA || !nA_dev || !rowsA || !uB || !nB_dev || !rowsB || !uniq_out || !n_out_dev ||
+      !rows_out || !status || capA < 0 || capB < 0 || cap <= 0 || cap >= (int64_t)kOsVal ||
+      d <= 0 || d > 1024) {
+    set_error("mirec_segment_merge2_f32: bad arguments");
+    return -1;
+  }
+  const int64_t tiles = (cap + kMergeTile - 1) / kMergeTile;
+  if (!ws || ws_bytes < (size_t)(2 * cap) * sizeof(int32_t) || n_status < tiles + 1) {
+    set_error("mirec_segment_merge2_f32: workspace (%lld B) or status (%lld words) too small",
+              (long long)(2 * cap * 4), (long long)(tiles + 1));
+    return -1;
+  }
+  int32_t* mk = (int32_t*)ws;
+  int32_t* ref = mk + cap;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(merge_place_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st,
+                     uA, nA_dev, (int)capA, uB, nB_dev, (int)capB, mk, ref);
+  if (d % 4 == 0)
+    hipLaunchKernelGGL(merge_compact_kernel<4>, dim3((unsigned)tiles), dim3(kMergeThreads), 0, st,
+                       mk, ref, nA_dev, nB_dev, rowsA, rowsB, d, a_pre, uniq_out, n_out_dev,
+                       rows_out, (uint32_t*)status, (uint32_t*)status + tiles);
+  else
+    hipLaunchKernelGGL(merge_compact_kernel<1>, dim3((unsigned)tiles), dim3(kMergeThreads), 0, st,
+                       mk, ref, nA_dev, nB_dev, rowsA, rowsB, d, a_pre, uniq_out, n_out_dev,
+                       rows_out, (uint32_t*)status, (uint32_t*)status + tiles);
+  return launch_status("mirec_segment_merge2_f32");
 }
 
 extern "C" int mirec_segment_reduce_f32(const float* rows, int32_t d, const int32_t* perm,

@@ -571,6 +571,44 @@ def segment_reduce(rows: torch.Tensor, segs: Segments):
     return out, ident
 
 
+def segment_merge2(a, b, a_pre=False):
+    """Union of two reduced sources of one table — a, b: (compact rows, identity Segments
+    with uniq / n_uniq) as segment_reduce returns them — into (rows, identity Segments):
+    the second-level segment_reduce of their concatenation, bit for bit, in two launches
+    (mirec_segment_merge2_f32). a_pre: a is a previous merge's output."""
+    (ra, sa), (rb, sb) = a, b
+    _dev(ra, torch.float32, "rows a")
+    _dev(rb, torch.float32, "rows b")
+    d = ra.shape[1]
+    if rb.shape[1] != d:
+        raise ValueError("segment_merge2: row widths differ")
+    capA, capB = sa.n, sb.n
+    cap = max(capA + capB, 1)
+    dev = ra.device
+    out = torch.empty(cap, d, dtype=torch.float32, device=dev)
+    uniq = torch.empty(cap, dtype=torch.int32, device=dev)
+    n_uniq = torch.empty(1, dtype=torch.int32, device=dev)
+    ws = _scatter_ws(dev, 8 * cap)
+    status = _sort_status(dev, cap // 512 + 2)
+    if status is None:
+        raise NativeError("segment_merge2: no status buffer inside a capture (run one step "
+                          "eagerly first)")
+    rc = lib().mirec_segment_merge2_f32(ptr(sa.uniq), ptr(sa.n_uniq), capA, ptr(ra),
+                                        ptr(sb.uniq), ptr(sb.n_uniq), capB, ptr(rb), d,
+                                        1 if a_pre else 0, ptr(uniq), ptr(n_uniq), ptr(out),
+                                        ptr(ws), ws.numel(), ptr(status), status.numel(),
+                                        stream_handle())
+    check(rc, "mirec_segment_merge2_f32")
+    ident = Segments.__new__(Segments)
+    ident.n = cap
+    iota = _iota(dev, cap + 1)
+    ident.perm = iota[:cap]
+    ident.seg = iota[:cap + 1]
+    ident.uniq, ident.n_uniq, ident.ws = uniq, n_uniq, sa.ws
+    ident.pos_seg = ident.perm
+    return out, ident
+
+
 def segment_reduce2(rows: torch.Tensor, rows1: torch.Tensor, segs: Segments):
     """segment_reduce of a [n, d] source (2 <= d <= 16) and a [n, 1] source grouped by
     the same segments, in one pass: (compact, compact1, identity Segments), bit for bit

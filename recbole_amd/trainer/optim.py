@@ -382,6 +382,14 @@ class FusedAdam(torch.optim.Optimizer):
         if len(parts) == 1:
             rows, segs = parts[0]
             return rows, segs, segs.n
+        if all(cr.shape[0] >= cs.n for cr, cs in parts):
+            # second level as merges of the sources' row lists (ops.segment_merge2): the
+            # sums of the sort + reduce below, bit for bit, in two launches per merge
+            acc = parts[0]
+            for k, part in enumerate(parts[1:]):
+                acc = ops.segment_merge2(acc, part, a_pre=k > 0)
+            rows, segs = acc
+            return rows, segs, segs.n
         # second level: key = the table row of each compact row, sentinel n_rows
         # beyond a source's n_uniq (dropped after the sort: it is the last group)
         keys, rows = [], []

@@ -805,6 +805,54 @@ def test_segment_reduce_pos_seg_equals_search(dev, d):
     assert torch.equal(a[:nu].view(torch.int32), b[:nu].view(torch.int32))
 
 
+def _second_level_sort_reduce(parts, n_rows, dev):
+    """The deferred optimizer's second level as a sort of the concatenated keys + a reduce
+    (optim.py before segment_merge2): the reference the merges must equal bit for bit."""
+    from recbole_amd import ops
+    keys, rows = [], []
+    for cr, cs in parts:
+        idx = torch.arange(cs.n, device=dev)
+        keys.append(torch.where(idx < cs.n_uniq.long(), cs.uniq[:cs.n].long(),
+                                torch.full_like(idx, n_rows)))
+        rows.append(cr[:cs.n])
+    keys, rows = torch.cat(keys), torch.cat(rows)
+    segs = ops.segment_sort(keys, n_rows + 1)
+    last = segs.uniq.gather(0, (segs.n_uniq.long() - 1).clamp(min=0))
+    segs.n_uniq.sub_((last == n_rows).to(torch.int32))
+    return ops.segment_reduce(rows, segs)
+
+
+@pytest.mark.parametrize('d,n_parts', [(128, 2), (16, 3), (100, 2), (1, 2)])
+def test_segment_merge_equals_sort_reduce(dev, d, n_parts):
+    """The second level as merges of the sources' reduced row lists equals sorting the
+    concatenated keys and reducing, bit for bit: rows in one, two or all sources, -0.0
+    partial sums, sources of different lengths, a source with no rows at all."""
+    from recbole_amd import ops
+    rng = np.random.default_rng(d * 10 + n_parts)
+    n_rows = 3_000_001
+    parts = []
+    for k in range(n_parts):
+        n = [60_000, 9_000, 0][k] if n_parts == 3 else [40_000, 90_000][k]
+        if n == 0:
+            n = 1
+            keys = np.array([5], np.int64)
+        else:
+            keys = (np.minimum(rng.zipf(1.1 + 0.1 * k, n), n_rows) - 1).astype(np.int64)
+        rows = torch.randn(n, d, generator=torch.Generator().manual_seed(k))
+        rows[::7] = -0.0
+        segs = ops.segment_sort(torch.as_tensor(keys, device=dev), n_rows)
+        parts.append(ops.segment_reduce(rows.to(dev), segs))
+    ref_rows, ref_segs = _second_level_sort_reduce(parts, n_rows, dev)
+    acc = parts[0]
+    for k, part in enumerate(parts[1:]):
+        acc = ops.segment_merge2(acc, part, a_pre=k > 0)
+    rows, segs = acc
+    nu = int(ref_segs.n_uniq.item())
+    assert int(segs.n_uniq.item()) == nu
+    assert torch.equal(segs.uniq[:nu], ref_segs.uniq[:nu])
+    assert torch.equal(rows[:nu].view(torch.int32), ref_rows[:nu].view(torch.int32))
+
+
 @pytest.mark.parametrize('d', [1, 16, 128])
 def test_segment_reduce_independent_of_position(dev, d):
     """The chunked fixed-order reduction cuts each row's contributions into pieces
