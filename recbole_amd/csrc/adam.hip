@@ -111,7 +111,12 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 // Block of the deferred kernel: one row when a row fills whole waves, else one
 // wave of rows. Small blocks: the launch's rows differ widely in replay length,
 // and a CU takes a new block only when a whole block's waves are free.
-__host__ __device__ constexpr int deferred_block(int vpr) { return vpr > 64 ? vpr : 64; }
+#ifndef MIREC_DEFERRED_MIN_BLOCK
+#define MIREC_DEFERRED_MIN_BLOCK 256     // lanes per block (C3 336.9 -> 340.1 K sequences/s against 64: a quarter of the workgroups to dispatch)
+#endif
+__host__ __device__ constexpr int deferred_block(int vpr) {
+  return vpr > MIREC_DEFERRED_MIN_BLOCK ? vpr : MIREC_DEFERRED_MIN_BLOCK;
+}
 
 template <int D, typename V>
 __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   replay<V, (VPR >= 64)>(p, m, v, idle ? st : last, st, consts, k);
   const bool fresh = !idle && last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
-  __syncthreads();
+  if (VPR > 64) __syncthreads();     // a row spans waves; else the row's lanes are one wave's
   if (!valid || !fresh) return;
   const int64_t off = row * VPR + c;
   reinterpret_cast<V*>((T.p_alt && ((st + 1) & 1)) ? T.p_alt : T.p)[off] = p;

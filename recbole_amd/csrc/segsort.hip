@@ -1195,16 +1195,20 @@ __global__ __launch_bounds__(64 * kFixWaves) void scatter_fixup_kernel(
       const float tv = ts[(int64_t)(b - 1) * ld + min(col[j], ld - 1)];
       acc[j] = (kl[j] == 0 && col[j] < ld) ? tv : 0.f;
     }
-    for (int r = 0; b + r * KL <= kend; ++r) {
-      float hv[4];
+    for (int r0 = 0; b + r0 * KL <= kend; r0 += 4) {   // four rounds' loads in flight
+      float hv[4][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = min(b + kl[j] + r * KL, kend);
-        hv[j] = hs[(int64_t)k * ld + min(col[j], ld - 1)];
-      }
+      for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (col[j] < ld && b + kl[j] + r * KL <= kend) acc[j] += hv[j];
+        for (int j = 0; j < 4; ++j) {
+          const int k = min(b + kl[j] + (r0 + rr) * KL, kend);
+          hv[rr][j] = hs[(int64_t)k * ld + min(col[j], ld - 1)];
+        }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (col[j] < ld && b + kl[j] + (r0 + rr) * KL <= kend) acc[j] += hv[rr][j];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) R[lane + 64 * j] = acc[j];
