@@ -112,7 +112,9 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 // wave of rows. Small blocks: the launch's rows differ widely in replay length,
 // and a CU takes a new block only when a whole block's waves are free.
 #ifndef MIREC_DEFERRED_MIN_BLOCK
-#define MIREC_DEFERRED_MIN_BLOCK 256     // lanes per block (C3 336.9 -> 340.1 K sequences/s against 64: a quarter of the workgroups to dispatch)
+// lanes per block: 256 (C3 336.9 -> 340.1 K sequences/s against 64 — a quarter of the
+// workgroups to dispatch)
+#define MIREC_DEFERRED_MIN_BLOCK 256
 #endif
 __host__ __device__ constexpr int deferred_block(int vpr) {
   return vpr > MIREC_DEFERRED_MIN_BLOCK ? vpr : MIREC_DEFERRED_MIN_BLOCK;
