@@ -175,7 +175,7 @@ class FusedBPRTrainStep(object):
     # timed region that holds its own preparation) on the model's stream instead of the
     # prep streams. Measured slower on the C2 driver window (16.45 vs 17.06-17.16 M
     # positives/s: the first launch started 218 µs after t0 instead of 72 µs)
-    MAIN_FIRST = False
+    MAIN_FIRST = os.environ.get('MIREC_MAIN_FIRST', '0') == '1'   # first chunk on the model stream
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None, fused_step=None):
