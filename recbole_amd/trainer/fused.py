@@ -724,6 +724,7 @@ class FusedBPRTrainStep(object):
         whose chunk (and every later one) is not prepared until release_prep() —
         so a timed region that starts there contains its own chunks' sampler walk
         and grouping."""
+        self._late_top_up = None
         data = self.data
         if data.shuffle:
             data._shuffle()                     # randperm (CPU RNG) + device reorder
@@ -788,8 +789,15 @@ class FusedBPRTrainStep(object):
         timed region does not also run the sampler walk of the batches after it."""
         self._prep_limit = (len(self._plan) if upto is None
                             else self._chunk_of(max(int(upto) - 1, 0)) + 1)
-        if not self.MAIN_FIRST and self._next_chunk < min(len(self._plan), self._prep_limit):
-            self._issue_prep()                 # the first released walk starts right away
+        if self._next_chunk < min(len(self._plan), self._prep_limit):
+            k = self._next_chunk               # the first released walk starts right away:
+            if self.MAIN_FIRST and not self._sharded(self._plan[k][2]):
+                # the whole preparation on the model's stream (no cross-queue hand-off
+                # before the first step); the next chunks' preparation after its launch
+                self._issue_prep(on=torch.cuda.current_stream(self.device))
+                self._late_top_up = k
+            else:
+                self._issue_prep()
 
     def _issue_prep(self, on=None):
         k = self._next_chunk
@@ -827,9 +835,12 @@ class FusedBPRTrainStep(object):
                                'call release_prep() first')
         # this chunk's grouping first (its stream waits for the walk on the GPU; issued
         # later, the host's enqueue of the next walks would delay it), then the walks of
-        # the next chunks (the same walk stream: they start as this chunk's walk ends)
+        # the next chunks (the same walk stream: they start as this chunk's walk ends) —
+        # unless this chunk was prepared on the model's stream: then they follow its
+        # launches (run_batches), which the GPU reaches first
         self._issue_groups(k + 1)
-        self._top_up_prep(k)
+        if getattr(self, '_late_top_up', None) != k:
+            self._top_up_prep(k)
         stream.wait_event(self.slots[k % S].ready)
         self._cur = k
 
@@ -864,6 +875,9 @@ class FusedBPRTrainStep(object):
                 if c1 == nb and flush:
                     self._flush(stream, flush)
                     self._current = True
+            if getattr(self, '_late_top_up', None) == k:
+                self._late_top_up = None
+                self._top_up_prep(k)
             self._issue_groups(k + len(self.slots))   # later chunks' groupings, behind
             b = b0 + c1
             self._batches_enqueued = b
