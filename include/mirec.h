@@ -287,6 +287,15 @@ int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n, int64_t bl
                                       int64_t key_space, int32_t* perm, int32_t* uniq,
                                       int32_t* seg, int32_t* n_uniq_dev, int32_t* status,
                                       int64_t n_status, int32_t* pos_seg, void* stream);
+/* The same for keys given as fields (mirec_offset_keys' inputs: block f = cols[f][0..B)
+ * + offsets[f], ranges increasing with f): the launch forms the keys, writes them to
+ * keys_out [n_fields * B] and sorts them — mirec_offset_keys + the chained sort in one
+ * launch. 1 <= n_fields <= 64, B <= 4,096; status >= n_fields + 1 words (as above). */
+int mirec_segment_sort_fields_chained(const int64_t* const* cols, const int64_t* offsets,
+                                      int32_t n_fields, int64_t B, int64_t key_space,
+                                      int64_t* keys_out, int32_t* perm, int32_t* uniq,
+                                      int32_t* seg, int32_t* n_uniq_dev, int32_t* status,
+                                      int64_t n_status, int32_t* pos_seg, void* stream);
 
 /* Look-ahead lists of the deferred Adam: for b < n_batches-1,
  * out[b*stride ..) = uniq(b+1) \ uniq(b) ascending, n_out[b] its length, where

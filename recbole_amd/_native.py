@@ -137,6 +137,8 @@ SIGNATURES = {
     "mirec_segment_sort_onesweep_status_words": (c_int64, [c_int64]),
     "mirec_segment_sort_onesweep": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, _P,
                                             c_size_t, _P, c_int64, _P]),
+    "mirec_segment_sort_fields_chained": (c_int, [_P, _P, c_int32, c_int64, c_int64, _P, _P, _P,
+                                                  _P, _P, _P, c_int64, _P, _P]),
     "mirec_segment_sort_blocks": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P,
                                           c_size_t, _P]),
     "mirec_segment_sort_blocks_chained": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, _P, _P,

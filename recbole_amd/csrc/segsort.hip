@@ -238,11 +238,20 @@ extern "C" int mirec_r8_probe_read(uint64_t* host) {
 // before b and publishes without waiting, so the wait ends) and writes straight into the
 // concatenated outputs; the block that takes the last ticket in status[nblocks] zeroes
 // status again for the next launch.
+// Keys given as fields (DeepFM: block b = field b's column + the field's table offset):
+// the kernel forms them itself and writes them out for the forward's gathers.
+constexpr int kSortFields = 64;
+struct SortFields {
+  const int64_t* col[kSortFields];
+  int64_t off[kSortFields];
+  int64_t* keys_out;
+};
+
 __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
     const int64_t* __restrict__ keys_all, int64_t n_total, int batch_n,
     int32_t* __restrict__ perm_all, int32_t* __restrict__ uniq_all,
     int32_t* __restrict__ seg_all, int32_t* __restrict__ n_uniq_all,
-    int32_t* __restrict__ status, int32_t* __restrict__ pu_all) {
+    int32_t* __restrict__ status, int32_t* __restrict__ pu_all, const SortFields SF) {
   __shared__ R8Lds L;
   R8T(0);
   R8C(12);
@@ -253,7 +262,14 @@ __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   int lo = INT32_MAX, hi = INT32_MIN;
   for (int i = tid; i < n; i += kR8Threads) {
-    const int32_t kv = (int32_t)keys[i];
+    int32_t kv;
+    if (SF.keys_out) {                           // field b's id + its table offset
+      const int64_t k64 = SF.col[b][i] + SF.off[b];
+      SF.keys_out[b * (int64_t)batch_n + i] = k64;
+      kv = (int32_t)k64;
+    } else {
+      kv = (int32_t)keys[i];
+    }
     L.k[0][i] = (uint32_t)kv;
     L.v[0][i] = (uint16_t)i;
     lo = min(lo, kv);
@@ -1667,7 +1683,7 @@ extern "C" int mirec_segment_sort_blocks(const int64_t* keys, int64_t n, int64_t
   if (block_n <= kR8Max)       // 8-bit digits over the block's key span
     hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0, st, keys,
                        n, (int)block_n, perm_t, uniq_t, seg_t, nu_t, (int32_t*)nullptr,
-                       (int32_t*)nullptr);
+                       (int32_t*)nullptr, SortFields{});
   else
     hipLaunchKernelGGL(segsort_lds_kernel, dim3((unsigned)nb), dim3(kSortThreads), 0, st, keys,
                        n, (int)block_n, nbits, perm_t, uniq_t, seg_t, nu_t);
@@ -1695,8 +1711,39 @@ extern "C" int mirec_segment_sort_blocks_chained(const int64_t* keys, int64_t n,
   }
   hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)nb), dim3(kR8Threads), 0,
                      (hipStream_t)stream, keys, n, (int)block_n, perm, uniq, seg, n_uniq_dev,
-                     status, pos_seg);
+                     status, pos_seg, SortFields{});
   return launch_status("mirec_segment_sort_blocks_chained");
+}
+
+extern "C" int mirec_segment_sort_fields_chained(const int64_t* const* cols,
+                                                 const int64_t* offsets, int32_t n_fields,
+                                                 int64_t B, int64_t key_space, int64_t* keys_out,
+                                                 int32_t* perm, int32_t* uniq, int32_t* seg,
+                                                 int32_t* n_uniq_dev, int32_t* status,
+                                                 int64_t n_status, int32_t* pos_seg,
+                                                 void* stream) {
+  if (n_fields <= 0 || n_fields > kSortFields || B <= 0 || B > kR8Max || key_space <= 0 ||
+      key_space > INT32_MAX || !cols || !offsets || !keys_out || !perm || !uniq || !seg ||
+      !n_uniq_dev || !status || n_status < n_fields + 1) {
+    set_error("mirec_segment_sort_fields_chained: bad arguments (1..%d fields of 1..%d keys)",
+              kSortFields, kR8Max);
+    return -1;
+  }
+  SortFields SF;
+  memset(&SF, 0, sizeof(SF));
+  for (int f = 0; f < n_fields; ++f) {
+    if (!cols[f]) {
+      set_error("mirec_segment_sort_fields_chained: field %d has no column", f);
+      return -1;
+    }
+    SF.col[f] = cols[f];
+    SF.off[f] = offsets[f];
+  }
+  SF.keys_out = keys_out;
+  hipLaunchKernelGGL(segsort_radix8_kernel, dim3((unsigned)n_fields), dim3(kR8Threads), 0,
+                     (hipStream_t)stream, (const int64_t*)keys_out, (int64_t)n_fields * B, (int)B,
+                     perm, uniq, seg, n_uniq_dev, status, pos_seg, SF);
+  return launch_status("mirec_segment_sort_fields_chained");
 }
 
 extern "C" int64_t mirec_segment_sort_onesweep_status_words(int64_t n) {

@@ -162,15 +162,23 @@ class _CtxFMFn(torch.autograd.Function):
             # keys[f*B + i] = id + the field's table offset, every field in one launch
             cols = [_col(interaction, n, torch.int64) for n in layout.token_names]
             nt = len(cols)
-            cptr = (ctypes.c_void_p * nt)(*[ptr(x) for x in cols])
-            offs = (ctypes.c_int64 * nt)(*layout.token_offsets)
-            check(lib().mirec_offset_keys(cptr, offs, nt, B, ptr(keys), stream_handle()),
-                  'mirec_offset_keys')
-            # one key block per field (ranges increase with the field offsets): K2
-            # sorts each field's B keys in LDS instead of a device-wide radix sort
-            blocks = B if (layout.blocks_ok and 0 < B <= 8192 and len(layout.token_names) > 1) \
-                else None
-            ctx.segs = h.catch_up(T, keys, blocks=blocks)
+            status = getattr(h, '_sort_status', None)
+            if (layout.blocks_ok and 0 < B <= ops.CHAIN_MAX_BLOCK_N and 1 < nt <= 64
+                    and status is not None and status.numel() > nt):
+                # the keys formed and grouped (one LDS sort per field block, chained) in
+                # one launch
+                keys, segs = ops.segment_sort_fields(cols, layout.token_offsets, B, T.shape[0],
+                                                     status)
+                ctx.segs = h.catch_up(T, keys, segs=segs)
+            else:
+                cptr = (ctypes.c_void_p * nt)(*[ptr(x) for x in cols])
+                offs = (ctypes.c_int64 * nt)(*layout.token_offsets)
+                check(lib().mirec_offset_keys(cptr, offs, nt, B, ptr(keys), stream_handle()),
+                      'mirec_offset_keys')
+                # one key block per field (ranges increase with the field offsets): K2
+                # sorts each field's B keys in LDS instead of a device-wide radix sort
+                blocks = B if (layout.blocks_ok and 0 < B <= 8192 and nt > 1) else None
+                ctx.segs = h.catch_up(T, keys, blocks=blocks)
             h1 = getattr(T1, '_mirec_deferred', None)
             if h1 is not None:                # the first-order [V, 1] table, same rows
                 h1.catch_up(T1, keys, ctx.segs)

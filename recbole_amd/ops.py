@@ -489,6 +489,30 @@ def segment_sort_blocks(keys: torch.Tensor, block_n: int, key_space: int,
     return segs
 
 
+def segment_sort_fields(cols, offsets, B: int, key_space: int, status: torch.Tensor):
+    """DeepFM's token keys (field f: cols[f] + offsets[f], ranges increasing with f) formed
+    and grouped in one launch (mirec_segment_sort_fields_chained): (keys [F * B] int64,
+    Segments with pos_seg). status: the chained sort's zeroed words (>= F + 1)."""
+    nf = len(cols)
+    for c in cols:
+        _dev(c, torch.int64, "field column")
+    _dev(status, torch.int32, "status")
+    dev = cols[0].device
+    n = nf * B
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    segs = Segments(n, dev)
+    segs.pos_seg = torch.empty(n, dtype=torch.int32, device=dev)
+    cptr = (ctypes.c_void_p * nf)(*[ptr(c) for c in cols])
+    offs = (ctypes.c_int64 * nf)(*[int(o) for o in offsets])
+    with timed_launch('k2_blocks'):
+        rc = lib().mirec_segment_sort_fields_chained(
+            cptr, offs, nf, B, key_space, ptr(keys), ptr(segs.perm), ptr(segs.uniq),
+            ptr(segs.seg), ptr(segs.n_uniq), ptr(status), status.numel(), ptr(segs.pos_seg),
+            stream_handle())
+    check(rc, "mirec_segment_sort_fields_chained")
+    return keys, segs
+
+
 def segment_sort_batched(keys: torch.Tensor, batch_n: int, key_space: int, perm, uniq, seg,
                          n_uniq, ws=None):
     """K2 over consecutive batches of `batch_n` keys, one workgroup per batch."""

@@ -929,6 +929,37 @@ def test_segment_sort_blocks_equals_global(dev, block_n, n_blocks, space, chaine
     assert torch.equal(a.seg[:nu + 1], b.seg[:nu + 1])
 
 
+def test_segment_sort_fields_equals_offset_keys_then_blocks(dev):
+    """The fields form of the chained block sort (keys formed from the columns + offsets
+    inside the sort launch) gives mirec_offset_keys' keys and the block sort's grouping."""
+    from recbole_amd import ops
+    from recbole_amd._native import lib, ptr, stream_handle, check
+    import ctypes
+    rng = np.random.default_rng(3)
+    B, F = 2048, 26
+    vocab = [10_000_000 // (j + 1) + 3 for j in range(F)]
+    offs = np.concatenate([[0], np.cumsum(vocab)[:-1]]).tolist()
+    cols = [torch.as_tensor(np.minimum(rng.zipf(1.1, B), vocab[j] - 1).astype(np.int64),
+                            device=dev) for j in range(F)]
+    space = int(sum(vocab))
+    status = torch.zeros(F + 1, dtype=torch.int32, device=dev)
+    keys, sf = ops.segment_sort_fields(cols, offs, B, space, status)
+    ref_keys = torch.empty(F * B, dtype=torch.int64, device=dev)
+    check(lib().mirec_offset_keys((ctypes.c_void_p * F)(*[ptr(c) for c in cols]),
+                                  (ctypes.c_int64 * F)(*offs), F, B, ptr(ref_keys),
+                                  stream_handle()), 'mirec_offset_keys')
+    assert torch.equal(keys, ref_keys)
+    sb = ops.segment_sort_blocks(ref_keys, B, space, status=status)
+    nu = int(sb.n_uniq.item())
+    assert int(sf.n_uniq.item()) == nu
+    for f in ('perm', 'uniq'):
+        assert torch.equal(getattr(sf, f)[:F * B if f == 'perm' else nu],
+                           getattr(sb, f)[:F * B if f == 'perm' else nu])
+    assert torch.equal(sf.seg[:nu + 1], sb.seg[:nu + 1])
+    assert torch.equal(sf.pos_seg, sb.pos_seg)
+    assert int(status.abs().sum().item()) == 0
+
+
 def test_segment_sort_blocks_spans(dev):
     """Block sort across key spans: a constant block (no digit pass), a two-key block,
     a Zipf-headed block and blocks spanning 20 and 30 bits (3 and 4 digit passes), ragged
