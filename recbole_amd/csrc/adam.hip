@@ -187,8 +187,8 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
   constexpr int RPP = kAdamThreads / VPR;
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si];
-  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[si]) * kAdamRows;
-  const int64_t hi = min(T.n_rows, lo + kAdamRows);
+  const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[si]) * kFlushRows;
+  const int64_t hi = min(T.n_rows, lo + kFlushRows);
   const int target = step_base[0] + step_off;
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
@@ -328,23 +328,25 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_scalar_kernel(
     int step_off, AdamConsts k) {
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si];
-  const int64_t r = ((int64_t)blockIdx.x - tabs.block_start[si]) * kAdamThreads + threadIdx.x;
   const int target = step_base[0] + step_off;
-  const bool valid = r < T.n_rows;
-  const int last = valid ? min(T.last[r], target) : target;
-  if (__all(last >= target)) return;
-  float p = 0.f, m = 0.f, v = 0.f;
-  if (last < target) {
-    p = T.p[r];
-    m = T.m[r];
-    v = T.v[r];
-  }
-  adam_replay(p, m, v, last, target, consts, k);
-  if (last < target) {
-    T.p[r] = p;
-    T.m[r] = m;
-    T.v[r] = v;
-    T.last[r] = target;
+  const int64_t r0 = ((int64_t)blockIdx.x - tabs.block_start[si]) * kFlushScalarRows;
+  for (int64_t r = r0 + threadIdx.x; r < r0 + kFlushScalarRows; r += kAdamThreads) {
+    const bool valid = r < T.n_rows;
+    const int last = valid ? min(T.last[r], target) : target;
+    if (__all(last >= target)) continue;         // wave-uniform
+    float p = 0.f, m = 0.f, v = 0.f;
+    if (last < target) {
+      p = T.p[r];
+      m = T.m[r];
+      v = T.v[r];
+    }
+    adam_replay(p, m, v, last, target, consts, k);
+    if (last < target) {
+      T.p[r] = p;
+      T.m[r] = m;
+      T.v[r] = v;
+      T.last[r] = target;
+    }
   }
 }
 
@@ -433,10 +435,12 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       if (t.ahead_uniq) blocks += nb;
     } else {
       tabs.block_start[q] = blocks;
-      const int64_t rows_per_block = d == 1 ? kAdamThreads
-                                     : scan ? (int64_t)(kAdamThreads / 64) * fr.r[q]
-                                     : (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64
-                                                                           : kAdamRows;
+      const int64_t rows_per_block =
+          d == 1 ? kFlushScalarRows                // adam_flush_scalar_kernel
+          : scan ? (int64_t)(kAdamThreads / 64) * fr.r[q]
+          : (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64
+          : sched == Sched::kFlush ? kFlushRows
+                                   : kAdamRows;
       blocks += (t.n_rows + rows_per_block - 1) / rows_per_block;
     }
   }

@@ -2,10 +2,10 @@
 # Round-4: DeepFM keys formed inside the chained sort — tests, C4 trace + lines.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r4aa
+O=gpurun_out/r4ab
 mkdir -p $O
 PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
-timeout -k 10 400 $PT tests/test_gpu_kernels.py -k "sort_fields or blocks" > $O/tests_k.log 2>&1
+timeout -k 10 400 $PT tests/test_gpu_kernels.py -k "flush or adam or deferred" > $O/tests_k.log 2>&1
 rc=$?; tail -2 $O/tests_k.log; [ $rc -eq 0 ] || exit 9
 timeout -k 10 700 $PT tests/test_gpu_deepfm.py tests/test_gpu_deferred.py tests/test_gpu_graph_step.py \
   tests/test_gpu_mlp.py tests/test_gpu_configs.py tests/test_gpu_shard.py > $O/tests.log 2>&1
