@@ -428,11 +428,28 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
                                'step shapes (median of 10)',
                      'note': 'fp32 dense peak; our own largest kernel in the step is listed in '
                              'step_breakdown'},
-        'k9b': {'kernel': f'K9b sampled_softmax<{d}> ({n_neg} negatives)', 'bound': 'hbm',
-                'achieved': round(k9_bytes / tk / 1e9, 1), 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': k9_bytes,
-                'launch_us_incl_host': round(tk * 1e6, 1)},
+        'k9b': _k9b_line(d, n_neg, k9_bytes, tk),
     }
+
+
+def _k9b_line(d, n_neg, k9_bytes, tk):
+    """K9b's roofline on its kernel time in the committed C3 step trace (rocprofv3,
+    profiles/r*_C3_step.json: the launch inside the captured step), the host-inclusive
+    HIP-event time of an eager launch beside it."""
+    import glob
+    import json
+    t_trace, src = None, None
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_C3_step.json')))[::-1]:
+        ks = [k for k in json.load(open(path))['kernels'] if 'sampled_softmax' in k['kernel']]
+        if ks:
+            t_trace, src = ks[0]['avg_us'] * 1e-6, os.path.basename(path)
+            break
+    t = t_trace if t_trace is not None else tk
+    return {'kernel': f'K9b sampled_softmax<{d}> ({n_neg} negatives)', 'bound': 'hbm',
+            'achieved': round(k9_bytes / t / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(k9_bytes / t / 1e9 / HBM_PEAK_GBS, 4), 'bytes_per_launch': k9_bytes,
+            'launch_us': round(t * 1e6, 1), 'timing_source': src or 'HIP events (eager)',
+            'launch_us_incl_host': round(tk * 1e6, 1)}
 
 
 # ----------------------------------------------------------------------------- C5
