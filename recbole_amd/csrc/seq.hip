@@ -289,28 +289,58 @@ __global__ __launch_bounds__(256) void sampled_softmax_kernel(
   float* lg = lds_logits + (threadIdx.x >> 6) * (N + 1);
   float m = -__builtin_inff(), lsum = 0.f, l0 = 0.f;
   float e0[V];
-  for (int j = 0; j <= N; ++j) {
+  // the ids of [pos | negs] up front (lane l holds items l and l + 64), then the rows
+  // eight at a time: their loads in flight together, the dots reduced side by side,
+  // the online softmax folded in item order as before
+  auto item_id = [&](int j) -> int64_t {
     int64_t id = j == 0 ? pos[b] : neg[(int64_t)(j - 1) * B + b];
-    id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
-    float row[V];
-    float dot = 0.f;
+    return id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
+  };
+  const int64_t ida = lane <= N ? item_id(lane) : 0;
+  const int64_t idb = lane + 64 <= N ? item_id(lane + 64) : 0;
+  for (int j0 = 0; j0 <= N; j0 += 8) {
+    float row[8][V], dot[8];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      row[v] = E[id * D + v * 64 + lane];
-      dot = fmaf(s[v], row[v], dot);
-    }
-    dot = wave_sum(dot);
-    lg[j] = dot;
-    if (j == 0) l0 = dot;
-    const float mn = fmaxf(m, dot);
-    const float cold = expf(m - mn), cnew = expf(dot - mn);
-    lsum = lsum * cold + cnew;
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = min(j0 + jj, N);
+      int64_t id;
+      if (j < 64) {
+        id = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(ida >> 32), j) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)ida, j));
+      } else if (j < 128) {
+        id = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(idb >> 32), j - 64)
+                        << 32) | (uint32_t)__builtin_amdgcn_readlane((int)idb, j - 64));
+      } else {
+        id = item_id(j);
+      }
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      acc[v] = acc[v] * cold + cnew * row[v];
-      if (j == 0) e0[v] = row[v];
+      for (int v = 0; v < V; ++v) row[jj][v] = E[id * D + v * 64 + lane];
     }
-    m = mn;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      float d0 = 0.f;
+#pragma unroll
+      for (int v = 0; v < V; ++v) d0 = fmaf(s[v], row[jj][v], d0);
+      dot[jj] = d0;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) dot[jj] = wave_sum(dot[jj]);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = j0 + jj;
+      if (j > N) break;
+      lg[j] = dot[jj];
+      if (j == 0) l0 = dot[jj];
+      const float mn = fmaxf(m, dot[jj]);
+      const float cold = expf(m - mn), cnew = expf(dot[jj] - mn);
+      lsum = lsum * cold + cnew;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        acc[v] = acc[v] * cold + cnew * row[jj][v];
+        if (j == 0) e0[v] = row[jj][v];
+      }
+      m = mn;
+    }
   }
   const float lse = m + logf(lsum);
   if (lane == 0) loss[b] = lse - l0;

@@ -2,7 +2,7 @@
 # Round-4: second-level merges — kernel tests, SASRec / deferred tests, C3 trace + line.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r4v
+O=${OV:-gpurun_out/r4v}
 mkdir -p $O
 PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
 timeout -k 10 400 $PT tests/test_gpu_kernels.py -k "merge or reduce or sort or scatter" > $O/tests_k.log 2>&1
