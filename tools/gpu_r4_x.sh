@@ -3,7 +3,7 @@
 # windows, kernel stats), the model configurations with CPU baselines.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r4x
+O=${OX:-gpurun_out/r4x}
 mkdir -p $O
 PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 170 --timeout-method thread -m gpu"
 timeout -k 10 900 $PT tests/ > $O/tests.log 2>&1
