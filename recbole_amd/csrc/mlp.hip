@@ -33,7 +33,10 @@ constexpr int kMlpRows = 16;       // rows per forward / data-grad block
 constexpr int kMlpThreads = 512;   // eight waves
 constexpr int kMlpWaves = kMlpThreads / 64;
 constexpr int kMlpU = 4;           // 16-wide slices per prefetch group (data grad)
-constexpr int kFwdU = 8;           // forward: 8 slices (32 MFMAs) per group
+#ifndef MIREC_FWD_U
+#define MIREC_FWD_U 8
+#endif
+constexpr int kFwdU = MIREC_FWD_U; // forward: 8 slices (32 MFMAs) per group
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -152,12 +155,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
         }
       };
       floatx4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
-      load(0);
-      for (int k0 = 0; k0 < K; k0 += 16 * kFwdU) {
-        float4 ca[kFwdU], cb[kFwdU];
-#pragma unroll
-        for (int u = 0; u < kFwdU; ++u) { ca[u] = pa[u]; cb[u] = pb[u]; }
-        if (k0 + 16 * kFwdU < K) load(k0 + 16 * kFwdU);
+      auto mfma_group = [&](const float4* ca, const float4* cb) {
 #pragma unroll
         for (int u = 0; u < kFwdU; ++u) {
           floatx4& acc = (u & 1) ? accB : accA;
@@ -166,7 +164,42 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
           acc = mfma4(ca[u].z, cb[u].z, acc);
           acc = mfma4(ca[u].w, cb[u].w, acc);
         }
+      };
+#if defined(MIREC_FWD_PF2)
+      // two groups' loads in flight while one group's MFMAs run: buffers q (even groups)
+      // and p (odd groups), taken two groups per iteration so every index is static
+      constexpr int GW = 16 * kFwdU;
+      float4 qa[kFwdU], qb[kFwdU];
+      auto load_q = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < kFwdU; ++u) {
+          const int k = k0 + 16 * u + 4 * lk;
+          const int kc = k < K ? k : K - 4;
+          qa[u] = *reinterpret_cast<const float4*>(cur + li * ld + kc);
+          qb[u] = *reinterpret_cast<const float4*>(wr + kc);
+          if (k >= K) qb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      };
+      load_q(0);
+      if (GW < K) load(GW);
+      for (int k0 = 0; k0 < K; k0 += 2 * GW) {
+        mfma_group(qa, qb);                       // group k0 (its loads were issued first)
+        if (k0 + 2 * GW < K) load_q(k0 + 2 * GW);
+        if (k0 + GW < K) {
+          mfma_group(pa, pb);                     // group k0 + GW
+          if (k0 + 3 * GW < K) load(k0 + 3 * GW);
+        }
       }
+#else
+      load(0);
+      for (int k0 = 0; k0 < K; k0 += 16 * kFwdU) {
+        float4 ca[kFwdU], cb[kFwdU];
+#pragma unroll
+        for (int u = 0; u < kFwdU; ++u) { ca[u] = pa[u]; cb[u] = pb[u]; }
+        if (k0 + 16 * kFwdU < K) load(k0 + 16 * kFwdU);
+        mfma_group(ca, cb);
+      }
+#endif
       const floatx4 acc0 = accA + accB;
       // epilogue: lane holds rows 4*lk + r of column c
       if (c < N) {
