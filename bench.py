@@ -160,16 +160,15 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
 def pmc_bytes(substr):
     """HBM bytes per launch of the kernel whose name contains `substr`, from the
     newest committed PMC summary (profiles/*_pmc.json, tools/summarize_prof.py:
-    FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+    FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction; the newest one that traced it: the
+    driver-window run launches no flush_row / K3), or None."""
     import glob
     files = sorted(f for f in glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json'))
                    if 'models_pmc' not in f)
-    if not files:
-        return None, None
-    data = json.load(open(files[-1]))
-    for k, v in data.items():
-        if substr in k:
-            return v.get('hbm_bytes_per_launch'), os.path.basename(files[-1])
+    for path in files[::-1]:          # newest summary that traced this kernel
+        for k, v in json.load(open(path)).items():
+            if substr in k:
+                return v.get('hbm_bytes_per_launch'), os.path.basename(path)
     return None, None
 
 
