@@ -489,9 +489,21 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
 }
 
 // Hand-off of a split row's contribution vectors between the blocks of one launch
-// (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off form: write-through
-// agent-scope stores, every storing wave drained before one lane's agent-scope add, the
-// last adder told by the returned value, agent-scope loads): no fence needed.
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off form): the vectors go
+// out as agent-scope atomic stores (write-through: past this XCD's L2), every storing
+// wave drains them (vmcnt(0)) before the row's threads meet and ONE lane counts the row
+// in with an agent-scope add; the last adder takes an agent-scope acquire and the row's
+// threads read the vectors back with agent-scope loads (sc1: from past the L2).
+//
+// Measured alternatives (round 4, tools/gpu_r4_af.sh):
+// - MIREC_STEP_HANDOFF_FORMAL: the C++ memory model's own producer form — each thread an
+//   agent-scope release fence before the meeting, acq_rel adds (here and at the look-ahead
+//   half-join). Bit-identical, but the release is `buffer_wbl2 sc1`: it writes back every
+//   dirty line of the XCD's L2 (K35's row-state stores), once per wave — C2 driver window
+//   23.5-23.9 M -> 5.6 M positives/s. Not adopted.
+// - a release on the counting lane only (the drains removed): a workgroup barrier does not
+//   wait for the other wave's stores, and test_gpu_e2e's bit-identity failed at d = 256 (a
+//   two-wave row) — the drain in every wave is what the hand-off rests on.
 __device__ __forceinline__ void part_store(float* p, float4 a) {
   auto q = (__attribute__((address_space(1))) unsigned long long*)(p);
   const unsigned long long lo =
@@ -510,6 +522,14 @@ __device__ __forceinline__ void part_load(const float* p, float2& a) {
   const unsigned long long w = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   a = make_float2(__uint_as_float((unsigned)w), __uint_as_float((unsigned)(w >> 32)));
 }
+
+#if defined(MIREC_STEP_HANDOFF_FORMAL)
+constexpr int kJoinOrder = __ATOMIC_ACQ_REL;
+constexpr int kHalfJoinOrder = __ATOMIC_ACQ_REL;
+#else
+constexpr int kJoinOrder = __ATOMIC_RELAXED;
+constexpr int kHalfJoinOrder = __ATOMIC_RELAXED;
+#endif
 
 // Row-state stores of K35. MIREC_STEP_WT (probe build): write-through (agent-scope)
 // stores, so the launch leaves no dirty lines for the kernel boundary's L2 write-back.
@@ -675,11 +695,12 @@ void bpr_adam_step_kernel(
     } else {
       // both halves read `last` before the first one counts in (its replay used it). No
       // data passes between the halves: the counter only elects the one that marks the
-      // row, after both have read its old mark (a relaxed add suffices)
+      // row, after both have read its old mark (a relaxed add suffices: the read has
+      // returned — the replay used it — before this lane's add issues)
       row_sync();
       if (t == 0) {
         int32_t* j = L.join[tb] + L.join_ahead[tb] + u / kAheadHalves;
-        if (__hip_atomic_fetch_add(j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        if (__hip_atomic_fetch_add(j, 1, kHalfJoinOrder, __HIP_MEMORY_SCOPE_AGENT) == 1) {
           __hip_atomic_store(j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           T_.last[row] = st + 1;
         }
@@ -810,22 +831,22 @@ void bpr_adam_step_kernel(
   }
   if (split) MIREC_WORK(9, 1);
   if (split) {
-    // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility). Producer: the vectors
-    // went out as 8-byte agent-scope atomic (write-through) stores; every storing wave
-    // drains them (vmcnt(0)) before the row's threads meet, then ONE lane counts the row
-    // in on join[x] with an agent-scope add. The add that returns nsh - 1 is the last:
-    // its lane takes an agent-scope acquire (this CU's L1 invalidated) and waits for it
-    // before the row's threads load the vectors with agent-scope loads — the consumer
-    // form the memory model asks for, whatever the placement or the load.
+    // Hand-off (see part_store): drain this wave's write-through stores, meet, one lane
+    // counts the row in on join[x]; the add that returns nsh - 1 is the last, whose lane
+    // takes an agent-scope acquire before the row's threads load the vectors.
+#if defined(MIREC_STEP_HANDOFF_FORMAL)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     row_sync();
     if (t == 0) {
       const int arrived =
-          __hip_atomic_fetch_add(L.join[tb] + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(L.join[tb] + x, 1, kJoinOrder, __HIP_MEMORY_SCOPE_AGENT);
       s_last = arrived == nsh - 1;
       if (s_last) {                                  // every participant has counted in
         __hip_atomic_store(L.join[tb] + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if !defined(MIREC_STEP_NO_ACQUIRE)
+#if !defined(MIREC_STEP_HANDOFF_FORMAL)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
