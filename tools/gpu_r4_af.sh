@@ -2,6 +2,7 @@
 # Round-4: K35 join memory orders — the memory-model form (MIREC_STEP_HANDOFF_FORMAL build "formal") vs the write-through
 # hand-off with explicit drains (default). Tests on the default library,
 # then C2 driver-window and default-window bench A/B.
+# build the variant first: tools/build_variant.sh formal -DMIREC_STEP_HANDOFF_FORMAL
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/r4af
