@@ -632,7 +632,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
   if (advance) {
     __syncthreads();                       // every lane's read of step_idx is done
     if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+        __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             (int)gridDim.x - 1) {
       advance[0] = advance[0] + 1;
       ticket[0] = 0;

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(1024) void chunk_finish_kernel(const float* __restr
   if (threadIdx.x == 0) {
     const int32_t st = __hip_atomic_load(step_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (loss_hist) loss_hist[st + c] = s / denom;
-    const int32_t t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == n_steps - 1) {
       __hip_atomic_store(step_base, st + n_steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -229,7 +229,6 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
   // the last block of a training forward with dropout advances the draw counter (every
   // block has read it above, before its first barrier)
   if (any_drop && tid == 0) {
-    __threadfence();
     const int prev = atomicAdd(a.arrive, 1);
     if (prev == (int)gridDim.x - 1) {
       atomicExch(a.arrive, 0);

@@ -370,14 +370,16 @@ __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
   int32_t *perm, *uniq, *seg;
   int32_t voff;                                  // added to block-local positions
   if (status) {
-    if (tid == 0) __hip_atomic_store(&status[b], nu + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // the count is the whole message: relaxed agent-scope store and loads (an agent
+    // release / acquire is buffer_wbl2 / buffer_inv on gfx950 — see step.hip, part_store)
+    if (tid == 0) __hip_atomic_store(&status[b], nu + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wid == 0) {
       int acc = 0;
       for (int64_t j0 = 0; j0 < b; j0 += 64) {
         const int64_t j = j0 + lane;
         int c = 0;
         if (j < b) {
-          while ((c = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE,
+          while ((c = __hip_atomic_load(&status[j], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT)) == 0)
             __builtin_amdgcn_s_sleep(1);
           c -= 1;
@@ -420,7 +422,8 @@ __global__ __launch_bounds__(kR8Threads) void segsort_radix8_kernel(
         seg[nu] = (int32_t)n_total;
         n_uniq_all[0] = L.base + nu;
       }
-      L.last = __hip_atomic_fetch_add(&status[nblocks], 1, __ATOMIC_ACQ_REL,
+      // relaxed: this block's look-back loads have returned (their sum is in L.base)
+      L.last = __hip_atomic_fetch_add(&status[nblocks], 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
     }
     __syncthreads();
@@ -829,7 +832,7 @@ __device__ __forceinline__ void os_cleanup(uint32_t* ticket, uint32_t* words, in
                                            int* flag_lds) {
   __syncthreads();
   if (threadIdx.x == 0)
-    *flag_lds = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+    *flag_lds = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                 gridDim.x - 1;
   __syncthreads();
   if (*flag_lds) {
