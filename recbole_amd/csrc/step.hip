@@ -846,7 +846,7 @@ void bpr_adam_step_kernel(
       s_last = arrived == nsh - 1;
       if (s_last) {                                  // every participant has counted in
         __hip_atomic_store(L.join[tb] + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if !defined(MIREC_STEP_HANDOFF_FORMAL)
+#if !defined(MIREC_STEP_HANDOFF_FORMAL) && !defined(MIREC_STEP_NO_ACQUIRE)   // (probe build)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
