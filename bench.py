@@ -100,12 +100,16 @@ def write_c2_inter(path, u, i, seed=2020):
 
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
                    dist=None, chunk=None, sharded=False, alias=False, fused_step=None,
-                   source='file'):
+                   source='file', shape=None):
     """C2 through the drop-in path. source='file' (default): the synthetic interactions
     are written as an atomic file (MIREC_BENCH_DATA, default /tmp/mirec_bench; reused
     when present) and built by create_dataset -> data_preparation, the reference's
     pipeline; source='memory': Dataset.from_interactions of the same arrays (no file).
-    The step object carries the setup timings (step.setup_info)."""
+    shape=(n_users, n_items, interactions): a smaller instance of the same generator
+    (source='memory' only; the smoke test). The step object carries the setup timings
+    (step.setup_info)."""
+    if shape is not None and source != 'memory':
+        raise ValueError('shape= needs source="memory"')
     from recbole_amd.config import Config
     from recbole_amd.data import create_dataset, data_preparation
     from recbole_amd.data.dataset import Dataset
@@ -124,7 +128,7 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
           'load_col': {'inter': ['user_id', 'item_id', 'rating', 'timestamp']}}
     t = time.perf_counter()
     if source == 'memory' or not os.path.exists(path):
-        u, i, nU, nI = make_c2(seed)
+        u, i, nU, nI = make_c2(seed) if shape is None else make_c2(seed, *shape)
         info['generate_s'] = round(time.perf_counter() - t, 2)
         if source == 'file':
             t = time.perf_counter()

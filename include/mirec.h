@@ -358,6 +358,10 @@ int mirec_chunk_group(const int64_t* user_keys, const int64_t* item_keys, int64_
                       int32_t* i_uniq, int32_t* i_seg, int32_t* i_nu, int32_t* u_rec,
                       int32_t* u_crec, int32_t* i_rec, int32_t* i_crec, int32_t* u_ahead,
                       int32_t* u_nah, int32_t* i_ahead, int32_t* i_nah, void* stream);
+/* 1 when mirec_chunk_group takes chunks of batches of Bc positives with T negatives over
+ * n_users x n_items tables (ahead: look-ahead lists asked for), else 0. Host only. */
+int mirec_chunk_group_fits(int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
+                           int32_t ahead);
 
 /* dense[uniq[u], :] += sum_{i in seg[u]..seg[u+1]} rows[perm[i], :] — the
  * dense-gradient form used by the autograd-compatible path. n = number of

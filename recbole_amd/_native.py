@@ -194,6 +194,7 @@ SIGNATURES = {
     "mirec_offset_keys": (c_int, [_P, _P, c_int32, c_int64, _P, _P]),
     "mirec_bpr_fwd_bwd_at_ids_f32": (c_int, [_P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32,
                                              ctypes.c_float, ctypes.c_float, _P, _P, _P]),
+    "mirec_chunk_group_fits": (c_int, [c_int64, c_int32, c_int64, c_int64, c_int32]),
     "mirec_chunk_group": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64] + [_P] * 16
                           + [_P]),
     "mirec_step_records": (c_int, [_P, _P, c_int64, c_int64, c_int32, c_int64, c_int64, _P, _P,

@@ -609,8 +609,10 @@ struct FlatParams {
 // read it — the block that takes the last ticket (agent-scope counter, zero between
 // launches) adds 1 and zeroes the ticket (graph mode's `step += 1` without a launch).
 __global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
-    const FlatParams fp, const float* __restrict__ consts, const int32_t* __restrict__ step_idx,
-    AdamConsts k, int32_t* __restrict__ advance, int32_t* __restrict__ ticket) {
+    const FlatParams fp, const float* __restrict__ consts, const int32_t* step_idx,
+    AdamConsts k, int32_t* advance, int32_t* __restrict__ ticket) {
+  // step_idx and advance may be the same word (mirec_adam_flat_multi_advance_f32): neither
+  // is __restrict__, and the advance is an atomic add after every block has read it
   int q = 0;
 #pragma unroll
   for (int t = 1; t < kFlatMax; ++t)
@@ -634,7 +636,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flat_multi_kernel(
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             (int)gridDim.x - 1) {
-      advance[0] = advance[0] + 1;
+      __hip_atomic_fetch_add(advance, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       ticket[0] = 0;
     }
   }

@@ -58,31 +58,6 @@ __device__ __forceinline__ int64_t clamp_id(int64_t id, int64_t n) {
   return id < 0 ? 0 : (id >= n ? n - 1 : id);
 }
 
-// Block = one table row, EPT elements per thread (float for D = 64, float2 for D >= 128:
-// one wave per row at D = 128, so a step's ~6,000 row blocks are resident at once and
-// the look-ahead replays overlap the touched rows' gather chains).
-// Diagnostic build only (tools/build_variant.sh step_stamps -DMIREC_STEP_STAMPS,
-// tools/probe_step_stamps.py): real-time (100 MHz, chip-wide) stamps per block at entry,
-// after the first load levels, after the contributions (touched) / the loads
-// (look-ahead), and at the end,
-// into a buffer of their own that no other code reads. No stamp executes in the product.
-#if defined(MIREC_STEP_STAMPS)
-constexpr int kStampBlocks = 32768;
-__device__ unsigned long long g_step_stamps[kStampBlocks * 4];
-#define MIREC_STAMP(slot)                                                                  \
-  do {                                                                                     \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    unsigned long long t_;                                                                 \
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");           \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    const int sb_ = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);              \
-    if ((threadIdx.x & 63) == 0 && sb_ < kStampBlocks) g_step_stamps[sb_ * 4 + (slot)] = t_; \
-  } while (0)
-#else
-#define MIREC_STAMP(slot) \
-  do {                    \
-  } while (0)
-#endif
 
 // Contribution records, built per chunk on the prep stream (mirec_step_records, after
 // the K2 grouping) so that a step's touched row reaches its partner rows in two
@@ -316,9 +291,6 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
       atomicOr(&L.bits[k >> 5], 1u << (k & 31));
     }
   }
-#if defined(MIREC_GRP_STOP)          // timing probes only (tools/build_variant.sh)
-  if (MIREC_GRP_STOP == 1) return;
-#endif
   // 2. sort of the composites key << pbits | position (distinct values: stability comes
   //    free). Bucket by the key's top bits (<= 4,096 buckets, LDS counters: atomics give
   //    each element a slot in its bucket in any order), scan the counts, scatter, then
@@ -382,9 +354,6 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     }
   }
   __syncthreads();
-#if defined(MIREC_GRP_STOP)
-  if (MIREC_GRP_STOP == 2) return;
-#endif
   // 3. segments: heads of equal-key runs, uniq / seg / perm
   const uint32_t* S = L.xa;
   int32_t* __restrict__ perm = J.perm + (int64_t)b * per;
@@ -422,9 +391,6 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     J.nu[b] = nu;
   }
   __syncthreads();
-#if defined(MIREC_GRP_STOP)
-  if (MIREC_GRP_STOP == 3) return;
-#endif
   // 4. K35 records (step_prep_kernel roles 1 and 2, from LDS)
   if (J.rec != nullptr) {
     int32_t* __restrict__ rec = J.rec + (int64_t)b * rec_ints(per);
@@ -464,9 +430,6 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
     for (int e = tid; e < per; e += kGrpThreads)
       contrib_record_lds((int)(S[e] & pm), tb, Bc, T, L.uk, L.ik, crec + (int64_t)e * kRecInts);
   }
-#if defined(MIREC_GRP_STOP)
-  if (MIREC_GRP_STOP == 4) return;
-#endif
   // 5. look-ahead list of batch b-1: this batch's rows that batch b-1 does not touch
   if (ahead) {
     int32_t* __restrict__ out = J.ahead + (int64_t)(b - 1) * per;
@@ -495,12 +458,12 @@ __global__ __launch_bounds__(kGrpThreads) void chunk_group_kernel(
 // in with an agent-scope add; the last adder takes an agent-scope acquire and the row's
 // threads read the vectors back with agent-scope loads (sc1: from past the L2).
 //
-// Measured alternatives (round 4, tools/gpu_r4_af.sh):
-// - MIREC_STEP_HANDOFF_FORMAL: the C++ memory model's own producer form — each thread an
-//   agent-scope release fence before the meeting, acq_rel adds (here and at the look-ahead
-//   half-join). Bit-identical, but the release is `buffer_wbl2 sc1`: it writes back every
-//   dirty line of the XCD's L2 (K35's row-state stores), once per wave — C2 driver window
-//   23.5-23.9 M -> 5.6 M positives/s. Not adopted.
+// Measured alternatives (round 4; the probe builds live on branch probes/k35-r4):
+// - the C++ memory model's own producer form — each thread an agent-scope release fence
+//   before the meeting, acq_rel adds (here and at the look-ahead half-join). Bit-identical,
+//   but the release is `buffer_wbl2 sc1`: it writes back every dirty line of the XCD's L2
+//   (K35's row-state stores), once per wave — C2 driver window 23.5-23.9 M -> 5.6 M
+//   positives/s. Not adopted.
 // - a release on the counting lane only (the drains removed): a workgroup barrier does not
 //   wait for the other wave's stores, and test_gpu_e2e's bit-identity failed at d = 256 (a
 //   two-wave row) — the drain in every wave is what the hand-off rests on.
@@ -523,44 +486,20 @@ __device__ __forceinline__ void part_load(const float* p, float2& a) {
   a = make_float2(__uint_as_float((unsigned)w), __uint_as_float((unsigned)(w >> 32)));
 }
 
-#if defined(MIREC_STEP_HANDOFF_FORMAL)
-constexpr int kJoinOrder = __ATOMIC_ACQ_REL;
-constexpr int kHalfJoinOrder = __ATOMIC_ACQ_REL;
-#else
 constexpr int kJoinOrder = __ATOMIC_RELAXED;
 constexpr int kHalfJoinOrder = __ATOMIC_RELAXED;
-#endif
 
-// Row-state stores of K35. MIREC_STEP_WT (probe build): write-through (agent-scope)
-// stores, so the launch leaves no dirty lines for the kernel boundary's L2 write-back.
+// Row-state stores of K35 (plain stores; write-through stores measured no better)
 template <typename V>
 __device__ __forceinline__ void state_store(V* p, const V& x) {
-#if defined(MIREC_STEP_WT)
-  if constexpr (sizeof(V) == 8) {
-    auto q = (__attribute__((address_space(1))) unsigned long long*)(p);
-    unsigned long long w;
-    memcpy(&w, &x, 8);
-    __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    auto q = (__attribute__((address_space(1))) unsigned int*)(p);
-    unsigned int w;
-    memcpy(&w, &x, 4);
-    __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#else
   *p = x;
-#endif
 }
 
 template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
-// Look-ahead rows: one element per thread over two half-row slots (default), or whole
-// rows in one slot (MIREC_STEP_AHEAD_WHOLE, probe: half the look-ahead waves).
-#if defined(MIREC_STEP_AHEAD_WHOLE)
-template <typename V> struct AheadVec { using T = V; };
-#else
+// Look-ahead rows: one element per thread over two half-row slots (whole rows in one
+// slot measured no better)
 template <typename V> struct AheadVec { using T = float; };
-#endif
 
 // Rows per workgroup: a row of D <= 128 is one wave, and RPB of them share a workgroup
 // (each wave works alone: wave-level synchronisation only), so the dispatcher hands out
@@ -605,7 +544,6 @@ void bpr_adam_step_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   };
-  MIREC_STAMP(0);
   int si = 0;
 #pragma unroll
   for (int q = 1; q < 6; ++q)
@@ -655,17 +593,10 @@ void bpr_adam_step_kernel(
   }
   const int st = step_base[0] + step_off;
   if (u >= n) return;                      // wave-uniform (row-uniform)
-#if defined(MIREC_STEP_PROBE_NO_AHEAD)     // timing probes only (tools/build_variant.sh)
-  if (ahead) return;
-#endif
-#if defined(MIREC_STEP_PROBE_NO_TOUCHED)
-  if (!ahead) return;
-#endif
   const float* __restrict__ Pr[2] = {T_.p, T_.p_alt};
   float* __restrict__ Pw = ((st + 1) & 1) ? T_.p_alt : T_.p;
   const int raw = T_.last[row];
   const int64_t off = row * (D / EPT) + t;           // in units of V
-  MIREC_STAMP(1);
 
   if (ahead) {
     // rows the next step reads and this one does not touch: replay last..st (zero
@@ -679,7 +610,6 @@ void bpr_adam_step_kernel(
     H p = reinterpret_cast<const H*>(Pr[raw & 1])[offh];
     H m = reinterpret_cast<const H*>(T_.m)[offh];
     H v = reinterpret_cast<const H*>(T_.v)[offh];
-    MIREC_STAMP(2);
     replay<H, true, kAheadHalves == 2 ? 8 : 4>(p, m, v, raw, st, consts, k);
     H z;
     memset(&z, 0, sizeof(H));
@@ -706,7 +636,6 @@ void bpr_adam_step_kernel(
         }
       }
     }
-    MIREC_STAMP(3);
     return;
   }
 
@@ -834,11 +763,7 @@ void bpr_adam_step_kernel(
     // Hand-off (see part_store): drain this wave's write-through stores, meet, one lane
     // counts the row in on join[x]; the add that returns nsh - 1 is the last, whose lane
     // takes an agent-scope acquire before the row's threads load the vectors.
-#if defined(MIREC_STEP_HANDOFF_FORMAL)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     row_sync();
     if (t == 0) {
       const int arrived =
@@ -846,10 +771,8 @@ void bpr_adam_step_kernel(
       s_last = arrived == nsh - 1;
       if (s_last) {                                  // every participant has counted in
         __hip_atomic_store(L.join[tb] + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if !defined(MIREC_STEP_HANDOFF_FORMAL) && !defined(MIREC_STEP_NO_ACQUIRE)   // (probe build)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
       }
     }
     row_sync();
@@ -877,7 +800,6 @@ void bpr_adam_step_kernel(
   }
 
   // ---- Adam step of the row (replaying skipped zero-gradient steps first)
-  MIREC_STAMP(2);
   replay<V, true>(p, m, v, last, st, consts, k);
   const bool fresh = last <= st;
   if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
@@ -891,7 +813,6 @@ void bpr_adam_step_kernel(
   state_store(reinterpret_cast<V*>(T_.m) + off, m);
   state_store(reinterpret_cast<V*>(T_.v) + off, v);
   if (t == 0) T_.last[row] = st + 1;
-  MIREC_STAMP(3);
 }
 
 }  // namespace mirec
@@ -947,6 +868,25 @@ static int bits_for(int64_t n) {        // bits of n - 1 (n >= 1)
 }
 }  // namespace mirec
 
+namespace mirec {
+// the shapes K36's one-workgroup form takes (else the K2 sort + mirec_step_records)
+static bool chunk_group_fits(int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
+                             bool ahead) {
+  if (Bc <= 0 || T < 1 || n_users <= 0 || n_items <= 0) return false;
+  const int64_t KI = (int64_t)(1 + T) * Bc;
+  const int pu = bits_for(Bc), pi = bits_for(KI);
+  return !(Bc > kGrpUserMax || KI > kGrpMax || bits_for(n_users) + pu > 32 ||
+           bits_for(n_items) + pi > 32 ||
+           (ahead && (n_users > 32 * (int64_t)kGrpBitmapWords ||
+                      n_items > 32 * (int64_t)kGrpBitmapWords)));
+}
+}  // namespace mirec
+
+extern "C" int mirec_chunk_group_fits(int64_t Bc, int32_t T, int64_t n_users, int64_t n_items,
+                                      int32_t ahead) {
+  return chunk_group_fits(Bc, T, n_users, n_items, ahead != 0) ? 1 : 0;
+}
+
 // K36 on a prepared chunk (include/mirec.h): 1 = done, 0 = shapes outside the one-
 // workgroup form (the caller runs the K2 sort + mirec_step_records), < 0 = error.
 extern "C" int mirec_chunk_group(const int64_t* user_keys, const int64_t* item_keys,
@@ -967,12 +907,7 @@ extern "C" int mirec_chunk_group(const int64_t* user_keys, const int64_t* item_k
   if (n_batches == 0 || Bc == 0) return 1;
   const int64_t KI = (int64_t)(1 + T) * Bc;
   const int pu = bits_for(Bc), pi = bits_for(KI);
-  const bool ahead = u_ahead != nullptr;
-  if (Bc > kGrpUserMax || KI > kGrpMax || bits_for(n_users) + pu > 32 ||
-      bits_for(n_items) + pi > 32 ||
-      (ahead && (n_users > 32 * (int64_t)kGrpBitmapWords ||
-                 n_items > 32 * (int64_t)kGrpBitmapWords)))
-    return 0;
+  if (!chunk_group_fits(Bc, T, n_users, n_items, u_ahead != nullptr)) return 0;
   GroupJob U = {u_perm, u_uniq, u_seg, u_nu, u_rec, u_crec, u_ahead, u_nah, n_users, pu};
   GroupJob I = {i_perm, i_uniq, i_seg, i_nu, i_rec, i_crec, i_ahead, i_nah, n_items, pi};
   hipLaunchKernelGGL(chunk_group_kernel, dim3((unsigned)(2 * n_batches)), dim3(kGrpThreads), 0,
@@ -1029,11 +964,7 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   // segments: the shares of split rows first (their row's step waits for them), then
   // the look-ahead rows (their replays are long chains), then the touched rows
   if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
-#if defined(MIREC_STEP_AHEAD_WHOLE)
-  const int halves = 1;
-#else
   const int halves = d >= 128 ? 2 : 1;            // look-ahead slots per table row
-#endif
   const int64_t rows[6] = {kSplitCap, kSplitCap,
                            L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0,
                            L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0,
@@ -1073,14 +1004,3 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   return launch_status(what);
 }
 
-#if defined(MIREC_STEP_STAMPS)
-// diagnostic build only: copy / clear the stamps (4 x kStampBlocks u64)
-extern "C" int mirec_step_stamps(void* dst, size_t bytes) {
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_step_stamps), bytes) == hipSuccess ? 0 : -1;
-}
-extern "C" int mirec_step_stamps_clear(void) {
-  void* p = nullptr;
-  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_step_stamps)) != hipSuccess) return -1;
-  return hipMemset(p, 0, sizeof(g_step_stamps)) == hipSuccess ? 0 : -1;
-}
-#endif

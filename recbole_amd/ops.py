@@ -411,6 +411,7 @@ class Segments:
 
 ONESWEEP_MIN = 8193          # above the single-workgroup LDS sort
 _SORT_STATUS = {}
+_RETIRED = []    # superseded shared scratch buffers: never freed (see _sort_status)
 
 
 def _sort_status(device, words):
@@ -418,12 +419,20 @@ def _sort_status(device, words):
     every call leaves it zero; calls are stream-ordered (the model's stream; a graph's
     warm-up and capture streams wait for each other), as for _scatter_ws. None while a
     graph capture is running and the buffer does not exist yet or is too small (the
-    caller then takes the radix path)."""
+    caller then takes the radix path).
+
+    A buffer that is replaced by a larger one stays allocated for the life of the
+    process: a HIP graph captured earlier holds its pointer and replays against it, and
+    memory handed back to the caching allocator could be reused for other data, so a
+    replay would read garbage look-back words (and scatter outside its outputs). A
+    retired buffer is still zero (every call leaves it so) and only graphs use it."""
     key = str(device)
     buf = _SORT_STATUS.get(key)
     if buf is None or buf.numel() < words:
         if torch.cuda.is_current_stream_capturing():
             return None
+        if buf is not None:
+            _RETIRED.append(buf)
         buf = torch.zeros(max(words, 1 << 16), dtype=torch.int32, device=device)
         _SORT_STATUS[key] = buf
     return buf
@@ -547,6 +556,8 @@ def _scatter_ws(device, nbytes):
     key = str(device)
     buf = _SCATTER_WS.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:                  # a captured graph may hold it (_sort_status)
+            _RETIRED.append(buf)
         buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
         _SCATTER_WS[key] = buf
     return buf
@@ -675,6 +686,8 @@ def _iota(device, n):
     if t is None or t.numel() < n:
         if torch.cuda.is_current_stream_capturing():   # graph-pool memory: not cached
             return torch.arange(n, dtype=torch.int32, device=device)
+        if t is not None:                    # a captured graph may hold it (_sort_status)
+            _RETIRED.append(t)
         t = _IOTA[key] = torch.arange(max(n, 1 << 16), dtype=torch.int32, device=device)
     return t[:n]
 

@@ -37,11 +37,8 @@ def _grouping(keys, space):
     return segs
 
 
-@pytest.mark.parametrize('d,T,s,Bc,few', [(64, 3, 6, 96, 0), (128, 4, 7, 96, 0),
-                                          (128, 4, 10, 96, 0), (256, 3, 9, 96, 0),
-                                          (128, 6, 8, 96, 0), (128, 4, 12, 640, 5),
-                                          (64, 3, 11, 640, 3)])
-def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
+def build_case(dev, d, T, s, Bc, few):
+    """Inputs of one K35 launch (step s) and the K3 + K5 reference result on them."""
     g = torch.Generator().manual_seed(d * 100 + T * 10 + s)
     nU, nI = 257, 301
     # batch 0 (the step) and batch 1 (whose rows the look-ahead completes)
@@ -106,7 +103,7 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
     ops.adam_multi(tabs, d, consts, base, 3, schedule='deferred',
                    n_max_uniq=[Bc, (1 + T) * Bc])
 
-    # ---- K35 on parity buffers: row state t in buffer t & 1, the other one poisoned
+    # ---- K35 inputs on parity buffers: row state t in buffer t & 1, the other poisoned
     bufs = []
     for p, last in ((pU, lastU), (pI, lastI)):
         P = [torch.full_like(p, float('nan')), torch.full_like(p, float('nan'))]
@@ -116,27 +113,45 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
         zs = last == ADAM_ZERO_STATE                       # zero-state: both buffers
         P[0][zs], P[1][zs] = p[zs], p[zs]
         bufs.append([to(P[0]), to(P[1])])
-    fmU, fvU, fmI, fvI = to(mU.clone()), to(vU.clone()), to(mI.clone()), to(vI.clone())
-    flU, flI = to(lastU.clone()), to(lastI.clone())
-    tabs2 = ops.adam_tables([
-        {'p': bufs[0][0], 'p_alt': bufs[0][1], 'm': fmU, 'v': fvU, 'grouping': gu0,
-         'last': flU, 'ahead': ahead[0]},
-        {'p': bufs[1][0], 'p_alt': bufs[1][1], 'm': fmI, 'v': fvI, 'grouping': gi0,
-         'last': flI, 'ahead': ahead[1]}])
-    loss_k = torch.full((Bc,), float('nan'), device=dev)
-    recs = ops.step_records(to(user0), to(items0), 1, Bc, T, nU, nI, gu0, gi0)
-    scratch = ops.step_scratch(Bc, T, d, dev)
-    ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, to(items0), Bc, T, grad_scale, loss_k, recs,
-                      scratch, consts, base, 3)
-    torch.cuda.synchronize()
-    assert int(scratch[1].abs().sum()) == 0 and int(scratch[3].abs().sum()) == 0
+    return dict(d=d, T=T, s=s, Bc=Bc, dev=dev, bufs=bufs, mv=[to(x) for x in (mU, vU, mI, vI)],
+                last=[to(lastU), to(lastI)], gu0=gu0, gi0=gi0, ahead=ahead, consts=consts,
+                base=base, grad_scale=grad_scale, user0=to(user0), items0=to(items0), nU=nU,
+                nI=nI, ref=dict(p=(rU, rI), m=(rmU, rmI), v=(rvU, rvI), last=(rlU, rlI),
+                                loss_k=o['loss_k']))
 
-    assert torch.equal(loss_k, o['loss_k'])
-    for (P, rp), rl, fl, (rm, fm), (rv, fv) in (
-            ((bufs[0], rU), rlU, flU, (rmU, fmU), (rvU, fvU)),
-            ((bufs[1], rI), rlI, flI, (rmI, fmI), (rvI, fvI))):
+
+def run_k35(c, stream=None):
+    """K35 on fresh copies of the case's inputs (on `stream`, default current); returns
+    the state it leaves: parity buffers, m, v, last, loss_k and the scratch."""
+    d, T, Bc, dev = c['d'], c['T'], c['Bc'], c['dev']
+    with torch.cuda.stream(stream or torch.cuda.current_stream(dev)):
+        bufs = [[b.clone() for b in pair] for pair in c['bufs']]
+        fmU, fvU, fmI, fvI = (x.clone() for x in c['mv'])
+        flU, flI = (x.clone() for x in c['last'])
+        tabs2 = ops.adam_tables([
+            {'p': bufs[0][0], 'p_alt': bufs[0][1], 'm': fmU, 'v': fvU, 'grouping': c['gu0'],
+             'last': flU, 'ahead': c['ahead'][0]},
+            {'p': bufs[1][0], 'p_alt': bufs[1][1], 'm': fmI, 'v': fvI, 'grouping': c['gi0'],
+             'last': flI, 'ahead': c['ahead'][1]}])
+        loss_k = torch.full((Bc,), float('nan'), device=dev)
+        recs = ops.step_records(c['user0'], c['items0'], 1, Bc, T, c['nU'], c['nI'], c['gu0'],
+                                c['gi0'])
+        scratch = ops.step_scratch(Bc, T, d, dev)
+        ops.bpr_adam_step(tabs2, [Bc, (1 + T) * Bc], d, c['items0'], Bc, T, c['grad_scale'],
+                          loss_k, recs, scratch, c['consts'], c['base'], 3)
+    return dict(bufs=bufs, m=(fmU, fmI), v=(fvU, fvI), last=(flU, flI), loss_k=loss_k,
+                scratch=scratch)
+
+
+def check_k35(c, r):
+    """Every word of the K35 result against the K3 + K5 reference."""
+    s, ref = c['s'], c['ref']
+    assert int(r['scratch'][1].abs().sum()) == 0 and int(r['scratch'][3].abs().sum()) == 0
+    assert torch.equal(r['loss_k'], ref['loss_k'])
+    for q in range(2):
+        P, rp, rl, fl = r['bufs'][q], ref['p'][q], ref['last'][q], r['last'][q]
         assert torch.equal(rl, fl)
-        assert torch.equal(rm, fm) and torch.equal(rv, fv)
+        assert torch.equal(ref['m'][q], r['m'][q]) and torch.equal(ref['v'][q], r['v'][q])
         moved = (fl == s + 1)                              # touched + look-ahead rows
         assert int(moved.sum()) > 0
         wb = P[(s + 1) & 1]
@@ -145,6 +160,17 @@ def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
         keep = ~moved & (fl != ADAM_ZERO_STATE)
         src = torch.where(((fl & 1) == 1)[:, None], P[1], P[0])
         assert torch.equal(src[keep], rp[keep])
+
+
+@pytest.mark.parametrize('d,T,s,Bc,few', [(64, 3, 6, 96, 0), (128, 4, 7, 96, 0),
+                                          (128, 4, 10, 96, 0), (256, 3, 9, 96, 0),
+                                          (128, 6, 8, 96, 0), (128, 4, 12, 640, 5),
+                                          (64, 3, 11, 640, 3)])
+def test_bpr_adam_step_equals_k3_k5(dev, d, T, s, Bc, few):
+    c = build_case(dev, d, T, s, Bc, few)
+    r = run_k35(c)
+    torch.cuda.synchronize()
+    check_k35(c, r)
 
 
 def test_bpr_adam_step_rejects_bad_tables(dev):
