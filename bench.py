@@ -488,9 +488,9 @@ def main():
     ap.add_argument('--flush-every', type=int, default=None)
     # diagnostic: the K3 + K5 launches per step instead of the one-launch K35 step
     ap.add_argument('--no-fused-step', action='store_true')
-    # diagnostic: prepare a pipeline-restart chunk on the model's stream (default: on the
-    # prep streams, FusedBPRTrainStep.MAIN_FIRST)
-    ap.add_argument('--main-first', action='store_true')
+    # diagnostic: prepare a pipeline-restart chunk on the prep streams (default: on the
+    # model's stream, FusedBPRTrainStep.MAIN_FIRST)
+    ap.add_argument('--no-main-first', action='store_true')
     # diagnostic: the synthetic interactions in memory instead of the atomic-file path
     ap.add_argument('--in-memory', action='store_true')
     args = ap.parse_args()
@@ -526,8 +526,8 @@ def main():
         step.RAMP = tuple(int(x) for x in args.ramp.split(','))
     if args.flush_every:
         step.FLUSH_EVERY = args.flush_every
-    if args.main_first:
-        step.MAIN_FIRST = True
+    if args.no_main_first:
+        step.MAIN_FIRST = False
 
     setup_s = time.time() - t_setup
     K, W = args.steps, args.warmup

@@ -841,12 +841,25 @@ typedef struct mirec_mlp {
   float* gz[MIREC_MLP_MAX_LAYERS];
   float* dW[MIREC_MLP_MAX_LAYERS];
   float* db[MIREC_MLP_MAX_LAYERS];
+  /* the wide backward's scratch (mirec_mlp_bwd_workspace: floats, and int32 counters that
+   * must be zero before a call and are left zero); NULL: the row-block backward */
+  float* wscratch;
+  int32_t* wcount;
 } mirec_mlp;
 
 int mirec_mlp_fwd_f32(const mirec_mlp* mlp, const float* x, int64_t B, float* y, int32_t train,
                       void* stream);
 int mirec_mlp_bwd_f32(const mirec_mlp* mlp, const float* x, const float* dy, int64_t B, float* gx,
                       void* stream);
+/* Wide layer 0 (dims[0] >= 256, >= 2 layers): the forward runs layer 0 over the whole chip
+ * (16 rows x 32 columns per 4-wave block, K split in two halves added in a fixed order)
+ * when xs[1] is given, then layers 1.. in row blocks; the backward (with wscratch /
+ * wcount) runs layers L-1..1 in row blocks, then layer 0's data gradient and every weight
+ * gradient as 64-column wave tiles over the whole chip (the batch in 4 x 4 slices summed
+ * in a fixed order). Returns 1 and the scratch sizes when the shapes take the wide
+ * backward, 0 otherwise, < 0 on bad arguments. */
+int mirec_mlp_bwd_workspace(const mirec_mlp* mlp, int64_t B, int64_t* scratch_floats,
+                            int64_t* counters);
 
 /* ---------------------------------------------------------------------------
  * K9  Sequential recommender (SASRec) embedding block and sampled softmax.

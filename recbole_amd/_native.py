@@ -52,7 +52,8 @@ class MlpDesc(ctypes.Structure):
                 ('keep_threshold', ctypes.c_uint32), ('scale', c_float),
                 ('seed', ctypes.c_uint64), ('counter', _P), ('arrive', _P),
                 ('W', _P * _L), ('b', _P * _L), ('xs', _P * _L), ('mask0', _P),
-                ('gz', _P * _L), ('dW', _P * _L), ('db', _P * _L)]
+                ('gz', _P * _L), ('dW', _P * _L), ('db', _P * _L), ('wscratch', _P),
+                ('wcount', _P)]
 
 
 class FlatParam(ctypes.Structure):
@@ -220,6 +221,7 @@ SIGNATURES = {
     "mirec_colsum_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
     "mirec_mlp_fwd_f32": (c_int, [_P, _P, c_int64, _P, c_int32, _P]),
     "mirec_mlp_bwd_f32": (c_int, [_P, _P, _P, c_int64, _P, _P]),
+    "mirec_mlp_bwd_workspace": (c_int, [_P, c_int64, _P, _P]),
     "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
                                            _P, c_float, _P, _P, _P, _P]),
     "mirec_seq_embed_ln_partials": (c_int64, [c_int64]),

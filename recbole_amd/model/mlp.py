@@ -44,6 +44,10 @@ def fused_supported(mlp_layers, predict, x) -> bool:
         return False
     if dims[0] != x.shape[1]:
         return False
+    # the row-block kernels' two LDS tiles (16 rows each; widths of even / odd index)
+    pad = lambda w: (w + 15) // 16 * 16 + 4
+    if 16 * 4 * (pad(max(dims[0::2])) + pad(max(dims[1::2]))) > 65536:
+        return False
     for m in lins:
         w = m.weight
         if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and
@@ -53,11 +57,15 @@ def fused_supported(mlp_layers, predict, x) -> bool:
 
 
 class _State(object):
-    """Per-MLPLayers K10 state: the draw counter and arrival scratch on the device."""
+    """Per-MLPLayers K10 state: the draw counter, the forward's arrival word and the wide
+    backward's hand-off counters (zero between launches) on the device."""
+
+    WCOUNT = 4096              # wave tiles of the wide backward's weight gradients, at most
 
     def __init__(self, device):
         self.counter = torch.zeros(1, dtype=torch.int64, device=device)
         self.arrive = torch.zeros(1, dtype=torch.int32, device=device)
+        self.wcount = torch.zeros(self.WCOUNT, dtype=torch.int32, device=device)
         self.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF
 
 
@@ -104,6 +112,7 @@ class _DeepFn(torch.autograd.Function):
         d.scale = dropout_scale(p) if train else 1.0
         d.seed = st.seed
         d.counter, d.arrive = ptr(st.counter), ptr(st.arrive)
+        d.wscratch = d.wcount = None
         E = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=dev)
         keep = []
         grad = torch.is_grad_enabled() or any(ctx.needs_input_grad)
@@ -122,7 +131,7 @@ class _DeepFn(torch.autograd.Function):
             rc = lib().mirec_mlp_fwd_f32(ctypes.byref(d), ptr(x), B, ptr(y), 1 if train else 0,
                                          stream_handle())
         check(rc, 'mirec_mlp_fwd_f32')
-        ctx.desc, ctx.keep, ctx.dims, ctx.L = d, keep, dims, L
+        ctx.desc, ctx.keep, ctx.dims, ctx.L, ctx.state = d, keep, dims, L, st
         ctx.has_bias = [b is not None for b in bs]
         ctx.save_for_backward(x, *Ws)
         return y
@@ -148,6 +157,15 @@ class _DeepFn(torch.autograd.Function):
             d.dW[l] = ptr(dW[l])
             d.db[l] = ptr(db[l])
         gx = E(B, dims[0])
+        # the wide backward (layer 0's data and every weight gradient over the whole chip)
+        # hands block partials over through a scratch buffer and zeroed counters
+        nf, nc = ctypes.c_int64(0), ctypes.c_int64(0)
+        wide = lib().mirec_mlp_bwd_workspace(ctypes.byref(d), B, ctypes.byref(nf), ctypes.byref(nc))
+        check(min(wide, 0), 'mirec_mlp_bwd_workspace')
+        scratch = None
+        if wide == 1 and nc.value <= ctx.state.wcount.numel():
+            scratch = E(nf.value)
+            d.wscratch, d.wcount = ptr(scratch), ptr(ctx.state.wcount)
         with ops.timed_launch('mlp_bwd'):            # two launches: data, weight gradients
             rc = lib().mirec_mlp_bwd_f32(ctypes.byref(d), ptr(x), ptr(gy), B, ptr(gx),
                                          stream_handle())

@@ -136,6 +136,11 @@ class _Slot(object):
         self.ready = torch.cuda.Event()
         self.walked = torch.cuda.Event()
         self.free = torch.cuda.Event()
+        # torch creates an event's HIP object at its first record (hipEventCreate, tens of
+        # microseconds of host time): record each one now, so a timed region never pays it
+        cur = torch.cuda.current_stream(dev)
+        for ev in (self.ready, self.walked, self.free):
+            ev.record(cur)
         self.free_recorded = False
         self.group_pending = False   # walked, grouping not yet issued
         self.chunk = None            # (first global batch, n batches, global batch size)
@@ -171,11 +176,13 @@ class FusedBPRTrainStep(object):
     # row is touched, and its slowest wave sets the step time: measured on C2 (64
     # warm-up + 256 steps) 18.0 M positives/s at 64, 12.4 M at 256, 12.3 M at 1,024.
     FLUSH_EVERY = 64
-    # diagnostic: prepare a chunk the model side waits for at once (pipeline start / a
-    # timed region that holds its own preparation) on the model's stream instead of the
-    # prep streams. Measured slower on the C2 driver window (16.45 vs 17.06-17.16 M
-    # positives/s: the first launch started 218 µs after t0 instead of 72 µs)
-    MAIN_FIRST = os.environ.get('MIREC_MAIN_FIRST', '0') == '1'   # first chunk on the model stream
+    # A chunk the model side waits for at once (pipeline (re)start: the epoch's first chunk,
+    # or a timed region that holds its own preparation) is walked and grouped on the model's
+    # stream — no hand-off between hardware queues (≈ 20 µs each) before the first step —
+    # and the next chunks' walks are issued on the prep stream right behind its walk (they
+    # run beside its grouping and steps). MIREC_MAIN_FIRST=0: the prep streams for it too.
+    MAIN_FIRST = os.environ.get('MIREC_MAIN_FIRST', '1') != '0'
+    _last_walked = None           # event after the latest issued walk (begin_epoch resets)
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None, fused_step=None):
@@ -356,9 +363,15 @@ class FusedBPRTrainStep(object):
                     self.device, nb * Bc * T)
                 cp.alias_thr, cp.alias_idx, cp.n_alias = thr.data_ptr(), idx.data_ptr(), thr.numel()
             st = on if on is not None else self.prep_stream
+            lw = self._last_walked
+            if on is not None and lw is not None and not lw.query():
+                # the walk pointer and the speculative walk's workspace are sequential
+                # state: a walk on the model's stream follows every walk issued before it
+                on.wait_event(lw)
             check(lib().mirec_prepare_chunk_walk(ctypes.byref(cp), st.cuda_stream),
                   'mirec_prepare_chunk_walk')
             slot.walked.record(st)
+            self._last_walked = slot.walked
             slot.chunk = chunk
             if on is None:
                 slot.group_pending = True      # the grouping half: _issue_groups
@@ -724,7 +737,6 @@ class FusedBPRTrainStep(object):
         whose chunk (and every later one) is not prepared until release_prep() —
         so a timed region that starts there contains its own chunks' sampler walk
         and grouping."""
-        self._late_top_up = None
         data = self.data
         if data.shuffle:
             data._shuffle()                     # randperm (CPU RNG) + device reorder
@@ -767,6 +779,7 @@ class FusedBPRTrainStep(object):
         if self.use_graph:                      # capture up front: capture synchronizes
             self._capture_variants()
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
+        self._last_walked = None               # event after the latest issued walk
         self._next_chunk = 0                   # chunks whose walk (or whole prep) is issued
         self._next_group = 0                   # chunks whose grouping is issued
         self._prep_limit = (len(self._plan) if hold_prep_from is None
@@ -793,9 +806,9 @@ class FusedBPRTrainStep(object):
             k = self._next_chunk               # the first released walk starts right away:
             if self.MAIN_FIRST and not self._sharded(self._plan[k][2]):
                 # the whole preparation on the model's stream (no cross-queue hand-off
-                # before the first step); the next chunks' preparation after its launch
+                # before the first step); the next chunks' walks at once, behind its walk
                 self._issue_prep(on=torch.cuda.current_stream(self.device))
-                self._late_top_up = k
+                self._top_up_prep(k)
             else:
                 self._issue_prep()
 
@@ -835,12 +848,9 @@ class FusedBPRTrainStep(object):
                                'call release_prep() first')
         # this chunk's grouping first (its stream waits for the walk on the GPU; issued
         # later, the host's enqueue of the next walks would delay it), then the walks of
-        # the next chunks (the same walk stream: they start as this chunk's walk ends) —
-        # unless this chunk was prepared on the model's stream: then they follow its
-        # launches (run_batches), which the GPU reaches first
+        # the next chunks (the same walk stream: they start as this chunk's walk ends)
         self._issue_groups(k + 1)
-        if getattr(self, '_late_top_up', None) != k:
-            self._top_up_prep(k)
+        self._top_up_prep(k)
         stream.wait_event(self.slots[k % S].ready)
         self._cur = k
 
@@ -875,9 +885,6 @@ class FusedBPRTrainStep(object):
                 if c1 == nb and flush:
                     self._flush(stream, flush)
                     self._current = True
-            if getattr(self, '_late_top_up', None) == k:
-                self._late_top_up = None
-                self._top_up_prep(k)
             self._issue_groups(k + len(self.slots))   # later chunks' groupings, behind
             b = b0 + c1
             self._batches_enqueued = b

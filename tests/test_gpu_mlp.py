@@ -50,7 +50,12 @@ def _reference(mlp, pred, x, masks, p):
 @pytest.mark.parametrize('dims,out,B,p', [([624, 128, 128, 128], 1, 2048, 0.2),
                                           ([624, 128, 128, 128], 1, 2048, 0.0),
                                           ([40, 24, 8], 3, 37, 0.5),
-                                          ([16, 256], 1, 300, 0.1)])
+                                          ([16, 256], 1, 300, 0.1),
+                                          # wide layer 0 (>= 256): ragged rows, column
+                                          # groups and K halves, 2 and 3 layers
+                                          ([520, 72, 36], 3, 300, 0.3),
+                                          ([272, 12], 5, 37, 0.0),
+                                          ([960, 20], 1, 129, 0.5)])
 def test_fused_deep_matches_reference(dev, dims, out, B, p):
     mlp, pred = _modules(dims, out, p, dev)
     mlp.train()
