@@ -794,6 +794,17 @@ int mirec_sigmoid_bce_mean_f32(const float* y_fm, const float* y_deep, const flo
 
 /* out[j] = sum_{i<n} x[i*m + j] in row order (fixed; float-field / bias grads). */
 int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream);
+/* The tail of nn.Linear's backward over a tall input (reference: torch's Linear backward
+ * under SASRec's layers, layers.py:338-461): dW = sum_c P[c] (C split-K partials of n_w
+ * floats, summed in c order; skipped when C == 1 and P == dW) and db = the column sum of
+ * g [K, n_out] (NULL: none; rows in chunks of 512, each in row order, chunks in order) in
+ * ONE launch. n_w and n_out multiples of 4, 16-B aligned P / dW / g. scratch: floats of
+ * mirec_linear_grad_finish_scratch(K, n_out); ticket: one int32, zero before a call and
+ * left zero. */
+int64_t mirec_linear_grad_finish_scratch(int64_t K, int32_t n_out);
+int mirec_linear_grad_finish_f32(const float* P, int32_t C, int64_t n_w, float* dW,
+                                 const float* g, int64_t K, int32_t n_out, float* db,
+                                 float* scratch, int32_t* ticket, void* stream);
 /* Several column sums in ONE launch (up to 4 jobs: out[q][j] = sum_i x[q][i*m[q] + j],
  * x[q] of n[q] rows): each job summed exactly as mirec_colsum_f32 sums it (same tile, same
  * order), the three of a DeepFM backward (float fields, their first-order terms, the bias)

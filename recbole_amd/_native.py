@@ -222,6 +222,9 @@ SIGNATURES = {
     "mirec_mlp_fwd_f32": (c_int, [_P, _P, c_int64, _P, c_int32, _P]),
     "mirec_mlp_bwd_f32": (c_int, [_P, _P, _P, c_int64, _P, _P]),
     "mirec_mlp_bwd_workspace": (c_int, [_P, c_int64, _P, _P]),
+    "mirec_linear_grad_finish_scratch": (c_int64, [c_int64, c_int32]),
+    "mirec_linear_grad_finish_f32": (c_int, [_P, c_int32, c_int64, _P, _P, c_int64, c_int32, _P,
+                                             _P, _P, _P]),
     "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
                                            _P, c_float, _P, _P, _P, _P]),
     "mirec_seq_embed_ln_partials": (c_int64, [c_int64]),

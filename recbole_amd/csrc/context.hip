@@ -291,6 +291,111 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(const ColsumJobs J) 
     colsum_tile<1>(J.x[q], J.n[q], J.m[q], J.out[q], tile, part);
 }
 
+// The tail of a Linear's backward over a tall input (SASRec's 12 Linears at K = B x L =
+// 10^5 rows, model/layers.py _SplitKLinearFn): the sum of the C split-K weight-gradient
+// partials and the bias gradient (the column sum of g [K, n_out]) in ONE launch, where
+// torch ran two reductions (24 reduce launches per C3 step). Fixed orders: the partials
+// in c order; the bias rows in chunks of kLgRows, each chunk's rows in row order (8 row
+// lanes, added in lane order), the chunks in chunk order — the last block to finish a
+// chunk (agent-scope ticket; write-through partial stores drained before it, an agent
+// acquire after) adds them.
+constexpr int kLgThreads = 256;
+constexpr int kLgRows = 512;          // bias rows per chunk
+struct LinearGradFinish {
+  const float* P; int C; int64_t n4;  // partials [C, 4 n4] -> dW
+  float* dW;
+  const float* g; int64_t K; int n_out; float* db;
+  float* scratch; int32_t* ticket;
+  int nS;                             // blocks of the partial sum
+  int nB;                             // bias chunks
+};
+
+__global__ __launch_bounds__(kLgThreads) void linear_grad_finish_kernel(const LinearGradFinish F) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < F.nS) {
+    const int64_t i = (int64_t)blockIdx.x * kLgThreads + tid;
+    if (i >= F.n4) return;
+    const float4* P4 = reinterpret_cast<const float4*>(F.P);
+    float4 v = P4[i];
+    for (int c = 1; c < F.C; ++c) {
+      const float4 w = P4[(int64_t)c * F.n4 + i];
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    reinterpret_cast<float4*>(F.dW)[i] = v;
+    return;
+  }
+  // bias chunk: thread = (row lane rl of 8, column float4 cg); 256 / 8 = 32 float4 groups
+  // per pass over the columns
+  __shared__ float4 part[8][33];
+  __shared__ int s_last;
+  const int chunk = (int)blockIdx.x - F.nS;
+  const int rl = tid >> 5, cgl = tid & 31;
+  const int64_t r0 = (int64_t)chunk * kLgRows;
+  const int64_t r1 = r0 + kLgRows < F.K ? r0 + kLgRows : F.K;
+  const int ng = F.n_out / 4;
+  float* mine = F.scratch + (int64_t)chunk * F.n_out;
+  for (int cg0 = 0; cg0 < ng; cg0 += 32) {
+    const int cg = cg0 + cgl;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cg < ng) {
+      const float4* g4 = reinterpret_cast<const float4*>(F.g) + cg;
+      int64_t r = r0 + rl;
+      for (; r + 24 < r1; r += 32) {                   // 4 rows' loads in flight
+        const float4 a = g4[r * ng], b = g4[(r + 8) * ng], c = g4[(r + 16) * ng],
+                     d = g4[(r + 24) * ng];
+        s.x = (((s.x + a.x) + b.x) + c.x) + d.x;
+        s.y = (((s.y + a.y) + b.y) + c.y) + d.y;
+        s.z = (((s.z + a.z) + b.z) + c.z) + d.z;
+        s.w = (((s.w + a.w) + b.w) + c.w) + d.w;
+      }
+      for (; r < r1; r += 8) {
+        const float4 a = g4[r * ng];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+    }
+    part[rl][cgl] = s;
+    __syncthreads();
+    if (rl == 0 && cg < ng) {
+      float4 t = part[0][cgl];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) {
+        t.x += part[q][cgl].x; t.y += part[q][cgl].y; t.z += part[q][cgl].z; t.w += part[q][cgl].w;
+      }
+      auto q8 = (__attribute__((address_space(1))) unsigned long long*)(mine + 4 * cg);
+      __hip_atomic_store(q8, (unsigned long long)__float_as_uint(t.x) |
+                                 ((unsigned long long)__float_as_uint(t.y) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q8 + 1, (unsigned long long)__float_as_uint(t.z) |
+                                     ((unsigned long long)__float_as_uint(t.w) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  // hand-off: every storing wave drained, meet, one add; the last chunk sums them all
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(F.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == F.nB - 1;
+    if (s_last) {
+      __hip_atomic_store(F.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int j = tid; j < F.n_out; j += kLgThreads) {
+    float t = 0.f;
+    for (int c = 0; c < F.nB; ++c) {
+      auto q = (const __attribute__((address_space(1))) unsigned int*)(F.scratch + (int64_t)c * F.n_out + j);
+      const float v = __uint_as_float(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      t = c ? t + v : v;
+    }
+    F.db[j] = t;
+  }
+}
+
 // keys[f * B + i] = cols[f][i] + offsets[f]: DeepFM's token keys (every token field's ids at
 // its offset in the shared table) in one launch (a stack + add in torch: two)
 constexpr int kKeyFields = 64;
@@ -490,6 +595,36 @@ extern "C" int mirec_offset_keys(const int64_t* const* cols, const int64_t* offs
   hipLaunchKernelGGL(offset_keys_kernel, dim3(gx, (unsigned)n_fields), dim3(256), 0,
                      (hipStream_t)stream, F, n_fields, B, out);
   return launch_status("mirec_offset_keys");
+}
+
+extern "C" int64_t mirec_linear_grad_finish_scratch(int64_t K, int32_t n_out) {
+  if (K < 0 || n_out < 0) return -1;
+  return ((K + kLgRows - 1) / kLgRows) * (int64_t)n_out;
+}
+
+extern "C" int mirec_linear_grad_finish_f32(const float* P, int32_t C, int64_t n_w, float* dW,
+                                            const float* g, int64_t K, int32_t n_out, float* db,
+                                            float* scratch, int32_t* ticket, void* stream) {
+  const char* what = "mirec_linear_grad_finish_f32";
+  const bool sum = P && C >= 1 && n_w > 0 && !(C == 1 && P == dW);
+  const bool bias = db != nullptr && K > 0;
+  if (C < 1 || n_w < 0 || (n_w % 4) != 0 || (sum && !dW) ||
+      ((uintptr_t)P % 16) != 0 || ((uintptr_t)dW % 16) != 0 ||
+      (bias && (!g || n_out <= 0 || (n_out % 4) != 0 || ((uintptr_t)g % 16) != 0 || !scratch ||
+                !ticket || ((uintptr_t)scratch % 8) != 0))) {
+    set_error("%s: bad arguments", what);
+    return -1;
+  }
+  LinearGradFinish F;
+  memset(&F, 0, sizeof(F));
+  F.P = P; F.C = C; F.n4 = n_w / 4; F.dW = dW;
+  F.g = g; F.K = K; F.n_out = n_out; F.db = db; F.scratch = scratch; F.ticket = ticket;
+  F.nS = sum ? (int)((F.n4 + kLgThreads - 1) / kLgThreads) : 0;
+  F.nB = bias ? (int)((K + kLgRows - 1) / kLgRows) : 0;
+  if (F.nS + F.nB == 0) return 0;
+  hipLaunchKernelGGL(linear_grad_finish_kernel, dim3((unsigned)(F.nS + F.nB)), dim3(kLgThreads), 0,
+                     (hipStream_t)stream, F);
+  return launch_status(what);
 }
 
 extern "C" int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* stream) {

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 from torch.nn.init import normal_
 
+from recbole_amd import ops
 from recbole_amd._native import check, lib, ptr, stream_handle
 from recbole_amd.utils import FeatureType
 
@@ -178,11 +179,27 @@ class _SplitKLinearFn(torch.autograd.Function):
             C *= 2
         dx = torch.matmul(gy, W)
         if C > 1:
-            dW = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2),
-                           x2.view(C, K // C, n_in)).sum(0)
+            P = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2), x2.view(C, K // C, n_in))
+            dW = torch.empty_like(W)
         else:
-            dW = g2.t().mm(x2)
-        db = g2.sum(0) if ctx.has_b else None
+            P = dW = g2.t().mm(x2)
+        db = None
+        if ctx.has_b and (n_out % 4 or n_in % 4):        # outside the finish kernel's shapes
+            if C > 1:
+                dW = P.sum(0)
+            return dx, dW, g2.sum(0)
+        if ctx.has_b or C > 1:
+            # the C partials' sum and the bias column sum in one launch (two torch
+            # reductions before)
+            g2 = g2.contiguous()
+            if ctx.has_b:
+                db = torch.empty(n_out, dtype=torch.float32, device=gy.device)
+            scratch = torch.empty(max(lib().mirec_linear_grad_finish_scratch(K, n_out), 2),
+                                  dtype=torch.float32, device=gy.device)
+            check(lib().mirec_linear_grad_finish_f32(
+                ptr(P), C, n_out * n_in, ptr(dW), ptr(g2), K, n_out, ptr(db) if db is not None
+                else None, ptr(scratch), ptr(ops.finish_ticket(gy.device, 'linear')),
+                stream_handle()), 'mirec_linear_grad_finish_f32')
         return dx, dW, db
 
 

@@ -924,9 +924,10 @@ def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
 _TICKETS = {}
 
 
-def finish_ticket(device):
-    """Per-device zeroed int32 of mirec_chunk_finish (left zero by every launch)."""
-    key = str(device)
+def finish_ticket(device, tag=''):
+    """Per-device zeroed int32 of mirec_chunk_finish (tag '') or another kernel's
+    last-block ticket (left zero by every launch)."""
+    key = (str(device), tag)
     t = _TICKETS.get(key)
     if t is None:
         t = _TICKETS[key] = torch.zeros(1, dtype=torch.int32, device=device)
