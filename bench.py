@@ -647,9 +647,28 @@ def main():
         torch.cuda.synchronize()
         e_dt = time.perf_counter() - e0
         n_users = len(test.uid_list)
+        # K6's own time: HIP events around each launch (on its stream) of one more pass
+        from recbole_amd import ops
+        ops.KERNEL_EVENTS = {'fullsort': []}
+        fused_full_sort_eval(model, test, ev)
+        torch.cuda.synchronize()
+        k6 = [a.elapsed_time(b) * 1e-3 for a, b in ops.KERNEL_EVENTS['fullsort']]
+        ops.KERNEL_EVENTS = None
+        k6_s = float(sum(k6))
+        flops = 2.0 * step.nI * d * n_users
         result['eval'] = {'metric': 'full-sort eval users/sec', 'value': round(n_users / e_dt, 1),
                           'users': n_users, 'seconds': round(e_dt, 4),
-                          'flops_per_user': 2 * step.nI * d}
+                          'flops_per_user': 2 * step.nI * d,
+                          'roofline': {
+                              'kernel': f'K6 fullsort_topk<{d}> (fp32 MFMA scores + mask + '
+                                        f'top-{max(ev.topk)} + positive flags) x {len(k6)}',
+                              'bound': 'mfma', 'achieved': round(flops / k6_s / 1e12, 2),
+                              'peak': VALU_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                              'frac': round(flops / k6_s / 1e12 / VALU_PEAK_TFLOPS, 4),
+                              'kernel_s': round(k6_s, 5), 'launches': len(k6),
+                              'end_to_end_frac': round(flops / e_dt / 1e12 / VALU_PEAK_TFLOPS, 4),
+                              'flops_formula': '2 * n_items * d per user (the score matmul)',
+                              'timing': 'HIP events around each K6 launch on its stream'}}
     if rank == 0 and not args.no_eval:
         result['gather_throughput'] = gather_throughput(step, d, neg)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -972,17 +972,19 @@ def fullsort_topk(Uq, EI, K: int, hist_ptr=None, hist_cols=None, pos_ptr=None, p
     if n_split > 1:                      # item range split over n_split workgroups + merge
         wsz = lib().mirec_fullsort_topk_split_workspace_size(nq, K, n_split)
         ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
-        rc = lib().mirec_fullsort_topk_split_f32(
-            ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr), ptr(hist_cols), ptr(pos_ptr),
-            ptr(pos_cols), K, n_split, ptr(ws), wsz, ptr(o["scores"]), ptr(o["ids"]),
-            ptr(o.get("pos_flags")), stream_handle())
+        with timed_launch('fullsort'):
+            rc = lib().mirec_fullsort_topk_split_f32(
+                ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr), ptr(hist_cols),
+                ptr(pos_ptr), ptr(pos_cols), K, n_split, ptr(ws), wsz, ptr(o["scores"]),
+                ptr(o["ids"]), ptr(o.get("pos_flags")), stream_handle())
         check(rc, "mirec_fullsort_topk_split_f32")
         o["_ws"] = ws
         return o
-    rc = lib().mirec_fullsort_topk_f32(ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr),
-                                       ptr(hist_cols), ptr(pos_ptr), ptr(pos_cols), K,
-                                       ptr(o["scores"]), ptr(o["ids"]), ptr(o.get("pos_flags")),
-                                       stream_handle())
+    with timed_launch('fullsort'):
+        rc = lib().mirec_fullsort_topk_f32(ptr(Uq), nq, ptr(EI), EI.shape[0], d, ptr(hist_ptr),
+                                           ptr(hist_cols), ptr(pos_ptr), ptr(pos_cols), K,
+                                           ptr(o["scores"]), ptr(o["ids"]),
+                                           ptr(o.get("pos_flags")), stream_handle())
     check(rc, "mirec_fullsort_topk_f32")
     return o
 

@@ -103,15 +103,22 @@ def _window_events(step, names, steps=8):
 
 
 def _pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed models PMC summary
-    (profiles/r*_models_pmc.json, tools/models_pmc.py), or None."""
+    """HBM bytes per launch of `kernel` (a name, or a tuple of names whose per-launch
+    traffic is summed: one call's launches) from the newest committed models PMC summary
+    (profiles/r*_models_pmc.json, tools/models_pmc.py), or None when that summary did not
+    trace every one of them (never an older file's entry for a kernel the step no longer
+    runs)."""
     import glob
     import json
     paths = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_models_pmc.json')))
     if not paths:
         return None, None
-    rec = json.load(open(paths[-1])).get(kernel)
-    return (rec['traffic'], os.path.basename(paths[-1])) if rec else (None, None)
+    recs = json.load(open(paths[-1]))
+    names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
+    got = [recs.get(k) for k in names]
+    if any(r is None for r in got):
+        return None, None
+    return sum(r['traffic'] for r in got), os.path.basename(paths[-1])
 
 
 def _step_breakdown(config):
@@ -254,23 +261,25 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                          f'table), {sum(r[1] for r in runs):.1f} s timed in all; bounded below '
                          f'the 20 + 200 of SURVEY.md 8d: a CPU step moves the 2.1 GB tables '
                          f'several times (~1 s), and the run-to-run spread (cv) is reported'}
-    k10 = {'kernel': 'mlp_fwd_kernel (K10 forward: MLPLayers 624-128-128-128 + '
-                     'deep_predict_layer, dropout, ReLU)', 'bound': 'mfma',
+    fwd_k = ('mlp_l0_fwd_kernel', 'mlp_fwd_kernel')
+    k10 = {'kernel': 'mlp_l0_fwd_kernel + mlp_fwd_kernel (K10 forward: the wide layer 0 over '
+                     'the whole chip, then layers 1.. + deep_predict_layer; dropout, ReLU; '
+                     'one event pair around both launches)', 'bound': 'mfma',
            'achieved': round(mlp_flops / (mf_us * 1e-6) / 1e12, 2),
            'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
            'frac': round(mlp_flops / (mf_us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
-           'traffic': _pmc_traffic('mlp_fwd_kernel')[0],
-           'traffic_source': _pmc_traffic('mlp_fwd_kernel')[1],
+           'traffic': _pmc_traffic(fwd_k)[0],
+           'traffic_source': _pmc_traffic(fwd_k)[1],
            'flops_per_launch': mlp_flops, 'launch_us': round(mf_us, 2),
            'launches_per_step': mf_n,
            'timing': 'HIP events around each launch on its stream, 8 eager steps'}
-    k2 = {'kernel': 'segsort_lds_kernel + blocks_concat_kernel (K2 grouping of the 26 '
-                    'token fields, one event pair around both launches; latency-bound)',
+    k2 = {'kernel': 'segsort_radix8_kernel (K2 grouping of the 26 token fields: one chained '
+                    'launch, keys formed from the field columns; latency-bound)',
           'bound': 'hbm', 'achieved': round(k2_bytes / (k2_us * 1e-6) / 1e9, 1),
           'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
           'frac': round(k2_bytes / (k2_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
-          'traffic': _pmc_traffic('segsort_lds_kernel')[0],
-          'traffic_source': _pmc_traffic('segsort_lds_kernel')[1],
+          'traffic': _pmc_traffic('segsort_radix8_kernel')[0],
+          'traffic_source': _pmc_traffic('segsort_radix8_kernel')[1],
           'bytes_per_launch': k2_bytes, 'launch_us': round(k2_us, 2), 'launches_per_step': k2_n,
           'timing': 'HIP events around each call on its stream, 8 eager steps'}
     # the roofline of the timed step's dominant kernel (committed trace breakdown)
@@ -289,8 +298,11 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
         'roofline': roof,
         'k10_fwd': k10,
         'k2_grouping': k2,
-        'k10_bwd': {'kernel': 'mlp_bwd_data_kernel + mlp_bwd_weight_kernel (K10 backward, one '
-                              'event pair around both launches)', 'bound': 'mfma',
+        'k10_bwd': {'kernel': 'mlp_bwd_data_kernel + mlp_bwd_wide_kernel (K10 backward: layers '
+                              'L-1..1 in row blocks, then layer 0\'s data gradient and every '
+                              'weight gradient over the whole chip; one event pair around both '
+                              'launches)', 'bound': 'mfma',
+                    'traffic': _pmc_traffic(('mlp_bwd_data_kernel', 'mlp_bwd_wide_kernel'))[0],
                     'achieved': round(2 * mlp_flops / (mb_us * 1e-6) / 1e12, 2),
                     'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                     'frac': round(2 * mlp_flops / (mb_us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
