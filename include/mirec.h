@@ -978,6 +978,54 @@ int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const int32_t* n_un
 int mirec_shard_gather_f32(const float* U, const float* I, int32_t d, const int64_t* idx,
                            int64_t n, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Cross-GPU exchange (SURVEY.md §8b comm entry points, §8e; csrc/comm.hip). One
+ * process per GPU; every rank's receive WINDOW (one uncached device allocation) is
+ * mapped into every other rank through HIP IPC over xGMI, and the exchanges are
+ * kernels storing straight into the peers' windows with one flag per (source,
+ * exchange set) — replacing the row-sharded step's two RCCL all-to-alls per step
+ * (reference: the DDP-style exchange the survey maps trainer.py:157-173 onto).
+ * Setup (host): mirec_comm_init -> mirec_comm_window (this rank's window + its IPC
+ * handle) -> the caller shares the handles (e.g. torch.distributed all_gather_object)
+ * -> mirec_comm_connect. Window: [fwd rows: world x wcap x d][bwd rows: same][flags];
+ * an exchange with a plan cap <= wcap puts source src's block at src * cap rows.
+ * Ordering: a pushing launch's last block raises the flags (system-scope release);
+ * mirec_comm_wait polls this rank's flags (bounded: status -5 on a lost peer) and
+ * acquires; launches after it on the stream read the window. Graph-capturable.
+ * ------------------------------------------------------------------------- */
+typedef struct mirec_comm mirec_comm;
+int mirec_comm_init(int rank, int world, const void* unique_id, mirec_comm** out);
+int64_t mirec_comm_handle_bytes(void);
+int mirec_comm_window(mirec_comm* comm, int64_t wcap, int32_t d, void** local, void* handle_out);
+int mirec_comm_connect(mirec_comm* comm, const void* handles);
+int mirec_comm_layout(const mirec_comm* comm, int64_t* fwd_off, int64_t* bwd_off,
+                      int32_t** status_dev);
+int mirec_comm_status(const mirec_comm* comm, int32_t* out);
+int mirec_comm_destroy(mirec_comm* comm);
+/* set 0: forward rows, 1: backward rows (2, 3: the generic calls below) */
+int mirec_comm_wait(mirec_comm* comm, int32_t set, void* stream);
+/* The row-sharded step's forward exchange: entry g*cap + j of idx (mirec_shard_plan's
+ * fwd_rows: >= 0 a row of U, < 0 row -id-1 of I) into rank g's forward region at
+ * me*cap + j; raises set 0. */
+int mirec_comm_push_rows_f32(mirec_comm* comm, const float* U, const float* I,
+                             const int64_t* idx, int64_t cap, void* stream);
+/* K3 on this rank's slice reading the forward region at the plan's positions (user
+ * [B], pos [B], neg [times x B] message positions o*cap + j), each gradient row into
+ * owner o's backward region at me*cap + j (where its perm2 reads it); per-positive
+ * losses to loss_k; raises set 1. Same arithmetic as mirec_bpr_fwd_bwd_at_ids_f32. */
+int mirec_comm_bpr_f32(mirec_comm* comm, const int64_t* user, const int64_t* pos,
+                       const int64_t* neg, int64_t B, int32_t times, float gamma,
+                       float grad_scale, float* loss_k, int64_t cap, void* stream);
+/* Equal-block all-to-all of rows: send [world x wcap x d] (block g to rank g, its first
+ * send_counts[g] rows, device array or NULL = all); afterwards this rank's forward
+ * region (recv must be the window base, or NULL) holds block src at src * wcap.
+ * Includes the wait. */
+int mirec_alltoallv_rows_f32(mirec_comm* comm, const float* send, const int64_t* send_counts,
+                             float* recv, const int64_t* recv_counts, int32_t d, void* stream);
+/* buf[n] <- the sum of every rank's buf, added in rank order (the same bits on every
+ * rank); n <= wcap*d, a multiple of 4, buf 16-B aligned. Includes the wait. */
+int mirec_allreduce_sum_f32(mirec_comm* comm, float* buf, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -223,6 +223,19 @@ SIGNATURES = {
     "mirec_mlp_bwd_f32": (c_int, [_P, _P, _P, c_int64, _P, _P]),
     "mirec_mlp_bwd_workspace": (c_int, [_P, c_int64, _P, _P]),
     "mirec_linear_grad_finish_scratch": (c_int64, [c_int64, c_int32]),
+    "mirec_comm_init": (c_int, [ctypes.c_int, ctypes.c_int, _P, _P]),
+    "mirec_comm_handle_bytes": (c_int64, []),
+    "mirec_comm_window": (c_int, [_P, c_int64, c_int32, _P, _P]),
+    "mirec_comm_connect": (c_int, [_P, _P]),
+    "mirec_comm_layout": (c_int, [_P, _P, _P, _P]),
+    "mirec_comm_destroy": (c_int, [_P]),
+    "mirec_comm_status": (c_int, [_P, _P]),
+    "mirec_comm_wait": (c_int, [_P, c_int32, _P]),
+    "mirec_comm_push_rows_f32": (c_int, [_P, _P, _P, _P, c_int64, _P]),
+    "mirec_comm_bpr_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int32, c_float, c_float, _P,
+                                   c_int64, _P]),
+    "mirec_alltoallv_rows_f32": (c_int, [_P, _P, _P, _P, _P, c_int32, _P]),
+    "mirec_allreduce_sum_f32": (c_int, [_P, _P, c_int64, _P]),
     "mirec_linear_grad_finish_f32": (c_int, [_P, c_int32, c_int64, _P, _P, c_int64, c_int32, _P,
                                              _P, _P, _P]),
     "mirec_seq_embed_ln_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,

@@ -1,0 +1,498 @@
+// Cross-GPU exchange for the row-sharded C2 step: one process per
+// GPU, every rank's receive WINDOW mapped into every other rank's address space (HIP
+// IPC over xGMI), and the per-step exchanges done by kernels storing straight into the
+// peers' windows, with a flag per (source, exchange) instead of RCCL collectives.
+//
+// Why: a row-sharded step exchanges ~1.5 MB per rank twice (the rows each slice reads,
+// then its gradient rows back): latency-bound RCCL all-to-alls of ~10-20 µs each, two
+// extra launches per step. Here the owner's gather stores each message row directly
+// into the receiving rank's window and the last block raises one flag per peer; the
+// consumer's next launch waits for the flags on the GPU (no host, no collective).
+//
+// Window (one uncached device allocation per rank, hipDeviceMallocUncached: no cache
+// on either side holds its lines, so a peer's stores are what a later load reads):
+//   [fwd rows: G x wcap x d floats][bwd rows: G x wcap x d][flags: kFlagSets x kMaxPeers int32]
+// wcap = the largest message a plan can ask for; the step's exchanges use the plan's own
+// cap (<= wcap) as the block stride, so a region holds block `src` (the rows rank src
+// sent) at src * cap — the layout of the equal-block all-to-all it replaces.
+//
+// Hand-off (release / acquire at SYSTEM scope, the C++ memory model's own form: the
+// producers run on other GPUs): every block of a pushing launch drains its stores
+// (s_waitcnt vmcnt(0) in each wave), meets, and one lane adds to the launch's arrival
+// counter with a system-scope acq_rel add; the block whose add is last stores the
+// exchange's sequence number into flag[set][me] of every peer with a system-scope
+// release store. The waiting side polls its own flags with system-scope loads, then a
+// system-scope acquire; the kernels after it (stream order) read the window.
+//
+// Sequence numbers: each exchange set keeps a device counter per rank (cnt); a push
+// raises flags to cnt + 1 and the wait for it sets cnt = cnt + 1 — every rank runs the
+// same exchanges in the same order, so the counters agree without communication, and
+// captured graphs replay with advancing values. A rank cannot run ahead by a whole
+// exchange of the same set (its next push of a set needs the other set's flags, which
+// need the peer's wait), so a flag never exceeds the value being waited for by more
+// than nothing, and a window block is never overwritten while its reader still reads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "bpr_math.h"
+
+namespace mirec {
+
+constexpr int kMaxPeers = 64;
+constexpr int kFlagSets = 4;            // 0 forward rows, 1 backward rows, 2-3 generic
+constexpr int kXThreads = 256;
+
+struct Peers {
+  char* base[kMaxPeers];                // every rank's window in this process
+};
+
+struct XSig {                           // the flag raised at the end of a pushing launch
+  int32_t* arrive;                      // launch arrival counter (device, zero between)
+  const int32_t* cnt;                   // this exchange set's counter (read)
+  int64_t flag_off;                     // byte offset of flag set 0 in a window
+  int32_t set, G, me;
+};
+
+__device__ __forceinline__ int32_t* flag_at(char* win, int64_t flag_off, int set, int src) {
+  return reinterpret_cast<int32_t*>(win + flag_off) + set * kMaxPeers + src;
+}
+
+// the end of a pushing launch: this block's stores drained and published; the last
+// block raises the flags
+__device__ __forceinline__ void push_done(const Peers& P, const XSig& s) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const int prev = __hip_atomic_fetch_add(s.arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (prev != (int)(gridDim.x * gridDim.y) - 1) return;
+  __hip_atomic_store(s.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int32_t v = s.cnt[0] + 1;
+  for (int q = 0; q < s.G; ++q)
+    if (q != s.me)
+      __hip_atomic_store(flag_at(P.base[q], s.flag_off, s.set, s.me), v, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait for flag[set][src] >= cnt + 1 of every src != me, then cnt += 1. One block;
+// a bounded spin (status -5 and an early exit instead of a hang).
+__global__ __launch_bounds__(64) void xchg_wait_kernel(char* win, int64_t flag_off, int set,
+                                                       int G, int me, int32_t* cnt,
+                                                       int32_t* status, int64_t max_polls) {
+  const int32_t target = cnt[0] + 1;
+  bool ok = true;
+  for (int q = threadIdx.x; q < G; q += 64) {
+    if (q == me) continue;
+    const int32_t* f = flag_at(win, flag_off, set, q);
+    int64_t n = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      if (++n > max_polls) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  if (!ok) __hip_atomic_store(status, -5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[0] = target;
+}
+
+// The owner's forward message rows into the readers' windows: entry q = g * cap + j
+// of idx (the exchange plan, mirec_shard_plan fwd_rows: >= 0 a user-shard row, < 0 an
+// item-shard row -id - 1) goes to rank g's window, block `me`, row j. D/4 lanes per row.
+template <int D>
+__global__ __launch_bounds__(kXThreads) void xchg_push_rows_kernel(
+    const float* __restrict__ U, const float* __restrict__ I, const int64_t* __restrict__ idx,
+    int64_t cap, int64_t region_off, Peers P, XSig s) {
+  constexpr int LPR = D / 4;
+  const int64_t q = ((int64_t)blockIdx.x * kXThreads + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  const int64_t n = (int64_t)s.G * cap;
+  if (q < n) {
+    const int g = (int)(q / cap);
+    const int64_t j = q - (int64_t)g * cap;
+    const int64_t r = idx[q];
+    const float4 v = reinterpret_cast<const float4*>(r >= 0 ? U + r * D : I + (-r - 1) * D)[c];
+    float* dst = reinterpret_cast<float*>(P.base[g] + region_off) + ((int64_t)s.me * cap + j) * D;
+    reinterpret_cast<float4*>(dst)[c] = v;
+  }
+  push_done(P, s);
+}
+
+// Rows of this rank's send buffer [G x cap x D] (block g for rank g) into the readers'
+// windows (block `me`): the generic equal-block all-to-all, and the backward rows.
+template <int D>
+__global__ __launch_bounds__(kXThreads) void xchg_push_blocks_kernel(
+    const float* __restrict__ send, const int64_t* __restrict__ counts, int64_t cap,
+    int64_t wcap, int64_t region_off, Peers P, XSig s) {
+  constexpr int LPR = D / 4;
+  const int64_t q = ((int64_t)blockIdx.x * kXThreads + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  if (q < (int64_t)s.G * cap) {
+    const int g = (int)(q / cap);
+    const int64_t j = q - (int64_t)g * cap;
+    if (!counts || j < counts[g]) {
+      const float4 v = reinterpret_cast<const float4*>(send + q * D)[c];
+      float* dst = reinterpret_cast<float*>(P.base[g] + region_off) + ((int64_t)s.me * wcap + j) * D;
+      reinterpret_cast<float4*>(dst)[c] = v;
+    }
+  }
+  push_done(P, s);
+}
+
+// K3 of this rank's slice on the received rows, its gradient rows straight into the
+// owners' windows. The BPR arithmetic is K3's (bpr_math.h, bpr.hip AT_IDS): a slot's
+// row sits at message position pos = o * cap + j of the forward region (owner o's
+// message), and its gradient row goes to owner o's backward region at me * cap + j —
+// the position the owner's plan (shard.hip: perm2 = g * cap + j) reads it from. The
+// last block raises the backward flags.
+template <int D>
+__global__ __launch_bounds__(kXThreads) void bpr_xchg_kernel(
+    const char* __restrict__ win, int64_t fwd_off, int64_t bwd_off, const int64_t* __restrict__ user,
+    const int64_t* __restrict__ pos, const int64_t* __restrict__ neg, int64_t B, int times,
+    float gamma, float grad_scale, float* __restrict__ loss_k, int64_t cap, Peers P, XSig s) {
+  constexpr int LPR = D / 4;
+  constexpr int GPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR;
+  const int l = lane - g * LPR;
+  const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
+  const float* __restrict__ E = reinterpret_cast<const float*>(win + fwd_off);
+  auto row_of = [&](int64_t p) -> int64_t { return p; };
+  auto out_of = [&](int64_t p) -> float* {    // message position -> the owner's window row
+    const int64_t o = p / cap;
+    return reinterpret_cast<float*>(P.base[o] + bwd_off) + ((int64_t)s.me * cap + (p - o * cap)) * D;
+  };
+  if (k < B) {
+    const int64_t pu = user[k], pp = pos[k];
+    const float4 u = reinterpret_cast<const float4*>(E + row_of(pu) * D)[l];
+    const float4 p = reinterpret_cast<const float4*>(E + row_of(pp) * D)[l];
+    const float sp = group_sum<LPR>(dot4(u, p));
+    float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gp = gu;
+    float lsum = 0.f;
+    const float ng = -grad_scale;
+    for (int j0 = 0; j0 < times; j0 += 4) {
+      float4 n[4];
+      int64_t pn[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = j0 + q;
+        pn[q] = j < times ? neg[(int64_t)j * B + k] : 0;
+        n[q] = j < times ? reinterpret_cast<const float4*>(E + row_of(pn[q]) * D)[l]
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      float sn[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sn[q] = group_sum<LPR>(dot4(u, n[q]));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (j0 + q < times) {
+          const BprCoef cf = bpr_coef(sp, sn[q], gamma, ng);
+          lsum += cf.nll;
+          float4 gn;
+          pair_contrib(gu, gp, gn, cf.dx, u, p, n[q]);
+          reinterpret_cast<float4*>(out_of(pn[q]))[l] = gn;
+        }
+      }
+    }
+    reinterpret_cast<float4*>(out_of(pu))[l] = gu;
+    reinterpret_cast<float4*>(out_of(pp))[l] = gp;
+    if (l == 0 && loss_k) loss_k[k] = lsum;
+  }
+  push_done(P, s);
+}
+
+// The same n floats (n4 float4) of this rank into block `me` (stride floats apart) of
+// every rank's region: the all-reduce's contribution.
+__global__ __launch_bounds__(kXThreads) void xchg_push_bcast_kernel(
+    const float* __restrict__ buf, int64_t n4, int64_t stride, int64_t region_off, Peers P,
+    XSig s) {
+  const int64_t q = (int64_t)blockIdx.x * kXThreads + threadIdx.x;
+  if (q < (int64_t)s.G * n4) {
+    const int g = (int)(q / n4);
+    const int64_t i = q - (int64_t)g * n4;
+    float* dst = reinterpret_cast<float*>(P.base[g] + region_off) + (int64_t)s.me * stride;
+    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(buf)[i];
+  }
+  push_done(P, s);
+}
+
+// buf <- the sum over ranks (in rank order: the same bits on every rank) of every
+// rank's n floats in region rows [src * wcap * d ...) of the window (after the wait)
+__global__ __launch_bounds__(kXThreads) void xchg_sum_kernel(const char* __restrict__ win,
+                                                             int64_t region_off, int64_t stride,
+                                                             int G, int64_t n,
+                                                             float* __restrict__ buf) {
+  const int64_t i = (int64_t)blockIdx.x * kXThreads + threadIdx.x;
+  if (i >= n) return;
+  const float* r = reinterpret_cast<const float*>(win + region_off);
+  float t = r[i];
+  for (int q = 1; q < G; ++q) t += r[(int64_t)q * stride + i];
+  buf[i] = t;
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+struct mirec_comm {
+  int rank, world;
+  char* window;
+  size_t window_bytes;
+  int64_t wcap;                         // rows per source block of a row region
+  int32_t d;
+  char* peers[kMaxPeers];
+  bool opened[kMaxPeers];
+  int32_t* ctl;                         // device: [arrive | cnt[kFlagSets] | status]
+};
+
+namespace {
+int64_t region_bytes(const mirec_comm* c) { return (int64_t)c->world * c->wcap * c->d * 4; }
+int64_t flag_off(const mirec_comm* c) { return 2 * region_bytes(c); }
+Peers peers_of(const mirec_comm* c) {
+  Peers P;
+  memset(&P, 0, sizeof(P));
+  for (int q = 0; q < c->world; ++q) P.base[q] = c->peers[q];
+  return P;
+}
+XSig sig_of(const mirec_comm* c, int set) {
+  XSig s;
+  s.arrive = c->ctl;
+  s.cnt = c->ctl + 1 + set;
+  s.flag_off = flag_off(c);
+  s.set = set;
+  s.G = c->world;
+  s.me = c->rank;
+  return s;
+}
+bool connected(const mirec_comm* c) {
+  for (int q = 0; q < c->world; ++q)
+    if (!c->peers[q]) return false;
+  return true;
+}
+}  // namespace
+
+// unique_id: the job's 64-byte token (every rank passes the same one; the windows of
+// different jobs never meet: their handles come only through the caller's exchange).
+extern "C" int mirec_comm_init(int rank, int world, const void* unique_id, mirec_comm** out) {
+  if (!out || !unique_id || world < 1 || world > kMaxPeers || rank < 0 || rank >= world) {
+    set_error("mirec_comm_init: bad arguments (world 1..%d)", kMaxPeers);
+    return -1;
+  }
+  mirec_comm* c = new mirec_comm;
+  memset(c, 0, sizeof(*c));
+  c->rank = rank;
+  c->world = world;
+  hipError_t e = hipMalloc(&c->ctl, (2 + kFlagSets) * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemset(c->ctl, 0, (2 + kFlagSets) * sizeof(int32_t));
+  if (e != hipSuccess) {
+    delete c;
+    return hip_status(e, "mirec_comm_init");
+  }
+  *out = c;
+  return 0;
+}
+
+// This rank's window for rows of d floats, wcap rows per source block; its IPC handle
+// (HIP_IPC_HANDLE_SIZE bytes) goes to handle_out for the caller to share.
+extern "C" int mirec_comm_window(mirec_comm* c, int64_t wcap, int32_t d, void** local,
+                                 void* handle_out) {
+  if (!c || wcap < 1 || d < 4 || d % 4 || !handle_out || c->window) {
+    set_error("mirec_comm_window: bad arguments (one window per communicator)");
+    return -1;
+  }
+  c->wcap = wcap;
+  c->d = d;
+  c->window_bytes = (size_t)flag_off(c) + kFlagSets * kMaxPeers * sizeof(int32_t);
+  hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->window), c->window_bytes,
+                                       hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(c->window, 0, c->window_bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipIpcMemHandle_t h;
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&h, c->window);
+  if (e != hipSuccess) return hip_status(e, "mirec_comm_window");
+  memcpy(handle_out, &h, sizeof(h));
+  c->peers[c->rank] = c->window;
+  if (local) *local = c->window;
+  return 0;
+}
+
+extern "C" int64_t mirec_comm_handle_bytes(void) { return (int64_t)sizeof(hipIpcMemHandle_t); }
+
+// Map every other rank's window (handles: world x mirec_comm_handle_bytes(), rank order).
+extern "C" int mirec_comm_connect(mirec_comm* c, const void* handles) {
+  if (!c || !handles || !c->window) {
+    set_error("mirec_comm_connect: bad arguments (window first)");
+    return -1;
+  }
+  for (int q = 0; q < c->world; ++q) {
+    if (q == c->rank || c->peers[q]) continue;
+    hipIpcMemHandle_t h;
+    memcpy(&h, static_cast<const char*>(handles) + (size_t)q * sizeof(h), sizeof(h));
+    void* p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return hip_status(e, "mirec_comm_connect");
+    c->peers[q] = static_cast<char*>(p);
+    c->opened[q] = true;
+  }
+  return 0;
+}
+
+// Byte offsets of the forward / backward row regions and the device status word (-5:
+// a wait timed out; never reset by the library).
+extern "C" int mirec_comm_layout(const mirec_comm* c, int64_t* fwd_off, int64_t* bwd_off,
+                                 int32_t** status_dev) {
+  if (!c || !c->window) {
+    set_error("mirec_comm_layout: no window");
+    return -1;
+  }
+  if (fwd_off) *fwd_off = 0;
+  if (bwd_off) *bwd_off = region_bytes(c);
+  if (status_dev) *status_dev = c->ctl + 1 + kFlagSets;
+  return 0;
+}
+
+// The status word to the host (synchronous: after the stream's work): 0, or -5 when a
+// wait gave up on a peer.
+extern "C" int mirec_comm_status(const mirec_comm* c, int32_t* out) {
+  if (!c || !out) {
+    set_error("mirec_comm_status: bad arguments");
+    return -1;
+  }
+  const hipError_t e = hipMemcpy(out, c->ctl + 1 + kFlagSets, sizeof(int32_t), hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : hip_status(e, "mirec_comm_status");
+}
+
+extern "C" int mirec_comm_destroy(mirec_comm* c) {
+  if (!c) return 0;
+  (void)hipDeviceSynchronize();
+  for (int q = 0; q < c->world; ++q)
+    if (c->opened[q]) (void)hipIpcCloseMemHandle(c->peers[q]);
+  if (c->window) (void)hipFree(c->window);
+  if (c->ctl) (void)hipFree(c->ctl);
+  delete c;
+  return 0;
+}
+
+namespace {
+constexpr int64_t kMaxPolls = 1ll << 24;   // seconds of polling: a lost peer ends as status -5
+
+int wait_set(mirec_comm* c, int set, hipStream_t st, const char* what) {
+  hipLaunchKernelGGL(xchg_wait_kernel, dim3(1), dim3(64), 0, st, c->window, flag_off(c), set,
+                     c->world, c->rank, c->ctl + 1 + set, c->ctl + 1 + kFlagSets, kMaxPolls);
+  return launch_status(what);
+}
+}  // namespace
+
+// The exchange's wait, alone (set 0 forward rows, 1 backward rows).
+extern "C" int mirec_comm_wait(mirec_comm* c, int32_t set, void* stream) {
+  if (!c || !c->window || !connected(c) || set < 0 || set >= kFlagSets) {
+    set_error("mirec_comm_wait: bad arguments");
+    return -1;
+  }
+  return wait_set(c, set, (hipStream_t)stream, "mirec_comm_wait");
+}
+
+#define MIREC_XD(DD, ...)                     \
+  switch (DD) {                               \
+    case 32: { constexpr int D = 32; __VA_ARGS__; break; }   \
+    case 64: { constexpr int D = 64; __VA_ARGS__; break; }   \
+    case 128: { constexpr int D = 128; __VA_ARGS__; break; } \
+    case 256: { constexpr int D = 256; __VA_ARGS__; break; } \
+    default: set_error("d must be 32, 64, 128 or 256"); return -1; \
+  }
+
+// Forward rows of the row-sharded step (shard.hip plan): owner -> readers' windows.
+extern "C" int mirec_comm_push_rows_f32(mirec_comm* c, const float* U, const float* I,
+                                        const int64_t* idx, int64_t cap, void* stream) {
+  if (!c || !c->window || !connected(c) || !U || !I || !idx || cap < 1 || cap > c->wcap) {
+    set_error("mirec_comm_push_rows_f32: bad arguments (cap <= the window's)");
+    return -1;
+  }
+  const int64_t n = (int64_t)c->world * cap;
+  const unsigned blocks = (unsigned)((n * (c->d / 4) + kXThreads - 1) / kXThreads);
+  hipStream_t st = (hipStream_t)stream;
+  const Peers P = peers_of(c);
+  const XSig s = sig_of(c, 0);
+  MIREC_XD(c->d, hipLaunchKernelGGL(xchg_push_rows_kernel<D>, dim3(blocks), dim3(kXThreads), 0,
+                                    st, U, I, idx, cap, (int64_t)0, P, s));
+  return launch_status("mirec_comm_push_rows_f32");
+}
+
+// K3 on the received rows (after mirec_comm_wait(0)); gradient rows to the owners.
+extern "C" int mirec_comm_bpr_f32(mirec_comm* c, const int64_t* user, const int64_t* pos,
+                                  const int64_t* neg, int64_t B, int32_t times, float gamma,
+                                  float grad_scale, float* loss_k, int64_t cap, void* stream) {
+  if (!c || !c->window || !connected(c) || B < 0 || times < 0 || cap < 1 || cap > c->wcap ||
+      (B > 0 && (!user || !pos || (times > 0 && !neg)))) {
+    set_error("mirec_comm_bpr_f32: bad arguments");
+    return -1;
+  }
+  const int64_t GPW = 64 / (c->d / 4);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, (B + (kXThreads / 64) * GPW - 1) /
+                                                            ((kXThreads / 64) * GPW));
+  hipStream_t st = (hipStream_t)stream;
+  const Peers P = peers_of(c);
+  const XSig s = sig_of(c, 1);
+  MIREC_XD(c->d, hipLaunchKernelGGL(bpr_xchg_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
+                                    (const char*)c->window, (int64_t)0, region_bytes(c), user,
+                                    pos, neg, B, times, gamma, grad_scale, loss_k, cap, P, s));
+  return launch_status("mirec_comm_bpr_f32");
+}
+
+// rows of send [world x cap x d] (block g for rank g, its first
+// send_counts[g] rows; counts on the device, NULL: all cap) into every rank's window;
+// after the call recv (= the forward region of this rank's window, block src at
+// src * wcap rows) holds what every rank sent here. recv_counts: unused (the window
+// layout fixes them; kept for the signature), may be NULL. Stream-ordered; generic set 2.
+extern "C" int mirec_alltoallv_rows_f32(mirec_comm* c, const float* send,
+                                        const int64_t* send_counts, float* recv,
+                                        const int64_t* recv_counts, int32_t d, void* stream) {
+  (void)recv_counts;
+  if (!c || !c->window || !connected(c) || !send || d != c->d ||
+      (recv && recv != reinterpret_cast<float*>(c->window))) {
+    set_error("mirec_alltoallv_rows_f32: bad arguments (recv must be the window or NULL)");
+    return -1;
+  }
+  const int64_t n = (int64_t)c->world * c->wcap;
+  const unsigned blocks = (unsigned)((n * (d / 4) + kXThreads - 1) / kXThreads);
+  hipStream_t st = (hipStream_t)stream;
+  const Peers P = peers_of(c);
+  const XSig s = sig_of(c, 2);
+  MIREC_XD(d, hipLaunchKernelGGL(xchg_push_blocks_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
+                                 send, send_counts, c->wcap, c->wcap, (int64_t)0, P, s));
+  const int rc = launch_status("mirec_alltoallv_rows_f32");
+  return rc ? rc : wait_set(c, 2, st, "mirec_alltoallv_rows_f32");
+}
+
+// buf[n] <- the sum over ranks of every rank's buf, added in rank order
+// (bit-identical on every rank). n <= the window's region (world x wcap x d floats
+// split into world blocks of wcap x d). Generic set 3, backward region as staging.
+extern "C" int mirec_allreduce_sum_f32(mirec_comm* c, float* buf, int64_t n, void* stream) {
+  if (!c || !c->window || !connected(c) || !buf || n < 0 || n > c->wcap * c->d ||
+      ((uintptr_t)buf % 16) != 0 || n % 4) {
+    set_error("mirec_allreduce_sum_f32: bad arguments (n <= wcap * d, a multiple of 4)");
+    return -1;
+  }
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const Peers P = peers_of(c);
+  const XSig s = sig_of(c, 3);
+  // every rank's buffer into block `me` of every window's backward region, seen as
+  // [world x (wcap x d)] floats
+  const int64_t stride = c->wcap * c->d;
+  const unsigned blocks = (unsigned)(((int64_t)c->world * (n / 4) + kXThreads - 1) / kXThreads);
+  hipLaunchKernelGGL(xchg_push_bcast_kernel, dim3(blocks), dim3(kXThreads), 0, st, buf, n / 4,
+                     stride, region_bytes(c), P, s);
+  int rc = launch_status("mirec_allreduce_sum_f32");
+  if (rc) return rc;
+  rc = wait_set(c, 3, st, "mirec_allreduce_sum_f32");
+  if (rc) return rc;
+  hipLaunchKernelGGL(xchg_sum_kernel, dim3((unsigned)((n + kXThreads - 1) / kXThreads)),
+                     dim3(kXThreads), 0, st, (const char*)c->window, region_bytes(c), stride,
+                     c->world, n, buf);
+  return launch_status("mirec_allreduce_sum_f32");
+}

@@ -968,11 +968,18 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
     one rank (G = 1; the all-to-alls are copies)."""
 
     CAP_SLACK = 1.25
+    # the per-step row exchanges: 'rccl' (two all-to-alls of equal blocks) or 'ipc' (the
+    # owners' gather stores into the readers' IPC-mapped windows, K3 stores the gradient
+    # rows into the owners' windows, flags on the GPU: csrc/comm.hip, trainer/comm.py)
+    EXCHANGE = os.environ.get('MIREC_EXCHANGE', 'rccl')
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
-                 adam_mode='deferred', dist=None, cap=None):
+                 adam_mode='deferred', dist=None, cap=None, exchange=None):
         if adam_mode != 'deferred':
             raise ValueError('the row-sharded step runs the deferred Adam schedule')
+        exchange = exchange or self.EXCHANGE
+        if exchange not in ('rccl', 'ipc'):
+            raise ValueError(f"exchange must be 'rccl' or 'ipc', got {exchange!r}")
         super().__init__(model, optimizer, train_data, chunk=chunk, use_graph=use_graph,
                          adam_mode=adam_mode, dist=dist, fused_step=False)
         G, B, T, d, dev = self.G, self.B, self.times, self.d, self.device
@@ -987,6 +994,11 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         self.lastU = torch.zeros(self.SU, dtype=torch.int32, device=dev)
         self.lastI = torch.zeros(self.SI, dtype=torch.int32, device=dev)
         self._solo = dist is None            # one rank, no process group: no collectives
+        self.exchange = 'rccl' if self._solo else exchange
+        self.win = None
+        if self.exchange == 'ipc':           # every rank's receive window, mapped everywhere
+            from recbole_amd.trainer.comm import PeerWindows
+            self.win = PeerWindows(dist, (2 + T) * B, d, dev)
         self.loss_g = torch.empty(G * self.C * B, dtype=torch.float32, device=dev)
         self.loss_mine = torch.zeros(self.C * B, dtype=torch.float32, device=dev)
         self.status = torch.zeros(2, dtype=torch.int32, device=dev)    # epoch backstop
@@ -1016,13 +1028,15 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         self._fill_tables()
 
     def _alloc_exchange(self):
-        """Buffers sized by `cap`: the two all-to-all send / receive buffers and the
-        per-slot message plans."""
+        """Buffers sized by `cap`: the two all-to-all send / receive buffers (rccl; the
+        ipc exchange receives in the windows, sized for the largest cap) and the per-slot
+        message plans."""
         M, d, dev = self.G * self.cap, self.d, self.device
-        self.sendF = torch.empty(M, d, device=dev)
-        self.recvF = self.sendF if self._solo else torch.empty(M, d, device=dev)
-        self.sendB = torch.empty(M, d, device=dev)
-        self.recvB = self.sendB if self._solo else torch.empty(M, d, device=dev)
+        if self.win is None:
+            self.sendF = torch.empty(M, d, device=dev)
+            self.recvF = self.sendF if self._solo else torch.empty(M, d, device=dev)
+            self.sendB = torch.empty(M, d, device=dev)
+            self.recvB = self.sendB if self._solo else torch.empty(M, d, device=dev)
         for sl in self.slots:
             sl.fwd_rows = torch.empty(self.C * M, dtype=torch.int64, device=dev)
             sl.bwd_src = torch.empty(self.C * M, dtype=torch.int32, device=dev)
@@ -1190,7 +1204,7 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             t[q].n_rows = S
             t[q].last = last.data_ptr()
             t[q].dense_grad = None
-            t[q].rows = self.recvB.data_ptr()
+            t[q].rows = self.win.bwd if self.win is not None else self.recvB.data_ptr()
 
     def _adam_state(self):
         return [(self.shU[1], self.shU[2], self.lastU), (self.shI[1], self.shI[2], self.lastI)]
@@ -1201,9 +1215,66 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
     def _n_local(self, Bc):
         return max(0, min(self.B, Bc - self.rank * self.B))
 
+    def _step_ipc(self, slot, c, Bc, stream):
+        """The two exchanges of a step through the peer windows (csrc/comm.hip): the
+        owner's gather stores its rows into the readers' windows, K3 reads them there and
+        stores each gradient row into its owner's window; two flag waits on the GPU."""
+        T, B, M = self.times, self.B, self.G * self.cap
+        L = lib()
+        st = stream.cuda_stream
+        n = self._n_local(Bc)
+        w = self.win.comm
+
+        def push():
+            check(L.mirec_comm_push_rows_f32(w, self.shU[0].data_ptr(), self.shI[0].data_ptr(),
+                                             slot.fwd_rows.data_ptr() + 8 * c * M, self.cap, st),
+                  'mirec_comm_push_rows_f32')
+        self._record('gather', stream, push)
+        self._record('exchange', stream, lambda: check(L.mirec_comm_wait(w, 0, st),
+                                                       'mirec_comm_wait'))
+        loss_p = self.loss_mine.data_ptr() + 4 * c * B
+        pos_p = slot.pos.data_ptr() + 8 * c * (2 + T) * B
+
+        def bpr():                      # every rank launches it: its last block raises the flags
+            check(L.mirec_comm_bpr_f32(w, pos_p, pos_p + 8 * n, pos_p + 16 * n, n, T, 1e-10,
+                                       self._grad_scale(Bc), loss_p, self.cap, st),
+                  'mirec_comm_bpr_f32')
+        self._record('bpr', stream, bpr)
+        self._record('exchange_bwd', stream, lambda: check(L.mirec_comm_wait(w, 1, st),
+                                                           'mirec_comm_wait'))
+
     def _step(self, slot, c, Bc, stream, step_off, ahead):
         T, d, G, B, M = self.times, self.d, self.G, self.B, self.G * self.cap
         KI = (1 + T) * Bc
+        L = lib()
+        st = stream.cuda_stream
+        n = self._n_local(Bc)
+        if self.win is not None:
+            self._step_ipc(slot, c, Bc, stream)
+        else:
+            self._step_rccl(slot, c, Bc, stream)
+        t = self._tables
+        for q, (tag, per) in enumerate((('u', Bc), ('i', KI))):
+            t[q].perm = getattr(slot, f'perm2_{tag}').data_ptr() + 4 * c * per
+            t[q].uniq = getattr(slot, f'own_{tag}').data_ptr() + 4 * c * per
+            t[q].seg = getattr(slot, f'own_{tag}_seg').data_ptr() + 4 * c * (per + 1)
+            t[q].n_uniq = getattr(slot, f'own_{tag}_n').data_ptr() + 4 * c
+            if ahead:
+                t[q].ahead_uniq = getattr(slot, f'own_{tag}_ah').data_ptr() + 4 * c * per
+                t[q].ahead_n_uniq = getattr(slot, f'own_{tag}_nah').data_ptr() + 4 * c
+            else:
+                t[q].ahead_uniq = t[q].ahead_n_uniq = None
+
+        def adam():
+            check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
+                                            self.step_idx.data_ptr(), step_off,
+                                            *self._adam_args, st), 'mirec_adam_deferred_f32')
+        self._record('adam', stream, adam)
+        if self.kernel_events is not None:
+            self.kernel_uniq.append(torch.stack([slot.own_u_n[c], slot.own_i_n[c]]))
+
+    def _step_rccl(self, slot, c, Bc, stream):
+        T, d, G, B, M = self.times, self.d, self.G, self.B, self.G * self.cap
         L = lib()
         st = stream.cuda_stream
         n = self._n_local(Bc)
@@ -1230,25 +1301,6 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                   'mirec_bpr_fwd_bwd_at_ids_f32')
         self._record('bpr', stream, bpr)
         self._record('exchange_bwd', stream, lambda: self._all_to_all(self.recvB, self.sendB))
-        t = self._tables
-        for q, (tag, per) in enumerate((('u', Bc), ('i', KI))):
-            t[q].perm = getattr(slot, f'perm2_{tag}').data_ptr() + 4 * c * per
-            t[q].uniq = getattr(slot, f'own_{tag}').data_ptr() + 4 * c * per
-            t[q].seg = getattr(slot, f'own_{tag}_seg').data_ptr() + 4 * c * (per + 1)
-            t[q].n_uniq = getattr(slot, f'own_{tag}_n').data_ptr() + 4 * c
-            if ahead:
-                t[q].ahead_uniq = getattr(slot, f'own_{tag}_ah').data_ptr() + 4 * c * per
-                t[q].ahead_n_uniq = getattr(slot, f'own_{tag}_nah').data_ptr() + 4 * c
-            else:
-                t[q].ahead_uniq = t[q].ahead_n_uniq = None
-
-        def adam():
-            check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
-                                            self.step_idx.data_ptr(), step_off,
-                                            *self._adam_args, st), 'mirec_adam_deferred_f32')
-        self._record('adam', stream, adam)
-        if self.kernel_events is not None:
-            self.kernel_uniq.append(torch.stack([slot.own_u_n[c], slot.own_i_n[c]]))
 
     def _finish(self, c0, n_steps, Bc, stream):
         """Losses of this rank's slices of steps c0..c0+n_steps -> all ranks (one
@@ -1266,8 +1318,17 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         self._load_shards()
         return super().begin_epoch(cuts=cuts, hold_prep_from=hold_prep_from, flush_at=flush_at)
 
+    def close(self):
+        super().close()
+        if self.win is not None:             # after a barrier: no rank still stores into it
+            self.win.close()
+            self.win = None
+
     def end_epoch(self, n_done=None):
         losses = super().end_epoch(n_done)
+        if self.win is not None and self.win.status() == -5:
+            raise RuntimeError('row exchange: a wait for a peer\'s flags timed out (a rank '
+                               'stopped or fell out of step)')
         if int(self.status[0].item()) == -4:                 # backstop: _enter_chunk re-plans
             raise RuntimeError(f'row exchange overflow: a (slice, owner) message exceeded '
                                f'cap={self.cap} rows')

@@ -164,7 +164,7 @@ def test_sharded_cap_overflow_replans(tmp_path, graph):
         assert torch.equal(a, b)
 
 
-def _worker(rank, port, root, q, cap=None):
+def _worker(rank, port, root, q, cap=None, exchange='rccl'):
     import torch.distributed as tdist
     from recbole_amd.trainer.fused import ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
@@ -175,24 +175,30 @@ def _worker(rank, port, root, q, cap=None):
         config, train, valid, test, model = _pipeline(root, 256)
         opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
         step = ShardedBPRTrainStep(model, opt, train, chunk=CHUNK, dist=tdist.group.WORLD,
-                                   cap=cap)
+                                   cap=cap, exchange=exchange)
+        assert step.exchange == exchange
         tensors, losses = _train(step)
         assert cap is None or step.cap_growths >= 1
+        step.close()
         q.put((rank, step.Bg, step.SU, [t.numpy() for t in tensors], losses))
     finally:
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize('cap', [None, 40])
-def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap):
-    """cap=40: both ranks detect the same overflow and grow cap identically."""
+@pytest.mark.parametrize('cap,exchange', [(None, 'rccl'), (40, 'rccl'), (None, 'ipc'),
+                                          (40, 'ipc')])
+def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange):
+    """cap=40: both ranks detect the same overflow and grow cap identically.
+    exchange='ipc': the rows go through the peer windows (csrc/comm.hip: IPC-mapped, in-
+    kernel stores, flags on the GPU; both ranks on cuda:0 here, over xGMI on a node)."""
     from recbole_amd.trainer.fused import FusedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     root = str(tmp_path)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap, exchange))
+             for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=600) for _ in range(2)]
