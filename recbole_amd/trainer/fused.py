@@ -183,6 +183,9 @@ class FusedBPRTrainStep(object):
     # run beside its grouping and steps). MIREC_MAIN_FIRST=0: the prep streams for it too.
     MAIN_FIRST = os.environ.get('MIREC_MAIN_FIRST', '1') != '0'
     _last_walked = None           # event after the latest issued walk (begin_epoch resets)
+    _deferred_waits = ()          # cross-stream waits on a restart chunk, issued with the next walk
+    _urgent = False               # the next chunk prepared is the one after a restart
+    _late_top_up = None           # restart chunk whose next walks follow its model launch
 
     def __init__(self, model, optimizer, train_data, chunk=None, use_graph=True,
                  adam_mode='deferred', dist=None, fused_step=None):
@@ -363,6 +366,9 @@ class FusedBPRTrainStep(object):
                     self.device, nb * Bc * T)
                 cp.alias_thr, cp.alias_idx, cp.n_alias = thr.data_ptr(), idx.data_ptr(), thr.numel()
             st = on if on is not None else self.prep_stream
+            slot.ready_on_model = on is not None
+            if on is None:
+                self._apply_deferred_waits()
             lw = self._last_walked
             if on is not None and lw is not None and not lw.query():
                 # the walk pointer and the speculative walk's workspace are sequential
@@ -374,13 +380,26 @@ class FusedBPRTrainStep(object):
             self._last_walked = slot.walked
             slot.chunk = chunk
             if on is None:
+                if self._urgent:
+                    # the chunk right after a restart: its grouping at once, on the same
+                    # stream behind its walk (no hand-off between hardware queues)
+                    self._urgent = False
+                    check(lib().mirec_prepare_chunk_group(ctypes.byref(cp), st.cuda_stream),
+                          'mirec_prepare_chunk_group')
+                    slot.ready.record(st)
+                    self.group_stream.wait_event(slot.ready)     # shared sort workspace
+                    slot.group_pending = False
+                    return
                 slot.group_pending = True      # the grouping half: _issue_groups
                 return
-            self.prep_stream.wait_event(slot.walked)     # the next walks continue the walk
             check(lib().mirec_prepare_chunk_group(ctypes.byref(cp), st.cuda_stream),
                   'mirec_prepare_chunk_group')
             slot.ready.record(st)
-            self.group_stream.wait_event(slot.ready)     # shared sort workspace
+            # the prep / group streams' waits on this chunk (the next walks continue its walk
+            # pointer; the sort workspace is shared) go in with the next walk — after the
+            # chunk's model launch, so the host's time first goes to what the GPU reaches first
+            self._deferred_waits = [(self.prep_stream, slot.walked),
+                                    (self.group_stream, slot.ready)]
             slot.group_pending = False
             return
         with torch.cuda.stream(self.prep_stream):
@@ -408,9 +427,15 @@ class FusedBPRTrainStep(object):
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
 
+    def _apply_deferred_waits(self):
+        for st, ev in self._deferred_waits:
+            st.wait_event(ev)
+        self._deferred_waits = []
+
     def _prepare_group(self, slot):
         """The grouping half of a chunk's preparation (K2 + look-ahead lists) on the
         group stream, after the chunk's walk."""
+        self._apply_deferred_waits()
         self.group_stream.wait_event(slot.walked)
         check(lib().mirec_prepare_chunk_group(ctypes.byref(slot.prep),
                                               self.group_stream.cuda_stream),
@@ -780,6 +805,7 @@ class FusedBPRTrainStep(object):
             self._capture_variants()
         self.prep_stream.wait_stream(torch.cuda.current_stream(self.device))
         self._last_walked = None               # event after the latest issued walk
+        self._deferred_waits, self._urgent, self._late_top_up = [], False, None
         self._next_chunk = 0                   # chunks whose walk (or whole prep) is issued
         self._next_group = 0                   # chunks whose grouping is issued
         self._prep_limit = (len(self._plan) if hold_prep_from is None
@@ -806,9 +832,9 @@ class FusedBPRTrainStep(object):
             k = self._next_chunk               # the first released walk starts right away:
             if self.MAIN_FIRST and not self._sharded(self._plan[k][2]):
                 # the whole preparation on the model's stream (no cross-queue hand-off
-                # before the first step); the next chunks' walks at once, behind its walk
+                # before the first step); the next chunks' walks after its model launch
                 self._issue_prep(on=torch.cuda.current_stream(self.device))
-                self._top_up_prep(k)
+                self._late_top_up = k
             else:
                 self._issue_prep()
 
@@ -840,6 +866,7 @@ class FusedBPRTrainStep(object):
         if (self.MAIN_FIRST and self._next_chunk == k and k < min(len(self._plan), self._prep_limit)
                 and not self._sharded(self._plan[k][2])):
             self._issue_prep(on=stream)        # pipeline (re)start: prepared on this stream
+            self._late_top_up = k
         while self._next_chunk <= k and self._next_chunk < min(len(self._plan),
                                                                self._prep_limit):
             self._issue_prep()
@@ -848,10 +875,15 @@ class FusedBPRTrainStep(object):
                                'call release_prep() first')
         # this chunk's grouping first (its stream waits for the walk on the GPU; issued
         # later, the host's enqueue of the next walks would delay it), then the walks of
-        # the next chunks (the same walk stream: they start as this chunk's walk ends)
+        # the next chunks (the same walk stream: they start as this chunk's walk ends) —
+        # unless this chunk was prepared on the model's stream: then they follow its model
+        # launch (run_batches), which the GPU reaches first
         self._issue_groups(k + 1)
-        self._top_up_prep(k)
-        stream.wait_event(self.slots[k % S].ready)
+        slot = self.slots[k % S]
+        if self._late_top_up != k:
+            self._top_up_prep(k)
+        if not getattr(slot, 'ready_on_model', False):
+            stream.wait_event(slot.ready)
         self._cur = k
 
     def run_batches(self, b_start, b_end):
@@ -885,6 +917,11 @@ class FusedBPRTrainStep(object):
                 if c1 == nb and flush:
                     self._flush(stream, flush)
                     self._current = True
+            if self._late_top_up == k:         # after a restart chunk's launch: the next
+                self._late_top_up = None       # walks, the first one grouped at once
+                self._urgent = True
+                self._top_up_prep(k)
+                self._urgent = False
             self._issue_groups(k + len(self.slots))   # later chunks' groupings, behind
             b = b0 + c1
             self._batches_enqueued = b

