@@ -797,7 +797,7 @@ int mirec_colsum_f32(const float* x, int64_t n, int64_t m, float* out, void* str
 /* The tail of nn.Linear's backward over a tall input (reference: torch's Linear backward
  * under SASRec's layers, layers.py:338-461): dW = sum_c P[c] (C split-K partials of n_w
  * floats, summed in c order; skipped when C == 1 and P == dW) and db = the column sum of
- * g [K, n_out] (NULL: none; rows in chunks of 512, each in row order, chunks in order) in
+ * g [K, n_out] (NULL: none; rows in chunks of 2048, each in row order, chunks in order) in
  * ONE launch. n_w and n_out multiples of 4, 16-B aligned P / dW / g. scratch: floats of
  * mirec_linear_grad_finish_scratch(K, n_out); ticket: one int32, zero before a call and
  * left zero. */

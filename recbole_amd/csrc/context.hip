@@ -298,9 +298,9 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(const ColsumJobs J) 
 // in c order; the bias rows in chunks of kLgRows, each chunk's rows in row order (8 row
 // lanes, added in lane order), the chunks in chunk order — the last block to finish a
 // chunk (agent-scope ticket; write-through partial stores drained before it, an agent
-// acquire after) adds them.
+// acquire after, then plain loads) adds them.
 constexpr int kLgThreads = 256;
-constexpr int kLgRows = 512;          // bias rows per chunk
+constexpr int kLgRows = 2048;         // bias rows per chunk
 struct LinearGradFinish {
   const float* P; int C; int64_t n4;  // partials [C, 4 n4] -> dW
   float* dW;
@@ -385,13 +385,19 @@ __global__ __launch_bounds__(kLgThreads) void linear_grad_finish_kernel(const Li
   }
   __syncthreads();
   if (!s_last) return;
+  // after the acquire: plain loads (the guide's consumer form), 8 chunks' loads in flight
   for (int j = tid; j < F.n_out; j += kLgThreads) {
-    float t = 0.f;
-    for (int c = 0; c < F.nB; ++c) {
-      auto q = (const __attribute__((address_space(1))) unsigned int*)(F.scratch + (int64_t)c * F.n_out + j);
-      const float v = __uint_as_float(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      t = c ? t + v : v;
+    const float* src = F.scratch + j;
+    float t = src[0];
+    int c = 1;
+    for (; c + 8 <= F.nB; c += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(c + u) * F.n_out];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += v[u];
     }
+    for (; c < F.nB; ++c) t += src[(int64_t)c * F.n_out];
     F.db[j] = t;
   }
 }

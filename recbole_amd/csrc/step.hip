@@ -34,6 +34,8 @@
 // behind) and applies the step. Look-ahead rows: the deferred kernel's replay of steps
 // last..s. Per element the arithmetic is adam_deferred_kernel's (adam_core.h), whatever
 // the number of elements a thread holds.
+#include <type_traits>
+
 #include "adam_core.h"
 #include "bpr_math.h"
 #include "ahead.h"
@@ -499,7 +501,13 @@ template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
 // Look-ahead rows: one element per thread over two half-row slots (whole rows in one
 // slot measured no better)
-template <typename V> struct AheadVec { using T = float; };
+#ifndef MIREC_STEP_AHEAD_WHOLE           // probe knob: 1 = whole look-ahead rows per slot
+#define MIREC_STEP_AHEAD_WHOLE 0
+#endif
+template <typename V> struct AheadVec { using T = typename std::conditional<MIREC_STEP_AHEAD_WHOLE, V, float>::type; };
+#ifndef MIREC_STEP_AHEAD_GROUP            // replay steps in flight per look-ahead slot
+#define MIREC_STEP_AHEAD_GROUP 0         // 0: 8 for half rows, 4 for whole rows
+#endif
 
 // Rows per workgroup: a row of D <= 128 is one wave, and RPB of them share a workgroup
 // (each wave works alone: wave-level synchronisation only), so the dispatcher hands out
@@ -509,6 +517,10 @@ template <typename V> struct AheadVec { using T = float; };
 #define MIREC_STEP_RPB 4
 #endif
 template <int D> struct StepRows { static constexpr int n = D <= 128 ? MIREC_STEP_RPB : 1; };
+#ifndef MIREC_STEP_SUM_LOADS
+#define MIREC_STEP_SUM_LOADS 8           // a split row's vectors loaded at once by its last
+#endif                                   // arriver (one dependent round per group)
+constexpr int kSumLoads = MIREC_STEP_SUM_LOADS;
 #ifndef MIREC_STEP_WAVES
 #define MIREC_STEP_WAVES 5               // waves per SIMD the register budget allows (6: 80
 #endif                                   // VGPRs, 28 B/lane spilled; 5: 86, no spill)
@@ -610,7 +622,8 @@ void bpr_adam_step_kernel(
     H p = reinterpret_cast<const H*>(Pr[raw & 1])[offh];
     H m = reinterpret_cast<const H*>(T_.m)[offh];
     H v = reinterpret_cast<const H*>(T_.v)[offh];
-    replay<H, true, kAheadHalves == 2 ? 8 : 4>(p, m, v, raw, st, consts, k);
+    replay<H, true, MIREC_STEP_AHEAD_GROUP ? MIREC_STEP_AHEAD_GROUP : (kAheadHalves == 2 ? 8 : 4)>(
+        p, m, v, raw, st, consts, k);
     H z;
     memset(&z, 0, sizeof(H));
     adam_vec(p, m, v, z, step_consts(consts, st), k);   // step st: zero gradient
@@ -779,12 +792,12 @@ void bpr_adam_step_kernel(
     if (!s_last) return;                             // row-uniform
     const float* __restrict__ pe = part + EPT * t;
     int c = 0;
-    for (; c + 8 <= nc; c += 8) {
-      V cv[8];
+    for (; c + kSumLoads <= nc; c += kSumLoads) {
+      V cv[kSumLoads];
 #pragma unroll
-      for (int h = 0; h < 8; ++h) part_load(pe + (int64_t)(c + h) * D, cv[h]);
+      for (int h = 0; h < kSumLoads; ++h) part_load(pe + (int64_t)(c + h) * D, cv[h]);
 #pragma unroll
-      for (int h = 0; h < 8; ++h)
+      for (int h = 0; h < kSumLoads; ++h)
 #pragma unroll
         for (int e = 0; e < EPT; ++e) Lanes<V>::at(g, e) += Lanes<V>::at(cv[h], e);
     }
@@ -964,7 +977,7 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   // segments: the shares of split rows first (their row's step waits for them), then
   // the look-ahead rows (their replays are long chains), then the touched rows
   if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
-  const int halves = d >= 128 ? 2 : 1;            // look-ahead slots per table row
+  const int halves = (d >= 128 && !MIREC_STEP_AHEAD_WHOLE) ? 2 : 1;   // look-ahead slots per row
   const int64_t rows[6] = {kSplitCap, kSplitCap,
                            L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0,
                            L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0,

@@ -21,11 +21,17 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--ramp', default=None)
+    ap.add_argument('--eager', action='store_true', help='no graphs: events around every launch')
     args = ap.parse_args()
     import bench
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     _, _, _, _, _, step = bench.build_workload(dev)
+    if args.ramp:
+        step.RAMP = tuple(int(x) for x in args.ramp.split(','))
+    if args.eager:
+        step.use_graph = False
     W, K = args.warmup, args.steps
     evs = []           # (name, event, host us)
     t_ref = [0.0]
@@ -38,11 +44,12 @@ def main():
     orig_prepare, orig_group = step._prepare, step._prepare_group
     slot_chunk = {}
 
-    def prepare(slot, chunk):
-        mark(f'walk{chunk[:2]} issue', step.prep_stream)
-        orig_prepare(slot, chunk)
+    def prepare(slot, chunk, on=None):
+        st = on if on is not None else step.prep_stream
+        mark(f'walk{chunk[:2]} issue' + (' (model stream)' if on is not None else ''), st)
+        orig_prepare(slot, chunk, on)
         slot_chunk[id(slot)] = chunk
-        mark(f'walk{chunk[:2]} done', step.prep_stream)
+        mark(f'walk{chunk[:2]} done', st)
 
     def group(slot):
         c = slot_chunk.get(id(slot), ('?', '?'))[:2]
@@ -61,6 +68,8 @@ def main():
         t_ref[0] = t0 = time.perf_counter()
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(main_s)
+        if args.eager:
+            step.kernel_events = []
         step.release_prep(upto=W + K)
         b = W
         while b < W + K:                       # chunk by chunk, marks around each launch
@@ -78,6 +87,11 @@ def main():
         print(f'rep {rep}: {el * 1e6:.1f} us = {K * step.Bg / el / 1e6:.2f} M pos/s')
         for name, e, h in evs:
             print(f'   gpu {e0.elapsed_time(e) * 1e3:8.1f}  host {h:8.1f}  {name}')
+        if args.eager:
+            for name, a, b_ in step.kernel_events:
+                print(f'   kernel {name:8s} {e0.elapsed_time(a) * 1e3:8.1f} -> '
+                      f'{e0.elapsed_time(b_) * 1e3:8.1f}  ({a.elapsed_time(b_) * 1e3:6.1f})')
+            step.kernel_events = None
         step.release_prep()
         step.end_epoch(W + K)
 

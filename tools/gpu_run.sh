@@ -105,8 +105,10 @@ for task in "$@"; do
       script=${arg%%:*}
       rest=""
       [ "$script" != "$arg" ] && rest=${arg#*:}
-      run py_$(basename $script .py) 600 python -u $script ${rest//:/ }
-      say "py $script: $(tail -3 $O/py_$(basename $script .py).log | tr '\n' ' ' | cut -c1-400)";;
+      PYN=$(( ${PYN:-0} + 1 ))
+      log=py_$(basename $script .py)_$PYN
+      run $log 600 python -u $script ${rest//:/ }
+      say "py $script: $(tail -3 $O/$log.log | tr '\n' ' ' | cut -c1-400)";;
     *)
       say "unknown task $task"; exit 2;;
   esac

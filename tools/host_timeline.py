@@ -54,6 +54,13 @@ def main():
     for name in ('_enter_chunk', '_prepare_group', '_issue_groups', '_top_up_prep', '_entry',
                  '_flush', '_finish'):
         wrap(name)
+    orig_replay = torch.cuda.CUDAGraph.replay
+
+    def replay(self):
+        mark('graph replay in')
+        orig_replay(self)
+        mark('graph replay out')
+    torch.cuda.CUDAGraph.replay = replay
     for rep in range(args.reps):
         M = step.C
         nb = step.begin_epoch(cuts=(W, W + K, W + K + M), hold_prep_from=W)
