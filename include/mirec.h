@@ -560,9 +560,9 @@ int mirec_adam_flush_rows_f32(const mirec_adam_table* tables, int32_t n_tables, 
  * grouped position) of this batch. Rows with more than 2 contributions are split: their
  * contributions are formed by several blocks of the launch, which hand the vectors over
  * through u_part / i_part (scratch, Bc / (1+T)*Bc positions x d floats) and count in on
- * u_join / i_join (2*Bc / 2*(1+T)*Bc int32: per row slot, then per look-ahead slot —
- * at d >= 128 a look-ahead row is replayed by two blocks, the second to finish marks
- * it; all ZERO before the first launch, every launch leaves them zero). The sums keep
+ * u_join / i_join (2*Bc / 2*(1+T)*Bc int32; the first half counts the arrivals per row
+ * slot, the second is spare: all ZERO before the first launch, every launch leaves them
+ * zero). The sums keep
  * the grouping order, so split rows give the same bits.
  * The step s = step_base_dev[0] + step_off reads every
  * row from buffer s & 1 (all rows the batch reads must be complete through s - 1) and
@@ -973,6 +973,13 @@ int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const int32_t* n_un
                     int64_t map_stride, int64_t map_off, int64_t S, int32_t rank,
                     int32_t* own_uniq, int32_t* own_seg, int32_t* own_n, int32_t* perm2,
                     int32_t* own_ahead, int32_t* own_nah, void* stream);
+/* Where each entry of step c's owned lists (mirec_shard_own: own / own_ahead) sits in
+ * step c+1's owned list, for c < n_batches - 1: next_t[c*per_batch + i] = that index
+ * (-1: step c+1 does not read the row), next_a[c*per_batch + a] likewise for the
+ * look-ahead list — the push lists of mirec_comm_adam_deferred_f32. */
+int mirec_shard_next(const int32_t* own, const int32_t* own_n, const int32_t* own_ahead,
+                     const int32_t* own_nah, int64_t per_batch, int64_t n_batches,
+                     int32_t* next_t, int32_t* next_a, void* stream);
 /* out[i] = idx[i] >= 0 ? U[idx[i]] : I[-idx[i]-1] (rows of d floats; d in
  * {32,64,128,256}): an owner's forward message from its two shards. */
 int mirec_shard_gather_f32(const float* U, const float* I, int32_t d, const int64_t* idx,
@@ -1012,10 +1019,28 @@ int mirec_comm_push_rows_f32(mirec_comm* comm, const float* U, const float* I,
 /* K3 on this rank's slice reading the forward region at the plan's positions (user
  * [B], pos [B], neg [times x B] message positions o*cap + j), each gradient row into
  * owner o's backward region at me*cap + j (where its perm2 reads it); per-positive
- * losses to loss_k; raises set 1. Same arithmetic as mirec_bpr_fwd_bwd_at_ids_f32. */
+ * losses to loss_k. Its blocks first wait for set 0 (no separate mirec_comm_wait); its
+ * last block raises set 1. Same arithmetic as mirec_bpr_fwd_bwd_at_ids_f32. */
 int mirec_comm_bpr_f32(mirec_comm* comm, const int64_t* user, const int64_t* pos,
                        const int64_t* neg, int64_t B, int32_t times, float gamma,
                        float grad_scale, float* loss_k, int64_t cap, void* stream);
+/* The owner's deferred Adam of a row-sharded step with both exchanges folded in (one
+ * launch; mirec_adam_deferred_f32's rows, arithmetic and bits): its blocks wait for
+ * set 1 (the readers' gradient rows: tables' `rows` = this rank's backward region);
+ * with push lists, every row of the next step (each is in this step's touched or
+ * look-ahead list) is stored, right after its update, into each reader's forward
+ * region at its message positions, and the last block raises set 0. next[2q] / [2q+1]:
+ * mirec_shard_next's next_t / next_a of table q for this step; next_seg[q] / next_dst[q]:
+ * the next step's own_seg / perm2 of table q (message positions g*cap + idx); next
+ * NULL: no push (a chunk's last step: the next chunk's first rows go by
+ * mirec_comm_push_rows_f32 after its entry catch-up). n_max: host bounds of the lists. */
+int mirec_comm_adam_deferred_f32(mirec_comm* comm, const mirec_adam_table* tables,
+                                 int32_t n_tables, const int64_t* n_max, int32_t d,
+                                 const float* step_consts_dev, const int32_t* step_base_dev,
+                                 int32_t step_off, double beta1, double beta2, double eps,
+                                 double weight_decay, const int32_t* const* next,
+                                 const int32_t* const* next_seg, const int32_t* const* next_dst,
+                                 int64_t cap, void* stream);
 /* Equal-block all-to-all of rows: send [world x wcap x d] (block g to rank g, its first
  * send_counts[g] rows, device array or NULL = all); afterwards this rank's forward
  * region (recv must be the window base, or NULL) holds block src at src * wcap.

@@ -116,6 +116,7 @@ SIGNATURES = {
                                  c_int64, _P, _P, _P, _P, _P, _P]),
     "mirec_shard_own": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P, c_int64, c_int64,
                                 c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P]),
+    "mirec_shard_next": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P]),
     "mirec_shard_gather_f32": (c_int, [_P, _P, c_int32, _P, c_int64, _P, _P]),
     "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),
@@ -234,6 +235,9 @@ SIGNATURES = {
     "mirec_comm_push_rows_f32": (c_int, [_P, _P, _P, _P, c_int64, _P]),
     "mirec_comm_bpr_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int32, c_float, c_float, _P,
                                    c_int64, _P]),
+    "mirec_comm_adam_deferred_f32": (c_int, [_P, ctypes.POINTER(AdamTable), c_int32, _P, c_int32,
+                                             _P, _P, c_int32, c_double, c_double, c_double,
+                                             c_double, _P, _P, _P, c_int64, _P]),
     "mirec_alltoallv_rows_f32": (c_int, [_P, _P, _P, _P, _P, c_int32, _P]),
     "mirec_allreduce_sum_f32": (c_int, [_P, _P, c_int64, _P]),
     "mirec_linear_grad_finish_f32": (c_int, [_P, c_int32, c_int64, _P, _P, c_int64, c_int32, _P,

@@ -99,15 +99,8 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 // takes as long as its longest chain, so one column per lane (shortest chains);
 // a launch with many rows (a data-parallel global batch) is issue-bound, so two
 // (half the per-wave overhead). The host picks by the launch's row bound.
-// RPB = 256 / (D / |V|) whole rows per block.
-//  segment 2q   (touched): row = uniq[u] of table q. Replays last..s-1 with a
-//               zero gradient, applies step s with its gradient; last = s+1.
-//  segment 2q+1 (look-ahead): row = ahead_uniq[u], rows the NEXT batch reads
-//               and this one does not touch (the caller's set difference).
-//               Replays last..s (zero gradient); last = s+1 — so the next
-//               forward pass reads rows that are complete through step s.
-// `last` is read by every thread of a row before the barrier and written
-// after it (a row of D = 256 spans two waves).
+// RPB = 256 / (D / |V|) whole rows per block. Segment 2q: table q's touched rows,
+// 2q+1: its look-ahead rows (the entry's work: adam_core.h deferred_row).
 // Block of the deferred kernel: one row when a row fills whole waves, else one
 // wave of rows. Small blocks: the launch's rows differ widely in replay length,
 // and a CU takes a new block only when a whole block's waves are free.
@@ -132,50 +125,12 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   const bool ahead = si & 1;
   const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
-  // Dependent-load chain kept to three levels: (count, row id) -> (last, p, m,
-  // v, the row's gradient contributions) -> replay + step. The block barrier
-  // that orders every thread's read of `last` before the row's write sits at
-  // the end, so no thread leaves early.
   const int n = ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
   // the grid is sized for the host's bound on the lists: blocks past the actual
   // count leave at once (block-uniform: no thread reaches the barrier below)
   if ((int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) >= n) return;
-  const int st = step_base[0] + step_off;
-  const bool valid = u < n;
-  int64_t row = 0;
-  int last = st;
-  bool idle = !valid;   // nothing to load or store: outside the list, or a look-ahead
-                        // row in the zero state (already current for every step)
-  V p, m, v, g;
-  memset(&p, 0, sizeof(V)); m = p; v = p; g = p;
-  if (valid) {
-    row = ahead ? T.ahead_uniq[u] : T.uniq[u];
-    const int64_t off = row * VPR + c;
-    const int raw = T.last[row];
-    last = raw == kZeroState ? st : raw;
-    idle = ahead && raw == kZeroState;
-    if (!idle) {
-      // parity buffers (p_alt): the row's state `last` lives in last & 1 ? p_alt : p
-      const float* src = (T.p_alt && (last & 1)) ? T.p_alt : T.p;
-      p = reinterpret_cast<const V*>(src)[off];
-      m = reinterpret_cast<const V*>(T.m)[off];
-      v = reinterpret_cast<const V*>(T.v)[off];
-      if (!ahead) g = grouped_grad<V>(T, u, VPR, c);
-    }
-  }
-  // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop);
-  // a row already complete through st (last > st: a repeated look-ahead of the
-  // same step) is left as it is
-  replay<V, (VPR >= 64)>(p, m, v, idle ? st : last, st, consts, k);
-  const bool fresh = !idle && last <= st;
-  if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
-  if (VPR > 64) __syncthreads();     // a row spans waves; else the row's lanes are one wave's
-  if (!valid || !fresh) return;
-  const int64_t off = row * VPR + c;
-  reinterpret_cast<V*>((T.p_alt && ((st + 1) & 1)) ? T.p_alt : T.p)[off] = p;
-  reinterpret_cast<V*>(T.m)[off] = m;
-  reinterpret_cast<V*>(T.v)[off] = v;
-  if (c == 0) T.last[row] = st + 1;
+  deferred_row<D, V>(T, ahead, u, n, step_base[0] + step_off, consts, k, c,
+                     [](bool, bool, int64_t, const V&) {});
 }
 
 // Bring every row up to `n_steps` applied steps (zero-gradient replays).

@@ -548,4 +548,62 @@ __device__ __forceinline__ V grouped_grad(const mirec_adam_table& T, int s, int 
   return g;
 }
 
+// One entry of the deferred schedule (adam.hip adam_deferred_kernel; comm.hip's
+// exchange form): lane c of entry u of table T's touched list (ahead = false) or
+// look-ahead list (ahead = true), n entries in the list, step st.
+//  touched:    row = uniq[u]. Replays last..st-1 with a zero gradient, applies step st
+//              with its gradient; last = st+1.
+//  look-ahead: row = ahead_uniq[u], a row the NEXT batch reads and this one does not
+//              touch. Replays last..st (zero gradient); last = st+1 — so the next
+//              forward pass reads rows that are complete through step st.
+// `last` is read by every thread of a row before the barrier and written after it (a
+// row of VPR > 64 lanes spans waves: every thread of the block calls this together).
+// done(valid, loaded, row, p): after the row's stores, p = the row's state through
+// st+1 when loaded (false: an idle zero-state row, p not read).
+template <int D, typename V, typename Done>
+__device__ __forceinline__ void deferred_row(const mirec_adam_table& T, bool ahead, int u, int n,
+                                             int st, const float* __restrict__ consts,
+                                             const AdamConsts& k, int c, Done&& done) {
+  constexpr int VPR = D / Lanes<V>::n;
+  // Dependent-load chain kept to three levels: (count, row id) -> (last, p, m, v, the
+  // row's gradient contributions) -> replay + step.
+  const bool valid = u < n;
+  int64_t row = 0;
+  int last = st;
+  bool idle = !valid;   // nothing to load or store: outside the list, or a look-ahead
+                        // row in the zero state (already current for every step)
+  V p, m, v, g;
+  memset(&p, 0, sizeof(V)); m = p; v = p; g = p;
+  if (valid) {
+    row = ahead ? T.ahead_uniq[u] : T.uniq[u];
+    const int64_t off = row * VPR + c;
+    const int raw = T.last[row];
+    last = raw == kZeroState ? st : raw;
+    idle = ahead && raw == kZeroState;
+    if (!idle) {
+      // parity buffers (p_alt): the row's state `last` lives in last & 1 ? p_alt : p
+      const float* src = (T.p_alt && (last & 1)) ? T.p_alt : T.p;
+      p = reinterpret_cast<const V*>(src)[off];
+      m = reinterpret_cast<const V*>(T.m)[off];
+      v = reinterpret_cast<const V*>(T.v)[off];
+      if (!ahead) g = grouped_grad<V>(T, u, VPR, c);
+    }
+  }
+  // the zero-gradient steps it skipped (all lanes take part: wave-uniform loop); a row
+  // already complete through st (last > st: a repeated look-ahead of the same step) is
+  // left as it is
+  replay<V, (VPR >= 64)>(p, m, v, idle ? st : last, st, consts, k);
+  const bool fresh = !idle && last <= st;
+  if (fresh) adam_vec(p, m, v, g, step_consts(consts, st), k);
+  if (VPR > 64) __syncthreads();     // a row spans waves; else the row's lanes are one wave's
+  if (valid && fresh) {
+    const int64_t off = row * VPR + c;
+    reinterpret_cast<V*>((T.p_alt && ((st + 1) & 1)) ? T.p_alt : T.p)[off] = p;
+    reinterpret_cast<V*>(T.m)[off] = m;
+    reinterpret_cast<V*>(T.v)[off] = v;
+    if (c == 0) T.last[row] = st + 1;
+  }
+  done(valid, !idle, row, p);
+}
+
 }  // namespace mirec

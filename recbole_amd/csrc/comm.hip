@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "adam_core.h"
 #include "bpr_math.h"
 
 namespace mirec {
@@ -72,6 +73,62 @@ __device__ __forceinline__ void push_done(const Peers& P, const XSig& s) {
   for (int q = 0; q < s.G; ++q)
     if (q != s.me)
       __hip_atomic_store(flag_at(P.base[q], s.flag_off, s.set, s.me), v, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The step form of a hand-off (the row-sharded step's two launches, bpr_xchg_kernel and
+// adam_xchg_kernel): every block first waits for the exchange set it consumes (its
+// flags from every peer at the set's counter + 1); the last block to finish advances
+// that counter and raises the flags of the set it produces (none: raise_cnt null).
+struct XStep {
+  int32_t* arrive;                      // launch arrival counter (device, zero between)
+  int32_t* wait_cnt;                    // counter of the consumed set (null: no wait)
+  const int32_t* raise_cnt;             // counter of the produced set (null: no flags)
+  int32_t* status;                      // -5 when a wait gave up
+  int64_t flag_off, max_polls;
+  int32_t wait_set, raise_set, G, me;
+};
+
+// All threads of the block: the flags of the consumed set from every peer, then a
+// system-scope acquire (the peers' rows in this window are visible to the block).
+__device__ __forceinline__ void xstep_wait(char* win, const XStep& x) {
+  if (!x.wait_cnt) return;
+  if (threadIdx.x < 64) {
+    const int32_t target = x.wait_cnt[0] + 1;
+    bool ok = true;
+    for (int q = threadIdx.x; q < x.G; q += 64) {
+      if (q == x.me) continue;
+      const int32_t* f = flag_at(win, x.flag_off, x.wait_set, q);
+      int64_t n = 0;
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+        if (++n > x.max_polls) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (!ok) __hip_atomic_store(x.status, -5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+// The end of a step launch: this block's stores drained; the last block advances the
+// consumed set's counter and raises the produced set's flags in every peer's window.
+__device__ __forceinline__ void xstep_end(const Peers& P, const XStep& x) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const int prev = __hip_atomic_fetch_add(x.arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (prev != (int)(gridDim.x * gridDim.y) - 1) return;
+  __hip_atomic_store(x.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (x.wait_cnt) x.wait_cnt[0] = x.wait_cnt[0] + 1;
+  if (!x.raise_cnt) return;
+  const int32_t v = x.raise_cnt[0] + 1;
+  for (int q = 0; q < x.G; ++q)
+    if (q != x.me)
+      __hip_atomic_store(flag_at(P.base[q], x.flag_off, x.raise_set, x.me), v, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -153,13 +210,14 @@ template <int D>
 __global__ __launch_bounds__(kXThreads) void bpr_xchg_kernel(
     const char* __restrict__ win, int64_t fwd_off, int64_t bwd_off, const int64_t* __restrict__ user,
     const int64_t* __restrict__ pos, const int64_t* __restrict__ neg, int64_t B, int times,
-    float gamma, float grad_scale, float* __restrict__ loss_k, int64_t cap, Peers P, XSig s) {
+    float gamma, float grad_scale, float* __restrict__ loss_k, int64_t cap, Peers P, XStep s) {
   constexpr int LPR = D / 4;
   constexpr int GPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int g = lane / LPR;
   const int l = lane - g * LPR;
   const int64_t k = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * GPW + g;
+  xstep_wait(const_cast<char*>(win), s);        // the owners' rows of this step are here
   const float* __restrict__ E = reinterpret_cast<const float*>(win + fwd_off);
   auto row_of = [&](int64_t p) -> int64_t { return p; };
   auto out_of = [&](int64_t p) -> float* {    // message position -> the owner's window row
@@ -202,7 +260,7 @@ __global__ __launch_bounds__(kXThreads) void bpr_xchg_kernel(
     reinterpret_cast<float4*>(out_of(pp))[l] = gp;
     if (l == 0 && loss_k) loss_k[k] = lsum;
   }
-  push_done(P, s);
+  xstep_end(P, s);
 }
 
 // The same n floats (n4 float4) of this rank into block `me` (stride floats apart) of
@@ -232,6 +290,72 @@ __global__ __launch_bounds__(kXThreads) void xchg_sum_kernel(const char* __restr
   float t = r[i];
   for (int q = 1; q < G; ++q) t += r[(int64_t)q * stride + i];
   buf[i] = t;
+}
+
+// Where the rows of the next step go (the owner's fold of the next forward exchange
+// into this step's optimizer launch): entry u of segment si (2q touched, 2q+1 look-ahead
+// of table q) is entry next[si][u] (-1: none) of the next step's owned list of table q,
+// whose slots' message positions are dst[q][seg[q][j] .. seg[q][j+1]) (g * cap + idx:
+// reader g's forward region, block me, row idx). next[si] null: no push.
+struct XNext {
+  const int32_t* next[2 * kMaxTables];
+  const int32_t* seg[kMaxTables];
+  const int32_t* dst[kMaxTables];
+  int64_t cap;
+};
+
+// The owner's deferred Adam of a row-sharded step (adam_core.h deferred_row: the same
+// rows, the same arithmetic, the same bits as mirec_adam_deferred_f32) with both
+// exchanges folded in: every block waits for the backward flags (the readers' gradient
+// rows in this window), and every row the NEXT step reads — each is in this launch's
+// touched or look-ahead list, current through st+1 once its entry is done — is stored
+// from registers into each reader's forward region at its message positions; the last
+// block raises the forward flags. Grid-stride over the lists (the host's grid is a
+// bound, not the count).
+template <int D, typename V>
+__global__ __launch_bounds__(kAdamThreads) void adam_xchg_kernel(
+    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
+    int step_off, AdamConsts k, XNext nx, char* win, Peers P, XStep xs) {
+  constexpr int VPR = D / Lanes<V>::n;
+  constexpr int RPB = (VPR >= kAdamThreads ? VPR : kAdamThreads) / VPR;
+  constexpr int LW = Lanes<V>::n;
+  xstep_wait(win, xs);
+  const int c = threadIdx.x % VPR;
+  const int st = step_base[0] + step_off;
+  for (int si = 0; si < tabs.n_seg; ++si) {
+    const mirec_adam_table& T = tabs.t[si >> 1];
+    const bool ahead = si & 1;
+    if (ahead && !T.ahead_uniq) continue;
+    const int n = ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
+    const int32_t* __restrict__ nxt = nx.next[si];
+    const int32_t* __restrict__ sg = nx.seg[si >> 1];
+    const int32_t* __restrict__ ds = nx.dst[si >> 1];
+    for (int base = blockIdx.x * RPB; base < n; base += gridDim.x * RPB) {   // block-uniform
+      const int u = base + threadIdx.x / VPR;
+      int e0 = 0, e1 = 0;                  // the next step's slots of this row (issued early)
+      if (nxt && u < n) {
+        const int j = nxt[u];
+        if (j >= 0) {
+          e0 = sg[j];
+          e1 = sg[j + 1];
+        }
+      }
+      deferred_row<D, V>(T, ahead, u, n, st, consts, k, c,
+                         [&](bool valid, bool loaded, int64_t row, V p) {
+        if (!valid || e0 >= e1) return;
+        if (!loaded) p = reinterpret_cast<const V*>(T.p)[row * VPR + c];   // zero-state row
+        for (int e = e0; e < e1; ++e) {
+          const int32_t q = ds[e];
+          const int g = (int)(q / nx.cap);
+          const int64_t idx = q - (int64_t)g * nx.cap;
+          float* dst = reinterpret_cast<float*>(P.base[g]) + ((int64_t)xs.me * nx.cap + idx) * D;
+          reinterpret_cast<V*>(dst)[c] = p;
+        }
+      });
+    }
+  }
+  (void)LW;
+  xstep_end(P, xs);
 }
 
 }  // namespace mirec
@@ -267,6 +391,21 @@ XSig sig_of(const mirec_comm* c, int set) {
   s.G = c->world;
   s.me = c->rank;
   return s;
+}
+// A step launch that consumes set `wait` (-1: none) and produces set `raise` (-1: none).
+XStep xstep_of(const mirec_comm* c, int wait, int raise, int64_t max_polls) {
+  XStep x;
+  x.arrive = c->ctl;
+  x.wait_cnt = wait >= 0 ? c->ctl + 1 + wait : nullptr;
+  x.raise_cnt = raise >= 0 ? c->ctl + 1 + raise : nullptr;
+  x.status = c->ctl + 1 + kFlagSets;
+  x.flag_off = flag_off(c);
+  x.max_polls = max_polls;
+  x.wait_set = wait;
+  x.raise_set = raise;
+  x.G = c->world;
+  x.me = c->rank;
+  return x;
 }
 bool connected(const mirec_comm* c) {
   for (int q = 0; q < c->world; ++q)
@@ -422,7 +561,8 @@ extern "C" int mirec_comm_push_rows_f32(mirec_comm* c, const float* U, const flo
   return launch_status("mirec_comm_push_rows_f32");
 }
 
-// K3 on the received rows (after mirec_comm_wait(0)); gradient rows to the owners.
+// K3 on the received rows (its blocks wait for the forward flags); gradient rows to the
+// owners, backward flags raised by its last block.
 extern "C" int mirec_comm_bpr_f32(mirec_comm* c, const int64_t* user, const int64_t* pos,
                                   const int64_t* neg, int64_t B, int32_t times, float gamma,
                                   float grad_scale, float* loss_k, int64_t cap, void* stream) {
@@ -436,11 +576,82 @@ extern "C" int mirec_comm_bpr_f32(mirec_comm* c, const int64_t* user, const int6
                                                             ((kXThreads / 64) * GPW));
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
-  const XSig s = sig_of(c, 1);
+  const XStep s = xstep_of(c, 0, 1, kMaxPolls);
   MIREC_XD(c->d, hipLaunchKernelGGL(bpr_xchg_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
                                     (const char*)c->window, (int64_t)0, region_bytes(c), user,
                                     pos, neg, B, times, gamma, grad_scale, loss_k, cap, P, s));
   return launch_status("mirec_comm_bpr_f32");
+}
+
+// The owner's deferred Adam of a row-sharded step with both exchanges folded in
+// (adam_xchg_kernel). tables: as mirec_adam_deferred_f32 (rows = this window's backward
+// region); next / next_seg / next_dst: XNext (per segment / per table; next NULL: no
+// push — the chunk's last step). n_max: host bounds of the lists (the grid).
+extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_table* tables,
+                                            int32_t n_tables, const int64_t* n_max, int32_t d,
+                                            const float* consts, const int32_t* step_base,
+                                            int32_t step_off, double beta1, double beta2,
+                                            double eps, double weight_decay,
+                                            const int32_t* const* next,
+                                            const int32_t* const* next_seg,
+                                            const int32_t* const* next_dst, int64_t cap,
+                                            void* stream) {
+  if (!c || !c->window || !connected(c) || !tables || n_tables < 1 || n_tables > kMaxTables ||
+      !n_max || !consts || !step_base || d != c->d || cap < 1 || cap > c->wcap ||
+      ((uintptr_t)consts & 15) != 0) {
+    set_error("mirec_comm_adam_deferred_f32: bad arguments");
+    return -1;
+  }
+  AdamTables tabs;
+  memset(&tabs, 0, sizeof(tabs));
+  tabs.n_seg = 2 * n_tables;
+  XNext nx;
+  memset(&nx, 0, sizeof(nx));
+  nx.cap = cap;
+  int64_t rows = 0;
+  for (int q = 0; q < n_tables; ++q) {
+    const mirec_adam_table& t = tables[q];
+    if (!t.p || !t.m || !t.v || !t.last || !t.uniq || !t.seg || !t.perm || !t.rows ||
+        !t.n_uniq || t.dense_grad || t.p_alt || n_max[q] < 0 ||
+        (t.ahead_uniq == nullptr) != (t.ahead_n_uniq == nullptr)) {
+      set_error("mirec_comm_adam_deferred_f32: bad table %d", q);
+      return -1;
+    }
+    tabs.t[q] = t;
+    rows += n_max[q] * (t.ahead_uniq ? 2 : 1);
+    if (next) {
+      if (!next[2 * q] || (t.ahead_uniq && !next[2 * q + 1]) || !next_seg || !next_seg[q] ||
+          !next_dst || !next_dst[q]) {
+        set_error("mirec_comm_adam_deferred_f32: table %d: incomplete push lists", q);
+        return -1;
+      }
+      nx.next[2 * q] = next[2 * q];
+      nx.next[2 * q + 1] = next[2 * q + 1];
+      nx.seg[q] = next_seg[q];
+      nx.dst[q] = next_dst[q];
+    }
+  }
+  AdamConsts k;
+  k.omb1 = (float)(1.0 - beta1);
+  k.omb1m1 = k.omb1 - 1.0f;
+  k.lerp_small = fabsf(k.omb1) < 0.5f;
+  k.b2 = (float)beta2;
+  k.omb2 = (float)(1.0 - beta2);
+  k.eps = (float)eps;
+  k.wd = (float)weight_decay;
+  const int rpb = std::max(1, kAdamThreads / d);
+  // a bound, not the count: grid-stride over the lists (the owned share of the global
+  // batch is ~1/world of the bound)
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(64, (rows / c->world + rpb - 1) / rpb),
+                                           4096);
+  hipStream_t st = (hipStream_t)stream;
+  const Peers P = peers_of(c);
+  const XStep xs = xstep_of(c, 1, next ? 0 : -1, kMaxPolls);
+  // the forward region sits at offset 0 of every window (Peers point at window starts)
+  MIREC_XD(d, hipLaunchKernelGGL((adam_xchg_kernel<D, float>), dim3((unsigned)blocks),
+                                 dim3(kAdamThreads), 0, st, tabs, consts, step_base, step_off, k,
+                                 nx, c->window, P, xs));
+  return launch_status("mirec_comm_adam_deferred_f32");
 }
 
 // rows of send [world x cap x d] (block g for rank g, its first

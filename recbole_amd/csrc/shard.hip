@@ -191,6 +191,35 @@ __global__ __launch_bounds__(kPlanThreads) void shard_own_kernel(
   }
 }
 
+// Where each entry of step c's owned lists sits in step c+1's owned list (the owner
+// folds step c+1's forward exchange into step c's optimizer launch: comm.hip
+// adam_xchg_kernel pushes a row right after its update). One workgroup per step
+// c < n_batches - 1 (the lists are sorted local row ids): next_t[c][i] = the index of
+// own[c][i] in own[c+1], -1 when step c+1 does not read it; next_a[c][a] = the index of
+// own_ahead[c][a] in own[c+1] (the look-ahead list is own[c+1] minus own[c]).
+__global__ __launch_bounds__(kPlanThreads) void shard_next_kernel(
+    const int32_t* __restrict__ own, const int32_t* __restrict__ own_n,
+    const int32_t* __restrict__ own_ah, const int32_t* __restrict__ own_nah, int64_t per_batch,
+    int32_t* __restrict__ next_t, int32_t* __restrict__ next_a) {
+  const int64_t c = blockIdx.x;
+  const int32_t* __restrict__ nx = own + (c + 1) * per_batch;
+  const int32_t nn = own_n[c + 1];
+  const int32_t* __restrict__ cur = own + c * per_batch;
+  const int32_t n = own_n[c];
+  for (int32_t i = threadIdx.x; i < n; i += kPlanThreads) {
+    const int32_t key = cur[i];
+    const int32_t j = lower_bound_i32(nx, nn, key);
+    next_t[c * per_batch + i] = (j < nn && nx[j] == key) ? j : -1;
+  }
+  const int32_t* __restrict__ ah = own_ah + c * per_batch;
+  const int32_t na = own_nah[c];
+  for (int32_t a = threadIdx.x; a < na; a += kPlanThreads) {
+    const int32_t key = ah[a];
+    const int32_t j = lower_bound_i32(nx, nn, key);
+    next_a[c * per_batch + a] = (j < nn && nx[j] == key) ? j : -1;
+  }
+}
+
 // out[i, :] = idx[i] >= 0 ? U[idx[i], :] : I[-idx[i] - 1, :]  (d/4 lanes per row,
 // 16-B vectors): the forward message of an owner, rows of its two shards.
 template <int D>
@@ -260,6 +289,20 @@ extern "C" int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const in
                      map_stride, map_off, S, rank, own_uniq, own_seg, own_n, perm2, own_ahead,
                      own_nah);
   return launch_status("mirec_shard_own");
+}
+
+extern "C" int mirec_shard_next(const int32_t* own, const int32_t* own_n, const int32_t* own_ahead,
+                                const int32_t* own_nah, int64_t per_batch, int64_t n_batches,
+                                int32_t* next_t, int32_t* next_a, void* stream) {
+  if (!own || !own_n || !own_ahead || !own_nah || !next_t || !next_a || per_batch < 1 ||
+      n_batches < 0) {
+    set_error("mirec_shard_next: bad arguments");
+    return -1;
+  }
+  if (n_batches < 2) return 0;
+  hipLaunchKernelGGL(shard_next_kernel, dim3((unsigned)(n_batches - 1)), dim3(kPlanThreads), 0,
+                     (hipStream_t)stream, own, own_n, own_ahead, own_nah, per_batch, next_t, next_a);
+  return launch_status("mirec_shard_next");
 }
 
 extern "C" int mirec_shard_gather_f32(const float* U, const float* I, int32_t d,

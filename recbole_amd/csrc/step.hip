@@ -34,8 +34,6 @@
 // behind) and applies the step. Look-ahead rows: the deferred kernel's replay of steps
 // last..s. Per element the arithmetic is adam_deferred_kernel's (adam_core.h), whatever
 // the number of elements a thread holds.
-#include <type_traits>
-
 #include "adam_core.h"
 #include "bpr_math.h"
 #include "ahead.h"
@@ -47,9 +45,7 @@ struct StepLaunch {
   const int32_t* rec[2];       // row records per touched-row slot (mirec_step_records)
   const int32_t* crec[2];      // contribution records per grouped position
   float* part[2];              // contribution vectors of split rows, per position x D
-  int32_t* join[2];            // arrivals per row slot of split rows, then per look-ahead
-                               // slot at join_ahead (zero between launches)
-  int64_t join_ahead[2];
+  int32_t* join[2];            // arrivals per row slot of split rows (zero between launches)
   int64_t block_start[7];      // segments: shares U, I, look-ahead U, I, touched U, I, end
   int32_t seg_rows[6];         // rows each segment is sized for (the buffers' bound)
 };
@@ -489,7 +485,6 @@ __device__ __forceinline__ void part_load(const float* p, float2& a) {
 }
 
 constexpr int kJoinOrder = __ATOMIC_RELAXED;
-constexpr int kHalfJoinOrder = __ATOMIC_RELAXED;
 
 // Row-state stores of K35 (plain stores; write-through stores measured no better)
 template <typename V>
@@ -499,16 +494,6 @@ __device__ __forceinline__ void state_store(V* p, const V& x) {
 
 template <int D> struct StepVec { using T = float2; };
 template <> struct StepVec<64> { using T = float; };
-// Look-ahead rows: one element per thread over two half-row slots (whole rows in one
-// slot measured no better)
-#ifndef MIREC_STEP_AHEAD_WHOLE           // probe knob: 1 = whole look-ahead rows per slot
-#define MIREC_STEP_AHEAD_WHOLE 0
-#endif
-template <typename V> struct AheadVec { using T = typename std::conditional<MIREC_STEP_AHEAD_WHOLE, V, float>::type; };
-#ifndef MIREC_STEP_AHEAD_GROUP            // replay steps in flight per look-ahead slot
-#define MIREC_STEP_AHEAD_GROUP 0         // 0: 8 for half rows, 4 for whole rows
-#endif
-
 // Rows per workgroup: a row of D <= 128 is one wave, and RPB of them share a workgroup
 // (each wave works alone: wave-level synchronisation only), so the dispatcher hands out
 // RPB times fewer workgroups (it deals ~2-3 per ns: ~10 K one-row workgroups were ~3 us
@@ -539,7 +524,6 @@ void bpr_adam_step_kernel(
   static_assert(RPB == 1 || TPB == 64, "several rows per workgroup need one wave per row");
   constexpr int LPR = D / 4;               // lanes per contribution (float4 each, K3's layout)
   constexpr int NG = TPB / LPR;            // contributions in flight per row
-  constexpr int kAheadHalves = EPT / Lanes<typename AheadVec<V>::T>::n;   // slots per look-ahead row
   __shared__ float cont_all[RPB][NG][D];
   __shared__ int s_last_all[RPB];
   // the row of this wave: wave-uniform, so the row's indices stay in scalar registers
@@ -578,9 +562,9 @@ void bpr_adam_step_kernel(
   int4 h0 = make_int4(0, 0, 0, 0), h1 = h0, ra = h0, rb = h0;
   int n;
   int64_t row;
-  if (ahead) {                             // two blocks per row when a thread holds 2
-    n = T_.ahead_n_uniq[0] * kAheadHalves;
-    row = T_.ahead_uniq[u / kAheadHalves];
+  if (ahead) {
+    n = T_.ahead_n_uniq[0];
+    row = T_.ahead_uniq[u];
   } else {
     const int32_t* __restrict__ Q;
     if (kind == 2) {
@@ -612,43 +596,24 @@ void bpr_adam_step_kernel(
 
   if (ahead) {
     // rows the next step reads and this one does not touch: replay last..st (zero
-    // gradient), as adam_deferred_kernel's look-ahead segment. The replay is a chain of
-    // dependent steps per element: with two elements per thread the row goes to two
-    // blocks of one element per thread (half the chain work per wave, eight steps'
-    // sqrt / division chains in flight); the second half to finish marks the row.
+    // gradient), as adam_deferred_kernel's look-ahead segment; whole rows, four steps'
+    // chains in flight (round 5: rows split over two half-row slots with eight in flight
+    // measured 4 % slower in the C2 driver window — more waves for the same work)
     if (raw == kZeroState || raw > st) return;    // current at every step / already done
-    using H = typename AheadVec<V>::T;
-    const int64_t offh = row * (D / Lanes<H>::n) + (u % kAheadHalves) * TPB + t;
-    H p = reinterpret_cast<const H*>(Pr[raw & 1])[offh];
-    H m = reinterpret_cast<const H*>(T_.m)[offh];
-    H v = reinterpret_cast<const H*>(T_.v)[offh];
-    replay<H, true, MIREC_STEP_AHEAD_GROUP ? MIREC_STEP_AHEAD_GROUP : (kAheadHalves == 2 ? 8 : 4)>(
-        p, m, v, raw, st, consts, k);
-    H z;
-    memset(&z, 0, sizeof(H));
+    V p = reinterpret_cast<const V*>(Pr[raw & 1])[off];
+    V m = reinterpret_cast<const V*>(T_.m)[off];
+    V v = reinterpret_cast<const V*>(T_.v)[off];
+    replay<V, true, 4>(p, m, v, raw, st, consts, k);
+    V z;
+    memset(&z, 0, sizeof(V));
     adam_vec(p, m, v, z, step_consts(consts, st), k);   // step st: zero gradient
-    MIREC_WORK(3, Lanes<H>::n * MIREC_WORK_LANES());
+    MIREC_WORK(3, EPT * MIREC_WORK_LANES());
     MIREC_WORK(5, 1);
-    state_store(reinterpret_cast<H*>(Pw) + offh, p);
-    state_store(reinterpret_cast<H*>(T_.m) + offh, m);
-    state_store(reinterpret_cast<H*>(T_.v) + offh, v);
-    if (kAheadHalves == 1) {
-      row_sync();                                  // every thread read `last`
-      if (t == 0) T_.last[row] = st + 1;
-    } else {
-      // both halves read `last` before the first one counts in (its replay used it). No
-      // data passes between the halves: the counter only elects the one that marks the
-      // row, after both have read its old mark (a relaxed add suffices: the read has
-      // returned — the replay used it — before this lane's add issues)
-      row_sync();
-      if (t == 0) {
-        int32_t* j = L.join[tb] + L.join_ahead[tb] + u / kAheadHalves;
-        if (__hip_atomic_fetch_add(j, 1, kHalfJoinOrder, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-          __hip_atomic_store(j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          T_.last[row] = st + 1;
-        }
-      }
-    }
+    state_store(reinterpret_cast<V*>(Pw) + off, p);
+    state_store(reinterpret_cast<V*>(T_.m) + off, m);
+    state_store(reinterpret_cast<V*>(T_.v) + off, v);
+    row_sync();                                    // every thread read `last`
+    if (t == 0) T_.last[row] = st + 1;
     return;
   }
 
@@ -972,15 +937,12 @@ extern "C" int mirec_bpr_adam_step_f32(const mirec_adam_table* tables,
   L.join[0] = u_join;
   L.part[1] = i_part;
   L.join[1] = i_join;
-  L.join_ahead[0] = Bc;                           // join: [row slots | look-ahead slots]
-  L.join_ahead[1] = (int64_t)(1 + T) * Bc;
   // segments: the shares of split rows first (their row's step waits for them), then
   // the look-ahead rows (their replays are long chains), then the touched rows
   if (n_max_uniq[0] == 0 && n_max_uniq[1] == 0) return 0;
-  const int halves = (d >= 128 && !MIREC_STEP_AHEAD_WHOLE) ? 2 : 1;   // look-ahead slots per row
   const int64_t rows[6] = {kSplitCap, kSplitCap,
-                           L.t[0].ahead_uniq ? halves * n_max_uniq[0] : 0,
-                           L.t[1].ahead_uniq ? halves * n_max_uniq[1] : 0,
+                           L.t[0].ahead_uniq ? n_max_uniq[0] : 0,
+                           L.t[1].ahead_uniq ? n_max_uniq[1] : 0,
                            n_max_uniq[0], n_max_uniq[1]};
   const int rpb = d <= 128 ? MIREC_STEP_RPB : 1;  // StepRows<d>
   int64_t b = 0;
