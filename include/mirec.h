@@ -997,8 +997,11 @@ int mirec_shard_gather_f32(const float* U, const float* I, int32_t d, const int6
  * -> mirec_comm_connect. Window: [fwd rows: world x wcap x d][bwd rows: same][flags];
  * an exchange with a plan cap <= wcap puts source src's block at src * cap rows.
  * Ordering: a pushing launch's last block raises the flags (system-scope release);
- * mirec_comm_wait polls this rank's flags (bounded: status -5 on a lost peer) and
- * acquires; launches after it on the stream read the window. Graph-capturable.
+ * the consuming launch's blocks poll this rank's flags (bounded: status -5 on a lost
+ * peer) and acquire. Step sets 0 / 1 alternate (each push of a set needs the other
+ * set's flags, which need the reader's consumption); the generic calls (sets 2, 3)
+ * are bracketed by a barrier (set 4) on entry and exit, so they may follow or precede
+ * a step chunk or each other on the stream. Graph-capturable. Design: DESIGN.md §7.
  * ------------------------------------------------------------------------- */
 typedef struct mirec_comm mirec_comm;
 int mirec_comm_init(int rank, int world, const void* unique_id, mirec_comm** out);
@@ -1007,9 +1010,16 @@ int mirec_comm_window(mirec_comm* comm, int64_t wcap, int32_t d, void** local, v
 int mirec_comm_connect(mirec_comm* comm, const void* handles);
 int mirec_comm_layout(const mirec_comm* comm, int64_t* fwd_off, int64_t* bwd_off,
                       int32_t** status_dev);
-int mirec_comm_status(const mirec_comm* comm, int32_t* out);
+/* The device status word (after a device synchronize), then cleared: 0, or -5 when a
+ * wait gave up on a peer since the last read. */
+int mirec_comm_status(mirec_comm* comm, int32_t* out);
 int mirec_comm_destroy(mirec_comm* comm);
-/* set 0: forward rows, 1: backward rows (2, 3: the generic calls below) */
+/* MIREC_COMM_PREWAIT: a one-block wait kernel ahead of each step launch (ranks that
+ * share a device: the launch's blocks must not spin on CUs the peer needs). */
+#define MIREC_COMM_PREWAIT 1
+int mirec_comm_config(mirec_comm* comm, int32_t flags);
+/* A stand-alone wait of set 0 / 1 that advances the set's counter (diagnostics; the
+ * step launches below wait by themselves — do not combine the two). */
 int mirec_comm_wait(mirec_comm* comm, int32_t set, void* stream);
 /* The row-sharded step's forward exchange: entry g*cap + j of idx (mirec_shard_plan's
  * fwd_rows: >= 0 a row of U, < 0 row -id-1 of I) into rank g's forward region at
@@ -1041,14 +1051,15 @@ int mirec_comm_adam_deferred_f32(mirec_comm* comm, const mirec_adam_table* table
                                  double weight_decay, const int32_t* const* next,
                                  const int32_t* const* next_seg, const int32_t* const* next_dst,
                                  int64_t cap, void* stream);
-/* Equal-block all-to-all of rows: send [world x wcap x d] (block g to rank g, its first
- * send_counts[g] rows, device array or NULL = all); afterwards this rank's forward
- * region (recv must be the window base, or NULL) holds block src at src * wcap.
- * Includes the wait. */
+/* All-to-all of ragged row blocks: send [world x wcap x d] (block g to rank g, its first
+ * send_counts[g] rows; device int64 [world], NULL = all wcap); afterwards recv [world x
+ * wcap x d] (the caller's buffer) holds block src at src * wcap rows, its first
+ * recv_counts[src] rows (device int64 [world], written when non-NULL) as rank src sent
+ * them; rows past a count are left as they were. Entry / exit barriers included. */
 int mirec_alltoallv_rows_f32(mirec_comm* comm, const float* send, const int64_t* send_counts,
-                             float* recv, const int64_t* recv_counts, int32_t d, void* stream);
+                             float* recv, int64_t* recv_counts, int32_t d, void* stream);
 /* buf[n] <- the sum of every rank's buf, added in rank order (the same bits on every
- * rank); n <= wcap*d, a multiple of 4, buf 16-B aligned. Includes the wait. */
+ * rank); n <= wcap*d, a multiple of 4, buf 16-B aligned. Entry / exit barriers included. */
 int mirec_allreduce_sum_f32(mirec_comm* comm, float* buf, int64_t n, void* stream);
 
 #ifdef __cplusplus

@@ -232,6 +232,7 @@ SIGNATURES = {
     "mirec_comm_destroy": (c_int, [_P]),
     "mirec_comm_status": (c_int, [_P, _P]),
     "mirec_comm_wait": (c_int, [_P, c_int32, _P]),
+    "mirec_comm_config": (c_int, [_P, c_int32]),
     "mirec_comm_push_rows_f32": (c_int, [_P, _P, _P, _P, c_int64, _P]),
     "mirec_comm_bpr_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int32, c_float, c_float, _P,
                                    c_int64, _P]),

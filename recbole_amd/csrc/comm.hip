@@ -42,7 +42,10 @@
 namespace mirec {
 
 constexpr int kMaxPeers = 64;
-constexpr int kFlagSets = 4;            // 0 forward rows, 1 backward rows, 2-3 generic
+// 0 forward rows, 1 backward rows (the step), 2 alltoallv rows, 3 allreduce blocks, 4 the
+// generic calls' entry / exit barriers
+constexpr int kFlagSets = 5;
+constexpr int kBarrierSet = 4;
 constexpr int kXThreads = 256;
 
 struct Peers {
@@ -132,11 +135,14 @@ __device__ __forceinline__ void xstep_end(const Peers& P, const XStep& x) {
                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Wait for flag[set][src] >= cnt + 1 of every src != me, then cnt += 1. One block;
-// a bounded spin (status -5 and an early exit instead of a hang).
+// Wait for flag[set][src] >= cnt + 1 of every src != me, then cnt += 1 (advance; without
+// it the wait only makes sure the flags are there: the pre-wait of a step launch, whose
+// own blocks wait again at once and advance the counter). One block; a bounded spin
+// (status -5 and an early exit instead of a hang).
 __global__ __launch_bounds__(64) void xchg_wait_kernel(char* win, int64_t flag_off, int set,
                                                        int G, int me, int32_t* cnt,
-                                                       int32_t* status, int64_t max_polls) {
+                                                       int32_t* status, int64_t max_polls,
+                                                       int advance) {
   const int32_t target = cnt[0] + 1;
   bool ok = true;
   for (int q = threadIdx.x; q < G; q += 64) {
@@ -154,7 +160,19 @@ __global__ __launch_bounds__(64) void xchg_wait_kernel(char* win, int64_t flag_o
   if (!ok) __hip_atomic_store(status, -5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   __syncthreads();
-  if (threadIdx.x == 0) cnt[0] = target;
+  if (threadIdx.x == 0 && advance) cnt[0] = target;
+}
+
+// One lane: flag[set][me] = cnt[set] + 1 in every peer's window (system-scope release
+// after this stream's earlier work): a barrier's arrival, waited for by xchg_wait_kernel.
+__global__ __launch_bounds__(64) void xchg_raise_kernel(Peers P, int64_t flag_off, int set, int G,
+                                                        int me, const int32_t* cnt) {
+  if (threadIdx.x != 0) return;
+  const int32_t v = cnt[0] + 1;
+  for (int q = 0; q < G; ++q)
+    if (q != me)
+      __hip_atomic_store(flag_at(P.base[q], flag_off, set, me), v, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The owner's forward message rows into the readers' windows: entry q = g * cap + j
@@ -179,25 +197,50 @@ __global__ __launch_bounds__(kXThreads) void xchg_push_rows_kernel(
   push_done(P, s);
 }
 
-// Rows of this rank's send buffer [G x cap x D] (block g for rank g) into the readers'
-// windows (block `me`): the generic equal-block all-to-all, and the backward rows.
+// Rows of this rank's send buffer [G x wcap x D] (block g for rank g, its first counts[g]
+// rows; counts NULL: all) into the readers' windows (block `me` of the forward region),
+// and each count into the reader's count slot `me` (published by the same flag).
 template <int D>
 __global__ __launch_bounds__(kXThreads) void xchg_push_blocks_kernel(
-    const float* __restrict__ send, const int64_t* __restrict__ counts, int64_t cap,
-    int64_t wcap, int64_t region_off, Peers P, XSig s) {
+    const float* __restrict__ send, const int64_t* __restrict__ counts, int64_t wcap,
+    int64_t count_off, Peers P, XSig s) {
   constexpr int LPR = D / 4;
   const int64_t q = ((int64_t)blockIdx.x * kXThreads + threadIdx.x) / LPR;
   const int c = threadIdx.x % LPR;
-  if (q < (int64_t)s.G * cap) {
-    const int g = (int)(q / cap);
-    const int64_t j = q - (int64_t)g * cap;
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)s.G) {
+    const int g = threadIdx.x;
+    const int64_t n = counts ? counts[g] : wcap;
+    reinterpret_cast<int64_t*>(P.base[g] + count_off)[s.me] = n < 0 ? 0 : (n > wcap ? wcap : n);
+  }
+  if (q < (int64_t)s.G * wcap) {
+    const int g = (int)(q / wcap);
+    const int64_t j = q - (int64_t)g * wcap;
     if (!counts || j < counts[g]) {
       const float4 v = reinterpret_cast<const float4*>(send + q * D)[c];
-      float* dst = reinterpret_cast<float*>(P.base[g] + region_off) + ((int64_t)s.me * wcap + j) * D;
+      float* dst = reinterpret_cast<float*>(P.base[g]) + ((int64_t)s.me * wcap + j) * D;
       reinterpret_cast<float4*>(dst)[c] = v;
     }
   }
   push_done(P, s);
+}
+
+// After the wait: every source's block of the forward region (its first count rows) into
+// the caller's recv [G x wcap x D] at the same place; the counts into recv_counts.
+template <int D>
+__global__ __launch_bounds__(kXThreads) void xchg_copy_out_kernel(
+    const char* __restrict__ win, int64_t wcap, int64_t count_off, int G, float* __restrict__ recv,
+    int64_t* __restrict__ recv_counts) {
+  constexpr int LPR = D / 4;
+  const int64_t q = ((int64_t)blockIdx.x * kXThreads + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  const int64_t* cnt = reinterpret_cast<const int64_t*>(win + count_off);
+  if (recv_counts && blockIdx.x == 0 && threadIdx.x < (unsigned)G) recv_counts[threadIdx.x] = cnt[threadIdx.x];
+  if (q >= (int64_t)G * wcap) return;
+  const int g = (int)(q / wcap);
+  const int64_t j = q - (int64_t)g * wcap;
+  if (j < cnt[g])
+    reinterpret_cast<float4*>(recv + q * D)[c] =
+        reinterpret_cast<const float4*>(reinterpret_cast<const float*>(win) + q * D)[c];
 }
 
 // K3 of this rank's slice on the received rows, its gradient rows straight into the
@@ -371,11 +414,16 @@ struct mirec_comm {
   char* peers[kMaxPeers];
   bool opened[kMaxPeers];
   int32_t* ctl;                         // device: [arrive | cnt[kFlagSets] | status]
+  int prewait;                          // MIREC_COMM_PREWAIT (mirec_comm_config)
 };
 
 namespace {
 int64_t region_bytes(const mirec_comm* c) { return (int64_t)c->world * c->wcap * c->d * 4; }
 int64_t flag_off(const mirec_comm* c) { return 2 * region_bytes(c); }
+// the alltoallv row counts: kMaxPeers int64 after the flags
+int64_t count_off(const mirec_comm* c) {
+  return flag_off(c) + kFlagSets * kMaxPeers * (int64_t)sizeof(int32_t);
+}
 Peers peers_of(const mirec_comm* c) {
   Peers P;
   memset(&P, 0, sizeof(P));
@@ -445,7 +493,7 @@ extern "C" int mirec_comm_window(mirec_comm* c, int64_t wcap, int32_t d, void** 
   }
   c->wcap = wcap;
   c->d = d;
-  c->window_bytes = (size_t)flag_off(c) + kFlagSets * kMaxPeers * sizeof(int32_t);
+  c->window_bytes = (size_t)count_off(c) + kMaxPeers * sizeof(int64_t);
   hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->window), c->window_bytes,
                                        hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->window, 0, c->window_bytes);
@@ -494,15 +542,33 @@ extern "C" int mirec_comm_layout(const mirec_comm* c, int64_t* fwd_off, int64_t*
   return 0;
 }
 
-// The status word to the host (synchronous: after the stream's work): 0, or -5 when a
-// wait gave up on a peer.
-extern "C" int mirec_comm_status(const mirec_comm* c, int32_t* out) {
+// The status word to the host (synchronous: after the device's work), then cleared: 0,
+// or -5 when a wait gave up on a peer since the last read.
+extern "C" int mirec_comm_status(mirec_comm* c, int32_t* out) {
   if (!c || !out) {
     set_error("mirec_comm_status: bad arguments");
     return -1;
   }
-  const hipError_t e = hipMemcpy(out, c->ctl + 1 + kFlagSets, sizeof(int32_t), hipMemcpyDeviceToHost);
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess)
+    e = hipMemcpy(out, c->ctl + 1 + kFlagSets, sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && *out != 0) e = hipMemset(c->ctl + 1 + kFlagSets, 0, sizeof(int32_t));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   return e == hipSuccess ? 0 : hip_status(e, "mirec_comm_status");
+}
+
+// flags: MIREC_COMM_PREWAIT (1) — each step launch (mirec_comm_bpr_f32,
+// mirec_comm_adam_deferred_f32) is preceded by a one-block wait for its flags, so its
+// own blocks never spin while a rank sharing this device needs the compute units to
+// raise them (ranks on one GPU; on a node of one rank per GPU the in-kernel waits alone
+// save the launch).
+extern "C" int mirec_comm_config(mirec_comm* c, int32_t flags) {
+  if (!c || (flags & ~1)) {
+    set_error("mirec_comm_config: bad arguments");
+    return -1;
+  }
+  c->prewait = flags & 1;
+  return 0;
 }
 
 extern "C" int mirec_comm_destroy(mirec_comm* c) {
@@ -519,10 +585,20 @@ extern "C" int mirec_comm_destroy(mirec_comm* c) {
 namespace {
 constexpr int64_t kMaxPolls = 1ll << 24;   // seconds of polling: a lost peer ends as status -5
 
-int wait_set(mirec_comm* c, int set, hipStream_t st, const char* what) {
+int wait_set(mirec_comm* c, int set, hipStream_t st, const char* what, int advance = 1) {
   hipLaunchKernelGGL(xchg_wait_kernel, dim3(1), dim3(64), 0, st, c->window, flag_off(c), set,
-                     c->world, c->rank, c->ctl + 1 + set, c->ctl + 1 + kFlagSets, kMaxPolls);
+                     c->world, c->rank, c->ctl + 1 + set, c->ctl + 1 + kFlagSets, kMaxPolls,
+                     advance);
   return launch_status(what);
+}
+
+// Every rank's stream has reached this point (its earlier launches, which read its own
+// window, are done) before any rank's stream goes on: the generic calls' entry and exit.
+int barrier(mirec_comm* c, hipStream_t st, const char* what) {
+  hipLaunchKernelGGL(xchg_raise_kernel, dim3(1), dim3(64), 0, st, peers_of(c), flag_off(c),
+                     kBarrierSet, c->world, c->rank, (const int32_t*)(c->ctl + 1 + kBarrierSet));
+  const int rc = launch_status(what);
+  return rc ? rc : wait_set(c, kBarrierSet, st, what);
 }
 }  // namespace
 
@@ -577,6 +653,10 @@ extern "C" int mirec_comm_bpr_f32(mirec_comm* c, const int64_t* user, const int6
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
   const XStep s = xstep_of(c, 0, 1, kMaxPolls);
+  if (c->prewait) {
+    const int rc = wait_set(c, 0, st, "mirec_comm_bpr_f32", 0);
+    if (rc) return rc;
+  }
   MIREC_XD(c->d, hipLaunchKernelGGL(bpr_xchg_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
                                     (const char*)c->window, (int64_t)0, region_bytes(c), user,
                                     pos, neg, B, times, gamma, grad_scale, loss_k, cap, P, s));
@@ -647,6 +727,10 @@ extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_tabl
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
   const XStep xs = xstep_of(c, 1, next ? 0 : -1, kMaxPolls);
+  if (c->prewait) {
+    const int rc = wait_set(c, 1, st, "mirec_comm_adam_deferred_f32", 0);
+    if (rc) return rc;
+  }
   // the forward region sits at offset 0 of every window (Peers point at window starts)
   MIREC_XD(d, hipLaunchKernelGGL((adam_xchg_kernel<D, float>), dim3((unsigned)blocks),
                                  dim3(kAdamThreads), 0, st, tabs, consts, step_base, step_off, k,
@@ -654,18 +738,20 @@ extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_tabl
   return launch_status("mirec_comm_adam_deferred_f32");
 }
 
-// rows of send [world x cap x d] (block g for rank g, its first
-// send_counts[g] rows; counts on the device, NULL: all cap) into every rank's window;
-// after the call recv (= the forward region of this rank's window, block src at
-// src * wcap rows) holds what every rank sent here. recv_counts: unused (the window
-// layout fixes them; kept for the signature), may be NULL. Stream-ordered; generic set 2.
+// rows of send [world x wcap x d] (block g for rank g, its first
+// send_counts[g] rows; counts on the device, NULL: all wcap) to every rank; afterwards
+// recv [world x wcap x d] (the caller's buffer, not the window) holds block src at
+// src * wcap — its first recv_counts[src] rows (device, written when non-NULL) — as
+// rank src sent them. Stream-ordered: an entry barrier (every peer's earlier work on its
+// window is done), the pushes (set 2), the wait, the copy out, an exit barrier (every
+// peer has copied out before anyone's next exchange writes its window).
 extern "C" int mirec_alltoallv_rows_f32(mirec_comm* c, const float* send,
                                         const int64_t* send_counts, float* recv,
-                                        const int64_t* recv_counts, int32_t d, void* stream) {
-  (void)recv_counts;
-  if (!c || !c->window || !connected(c) || !send || d != c->d ||
-      (recv && recv != reinterpret_cast<float*>(c->window))) {
-    set_error("mirec_alltoallv_rows_f32: bad arguments (recv must be the window or NULL)");
+                                        int64_t* recv_counts, int32_t d, void* stream) {
+  if (!c || !c->window || !connected(c) || !send || !recv || d != c->d ||
+      (reinterpret_cast<const char*>(recv) < c->window + c->window_bytes &&
+       reinterpret_cast<const char*>(recv) + region_bytes(c) > c->window)) {
+    set_error("mirec_alltoallv_rows_f32: bad arguments (recv: the caller's buffer, d = the window's)");
     return -1;
   }
   const int64_t n = (int64_t)c->world * c->wcap;
@@ -673,15 +759,24 @@ extern "C" int mirec_alltoallv_rows_f32(mirec_comm* c, const float* send,
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
   const XSig s = sig_of(c, 2);
+  int rc = barrier(c, st, "mirec_alltoallv_rows_f32");
+  if (rc) return rc;
   MIREC_XD(d, hipLaunchKernelGGL(xchg_push_blocks_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
-                                 send, send_counts, c->wcap, c->wcap, (int64_t)0, P, s));
-  const int rc = launch_status("mirec_alltoallv_rows_f32");
-  return rc ? rc : wait_set(c, 2, st, "mirec_alltoallv_rows_f32");
+                                 send, send_counts, c->wcap, count_off(c), P, s));
+  rc = launch_status("mirec_alltoallv_rows_f32");
+  if (!rc) rc = wait_set(c, 2, st, "mirec_alltoallv_rows_f32");
+  if (rc) return rc;
+  MIREC_XD(d, hipLaunchKernelGGL(xchg_copy_out_kernel<D>, dim3(blocks), dim3(kXThreads), 0, st,
+                                 (const char*)c->window, c->wcap, count_off(c), c->world, recv,
+                                 recv_counts));
+  rc = launch_status("mirec_alltoallv_rows_f32");
+  return rc ? rc : barrier(c, st, "mirec_alltoallv_rows_f32");
 }
 
 // buf[n] <- the sum over ranks of every rank's buf, added in rank order
-// (bit-identical on every rank). n <= the window's region (world x wcap x d floats
-// split into world blocks of wcap x d). Generic set 3, backward region as staging.
+// (bit-identical on every rank). n <= wcap x d, a multiple of 4, buf 16-B aligned. Entry
+// barrier, every rank's buf into block `me` of every window's backward region (set 3),
+// the wait, the sum, exit barrier.
 extern "C" int mirec_allreduce_sum_f32(mirec_comm* c, float* buf, int64_t n, void* stream) {
   if (!c || !c->window || !connected(c) || !buf || n < 0 || n > c->wcap * c->d ||
       ((uintptr_t)buf % 16) != 0 || n % 4) {
@@ -692,18 +787,18 @@ extern "C" int mirec_allreduce_sum_f32(mirec_comm* c, float* buf, int64_t n, voi
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
   const XSig s = sig_of(c, 3);
-  // every rank's buffer into block `me` of every window's backward region, seen as
-  // [world x (wcap x d)] floats
   const int64_t stride = c->wcap * c->d;
   const unsigned blocks = (unsigned)(((int64_t)c->world * (n / 4) + kXThreads - 1) / kXThreads);
+  int rc = barrier(c, st, "mirec_allreduce_sum_f32");
+  if (rc) return rc;
   hipLaunchKernelGGL(xchg_push_bcast_kernel, dim3(blocks), dim3(kXThreads), 0, st, buf, n / 4,
                      stride, region_bytes(c), P, s);
-  int rc = launch_status("mirec_allreduce_sum_f32");
-  if (rc) return rc;
-  rc = wait_set(c, 3, st, "mirec_allreduce_sum_f32");
+  rc = launch_status("mirec_allreduce_sum_f32");
+  if (!rc) rc = wait_set(c, 3, st, "mirec_allreduce_sum_f32");
   if (rc) return rc;
   hipLaunchKernelGGL(xchg_sum_kernel, dim3((unsigned)((n + kXThreads - 1) / kXThreads)),
                      dim3(kXThreads), 0, st, (const char*)c->window, region_bytes(c), stride,
                      c->world, n, buf);
-  return launch_status("mirec_allreduce_sum_f32");
+  rc = launch_status("mirec_allreduce_sum_f32");
+  return rc ? rc : barrier(c, st, "mirec_allreduce_sum_f32");
 }

@@ -18,6 +18,16 @@ import torch
 from recbole_amd._native import NativeError, check, lib
 
 
+def _device_id(device):
+    """A physical identity of the device (its UUID; the PCI location as a fallback)."""
+    p = torch.cuda.get_device_properties(device)
+    u = getattr(p, 'uuid', None)
+    if u is not None:
+        return str(u)
+    return f"{getattr(p, 'pci_domain_id', 0)}:{getattr(p, 'pci_bus_id', 0)}:" \
+           f"{getattr(p, 'pci_device_id', 0)}"
+
+
 class PeerWindows(object):
 
     def __init__(self, group, wcap, d, device):
@@ -45,6 +55,13 @@ class PeerWindows(object):
         allh = ctypes.create_string_buffer(b''.join(handles), hb * self.world)
         with torch.cuda.device(device):
             check(L.mirec_comm_connect(self._comm, allh), 'mirec_comm_connect')
+        # ranks sharing a device (tests on one GPU): a one-block wait ahead of each step
+        # launch, so the launch's blocks never spin on compute units a peer needs
+        ids = [None] * self.world
+        tdist.all_gather_object(ids, _device_id(device), group=group)
+        self.shared_device = ids.count(ids[self.rank]) > 1
+        check(L.mirec_comm_config(self._comm, 1 if self.shared_device else 0),
+              'mirec_comm_config')
         fo, bo = ctypes.c_int64(), ctypes.c_int64()
         status = ctypes.c_void_p()
         check(L.mirec_comm_layout(self._comm, ctypes.byref(fo), ctypes.byref(bo),
@@ -59,7 +76,8 @@ class PeerWindows(object):
         return self._comm
 
     def status(self):
-        """0, or -5 when a wait gave up on a peer (a host read after the device's work)."""
+        """0, or -5 when a wait gave up on a peer since the last read (a host read after
+        the device's work; the library clears the word)."""
         torch.cuda.synchronize(self.device)
         out = ctypes.c_int32(0)
         check(lib().mirec_comm_status(self._comm, ctypes.byref(out)), 'mirec_comm_status')

@@ -1060,6 +1060,11 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                 setattr(sl, f'perm2_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_ah', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_nah', torch.zeros(C, dtype=torch.int32, device=dev))
+                if self.win is not None:     # the owner's push lists (mirec_shard_next)
+                    setattr(sl, f'next_{tag}_t', torch.empty(C * per, dtype=torch.int32,
+                                                             device=dev))
+                    setattr(sl, f'next_{tag}_a', torch.empty(C * per, dtype=torch.int32,
+                                                             device=dev))
         self._alloc_exchange()
         self._n_max = (ctypes.c_int64 * 2)(min(Bg, self.SU), min(KI, self.SI))
         self._fill_tables()
@@ -1182,6 +1187,11 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                                     g_(f'own_{tag}_n'), g_(f'perm2_{tag}'),
                                     g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), st),
                   'mirec_shard_own')
+            if self.win is not None:
+                check(L.mirec_shard_next(g_(f'own_{tag}'), g_(f'own_{tag}_n'),
+                                         g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), per, nb,
+                                         g_(f'next_{tag}_t'), g_(f'next_{tag}_a'), st),
+                      'mirec_shard_next')
         # epoch backstop: overflow flag (min: -4 < 0) and the largest message (max)
         torch.minimum(self.status[:1], slot.plan_status[:1], out=self.status[:1])
         torch.maximum(self.status[1:], slot.plan_status[1:], out=self.status[1:])
@@ -1253,22 +1263,22 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         return max(0, min(self.B, Bc - self.rank * self.B))
 
     def _step_ipc(self, slot, c, Bc, stream):
-        """The two exchanges of a step through the peer windows (csrc/comm.hip): the
-        owner's gather stores its rows into the readers' windows, K3 reads them there and
-        stores each gradient row into its owner's window; two flag waits on the GPU."""
-        T, B, M = self.times, self.B, self.G * self.cap
+        """The forward half of a step through the peer windows (csrc/comm.hip). The chunk's
+        first step pushes its rows with a gather launch (after the entry catch-up); later
+        steps' rows were pushed by the step before's optimizer launch (_adam_ipc). K3's
+        blocks wait for the owners' flags on the GPU (no separate wait launch), read the
+        rows in the window and store each gradient row into its owner's window."""
+        T, B = self.times, self.B
         L = lib()
         st = stream.cuda_stream
         n = self._n_local(Bc)
         w = self.win.comm
-
-        def push():
-            check(L.mirec_comm_push_rows_f32(w, self.shU[0].data_ptr(), self.shI[0].data_ptr(),
-                                             slot.fwd_rows.data_ptr() + 8 * c * M, self.cap, st),
-                  'mirec_comm_push_rows_f32')
-        self._record('gather', stream, push)
-        self._record('exchange', stream, lambda: check(L.mirec_comm_wait(w, 0, st),
-                                                       'mirec_comm_wait'))
+        if c == 0:
+            def push():
+                check(L.mirec_comm_push_rows_f32(w, self.shU[0].data_ptr(),
+                                                 self.shI[0].data_ptr(), slot.fwd_rows.data_ptr(),
+                                                 self.cap, st), 'mirec_comm_push_rows_f32')
+            self._record('gather', stream, push)
         loss_p = self.loss_mine.data_ptr() + 4 * c * B
         pos_p = slot.pos.data_ptr() + 8 * c * (2 + T) * B
 
@@ -1277,8 +1287,30 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                                        self._grad_scale(Bc), loss_p, self.cap, st),
                   'mirec_comm_bpr_f32')
         self._record('bpr', stream, bpr)
-        self._record('exchange_bwd', stream, lambda: check(L.mirec_comm_wait(w, 1, st),
-                                                           'mirec_comm_wait'))
+
+    def _adam_ipc(self, slot, c, Bc, stream, step_off, ahead):
+        """The owner's deferred Adam with the backward wait and, unless c is the chunk's
+        last step, the next step's forward push folded in (mirec_comm_adam_deferred_f32):
+        every row step c+1 reads is in this launch's touched or look-ahead list, and goes
+        from registers to its readers' windows right after its update."""
+        KI = (1 + self.times) * Bc
+        t = self._tables
+        nxt = seg = dst = None
+        if ahead:
+            g_ = lambda n, off: getattr(slot, n).data_ptr() + 4 * off
+            nxt = (ctypes.c_void_p * 4)(g_('next_u_t', c * Bc), g_('next_u_a', c * Bc),
+                                        g_('next_i_t', c * KI), g_('next_i_a', c * KI))
+            seg = (ctypes.c_void_p * 2)(g_('own_u_seg', (c + 1) * (Bc + 1)),
+                                        g_('own_i_seg', (c + 1) * (KI + 1)))
+            dst = (ctypes.c_void_p * 2)(g_('perm2_u', (c + 1) * Bc), g_('perm2_i', (c + 1) * KI))
+        st = stream.cuda_stream
+
+        def adam():
+            check(lib().mirec_comm_adam_deferred_f32(
+                self.win.comm, t, 2, self._n_max, self.d, self.consts.data_ptr(),
+                self.step_idx.data_ptr(), step_off, *self._adam_args, nxt, seg, dst, self.cap, st),
+                'mirec_comm_adam_deferred_f32')
+        self._record('adam', stream, adam)
 
     def _step(self, slot, c, Bc, stream, step_off, ahead):
         T, d, G, B, M = self.times, self.d, self.G, self.B, self.G * self.cap
@@ -1302,11 +1334,14 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             else:
                 t[q].ahead_uniq = t[q].ahead_n_uniq = None
 
-        def adam():
-            check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
-                                            self.step_idx.data_ptr(), step_off,
-                                            *self._adam_args, st), 'mirec_adam_deferred_f32')
-        self._record('adam', stream, adam)
+        if self.win is not None:
+            self._adam_ipc(slot, c, Bc, stream, step_off, ahead)
+        else:
+            def adam():
+                check(L.mirec_adam_deferred_f32(t, 2, self._n_max, d, self.consts.data_ptr(),
+                                                self.step_idx.data_ptr(), step_off,
+                                                *self._adam_args, st), 'mirec_adam_deferred_f32')
+            self._record('adam', stream, adam)
         if self.kernel_events is not None:
             self.kernel_uniq.append(torch.stack([slot.own_u_n[c], slot.own_i_n[c]]))
 
@@ -1363,7 +1398,7 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
 
     def end_epoch(self, n_done=None):
         losses = super().end_epoch(n_done)
-        if self.win is not None and self.win.status() == -5:
+        if self.win is not None and self.win.status() != 0:
             raise RuntimeError('row exchange: a wait for a peer\'s flags timed out (a rank '
                                'stopped or fell out of step)')
         if int(self.status[0].item()) == -4:                 # backstop: _enter_chunk re-plans
