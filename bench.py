@@ -338,7 +338,46 @@ def roofline(step, events, uniq, d, M, W=None, K=None):
         adam.update({'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
                      'bytes_formula': '6 * (n_users + n_items) * d * 4 per step'})
+    if work is not None:
+        # K35 is a memory-latency kernel (two dependent load levels per row, ~1.3 row waves
+        # per wave slot): its binding resource is HBM, so the headline roofline is the HBM
+        # one — the bytes it must move per launch (touched + look-ahead rows' p, m, v read
+        # and written, plus the BPR partner rows it gathers) over its per-launch time. The
+        # VALU view stays as a secondary field.
+        pl = adam['k35_per_launch']
+        by = pl['algorithmic_bytes'] + pl['gathered_bytes']
+        t_step = kernels_us['step'] * 1e-6
+        gbs = by / t_step / 1e9
+        rp_us, rp_src = rocprof_avg_us(per_k)
+        hbm = {'kernel': f'K35 bpr_adam_step_kernel<{d}> (BPR fwd/bwd + touched-row Adam + '
+                         'look-ahead, one launch per step)',
+               'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+               'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': pl['pmc_bytes_per_launch'],
+               'traffic_source': pl['pmc_source'],
+               'bytes_per_launch': int(by),
+               'bytes_formula': '(touched + look-ahead rows) x (p, m, v) x d x 4 B read and '
+                                'written + the gathered BPR partner rows (counter run %s)' % wsrc,
+               'avg_launch_us': kernels_us['step'], 'avg_launch_source': 'HIP events in bench',
+               'rocprof_avg_us': rp_us, 'rocprof_source': rp_src,
+               'frac_at_rocprof_avg': (round(by / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                                       if rp_us else None),
+               'valu': adam}
+        return hbm, bpr, kernels_us
     return adam, bpr, kernels_us
+
+
+def rocprof_avg_us(substr):
+    """Average duration (µs) of the kernel whose name contains `substr` in the newest
+    committed driver-window rocprofv3 --stats summary (profiles/r*_c2_driver_kernel_stats.csv),
+    or (None, None)."""
+    import csv
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_c2_driver_kernel_stats.csv')))[::-1]:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if substr in row.get('Name', ''):
+                    return round(float(row['AverageNs']) / 1e3, 2), os.path.basename(path)
+    return None, None
 
 
 def gather_throughput(step, d, neg, B=65536, reps=20, big_rows=2_000_000):
@@ -587,7 +626,7 @@ def main():
     assert all(np.isfinite(losses)), 'non-finite loss'
     roof, roof_bpr, kernels_us = roofline(step, events, uniq, d, M, W, K)
     mine = {'rank': rank, 'timed_s': round(local_elapsed, 6), 'kernels_us': kernels_us,
-            'k5_us_per_step': roof['us_per_step'],
+            'k5_us_per_step': roof.get('us_per_step', roof.get('valu', {}).get('us_per_step')),
             'table_rows': int(getattr(step, 'SU', step.nU) + getattr(step, 'SI', step.nI))}
     per_rank = [mine]
     if dist:
