@@ -100,7 +100,7 @@ def write_c2_inter(path, u, i, seed=2020):
 
 def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='deferred',
                    dist=None, chunk=None, sharded=False, alias=False, fused_step=None,
-                   source='file', shape=None):
+                   source='file', shape=None, exchange=None):
     """C2 through the drop-in path. source='file' (default): the synthetic interactions
     are written as an atomic file (MIREC_BENCH_DATA, default /tmp/mirec_bench; reused
     when present) and built by create_dataset -> data_preparation, the reference's
@@ -153,7 +153,8 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
     model = BPR(config, train).to(dev)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
     if sharded:
-        step = ShardedBPRTrainStep(model, opt, train, adam_mode=adam_mode, dist=dist, chunk=chunk)
+        step = ShardedBPRTrainStep(model, opt, train, adam_mode=adam_mode, dist=dist, chunk=chunk,
+                                   exchange=exchange)
     else:
         step = FusedBPRTrainStep(model, opt, train, adam_mode=adam_mode, dist=dist, chunk=chunk,
                                  fused_step=fused_step)
@@ -518,6 +519,10 @@ def main():
     # multi-GPU table layout: row-sharded (default) or replicated;
     # 'sharded' with --gpus 1 runs the sharded protocol on one rank (diagnostic)
     ap.add_argument('--dp-mode', default=None, choices=['sharded', 'replicated'])
+    # the sharded step's row exchanges: RCCL all-to-alls (default) or the IPC peer windows
+    # (csrc/comm.hip); with --gpus 1 and no torchrun environment a 1-rank process group is
+    # made in-process (so rocprofv3 can trace it: no launcher in between)
+    ap.add_argument('--exchange', default=None, choices=['rccl', 'ipc'])
     # negative sampler: the bit-exact walk (default, the headline) or the alias-table
     # fast mode (labelled NON-PARITY: i.i.d. draws of the same distribution)
     ap.add_argument('--sampler', default='walk', choices=['walk', 'alias'])
@@ -536,6 +541,13 @@ def main():
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         sys.exit(_spawn_ranks(args.gpus))
+    if args.exchange and args.dp_mode == 'sharded' and 'WORLD_SIZE' not in os.environ:
+        import socket
+        with socket.socket() as s_:
+            s_.bind(('127.0.0.1', 0))
+            port = s_.getsockname()[1]
+        os.environ.update(WORLD_SIZE='1', RANK='0', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+                          MASTER_PORT=str(port))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -560,7 +572,7 @@ def main():
         dev, d=d, neg=neg, batch_rows=args.batch_rows, adam_mode=args.adam_mode, chunk=args.chunk,
         dist=tdist.group.WORLD if dist else None, sharded=dp_mode == 'sharded',
         alias=args.sampler == 'alias', fused_step=False if args.no_fused_step else None,
-        source='memory' if args.in_memory else 'file')
+        source='memory' if args.in_memory else 'file', exchange=args.exchange)
     if args.ramp:
         step.RAMP = tuple(int(x) for x in args.ramp.split(','))
     if args.flush_every:
@@ -655,9 +667,11 @@ def main():
                    'global_batch': step.Bg, 'per_gpu_batch': step.B, 'train_interactions': int(
                        train.dataset.inter_num), 'parallelism': {
                            'single': 'single',
-                           'sharded': f'dp{world} x row-sharded tables (cyclic ownership; 2 RCCL '
-                                      f'all-to-alls of rows per step, cap {getattr(step, "cap", 0)} '
-                                      f'rows per rank pair)',
+                           'sharded': f'dp{world} x row-sharded tables (cyclic ownership; ' + (
+                               'rows through the IPC peer windows: owner push + K3 + owner Adam'
+                               if getattr(step, 'exchange', 'rccl') == 'ipc' else
+                               '2 RCCL all-to-alls of rows per step') +
+                               f', cap {getattr(step, "cap", 0)} rows per rank pair)',
                            'replicated': f'dp{world} (replicated tables, RCCL all-gather of '
                                          f'per-row loss coefficients)'}[dp_mode],
                    'exchange_graph': bool(step.use_graph),

@@ -16,13 +16,21 @@
 // cap (<= wcap) as the block stride, so a region holds block `src` (the rows rank src
 // sent) at src * cap — the layout of the equal-block all-to-all it replaces.
 //
-// Hand-off (release / acquire at SYSTEM scope, the C++ memory model's own form: the
-// producers run on other GPUs): every block of a pushing launch drains its stores
-// (s_waitcnt vmcnt(0) in each wave), meets, and one lane adds to the launch's arrival
-// counter with a system-scope acq_rel add; the block whose add is last stores the
-// exchange's sequence number into flag[set][me] of every peer with a system-scope
-// release store. The waiting side polls its own flags with system-scope loads, then a
-// system-scope acquire; the kernels after it (stream order) read the window.
+// Hand-off. Everything a peer reads is in the windows, and the windows (rows and flags)
+// are UNCACHED memory: a store to them is not held in any L2 and is visible once it is
+// acknowledged (s_waitcnt vmcnt(0)), and a load of them is served from memory. The
+// memory model's system-scope release (buffer_wbl2 + waitcnt) and acquire (buffer_inv)
+// add L2 write-back / invalidation for CACHED data only — here that is pure cost: with
+// one such release + acquire per block, a 3,072-block owner-Adam launch took 104 µs
+// against 15.6 µs for the same rows without them (profiles/r06_ipc_adam_probe.txt).
+// So: every block of a pushing launch drains its stores (s_waitcnt vmcnt(0) in each
+// wave), meets, and one lane adds to the launch's arrival counter (a relaxed agent-scope
+// add: an L2 atomic, coherent across the XCDs); the block whose add is last stores the
+// exchange's sequence number into flag[set][me] of every peer (a relaxed system-scope
+// store to uncached memory). The waiting side polls its own flags with system-scope
+// loads and then reads the window (uncached) — a workgroup-scope acquire keeps the
+// compiler from hoisting the window loads above the poll. Build with
+// -DMIREC_COMM_FORMAL_FENCES for the memory model's own system-scope forms.
 //
 // Sequence numbers: each exchange set keeps a device counter per rank (cnt); a push
 // raises flags to cnt + 1 and the wait for it sets cnt = cnt + 1 — every rank runs the
@@ -47,13 +55,20 @@ constexpr int kMaxPeers = 64;
 constexpr int kFlagSets = 5;
 constexpr int kBarrierSet = 4;
 constexpr int kXThreads = 256;
+#ifdef MIREC_COMM_FORMAL_FENCES
+constexpr int kArriveOrder = __ATOMIC_ACQ_REL, kFlagOrder = __ATOMIC_RELEASE;
+constexpr int kArriveScope = __HIP_MEMORY_SCOPE_SYSTEM;
+#else
+constexpr int kArriveOrder = __ATOMIC_RELAXED, kFlagOrder = __ATOMIC_RELAXED;
+constexpr int kArriveScope = __HIP_MEMORY_SCOPE_AGENT;
+#endif
 
 struct Peers {
   char* base[kMaxPeers];                // every rank's window in this process
 };
 
 struct XSig {                           // the flag raised at the end of a pushing launch
-  int32_t* arrive;                      // launch arrival counter (device, zero between)
+  int32_t* arrive;                      // arrival counters (kArriveInts, zero between)
   const int32_t* cnt;                   // this exchange set's counter (read)
   int64_t flag_off;                     // byte offset of flag set 0 in a window
   int32_t set, G, me;
@@ -63,19 +78,44 @@ __device__ __forceinline__ int32_t* flag_at(char* win, int64_t flag_off, int set
   return reinterpret_cast<int32_t*>(win + flag_off) + set * kMaxPeers + src;
 }
 
+// Arrival of a launch's blocks in two levels (lane 0 of each block; true for the block
+// that arrives last): block b counts into group b % kArriveGroups (its own 64-B line),
+// the block completing a group into the top counter. A launch of a few thousand blocks
+// on one counter serialises that many L2 atomics on one address (the owner-Adam launch:
+// ~30 µs of its 47); here no address takes more than ~50. Counters are left zero.
+constexpr int kArriveGroups = 64, kArriveStride = 16;   // int32s: one 64-B line each
+constexpr int kArriveInts = (1 + kArriveGroups) * kArriveStride;
+
+__device__ __forceinline__ bool arrive_last(int32_t* arrive) {
+#ifdef MIREC_COMM_PROBE_NO_ARRIVE   // timing probe only (one rank: nothing waits on the flags)
+  return false;
+#endif
+  const int nb = (int)(gridDim.x * gridDim.y);
+  const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int g = b % kArriveGroups;
+  const int gsz = (nb - g + kArriveGroups - 1) / kArriveGroups;
+  if (gsz > 1) {
+    int32_t* cg = arrive + (1 + g) * kArriveStride;
+    if (__hip_atomic_fetch_add(cg, 1, kArriveOrder, kArriveScope) != gsz - 1) return false;
+    __hip_atomic_store(cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int ng = nb < kArriveGroups ? nb : kArriveGroups;
+  if (__hip_atomic_fetch_add(arrive, 1, kArriveOrder, kArriveScope) != ng - 1) return false;
+  __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // the end of a pushing launch: this block's stores drained and published; the last
 // block raises the flags
 __device__ __forceinline__ void push_done(const Peers& P, const XSig& s) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const int prev = __hip_atomic_fetch_add(s.arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (prev != (int)(gridDim.x * gridDim.y) - 1) return;
-  __hip_atomic_store(s.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!arrive_last(s.arrive)) return;
   const int32_t v = s.cnt[0] + 1;
   for (int q = 0; q < s.G; ++q)
     if (q != s.me)
-      __hip_atomic_store(flag_at(P.base[q], s.flag_off, s.set, s.me), v, __ATOMIC_RELEASE,
+      __hip_atomic_store(flag_at(P.base[q], s.flag_off, s.set, s.me), v, kFlagOrder,
                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -84,7 +124,7 @@ __device__ __forceinline__ void push_done(const Peers& P, const XSig& s) {
 // flags from every peer at the set's counter + 1); the last block to finish advances
 // that counter and raises the flags of the set it produces (none: raise_cnt null).
 struct XStep {
-  int32_t* arrive;                      // launch arrival counter (device, zero between)
+  int32_t* arrive;                      // arrival counters (kArriveInts, zero between)
   int32_t* wait_cnt;                    // counter of the consumed set (null: no wait)
   const int32_t* raise_cnt;             // counter of the produced set (null: no flags)
   int32_t* status;                      // -5 when a wait gave up
@@ -112,9 +152,12 @@ __device__ __forceinline__ void xstep_wait(char* win, const XStep& x) {
       }
     }
     if (!ok) __hip_atomic_store(x.status, -5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef MIREC_COMM_FORMAL_FENCES
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
   }
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // The end of a step launch: this block's stores drained; the last block advances the
@@ -123,15 +166,13 @@ __device__ __forceinline__ void xstep_end(const Peers& P, const XStep& x) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const int prev = __hip_atomic_fetch_add(x.arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (prev != (int)(gridDim.x * gridDim.y) - 1) return;
-  __hip_atomic_store(x.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!arrive_last(x.arrive)) return;
   if (x.wait_cnt) x.wait_cnt[0] = x.wait_cnt[0] + 1;
   if (!x.raise_cnt) return;
   const int32_t v = x.raise_cnt[0] + 1;
   for (int q = 0; q < x.G; ++q)
     if (q != x.me)
-      __hip_atomic_store(flag_at(P.base[q], x.flag_off, x.raise_set, x.me), v, __ATOMIC_RELEASE,
+      __hip_atomic_store(flag_at(P.base[q], x.flag_off, x.raise_set, x.me), v, kFlagOrder,
                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -353,51 +394,50 @@ struct XNext {
 // rows in this window), and every row the NEXT step reads — each is in this launch's
 // touched or look-ahead list, current through st+1 once its entry is done — is stored
 // from registers into each reader's forward region at its message positions; the last
-// block raises the forward flags. Grid-stride over the lists (the host's grid is a
-// bound, not the count).
+// block raises the forward flags. The blocks map onto the segments as in
+// adam_deferred_kernel (the host's block_start: each segment's rows on blocks of their
+// own, sized by the host's bound; blocks past a segment's count do no row work but
+// still arrive). A grid-stride form, where the first blocks walked all four segments
+// one after the other, took 6 µs more per launch (profiles/r06_ipc_adam_probe.txt).
 template <int D, typename V>
 __global__ __launch_bounds__(kAdamThreads) void adam_xchg_kernel(
     const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
     int step_off, AdamConsts k, XNext nx, char* win, Peers P, XStep xs) {
   constexpr int VPR = D / Lanes<V>::n;
   constexpr int RPB = (VPR >= kAdamThreads ? VPR : kAdamThreads) / VPR;
-  constexpr int LW = Lanes<V>::n;
-  xstep_wait(win, xs);
+  const int si = segment_of(tabs, blockIdx.x);
+  const mirec_adam_table& T = tabs.t[si >> 1];
+  const bool ahead = si & 1;
+  const int base = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB);
+  const int n = (ahead && !T.ahead_uniq) ? 0 : ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
+  const int32_t* __restrict__ nxt = nx.next[si];
+  const int32_t* __restrict__ sg = nx.seg[si >> 1];
+  const int32_t* __restrict__ ds = nx.dst[si >> 1];
+  const int u = base + threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
-  const int st = step_base[0] + step_off;
-  for (int si = 0; si < tabs.n_seg; ++si) {
-    const mirec_adam_table& T = tabs.t[si >> 1];
-    const bool ahead = si & 1;
-    if (ahead && !T.ahead_uniq) continue;
-    const int n = ahead ? T.ahead_n_uniq[0] : T.n_uniq[0];
-    const int32_t* __restrict__ nxt = nx.next[si];
-    const int32_t* __restrict__ sg = nx.seg[si >> 1];
-    const int32_t* __restrict__ ds = nx.dst[si >> 1];
-    for (int base = blockIdx.x * RPB; base < n; base += gridDim.x * RPB) {   // block-uniform
-      const int u = base + threadIdx.x / VPR;
-      int e0 = 0, e1 = 0;                  // the next step's slots of this row (issued early)
-      if (nxt && u < n) {
-        const int j = nxt[u];
-        if (j >= 0) {
-          e0 = sg[j];
-          e1 = sg[j + 1];
-        }
-      }
-      deferred_row<D, V>(T, ahead, u, n, st, consts, k, c,
-                         [&](bool valid, bool loaded, int64_t row, V p) {
-        if (!valid || e0 >= e1) return;
-        if (!loaded) p = reinterpret_cast<const V*>(T.p)[row * VPR + c];   // zero-state row
-        for (int e = e0; e < e1; ++e) {
-          const int32_t q = ds[e];
-          const int g = (int)(q / nx.cap);
-          const int64_t idx = q - (int64_t)g * nx.cap;
-          float* dst = reinterpret_cast<float*>(P.base[g]) + ((int64_t)xs.me * nx.cap + idx) * D;
-          reinterpret_cast<V*>(dst)[c] = p;
-        }
-      });
+  int e0 = 0, e1 = 0;                      // the next step's slots of this row (issued early)
+  if (nxt && u < n) {
+    const int j = nxt[u];
+    if (j >= 0) {
+      e0 = sg[j];
+      e1 = sg[j + 1];
     }
   }
-  (void)LW;
+  if (base < n) {                          // block-uniform; idle blocks only arrive
+    xstep_wait(win, xs);
+    deferred_row<D, V>(T, ahead, u, n, step_base[0] + step_off, consts, k, c,
+                       [&](bool valid, bool loaded, int64_t row, V p) {
+      if (!valid || e0 >= e1) return;
+      if (!loaded) p = reinterpret_cast<const V*>(T.p)[row * VPR + c];   // zero-state row
+      for (int e = e0; e < e1; ++e) {
+        const int32_t q = ds[e];
+        const int g = (int)(q / nx.cap);
+        const int64_t idx = q - (int64_t)g * nx.cap;
+        float* dst = reinterpret_cast<float*>(P.base[g]) + ((int64_t)xs.me * nx.cap + idx) * D;
+        reinterpret_cast<V*>(dst)[c] = p;
+      }
+    });
+  }
   xstep_end(P, xs);
 }
 
@@ -413,7 +453,8 @@ struct mirec_comm {
   int32_t d;
   char* peers[kMaxPeers];
   bool opened[kMaxPeers];
-  int32_t* ctl;                         // device: [arrive | cnt[kFlagSets] | status]
+  int32_t* ctl;                         // device: [unused | cnt[kFlagSets] | status]
+  int32_t* arrive;                      // device: the launches' arrival counters
   int prewait;                          // MIREC_COMM_PREWAIT (mirec_comm_config)
 };
 
@@ -432,7 +473,7 @@ Peers peers_of(const mirec_comm* c) {
 }
 XSig sig_of(const mirec_comm* c, int set) {
   XSig s;
-  s.arrive = c->ctl;
+  s.arrive = c->arrive;
   s.cnt = c->ctl + 1 + set;
   s.flag_off = flag_off(c);
   s.set = set;
@@ -443,7 +484,7 @@ XSig sig_of(const mirec_comm* c, int set) {
 // A step launch that consumes set `wait` (-1: none) and produces set `raise` (-1: none).
 XStep xstep_of(const mirec_comm* c, int wait, int raise, int64_t max_polls) {
   XStep x;
-  x.arrive = c->ctl;
+  x.arrive = c->arrive;
   x.wait_cnt = wait >= 0 ? c->ctl + 1 + wait : nullptr;
   x.raise_cnt = raise >= 0 ? c->ctl + 1 + raise : nullptr;
   x.status = c->ctl + 1 + kFlagSets;
@@ -475,7 +516,12 @@ extern "C" int mirec_comm_init(int rank, int world, const void* unique_id, mirec
   c->world = world;
   hipError_t e = hipMalloc(&c->ctl, (2 + kFlagSets) * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(c->ctl, 0, (2 + kFlagSets) * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc(&c->arrive, kArriveInts * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemset(c->arrive, 0, kArriveInts * sizeof(int32_t));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
+    if (c->ctl) (void)hipFree(c->ctl);
+    if (c->arrive) (void)hipFree(c->arrive);
     delete c;
     return hip_status(e, "mirec_comm_init");
   }
@@ -578,6 +624,7 @@ extern "C" int mirec_comm_destroy(mirec_comm* c) {
     if (c->opened[q]) (void)hipIpcCloseMemHandle(c->peers[q]);
   if (c->window) (void)hipFree(c->window);
   if (c->ctl) (void)hipFree(c->ctl);
+  if (c->arrive) (void)hipFree(c->arrive);
   delete c;
   return 0;
 }
@@ -685,10 +732,11 @@ extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_tabl
   AdamTables tabs;
   memset(&tabs, 0, sizeof(tabs));
   tabs.n_seg = 2 * n_tables;
+  const int rpb = std::max(1, kAdamThreads / d);
+  int64_t blocks = 0;
   XNext nx;
   memset(&nx, 0, sizeof(nx));
   nx.cap = cap;
-  int64_t rows = 0;
   for (int q = 0; q < n_tables; ++q) {
     const mirec_adam_table& t = tables[q];
     if (!t.p || !t.m || !t.v || !t.last || !t.uniq || !t.seg || !t.perm || !t.rows ||
@@ -698,7 +746,11 @@ extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_tabl
       return -1;
     }
     tabs.t[q] = t;
-    rows += n_max[q] * (t.ahead_uniq ? 2 : 1);
+    const int64_t nb = (n_max[q] + rpb - 1) / rpb;     // segment 2q, then 2q + 1
+    tabs.block_start[2 * q] = blocks;
+    blocks += nb;
+    tabs.block_start[2 * q + 1] = blocks;
+    if (t.ahead_uniq) blocks += nb;
     if (next) {
       if (!next[2 * q] || (t.ahead_uniq && !next[2 * q + 1]) || !next_seg || !next_seg[q] ||
           !next_dst || !next_dst[q]) {
@@ -719,11 +771,8 @@ extern "C" int mirec_comm_adam_deferred_f32(mirec_comm* c, const mirec_adam_tabl
   k.omb2 = (float)(1.0 - beta2);
   k.eps = (float)eps;
   k.wd = (float)weight_decay;
-  const int rpb = std::max(1, kAdamThreads / d);
-  // a bound, not the count: grid-stride over the lists (the owned share of the global
-  // batch is ~1/world of the bound)
-  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(64, (rows / c->world + rpb - 1) / rpb),
-                                           4096);
+  for (int q = tabs.n_seg; q <= 2 * kMaxTables; ++q) tabs.block_start[q] = blocks;
+  if (blocks == 0) blocks = 1;             // still one arrival: the flags are raised
   hipStream_t st = (hipStream_t)stream;
   const Peers P = peers_of(c);
   const XStep xs = xstep_of(c, 1, next ? 0 : -1, kMaxPolls);

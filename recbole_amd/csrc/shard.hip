@@ -155,7 +155,9 @@ __device__ __forceinline__ int32_t lower_bound_i32(const int32_t* __restrict__ a
   return lo;
 }
 
-// One workgroup per batch: rank r's sub-range [lo, hi) of the sorted (keyed) uniq
+// Workgroups (batch, tile) — tile y of gridDim.y strides the batch's entries, so a chunk
+// of a few large batches still spreads over the chip (one workgroup per batch took
+// 48 µs for 16 batches of 20 K item slots): rank r's sub-range [lo, hi) of the sorted (keyed) uniq
 // list -> local row ids, its segment offsets, and the contributions of those
 // segments remapped to their positions in the backward receive buffer; the same
 // for the look-ahead list.
@@ -177,23 +179,31 @@ __global__ __launch_bounds__(kPlanThreads) void shard_own_kernel(
   int32_t* __restrict__ ou = own_uniq + c * per_batch;
   int32_t* __restrict__ os = own_seg + c * (per_batch + 1);
   int32_t* __restrict__ p2 = perm2 + c * per_batch;
-  for (int32_t j = lo + threadIdx.x; j < hi; j += kPlanThreads) ou[j - lo] = (int32_t)(uq[j] - kb);
-  for (int32_t j = lo + threadIdx.x; j <= hi; j += kPlanThreads) os[j - lo] = sg[j];
-  for (int32_t p = sg[lo] + threadIdx.x; p < sg[hi]; p += kPlanThreads) p2[p] = m2[pm[p]];
-  if (threadIdx.x == 0) own_n[c] = hi - lo;
+  const int32_t t0 = (int32_t)(blockIdx.y * kPlanThreads + threadIdx.x);
+  const int32_t ts = (int32_t)(gridDim.y * kPlanThreads);
+  for (int32_t j = lo + t0; j < hi; j += ts) ou[j - lo] = (int32_t)(uq[j] - kb);
+  for (int32_t j = lo + t0; j <= hi; j += ts) os[j - lo] = sg[j];
+  for (int32_t p = sg[lo] + t0; p < sg[hi]; p += ts) p2[p] = m2[pm[p]];
+  if (t0 == 0) own_n[c] = hi - lo;
   if (ahead) {
     const int32_t* __restrict__ ah = ahead + c * per_batch;
     const int32_t na = n_ahead[c];
     const int32_t alo = lower_bound_i32(ah, na, kb), ahi = lower_bound_i32(ah, na, ke);
     int32_t* __restrict__ oa = own_ahead + c * per_batch;
-    for (int32_t j = alo + threadIdx.x; j < ahi; j += kPlanThreads) oa[j - alo] = (int32_t)(ah[j] - kb);
-    if (threadIdx.x == 0) own_nah[c] = ahi - alo;
+    for (int32_t j = alo + t0; j < ahi; j += ts) oa[j - alo] = (int32_t)(ah[j] - kb);
+    if (t0 == 0) own_nah[c] = ahi - alo;
   }
+}
+
+// tiles per batch of the (batch, tile) grids: ~4 entries per lane
+inline unsigned plan_tiles(int64_t per_batch) {
+  const int64_t t = (per_batch + 4 * kPlanThreads - 1) / (4 * kPlanThreads);
+  return (unsigned)(t < 1 ? 1 : t > 64 ? 64 : t);
 }
 
 // Where each entry of step c's owned lists sits in step c+1's owned list (the owner
 // folds step c+1's forward exchange into step c's optimizer launch: comm.hip
-// adam_xchg_kernel pushes a row right after its update). One workgroup per step
+// adam_xchg_kernel pushes a row right after its update). Workgroups (step, tile) for
 // c < n_batches - 1 (the lists are sorted local row ids): next_t[c][i] = the index of
 // own[c][i] in own[c+1], -1 when step c+1 does not read it; next_a[c][a] = the index of
 // own_ahead[c][a] in own[c+1] (the look-ahead list is own[c+1] minus own[c]).
@@ -206,14 +216,16 @@ __global__ __launch_bounds__(kPlanThreads) void shard_next_kernel(
   const int32_t nn = own_n[c + 1];
   const int32_t* __restrict__ cur = own + c * per_batch;
   const int32_t n = own_n[c];
-  for (int32_t i = threadIdx.x; i < n; i += kPlanThreads) {
+  const int32_t t0 = (int32_t)(blockIdx.y * kPlanThreads + threadIdx.x);
+  const int32_t ts = (int32_t)(gridDim.y * kPlanThreads);
+  for (int32_t i = t0; i < n; i += ts) {
     const int32_t key = cur[i];
     const int32_t j = lower_bound_i32(nx, nn, key);
     next_t[c * per_batch + i] = (j < nn && nx[j] == key) ? j : -1;
   }
   const int32_t* __restrict__ ah = own_ah + c * per_batch;
   const int32_t na = own_nah[c];
-  for (int32_t a = threadIdx.x; a < na; a += kPlanThreads) {
+  for (int32_t a = t0; a < na; a += ts) {
     const int32_t key = ah[a];
     const int32_t j = lower_bound_i32(nx, nn, key);
     next_a[c * per_batch + a] = (j < nn && nx[j] == key) ? j : -1;
@@ -284,7 +296,8 @@ extern "C" int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const in
     return -1;
   }
   if (n_batches == 0) return 0;
-  hipLaunchKernelGGL(shard_own_kernel, dim3((unsigned)n_batches), dim3(kPlanThreads), 0,
+  hipLaunchKernelGGL(shard_own_kernel, dim3((unsigned)n_batches, plan_tiles(per_batch)),
+                     dim3(kPlanThreads), 0,
                      (hipStream_t)stream, uniq, seg, n_uniq, perm, per_batch, ahead, n_ahead, map2,
                      map_stride, map_off, S, rank, own_uniq, own_seg, own_n, perm2, own_ahead,
                      own_nah);
@@ -300,7 +313,8 @@ extern "C" int mirec_shard_next(const int32_t* own, const int32_t* own_n, const 
     return -1;
   }
   if (n_batches < 2) return 0;
-  hipLaunchKernelGGL(shard_next_kernel, dim3((unsigned)(n_batches - 1)), dim3(kPlanThreads), 0,
+  hipLaunchKernelGGL(shard_next_kernel, dim3((unsigned)(n_batches - 1), plan_tiles(per_batch)),
+                     dim3(kPlanThreads), 0,
                      (hipStream_t)stream, own, own_n, own_ahead, own_nah, per_batch, next_t, next_a);
   return launch_status("mirec_shard_next");
 }
