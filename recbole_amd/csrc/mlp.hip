@@ -27,6 +27,8 @@
 // advances it, so captured steps (HIP graph replays) draw new masks every step.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace mirec {
 
 constexpr int kMlpRows = 16;       // rows per forward / data-grad block
@@ -755,8 +757,18 @@ static size_t wide_fwd_shm(const mirec_mlp& a) {
   const int ld = (a.dims[0] + 15) / 16 * 16 + 4;
   return (size_t)kMlpRows * ld * sizeof(float) + 2 * 64 * sizeof(floatx4);
 }
+// The wide layer-0 forward is OFF by default: with layers 1.. behind it in a second launch
+// it measured 37.5 µs for the C4 forward against 31.0 µs for the one fused launch
+// (profiles/r04_models.json vs round 5's models run). MIREC_MLP_WIDE_FWD=1 turns it on.
+static bool wide_fwd_on() {
+  static const bool on = [] {
+    const char* e = getenv("MIREC_MLP_WIDE_FWD");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 static bool wide_fwd_ok(const mirec_mlp& a) {
-  return a.n_layers >= 2 && a.dims[0] >= kWideMin && a.xs[1] != nullptr &&
+  return wide_fwd_on() && a.n_layers >= 2 && a.dims[0] >= kWideMin && a.xs[1] != nullptr &&
          wide_fwd_shm(a) <= 65536;
 }
 // the wide backward's plan (WidePlan) and wave tiles; false: the one-block-per-16-rows path

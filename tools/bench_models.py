@@ -262,9 +262,12 @@ def bench_c4(dev, steps, warmup, scale=1.0, B=2048, d=16, n_batches=16):
                          f'the 20 + 200 of SURVEY.md 8d: a CPU step moves the 2.1 GB tables '
                          f'several times (~1 s), and the run-to-run spread (cv) is reported'}
     fwd_k = ('mlp_l0_fwd_kernel', 'mlp_fwd_kernel')
-    k10 = {'kernel': 'mlp_l0_fwd_kernel + mlp_fwd_kernel (K10 forward: the wide layer 0 over '
-                     'the whole chip, then layers 1.. + deep_predict_layer; dropout, ReLU; '
-                     'one event pair around both launches)', 'bound': 'mfma',
+    wide = os.environ.get('MIREC_MLP_WIDE_FWD') == '1'       # csrc/mlp.hip wide_fwd_on
+    k10 = {'kernel': ('mlp_l0_fwd_kernel + mlp_fwd_kernel (K10 forward: the wide layer 0 over '
+                      'the whole chip, then layers 1.. + deep_predict_layer; dropout, ReLU; '
+                      'one event pair around both launches)') if wide else
+                     ('mlp_fwd_kernel (K10 forward: every layer + deep_predict_layer in one '
+                      'launch, one 16-row block per CU; dropout, ReLU)'), 'bound': 'mfma',
            'achieved': round(mlp_flops / (mf_us * 1e-6) / 1e12, 2),
            'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
            'frac': round(mlp_flops / (mf_us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
