@@ -91,7 +91,7 @@ def write_c2_inter(path, u, i, seed=2020):
     ts = (789652009 + np.sort(rng.integers(0, 600_000_000, len(u)))).astype(np.float64)
     tb = pa.table({'u': u, 'i': i, 'r': rating, 't': ts})
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    tmp = path + '.part'
+    tmp = f'{path}.part{os.getpid()}'          # one writer's temporary: rename is atomic
     with open(tmp, 'wb') as f:
         f.write(b'user_id:token\titem_id:token\trating:float\ttimestamp:float\n')
         pacsv.write_csv(tb, f, pacsv.WriteOptions(include_header=False, delimiter='\t'))
@@ -127,13 +127,18 @@ def build_workload(dev, d=128, neg=4, batch_rows=2048, seed=2020, adam_mode='def
           'neg_sampling_alias': alias,
           'load_col': {'inter': ['user_id', 'item_id', 'rating', 'timestamp']}}
     t = time.perf_counter()
-    if source == 'memory' or not os.path.exists(path):
+    # ranks of a job share the node's file: rank 0 writes it, the others wait at a barrier
+    # (every rank writing the same temporary raced: one rename found it gone)
+    writer = dist is None or torch.distributed.get_rank(dist) == 0
+    if source == 'memory' or (writer and not os.path.exists(path)):
         u, i, nU, nI = make_c2(seed) if shape is None else make_c2(seed, *shape)
         info['generate_s'] = round(time.perf_counter() - t, 2)
         if source == 'file':
             t = time.perf_counter()
             write_c2_inter(path, u, i, seed)
             info['write_s'] = round(time.perf_counter() - t, 2)
+    if source == 'file' and dist is not None:
+        torch.distributed.barrier(group=dist)
     if source == 'file':
         info['file'] = path
         info['file_mb'] = round(os.path.getsize(path) / 2 ** 20, 1)
@@ -556,10 +561,18 @@ def main():
     # a process group also at one rank when asked for the sharded protocol under
     # torchrun (exercises the RCCL path on a 1-GPU box)
     dist = world > 1 or (args.dp_mode == 'sharded' and 'WORLD_SIZE' in os.environ)
+    # rehearsal of the multi-rank flow on a one-GPU box (diagnostic, never the driver's
+    # run): every rank on cuda:0 and a gloo group (RCCL refuses two ranks on one device)
+    one_dev = os.environ.get('MIREC_BENCH_ONE_DEVICE') == '1'
+    if one_dev:
+        local = 0
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if one_dev:
+            tdist.init_process_group('gloo')
+        else:
+            tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
