@@ -973,6 +973,27 @@ int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const int32_t* n_un
                     int64_t map_stride, int64_t map_off, int64_t S, int32_t rank,
                     int32_t* own_uniq, int32_t* own_seg, int32_t* own_n, int32_t* perm2,
                     int32_t* own_ahead, int32_t* own_nah, void* stream);
+/* The owner-filtered grouping input (each rank sorts only the slots it owns, ~1/G of the
+ * global batch): per batch (ids [n_batches, per]), the slots i with ids[i] % G == rank in
+ * slot order, keyed rank*S + ids[i]/G (the mirec_shard_keys key) -> keys [n_batches,
+ * cap_sel], their positions -> sel_pos; padded with the key (rank+1)*S. sel_most[0] =
+ * max(sel_most[0], the largest owned count): over cap_sel, the batch was truncated and
+ * must be re-selected with a larger cap_sel. Sort keys with mirec_segment_sort_batched
+ * (stride cap_sel, key space G*S + 1), then mirec_shard_own_sel. */
+int mirec_shard_select(const int64_t* ids, int64_t n_batches, int64_t per, int32_t G, int64_t S,
+                       int32_t rank, int64_t cap_sel, int64_t* keys, int32_t* sel_pos,
+                       int32_t* sel_most, void* stream);
+/* mirec_shard_own on the owner-filtered grouping: input lists of stride cap_sel, a grouped
+ * position p's slot is sel_pos[perm[p]]; outputs with the global lists' stride per. Same
+ * owned lists and the same per-row contribution order as mirec_shard_own on the global
+ * grouping (the compaction keeps slot order; the sort is stable). */
+int mirec_shard_own_sel(const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq,
+                        const int32_t* perm, int64_t cap_sel, int64_t n_batches,
+                        const int32_t* ahead, const int32_t* n_ahead, const int32_t* map2,
+                        int64_t map_stride, int64_t map_off, int64_t S, int32_t rank,
+                        const int32_t* sel_pos, int64_t per, int32_t* own_uniq, int32_t* own_seg,
+                        int32_t* own_n, int32_t* perm2, int32_t* own_ahead, int32_t* own_nah,
+                        void* stream);
 /* Where each entry of step c's owned lists (mirec_shard_own: own / own_ahead) sits in
  * step c+1's owned list, for c < n_batches - 1: next_t[c*per_batch + i] = that index
  * (-1: step c+1 does not read the row), next_a[c*per_batch + a] likewise for the

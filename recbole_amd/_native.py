@@ -117,6 +117,11 @@ SIGNATURES = {
     "mirec_shard_own": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P, c_int64, c_int64,
                                 c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "mirec_shard_next": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P]),
+    "mirec_shard_select": (c_int, [_P, c_int64, c_int64, c_int32, c_int64, c_int32, c_int64, _P,
+                                   _P, _P, _P]),
+    "mirec_shard_own_sel": (c_int, [_P, _P, _P, _P, c_int64, c_int64, _P, _P, _P, c_int64,
+                                    c_int64, c_int64, c_int32, _P, c_int64, _P, _P, _P, _P, _P,
+                                    _P, _P]),
     "mirec_shard_gather_f32": (c_int, [_P, _P, c_int32, _P, c_int64, _P, _P]),
     "mirec_used_bitmap_build": (c_int, [_P, _P, c_int64, c_int64, _P, _P]),
     "mirec_gather_rows": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P]),

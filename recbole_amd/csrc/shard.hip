@@ -155,41 +155,98 @@ __device__ __forceinline__ int32_t lower_bound_i32(const int32_t* __restrict__ a
   return lo;
 }
 
+// Owner-filtered grouping input (each rank sorts only the slots whose rows it owns, ~1/G
+// of the global batch, instead of every rank sorting all of it): per batch, the slots i
+// with ids[i] % G == r in slot order (a stable compaction), keyed r*S + ids[i]/G — the
+// owner-major keys of the global path, so the sort, the look-ahead diff and shard_own
+// work unchanged — with sel_pos = i; padded to cap_sel with the key (r+1)*S (just past the
+// rank's range: shard_own's binary search leaves it out). sel_most[0] = max over the
+// batches of the owned count (atomicMax; zero it first): a count over cap_sel is
+// truncated here and the chunk must be re-planned with a larger cap_sel.
+constexpr int kSelThreads = 1024;
+__global__ __launch_bounds__(kSelThreads) void shard_select_kernel(
+    const int64_t* __restrict__ ids, int64_t per, int32_t G, int64_t S, int32_t r,
+    int64_t cap_sel, int64_t* __restrict__ keys, int32_t* __restrict__ sel_pos,
+    int32_t* __restrict__ sel_most) {
+  __shared__ int wtot[kSelThreads / 64];
+  const int64_t c = blockIdx.x;
+  const int64_t* __restrict__ id_c = ids + c * per;
+  int64_t* __restrict__ k_c = keys + c * cap_sel;
+  int32_t* __restrict__ p_c = sel_pos + c * cap_sel;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t kb = (int64_t)r * S;
+  int64_t base = 0;
+  for (int64_t i0 = 0; i0 < per; i0 += kSelThreads) {
+    const int64_t i = i0 + threadIdx.x;
+    int64_t id = 0;
+    bool own = false;
+    if (i < per) {
+      id = id_c[i];
+      own = id % G == r;
+    }
+    const uint64_t m = __ballot(own);
+    if (lane == 0) wtot[wid] = __popcll(m);
+    __syncthreads();
+    int64_t j = base + __popcll(m & ((1ull << lane) - 1ull));
+    int tot = 0;
+    for (int w = 0; w < kSelThreads / 64; ++w) {
+      if (w < wid) j += wtot[w];
+      tot += wtot[w];
+    }
+    if (own && j < cap_sel) {
+      k_c[j] = kb + id / G;
+      p_c[j] = (int32_t)i;
+    }
+    base += tot;
+    __syncthreads();                      // wtot is rewritten next round
+  }
+  for (int64_t j = base + threadIdx.x; j < cap_sel; j += kSelThreads) {
+    k_c[j] = kb + S;
+    p_c[j] = 0;
+  }
+  if (threadIdx.x == 0) atomicMax(sel_most, (int)base);
+}
+
 // Workgroups (batch, tile) — tile y of gridDim.y strides the batch's entries, so a chunk
 // of a few large batches still spreads over the chip (one workgroup per batch took
 // 48 µs for 16 batches of 20 K item slots): rank r's sub-range [lo, hi) of the sorted (keyed) uniq
 // list -> local row ids, its segment offsets, and the contributions of those
 // segments remapped to their positions in the backward receive buffer; the same
 // for the look-ahead list.
+// With sel_pos (the owner-filtered grouping, shard_select_kernel): the input lists have
+// stride per_batch (= cap_sel), a grouped position's slot is sel_pos[perm[p]], and the
+// outputs keep the stride out_per of the global lists.
 __global__ __launch_bounds__(kPlanThreads) void shard_own_kernel(
     const int32_t* __restrict__ uniq, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ n_uniq, const int32_t* __restrict__ perm, int64_t per_batch,
     const int32_t* __restrict__ ahead, const int32_t* __restrict__ n_ahead,
     const int32_t* __restrict__ map2, int64_t map_stride, int64_t map_off, int64_t S, int32_t r,
     int32_t* __restrict__ own_uniq, int32_t* __restrict__ own_seg, int32_t* __restrict__ own_n,
-    int32_t* __restrict__ perm2, int32_t* __restrict__ own_ahead, int32_t* __restrict__ own_nah) {
+    int32_t* __restrict__ perm2, int32_t* __restrict__ own_ahead, int32_t* __restrict__ own_nah,
+    const int32_t* __restrict__ sel_pos, int64_t out_per) {
   const int64_t c = blockIdx.x;
   const int32_t* __restrict__ uq = uniq + c * per_batch;
   const int32_t* __restrict__ sg = seg + c * (per_batch + 1);
   const int32_t* __restrict__ pm = perm + c * per_batch;
+  const int32_t* __restrict__ sp = sel_pos ? sel_pos + c * per_batch : nullptr;
   const int32_t* __restrict__ m2 = map2 + c * map_stride + map_off;
   const int64_t kb = (int64_t)r * S, ke = kb + S;
   const int32_t n = n_uniq[c];
   const int32_t lo = lower_bound_i32(uq, n, kb), hi = lower_bound_i32(uq, n, ke);
-  int32_t* __restrict__ ou = own_uniq + c * per_batch;
-  int32_t* __restrict__ os = own_seg + c * (per_batch + 1);
-  int32_t* __restrict__ p2 = perm2 + c * per_batch;
+  int32_t* __restrict__ ou = own_uniq + c * out_per;
+  int32_t* __restrict__ os = own_seg + c * (out_per + 1);
+  int32_t* __restrict__ p2 = perm2 + c * out_per;
   const int32_t t0 = (int32_t)(blockIdx.y * kPlanThreads + threadIdx.x);
   const int32_t ts = (int32_t)(gridDim.y * kPlanThreads);
   for (int32_t j = lo + t0; j < hi; j += ts) ou[j - lo] = (int32_t)(uq[j] - kb);
   for (int32_t j = lo + t0; j <= hi; j += ts) os[j - lo] = sg[j];
-  for (int32_t p = sg[lo] + t0; p < sg[hi]; p += ts) p2[p] = m2[pm[p]];
+  for (int32_t p = sg[lo] + t0; p < sg[hi]; p += ts) p2[p] = m2[sp ? sp[pm[p]] : pm[p]];
   if (t0 == 0) own_n[c] = hi - lo;
   if (ahead) {
     const int32_t* __restrict__ ah = ahead + c * per_batch;
     const int32_t na = n_ahead[c];
     const int32_t alo = lower_bound_i32(ah, na, kb), ahi = lower_bound_i32(ah, na, ke);
-    int32_t* __restrict__ oa = own_ahead + c * per_batch;
+    int32_t* __restrict__ oa = own_ahead + c * out_per;
     for (int32_t j = alo + t0; j < ahi; j += ts) oa[j - alo] = (int32_t)(ah[j] - kb);
     if (t0 == 0) own_nah[c] = ahi - alo;
   }
@@ -300,8 +357,44 @@ extern "C" int mirec_shard_own(const int32_t* uniq, const int32_t* seg, const in
                      dim3(kPlanThreads), 0,
                      (hipStream_t)stream, uniq, seg, n_uniq, perm, per_batch, ahead, n_ahead, map2,
                      map_stride, map_off, S, rank, own_uniq, own_seg, own_n, perm2, own_ahead,
-                     own_nah);
+                     own_nah, (const int32_t*)nullptr, per_batch);
   return launch_status("mirec_shard_own");
+}
+
+extern "C" int mirec_shard_select(const int64_t* ids, int64_t n_batches, int64_t per, int32_t G,
+                                  int64_t S, int32_t rank, int64_t cap_sel, int64_t* keys,
+                                  int32_t* sel_pos, int32_t* sel_most, void* stream) {
+  if (!ids || !keys || !sel_pos || !sel_most || n_batches < 0 || per < 1 || G < 1 || S < 1 ||
+      rank < 0 || rank >= G || cap_sel < 1 || cap_sel > per) {
+    set_error("mirec_shard_select: bad arguments");
+    return -1;
+  }
+  if (n_batches == 0) return 0;
+  hipLaunchKernelGGL(shard_select_kernel, dim3((unsigned)n_batches), dim3(kSelThreads), 0,
+                     (hipStream_t)stream, ids, per, G, S, rank, cap_sel, keys, sel_pos, sel_most);
+  return launch_status("mirec_shard_select");
+}
+
+extern "C" int mirec_shard_own_sel(const int32_t* uniq, const int32_t* seg, const int32_t* n_uniq,
+                                   const int32_t* perm, int64_t cap_sel, int64_t n_batches,
+                                   const int32_t* ahead, const int32_t* n_ahead,
+                                   const int32_t* map2, int64_t map_stride, int64_t map_off,
+                                   int64_t S, int32_t rank, const int32_t* sel_pos, int64_t per,
+                                   int32_t* own_uniq, int32_t* own_seg, int32_t* own_n,
+                                   int32_t* perm2, int32_t* own_ahead, int32_t* own_nah,
+                                   void* stream) {
+  if (!uniq || !seg || !n_uniq || !perm || !map2 || !sel_pos || !own_uniq || !own_seg ||
+      !own_n || !perm2 || cap_sel < 1 || per < cap_sel || n_batches < 0 || S < 1 || rank < 0 ||
+      (ahead && (!n_ahead || !own_ahead || !own_nah))) {
+    set_error("mirec_shard_own_sel: bad arguments");
+    return -1;
+  }
+  if (n_batches == 0) return 0;
+  hipLaunchKernelGGL(shard_own_kernel, dim3((unsigned)n_batches, plan_tiles(cap_sel)),
+                     dim3(kPlanThreads), 0, (hipStream_t)stream, uniq, seg, n_uniq, perm, cap_sel,
+                     ahead, n_ahead, map2, map_stride, map_off, S, rank, own_uniq, own_seg, own_n,
+                     perm2, own_ahead, own_nah, sel_pos, per);
+  return launch_status("mirec_shard_own_sel");
 }
 
 extern "C" int mirec_shard_next(const int32_t* own, const int32_t* own_n, const int32_t* own_ahead,

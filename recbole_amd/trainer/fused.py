@@ -1049,8 +1049,8 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             sl.pos = torch.empty(C * (2 + T) * B, dtype=torch.int64, device=dev)
             # this chunk's plan status ([overflow, largest message]), read by the host
             # before the chunk's model side is launched (_enter_chunk)
-            sl.plan_status = torch.zeros(2, dtype=torch.int32, device=dev)
-            sl.plan_status_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+            sl.plan_status = torch.zeros(4, dtype=torch.int32, device=dev)
+            sl.plan_status_host = torch.zeros(4, dtype=torch.int32).pin_memory()
             sl.planned = torch.cuda.Event()
             for tag, per in (('u', Bg), ('i', KI)):
                 setattr(sl, f'own_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
@@ -1060,11 +1060,18 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                 setattr(sl, f'perm2_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_ah', torch.empty(C * per, dtype=torch.int32, device=dev))
                 setattr(sl, f'own_{tag}_nah', torch.zeros(C, dtype=torch.int32, device=dev))
+                setattr(sl, f'sel_{tag}', torch.empty(C * per, dtype=torch.int32, device=dev))
                 if self.win is not None:     # the owner's push lists (mirec_shard_next)
                     setattr(sl, f'next_{tag}_t', torch.empty(C * per, dtype=torch.int32,
                                                              device=dev))
                     setattr(sl, f'next_{tag}_a', torch.empty(C * per, dtype=torch.int32,
                                                              device=dev))
+        # slots per (batch, table) a rank's owner-filtered grouping holds (its ~1/G share
+        # of the global batch with slack; a batch over it is re-selected at the table's
+        # full size before its chunk runs: _enter_chunk)
+        self.cap_sel = {tag: min(per, math.ceil(self.CAP_SLACK * per / G) + 64)
+                        for tag, per in (('u', Bg), ('i', KI))}
+        self.sel_growths = 0
         self._alloc_exchange()
         self._n_max = (ctypes.c_int64 * 2)(min(Bg, self.SU), min(KI, self.SI))
         self._fill_tables()
@@ -1147,26 +1154,17 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
             neg = slot.item_keys[Bc:nb * KI]
             self.data.sampler.launch_batches(users, Bc, nb, T, neg, out_stride=KI,
                                              ws=self.samp_ws)
-            items = slot.item_keys[:nb * KI]
-            check(L.mirec_shard_keys(users.data_ptr(), nb * Bc, G, self.SU,
-                                     slot.u_keyed.data_ptr(), st), 'mirec_shard_keys')
-            check(L.mirec_shard_keys(items.data_ptr(), nb * KI, G, self.SI,
-                                     slot.i_keyed.data_ptr(), st), 'mirec_shard_keys')
-            self.sort_ws = ops.segment_sort_batched(slot.u_keyed[:nb * Bc], Bc, G * self.SU,
-                                                    slot.u_perm, slot.u_uniq, slot.u_seg,
-                                                    slot.u_nu, ws=self.sort_ws)
-            self.sort_ws = ops.segment_sort_batched(slot.i_keyed[:nb * KI], KI, G * self.SI,
-                                                    slot.i_perm, slot.i_uniq, slot.i_seg,
-                                                    slot.i_nu, ws=self.sort_ws)
-            ops.uniq_ahead_diff(slot.u_uniq, slot.u_nu, Bc, nb, slot.u_ahead, slot.u_nah)
-            ops.uniq_ahead_diff(slot.i_uniq, slot.i_nu, KI, nb, slot.i_ahead, slot.i_nah)
             self._plan_chunk(slot, chunk, st)
             slot.ready.record(self.prep_stream)
         slot.chunk = chunk
 
     def _plan_chunk(self, slot, chunk, st):
-        """Exchange plans of a walked + grouped chunk and this rank's slice of its
-        grouping (on stream `st`); the plan status goes to pinned host memory."""
+        """This rank's grouping of a walked chunk and its exchange plans (on the current
+        stream, `st`): per table, the slots of the rows this rank owns (mirec_shard_select,
+        ~1/G of the global batch), their K2 grouping over owner-major keys and look-ahead
+        lists; the plans from the unsorted keys (mirec_shard_plan); the owned lists with the
+        contributions' places in the backward messages (mirec_shard_own_sel). The plan
+        status goes to pinned host memory."""
         _, nb, Bc = chunk
         T, G, r = self.times, self.G, self.rank
         KI = (1 + T) * Bc
@@ -1174,19 +1172,32 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         users = slot.user_keys[:nb * Bc]
         items = slot.item_keys[:nb * KI]
         slot.plan_status.zero_()
+        cs = {}
+        for k, (tag, ids, per, S) in enumerate((('u', users, Bc, self.SU),
+                                                ('i', items, KI, self.SI))):
+            cs[tag] = c_ = min(self.cap_sel[tag], per)
+            keyed = getattr(slot, f'{tag}_keyed')[:nb * c_]
+            check(L.mirec_shard_select(ids.data_ptr(), nb, per, G, S, r, c_, keyed.data_ptr(),
+                                       getattr(slot, f'sel_{tag}').data_ptr(),
+                                       slot.plan_status.data_ptr() + 4 * (2 + k), st),
+                  'mirec_shard_select')
+            g_ = lambda n: getattr(slot, f'{tag}_{n}')
+            self.sort_ws = ops.segment_sort_batched(keyed, c_, G * S + 1, g_('perm'), g_('uniq'),
+                                                    g_('seg'), g_('nu'), ws=self.sort_ws)
+            ops.uniq_ahead_diff(g_('uniq'), g_('nu'), c_, nb, g_('ahead'), g_('nah'))
         check(L.mirec_shard_plan(users.data_ptr(), items.data_ptr(), nb, Bc, self.B, T, G, r,
                                  self.cap, slot.fwd_rows.data_ptr(), slot.map2.data_ptr(),
                                  slot.pos.data_ptr(), slot.bwd_src.data_ptr(),
                                  slot.plan_status.data_ptr(), st), 'mirec_shard_plan')
         for tag, per, off, S in (('u', Bc, 0, self.SU), ('i', KI, Bc, self.SI)):
             g_ = lambda n: getattr(slot, n).data_ptr()
-            check(L.mirec_shard_own(g_(f'{tag}_uniq'), g_(f'{tag}_seg'), g_(f'{tag}_nu'),
-                                    g_(f'{tag}_perm'), per, nb, g_(f'{tag}_ahead'),
-                                    g_(f'{tag}_nah'), slot.map2.data_ptr(), Bc + KI, off,
-                                    S, r, g_(f'own_{tag}'), g_(f'own_{tag}_seg'),
-                                    g_(f'own_{tag}_n'), g_(f'perm2_{tag}'),
-                                    g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), st),
-                  'mirec_shard_own')
+            check(L.mirec_shard_own_sel(g_(f'{tag}_uniq'), g_(f'{tag}_seg'), g_(f'{tag}_nu'),
+                                        g_(f'{tag}_perm'), cs[tag], nb, g_(f'{tag}_ahead'),
+                                        g_(f'{tag}_nah'), slot.map2.data_ptr(), Bc + KI, off,
+                                        S, r, g_(f'sel_{tag}'), per, g_(f'own_{tag}'),
+                                        g_(f'own_{tag}_seg'), g_(f'own_{tag}_n'),
+                                        g_(f'perm2_{tag}'), g_(f'own_{tag}_ah'),
+                                        g_(f'own_{tag}_nah'), st), 'mirec_shard_own_sel')
             if self.win is not None:
                 check(L.mirec_shard_next(g_(f'own_{tag}'), g_(f'own_{tag}_n'),
                                          g_(f'own_{tag}_ah'), g_(f'own_{tag}_nah'), per, nb,
@@ -1194,7 +1205,7 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
                       'mirec_shard_next')
         # epoch backstop: overflow flag (min: -4 < 0) and the largest message (max)
         torch.minimum(self.status[:1], slot.plan_status[:1], out=self.status[:1])
-        torch.maximum(self.status[1:], slot.plan_status[1:], out=self.status[1:])
+        torch.maximum(self.status[1:], slot.plan_status[1:2], out=self.status[1:])
         slot.plan_status_host.copy_(slot.plan_status, non_blocking=True)
         slot.planned.record(torch.cuda.current_stream(self.device))
 
@@ -1210,9 +1221,33 @@ class ShardedBPRTrainStep(FusedBPRTrainStep):
         slot = self.slots[k % len(self.slots)]
         if not slot.planned.query():          # the plan status reaches pinned memory
             slot.planned.synchronize()
-        over, most = (int(x) for x in slot.plan_status_host)
+        over, most, sel_u, sel_i = (int(x) for x in slot.plan_status_host)
+        _, _, Bc = self._plan[k]
+        grow = {tag: n for tag, n, per in (('u', sel_u, Bc), ('i', sel_i, (1 + self.times) * Bc))
+                if n > min(self.cap_sel[tag], per)}
+        if grow:
+            self._grow_sel(grow)
+            over, most = (int(x) for x in slot.plan_status_host[:2])
         if over == -4:
             self._grow_cap(most)
+
+    def _grow_sel(self, grow):
+        """A batch owns more slots of a table than its owner-filtered grouping holds:
+        re-select + re-plan every prepared chunk with that table's full batch size (no
+        overflow possible). The graphs stay (they read the owned lists, whose strides do
+        not change)."""
+        T, Bg = self.times, self.Bg
+        logging.getLogger().warning(f'owner-filtered grouping: {grow} owned slots exceed '
+                                    f'cap_sel={self.cap_sel}; re-selecting at full size')
+        torch.cuda.synchronize(self.device)
+        for tag in grow:
+            self.cap_sel[tag] = Bg if tag == 'u' else (1 + T) * Bg
+        self.sel_growths += 1
+        for q in range(self._cur if self._cur is not None else 0, self._next_chunk):
+            slot = self.slots[q % len(self.slots)]
+            with torch.cuda.stream(self.prep_stream):
+                self._plan_chunk(slot, self._plan[q], self.prep_stream.cuda_stream)
+        torch.cuda.synchronize(self.device)
 
     def _grow_cap(self, most):
         """Larger messages: reallocate the cap-sized buffers, re-plan every prepared

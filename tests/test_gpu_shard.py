@@ -109,6 +109,82 @@ def test_shard_plan_and_own_match_spec(dev, G, Bc):
             assert int(bufs[1][owned].max()) < 2 * G
 
 
+@pytest.mark.parametrize('G,nb,per', [(1, 3, 240), (2, 4, 240), (3, 2, 1000), (8, 5, 2560)])
+def test_owner_filtered_grouping_matches_global(dev, G, nb, per):
+    """mirec_shard_select + K2 on the selected keys + mirec_shard_own_sel give every rank
+    the same owned rows, the same look-ahead lists and, per owned row, the same
+    contributions in the same order as mirec_shard_own on the global grouping."""
+    from recbole_amd import ops
+    from recbole_amd._native import check, lib
+    S, L = 97, lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator().manual_seed(G * 7 + per)
+    ids = torch.randint(0, G * S, (nb * per,), generator=g)
+    ids[:per // 4] = 5                                         # a hot row
+    idd = ids.to(dev)
+    map2 = torch.randperm(nb * per, generator=g).to(torch.int32).to(dev)   # stand-in plan
+
+    def group(keys, stride, space):
+        n = keys.numel()
+        out = [torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32,
+               device=dev), torch.empty(nb * (stride + 1), dtype=torch.int32, device=dev),
+               torch.zeros(nb, dtype=torch.int32, device=dev)]
+        ops.segment_sort_batched(keys, stride, space, *out)
+        ah = torch.empty(n, dtype=torch.int32, device=dev)
+        nah = torch.zeros(nb, dtype=torch.int32, device=dev)
+        ops.uniq_ahead_diff(out[1], out[3], stride, nb, ah, nah)
+        return out + [ah, nah]
+
+    def owned(res, stride, r, sel=None):
+        perm, uniq, seg, nu, ah, nah = res
+        own = torch.empty(nb * per, dtype=torch.int32, device=dev)
+        oseg = torch.empty(nb * (per + 1), dtype=torch.int32, device=dev)
+        on = torch.zeros(nb, dtype=torch.int32, device=dev)
+        p2 = torch.full((nb * per,), -9, dtype=torch.int32, device=dev)
+        oa = torch.empty(nb * per, dtype=torch.int32, device=dev)
+        ona = torch.zeros(nb, dtype=torch.int32, device=dev)
+        args = [uniq.data_ptr(), seg.data_ptr(), nu.data_ptr(), perm.data_ptr(), stride, nb,
+                ah.data_ptr(), nah.data_ptr(), map2.data_ptr(), per, 0, S, r]
+        outs = [own.data_ptr(), oseg.data_ptr(), on.data_ptr(), p2.data_ptr(), oa.data_ptr(),
+                ona.data_ptr(), st]
+        if sel is None:
+            check(L.mirec_shard_own(*args, *outs), 'own')
+        else:
+            check(L.mirec_shard_own_sel(*args, sel.data_ptr(), per, *outs), 'own_sel')
+        rows = []
+        for c in range(nb):
+            k = int(on[c])
+            o = own[c * per:c * per + k].tolist()
+            sg = oseg[c * (per + 1):c * (per + 1) + k + 1].tolist()
+            p = p2[c * per:(c + 1) * per].tolist()
+            rows.append((o, [p[sg[x]:sg[x + 1]] for x in range(k)],
+                         oa[c * per:c * per + int(ona[c])].tolist() if c + 1 < nb else None))
+        return rows
+
+    most_owned = max(int(((ids[c * per:(c + 1) * per] % G) == r).sum())
+                     for c in range(nb) for r in range(G))
+    cap_sel = min(per, most_owned + 16)            # padded batches on every rank
+    keyed = torch.empty_like(idd)
+    check(L.mirec_shard_keys(idd.data_ptr(), idd.numel(), G, S, keyed.data_ptr(), st), 'keys')
+    glob = group(keyed, per, G * S)
+    for r in range(G):
+        keys = torch.empty(nb * cap_sel, dtype=torch.int64, device=dev)
+        sel = torch.empty(nb * cap_sel, dtype=torch.int32, device=dev)
+        most = torch.zeros(1, dtype=torch.int32, device=dev)
+        check(L.mirec_shard_select(idd.data_ptr(), nb, per, G, S, r, cap_sel, keys.data_ptr(),
+                                   sel.data_ptr(), most.data_ptr(), st), 'select')
+        counts = [int(((ids[c * per:(c + 1) * per] % G) == r).sum()) for c in range(nb)]
+        assert int(most) == max(counts) <= cap_sel
+        assert owned(group(keys, cap_sel, G * S + 1), cap_sel, r, sel) == owned(glob, per, r)
+    # an over-full batch is reported (the caller re-selects at full size)
+    most = torch.zeros(1, dtype=torch.int32, device=dev)
+    keys = torch.empty(nb * 8, dtype=torch.int64, device=dev)
+    sel = torch.empty(nb * 8, dtype=torch.int32, device=dev)
+    check(L.mirec_shard_select(idd.data_ptr(), nb, per, G, S, 0, 8, keys.data_ptr(),
+                               sel.data_ptr(), most.data_ptr(), st), 'select')
+    assert int(most) > 8
+
+
 def _pipeline(root, batch_rows):
     import pathlib
     from test_gpu_e2e import _pipeline as pipe

@@ -5,3 +5,5 @@ for ex in rccl ipc; do
   grep '^{' $O/n2_$ex.log | python -c 'import json,sys
 d=json.loads(sys.stdin.read()); print(sys.argv[1], d["value"], d["ms_per_step"], d["n_gpus"], d["config"]["parallelism"], d.get("kernels_us"))' $ex
 done
+timeout -k 10 300 python tools/event_timeline.py --reps 3 > $O/event_timeline.log 2>&1 || { echo FAIL timeline; tail -20 $O/event_timeline.log; exit 3; }
+grep -A12 "^rep 2" $O/event_timeline.log
