@@ -266,7 +266,9 @@ def _worker(rank, port, root, q, cap=None, exchange='rccl'):
 def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange):
     """cap=40: both ranks detect the same overflow and grow cap identically.
     exchange='ipc': the rows go through the peer windows (csrc/comm.hip: IPC-mapped, in-
-    kernel stores, flags on the GPU; both ranks on cuda:0 here, over xGMI on a node)."""
+    kernel stores, flags on the GPU). Both ranks share cuda:0 here, so this pins the flag /
+    counter protocol, the push lists and the owner-Adam fold — NOT the cross-device mapping
+    over xGMI, which no test on a one-GPU box can reach (hence RCCL stays the default)."""
     from recbole_amd.trainer.fused import FusedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     root = str(tmp_path)
