@@ -300,7 +300,10 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(const ColsumJobs J) 
 // chunk (agent-scope ticket; write-through partial stores drained before it, an agent
 // acquire after, then plain loads) adds them.
 constexpr int kLgThreads = 256;
-constexpr int kLgRows = 2048;         // bias rows per chunk
+constexpr int kLgRows = 1024;         // bias rows per chunk (2048: 50 blocks for K = 10^5 rows,
+                                      // too few waves to stream g)
+constexpr int kLgSumThreads = 64;     // lanes per block of the partial sum (256: 16 blocks for
+                                      // a 128 x 128 dW, each lane walking C partials)
 struct LinearGradFinish {
   const float* P; int C; int64_t n4;  // partials [C, 4 n4] -> dW
   float* dW;
@@ -313,11 +316,23 @@ struct LinearGradFinish {
 __global__ __launch_bounds__(kLgThreads) void linear_grad_finish_kernel(const LinearGradFinish F) {
   const int tid = threadIdx.x;
   if ((int)blockIdx.x < F.nS) {
-    const int64_t i = (int64_t)blockIdx.x * kLgThreads + tid;
-    if (i >= F.n4) return;
+    // the first kLgSumThreads lanes of each block (the launch's block size serves the
+    // bias chunks); eight partials' loads in flight, added in c order
+    const int64_t i = (int64_t)blockIdx.x * kLgSumThreads + tid;
+    if (tid >= kLgSumThreads || i >= F.n4) return;
     const float4* P4 = reinterpret_cast<const float4*>(F.P);
     float4 v = P4[i];
-    for (int c = 1; c < F.C; ++c) {
+    int c = 1;
+    for (; c + 8 <= F.C; c += 8) {
+      float4 w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = P4[(int64_t)(c + u) * F.n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v.x += w[u].x; v.y += w[u].y; v.z += w[u].z; v.w += w[u].w;
+      }
+    }
+    for (; c < F.C; ++c) {
       const float4 w = P4[(int64_t)c * F.n4 + i];
       v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
@@ -385,17 +400,17 @@ __global__ __launch_bounds__(kLgThreads) void linear_grad_finish_kernel(const Li
   }
   __syncthreads();
   if (!s_last) return;
-  // after the acquire: plain loads (the guide's consumer form), 8 chunks' loads in flight
+  // after the acquire: plain loads (the guide's consumer form), 16 chunks' loads in flight
   for (int j = tid; j < F.n_out; j += kLgThreads) {
     const float* src = F.scratch + j;
     float t = src[0];
     int c = 1;
-    for (; c + 8 <= F.nB; c += 8) {
-      float v[8];
+    for (; c + 16 <= F.nB; c += 16) {
+      float v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(c + u) * F.n_out];
+      for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)(c + u) * F.n_out];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t += v[u];
+      for (int u = 0; u < 16; ++u) t += v[u];
     }
     for (; c < F.nB; ++c) t += src[(int64_t)c * F.n_out];
     F.db[j] = t;
@@ -625,7 +640,7 @@ extern "C" int mirec_linear_grad_finish_f32(const float* P, int32_t C, int64_t n
   memset(&F, 0, sizeof(F));
   F.P = P; F.C = C; F.n4 = n_w / 4; F.dW = dW;
   F.g = g; F.K = K; F.n_out = n_out; F.db = db; F.scratch = scratch; F.ticket = ticket;
-  F.nS = sum ? (int)((F.n4 + kLgThreads - 1) / kLgThreads) : 0;
+  F.nS = sum ? (int)((F.n4 + kLgSumThreads - 1) / kLgSumThreads) : 0;
   F.nB = bias ? (int)((K + kLgRows - 1) / kLgRows) : 0;
   if (F.nS + F.nB == 0) return 0;
   hipLaunchKernelGGL(linear_grad_finish_kernel, dim3((unsigned)(F.nS + F.nB)), dim3(kLgThreads), 0,
