@@ -255,6 +255,8 @@ def _worker(rank, port, root, q, cap=None, exchange='rccl'):
         assert step.exchange == exchange
         tensors, losses = _train(step)
         assert cap is None or step.cap_growths >= 1
+        if step.win is not None:                  # no wait gave up (end_epoch raises too)
+            assert step.win.status() == 0
         step.close()
         q.put((rank, step.Bg, step.SU, [t.numpy() for t in tensors], losses))
     finally:
