@@ -71,8 +71,10 @@ static void mlp_ld(const mirec_mlp& a, int* ldA, int* ldB, int l0 = 0) {
 // of W [N, K] over the 16-wide K slices [s0, s1). k = 16 s + 16 u + 4 lk + e: the four
 // MFMAs of a slice cover it once each; the next group's loads are issued before this
 // group's MFMAs (two accumulators, added at the end).
+template <int U = kFwdU>
 __device__ __forceinline__ floatx4 tile_dot(const float* cur, int ld, const float* __restrict__ W,
                                             int K, int N, int c0, int s0, int s1, int li, int lk) {
+  constexpr int kFwdU = U;          // slices per prefetch group (shadows the file default)
   const int c = c0 + li;
   const float* wr = W + (int64_t)(c < N ? c : N - 1) * K;
   const int kend = min(16 * s1, K);
@@ -160,14 +162,25 @@ __device__ __forceinline__ void stage_rows(const mirec_mlp& a, const float* __re
 }
 
 // Layers l0..L-1 for one block of 16 rows (l0 = 0: every layer; l0 = 1 behind the wide
-// layer-0 kernel below).
-__global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const float* __restrict__ x,
+// layer-0 kernel below). KS waves per 16-column output tile, each over 1/KS of the K
+// slices, their partial tiles added in LDS in kh order: the forward is latency-bound (one
+// block per 16 rows: 128 blocks on half the chip at C4, waves waiting on W's loads 43 % and
+// on MFMA results 34 % of their time with KS = 1, profiles/r06_C4_mlp_pmc.txt), and KS = 2
+// doubles the waves in flight and halves each wave's dependent chain.
+#ifndef MIREC_MLP_FWD_KS
+#define MIREC_MLP_FWD_KS 2
+#endif
+constexpr int kFwdKS = MIREC_MLP_FWD_KS;
+template <int KS>
+__global__ __launch_bounds__(kMlpThreads * KS) void mlp_fwd_kernel(mirec_mlp a, const float* __restrict__ x,
                                                               int64_t B, float* __restrict__ y,
                                                               int train, int ldA, int ldB, int l0) {
   extern __shared__ float lds[];
   float* const tA = lds;
   float* const tB = lds + kMlpRows * ldA;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  floatx4* const red = reinterpret_cast<floatx4*>(tB + kMlpRows * ldB);   // [KS-1][waves][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = (tid >> 6) % kMlpWaves, kh = (tid >> 6) / kMlpWaves;
   const int li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * kMlpRows;
   const int L = a.n_layers;
@@ -175,8 +188,8 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
   for (int l = 0; l < L; ++l) any_drop |= train && a.dropout[l];
   const uint64_t key = any_drop ? splitmix64(a.seed + (uint64_t)a.counter[0]) : 0ull;
 
-  stage_rows<kMlpThreads>(a, x, l0, B, r0, train && a.dropout[0], true, key,
-                          (l0 & 1) ? tB : tA, (l0 & 1) ? ldB : ldA);
+  stage_rows<kMlpThreads * KS>(a, x, l0, B, r0, train && a.dropout[0], true, key,
+                               (l0 & 1) ? tB : tA, (l0 & 1) ? ldB : ldA);
   __syncthreads();
 
   for (int l = l0; l < L; ++l) {
@@ -190,11 +203,23 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
     const bool relu = a.relu[l] != 0;
     float* __restrict__ save = last ? nullptr : a.xs[l + 1];
     const int ntile = (N + 15) / 16;
-    for (int t = wave; t < ntile; t += kMlpWaves) {     // one 16-column tile per wave
+    const int nsl = (K + 15) / 16, spk = (nsl + KS - 1) / KS;
+    for (int t0 = 0; t0 < ntile; t0 += kMlpWaves) {    // rounds: every wave at every barrier
+      const int t = t0 + wave;                          // one 16-column tile per wave (group)
       const int c = t * 16 + li;
-      const floatx4 acc0 = tile_dot(cur, ld, a.W[l], K, N, t * 16, 0, (K + 15) / 16, li, lk);
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      if (t < ntile)
+        acc0 = tile_dot<(kFwdU / KS > 1 ? kFwdU / KS : 1)>(cur, ld, a.W[l], K, N, t * 16, kh * spk,
+                                                           min(nsl, (kh + 1) * spk), li, lk);
+      if (KS > 1) {
+        if (kh > 0) red[((kh - 1) * kMlpWaves + wave) * 64 + lane] = acc0;
+        __syncthreads();
+        if (kh == 0)
+#pragma unroll
+          for (int h = 1; h < KS; ++h) acc0 = acc0 + red[((h - 1) * kMlpWaves + wave) * 64 + lane];
+      }
       // epilogue: lane holds rows 4*lk + r of column c
-      if (c < N) {
+      if (kh == 0 && t < ntile && c < N) {
         const float bc = bias ? bias[c] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -214,6 +239,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_fwd_kernel(mirec_mlp a, const
           nxt[i * ldn + c] = z;
         }
       }
+      if (KS > 1) __syncthreads();                      // red is rewritten next round
     }
     __syncthreads();
   }
@@ -835,10 +861,17 @@ extern "C" int mirec_mlp_fwd_f32(const mirec_mlp* mlp, const float* x, int64_t B
   }
   int ldA, ldB;
   mlp_ld(a, &ldA, &ldB, l0);
-  const size_t shm = (size_t)kMlpRows * (ldA + ldB) * sizeof(float);
+  const size_t shm1 = (size_t)kMlpRows * (ldA + ldB) * sizeof(float);
+  const size_t shmK = shm1 + (size_t)(kFwdKS - 1) * kMlpWaves * 64 * sizeof(floatx4);
+  const bool ks = kFwdKS > 1 && shmK <= 65536;
+  const size_t shm = ks ? shmK : shm1;
   if (mlp_lds_limit(shm, "mirec_mlp_fwd_f32")) return -1;
-  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(row_blocks), dim3(kMlpThreads), shm, st, a, x, B, y,
-                     (int)train, ldA, ldB, l0);
+  if (ks)
+    hipLaunchKernelGGL(mlp_fwd_kernel<kFwdKS>, dim3(row_blocks), dim3(kMlpThreads * kFwdKS), shm,
+                       st, a, x, B, y, (int)train, ldA, ldB, l0);
+  else
+    hipLaunchKernelGGL(mlp_fwd_kernel<1>, dim3(row_blocks), dim3(kMlpThreads), shm, st, a, x, B,
+                       y, (int)train, ldA, ldB, l0);
   return launch_status("mirec_mlp_fwd_f32");
 }
 
