@@ -104,6 +104,12 @@ __device__ __forceinline__ void load_user_operand(const float* __restrict__ Uq, 
   }
 }
 
+// NT = 32-item sub-tiles per staged tile: NT = 2 (64 items) for D <= 128 — two
+// independent MFMA accumulators per wave (the chains interleave) and one workgroup
+// barrier per 64 items instead of per 32: at D = 128 a 32-item tile is only 64 MFMAs
+// per wave between barriers.
+template <int D> struct FsSub { static constexpr int n = D <= 128 ? 2 : 1; };
+
 template <int D, int KC>
 // Two waves per SIMD (<= 256 VGPRs, no spills for D <= 128): the second wave's
 // VALU top-K work overlaps the first one's MFMAs — measured 1.43x over one wave
@@ -120,14 +126,16 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     uint8_t* __restrict__ pos_flags, int64_t span) {
   constexpr int LDR = D + 2;
   constexpr int V4 = D / 4;
-  constexpr int NPF = (32 * V4 + kFsThreads - 1) / kFsThreads;   // float4 per thread per tile
+  constexpr int NT = FsSub<D>::n;                                 // 32-item sub-tiles per tile
+  constexpr int TI = 32 * NT;                                     // items per tile
+  constexpr int NPF = (TI * V4 + kFsThreads - 1) / kFsThreads;    // float4 per thread per tile
   // item split (gridDim.y > 1): this workgroup sweeps items [ilo, ihi) and writes its
-  // partial lists (merged by fullsort_merge_kernel); span is a multiple of 32
+  // partial lists (merged by fullsort_merge_kernel); span is a multiple of TI
   const bool split = gridDim.y > 1;
   const int64_t ilo = (int64_t)blockIdx.y * span;
   const int64_t ihi = min(I, ilo + span);
-  __shared__ __attribute__((aligned(16))) float tile[2][32 * LDR];
-  __shared__ uint32_t hmask[2][128];   // history bits of the WG's 128 users over one tile
+  __shared__ __attribute__((aligned(16))) float tile[2][TI * LDR];
+  __shared__ uint32_t hmask[2][NT][128];   // history bits of the WG's 128 users over one tile
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int j = lane & 31;
@@ -163,101 +171,125 @@ __global__ __launch_bounds__(kFsThreads, MIREC_FS_WAVES_PER_EU(D)) void fullsort
     }
     if (hcur < hend) hnext = hist_cols[hcur];
   }
-  auto build_mask = [&](int64_t base, uint32_t* dst) {
+  auto build_mask = [&](int64_t base, uint32_t (*dst)[128]) {
     if (threadIdx.x < 128) {
-      uint32_t msk = 0;
-      while (hnext < base + 32) {
-        msk |= 1u << (uint32_t)(hnext - base);
-        ++hcur;
-        hnext = hcur < hend ? (int64_t)hist_cols[hcur] : INT64_MAX;
+#pragma unroll
+      for (int sub = 0; sub < NT; ++sub) {
+        const int64_t b0 = base + 32 * sub;
+        uint32_t msk = 0;
+        while (hnext < b0 + 32) {
+          msk |= 1u << (uint32_t)(hnext - b0);
+          ++hcur;
+          hnext = hcur < hend ? (int64_t)hist_cols[hcur] : INT64_MAX;
+        }
+        dst[sub][threadIdx.x] = msk;
       }
-      dst[threadIdx.x] = msk;
     }
   };
 
   const float4* __restrict__ E4 = reinterpret_cast<const float4*>(EI);
-  float4 pf[NPF];
-  auto load_tile = [&](int64_t base) {
+  // the next tile in flight in PH = NT parts (one sub-tile's worth of registers at a
+  // time: part p stored to LDS when sub-tile p + 1 starts, the next part issued)
+  constexpr int PH = NT;
+  constexpr int NPP = (NPF + PH - 1) / PH;
+  float4 pf[NPP];
+  auto load_tile = [&](int64_t base, int part = 0) {
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
+    for (int kk = 0; kk < NPP; ++kk) {
+      const int k = part * NPP + kk;
       const int f = threadIdx.x + k * kFsThreads;
       const int row = f / V4;
       const int c4 = f - row * V4;
       const int64_t item = base + row;
-      pf[k] = (f < 32 * V4 && item < I) ? E4[item * V4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      pf[kk] = (k < NPF && f < TI * V4 && item < I) ? E4[item * V4 + c4]
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store_tile = [&](float* dst) {
+  auto store_tile = [&](float* dst, int part = 0) {
 #pragma unroll
-    for (int k = 0; k < NPF; ++k) {
+    for (int kk = 0; kk < NPP; ++kk) {
+      const int k = part * NPP + kk;
       const int f = threadIdx.x + k * kFsThreads;
-      if (f < 32 * V4) {
+      if (k < NPF && f < TI * V4) {
         const int row = f / V4;
         const int c4 = f - row * V4;
         float2* p = reinterpret_cast<float2*>(dst + row * LDR + 4 * c4);
-        p[0] = make_float2(pf[k].x, pf[k].y);
-        p[1] = make_float2(pf[k].z, pf[k].w);
+        p[0] = make_float2(pf[kk].x, pf[kk].y);
+        p[1] = make_float2(pf[kk].z, pf[kk].w);
       }
     }
   };
 
-  const int64_t ntile = (ihi - ilo + 31) / 32;
-  load_tile(ilo);
-  store_tile(tile[0]);
+  const int64_t ntile = (ihi - ilo + TI - 1) / TI;
+#pragma unroll
+  for (int part = 0; part < PH; ++part) {
+    load_tile(ilo, part);
+    store_tile(tile[0], part);
+  }
   build_mask(ilo, hmask[0]);
   __syncthreads();
   int cur = 0;
   const int ul = w * 32 + j;   // this lane's user within the workgroup
   for (int64_t t = 0; t < ntile; ++t) {
-    const int64_t base = ilo + t * 32;
+    const int64_t base = ilo + t * TI;
     const bool more = t + 1 < ntile;
-    if (more) load_tile(base + 32);          // global loads in flight under the MFMAs
-    floatx16 acc;
+    if (more) load_tile(base + TI, 0);       // global loads in flight under the MFMAs
+    // the sub-tiles one after the other (one accumulator: the registers of the
+    // 32-item form), one workgroup barrier per tile
+#pragma unroll 1
+    for (int sub = 0; sub < NT; ++sub) {
+      if (sub > 0 && more) {                   // a part of the next tile to LDS, the next part
+        store_tile(tile[cur ^ 1], sub - 1);    // in flight
+        load_tile(base + TI, sub);
+      }
+      floatx16 acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const float* arow = tile[cur] + j * LDR + 2 * h;
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const float* arow = tile[cur] + (32 * sub + j) * LDR + 2 * h;
 #pragma unroll
-    for (int s2 = 0; s2 < D / 4; ++s2) {
-      const float2 a = *reinterpret_cast<const float2*>(arow + 4 * s2);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, ub[2 * s2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, ub[2 * s2 + 1], acc, 0, 0, 0);
-    }
-    // Rows of this lane that can enter its list: valid item, not pad, not history.
-    // C[item row][user col]: rows (r&3) + 8*(r>>2) + 4h
-    const uint32_t hm = hmask[cur][ul];
-    uint32_t ok = 0;
-    float best = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int64_t item = base + row;
-      const bool valid = qv & (item < ihi) & (item != 0) & !((hm >> row) & 1u);
-      ok |= (valid ? 1u : 0u) << r;
-      best = fmaxf(best, valid ? acc[r] : -INFINITY);
-    }
-    // The two lanes of a user scan disjoint item halves; an item below the
-    // partner's K-th best already has K better items, so it can never reach the
-    // final (merged) top-K: filter with the stronger of the two thresholds.
-    thr = fmaxf(thr, __shfl_xor(thr, 32, 64));
-#ifdef MIREC_FS_NO_TOPK   // profiling variant (tools/build_variant.sh): MFMA + mask only
-    thr = fmaxf(thr, best);
-    if (false) {
-#else
-    if (__any(best > thr)) {             // wave-uniform: rare once the lists fill up
-#endif
+      for (int s2 = 0; s2 < D / 4; ++s2) {
+        const float2 a = *reinterpret_cast<const float2*>(arow + 4 * s2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, ub[2 * s2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, ub[2 * s2 + 1], acc, 0, 0, 0);
+      }
+      // Rows of this lane that can enter its list: valid item, not pad, not history.
+      // C[item row][user col]: rows (r&3) + 8*(r>>2) + 4h
+      const int64_t sb = base + 32 * sub;
+      const uint32_t hm = hmask[cur][sub][ul];
+      uint32_t ok = 0;
+      float best = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float sc = acc[r];
-        if (((ok >> r) & 1u) && sc > thr) {
-          topk_insert<KC>(ts, ti, sc, (int)(base + row));
-          thr = fmaxf(thr, ts[KC - 1]);
+        const int64_t item = sb + row;
+        const bool valid = qv & (item < ihi) & (item != 0) & !((hm >> row) & 1u);
+        ok |= (valid ? 1u : 0u) << r;
+        best = fmaxf(best, valid ? acc[r] : -INFINITY);
+      }
+      // The two lanes of a user scan disjoint item halves; an item below the
+      // partner's K-th best already has K better items, so it can never reach the
+      // final (merged) top-K: filter with the stronger of the two thresholds.
+      thr = fmaxf(thr, __shfl_xor(thr, 32, 64));
+#ifdef MIREC_FS_NO_TOPK   // profiling variant (tools/build_variant.sh): MFMA + mask only
+      thr = fmaxf(thr, best);
+      if (false) {
+#else
+      if (__any(best > thr)) {             // wave-uniform: rare once the lists fill up
+#endif
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float sc = acc[r];
+          if (((ok >> r) & 1u) && sc > thr) {
+            topk_insert<KC>(ts, ti, sc, (int)(sb + row));
+            thr = fmaxf(thr, ts[KC - 1]);
+          }
         }
       }
     }
     if (more) {
-      build_mask(base + 32, hmask[cur ^ 1]);
-      store_tile(tile[cur ^ 1]);
+      build_mask(base + TI, hmask[cur ^ 1]);
+      store_tile(tile[cur ^ 1], PH - 1);
     }
     __syncthreads();
     cur ^= 1;
@@ -398,7 +430,7 @@ extern "C" int mirec_fullsort_topk_f32(const float* Uq, int64_t nq, const float*
 #define MIREC_FS(DD, KK)                                                                      \
   hipLaunchKernelGGL((fullsort_topk_kernel<DD, KK>), grd, dim3(kFsThreads), 0, st, Uq, nq, EI, \
                      I, hist_ptr, hist_cols, pos_ptr, pos_cols, K, top_scores, top_ids,        \
-                     pos_flags, (int64_t)((I + 31) / 32 * 32))
+                     pos_flags, (int64_t)((I + 63) / 64 * 64))
 #define MIREC_FS_D(DD)                                 \
   case DD:                                             \
     if (K <= 10) MIREC_FS(DD, 10);                     \
@@ -449,8 +481,8 @@ extern "C" int mirec_fullsort_topk_split_f32(const float* Uq, int64_t nq, const 
   }
   float* ps = (float*)ws;
   int32_t* pi = (int32_t*)(ps + (size_t)n_split * nq * K);
-  const int64_t tiles = (I + 31) / 32;
-  const int64_t span = (tiles + n_split - 1) / n_split * 32;
+  const int64_t tiles = (I + 63) / 64;               // 64: a multiple of every kernel's tile
+  const int64_t span = (tiles + n_split - 1) / n_split * 64;
   const int S = (int)((I + span - 1) / span);
   const dim3 grd((unsigned)((nq + 127) / 128), (unsigned)S);
   hipStream_t st = (hipStream_t)stream;
