@@ -240,7 +240,7 @@ def test_sharded_cap_overflow_replans(tmp_path, graph):
         assert torch.equal(a, b)
 
 
-def _worker(rank, port, root, q, cap=None, exchange='rccl'):
+def _worker(rank, port, root, q, cap=None, exchange='rccl', sel=None):
     import torch.distributed as tdist
     from recbole_amd.trainer.fused import ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
@@ -253,8 +253,12 @@ def _worker(rank, port, root, q, cap=None, exchange='rccl'):
         step = ShardedBPRTrainStep(model, opt, train, chunk=CHUNK, dist=tdist.group.WORLD,
                                    cap=cap, exchange=exchange)
         assert step.exchange == exchange
+        if sel is not None:                       # owner-filtered grouping too small: the
+            step.cap_sel = dict(sel)              # chunks are re-selected at full size
+        sel_growths0 = step.sel_growths
         tensors, losses = _train(step)
         assert cap is None or step.cap_growths >= 1
+        assert sel is None or step.sel_growths > sel_growths0
         if step.win is not None:                  # no wait gave up (end_epoch raises too)
             assert step.win.status() == 0
         step.close()
@@ -263,10 +267,13 @@ def _worker(rank, port, root, q, cap=None, exchange='rccl'):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize('cap,exchange', [(None, 'rccl'), (40, 'rccl'), (None, 'ipc'),
-                                          (40, 'ipc')])
-def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange):
+@pytest.mark.parametrize('cap,exchange,sel', [(None, 'rccl', None), (40, 'rccl', None),
+                                              (None, 'rccl', {'u': 4, 'i': 12}),
+                                              (None, 'ipc', None), (40, 'ipc', None)])
+def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange, sel):
     """cap=40: both ranks detect the same overflow and grow cap identically.
+    sel: an owner-filtered grouping too small for the batches' owned slots — every chunk
+    is re-selected at full size before it runs (ShardedBPRTrainStep._grow_sel).
     exchange='ipc': the rows go through the peer windows (csrc/comm.hip: IPC-mapped, in-
     kernel stores, flags on the GPU). Both ranks share cuda:0 here, so this pins the flag /
     counter protocol, the push lists and the owner-Adam fold — NOT the cross-device mapping
@@ -277,7 +284,7 @@ def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap, exchange))
+    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap, exchange, sel))
              for r in range(2)]
     for p in procs:
         p.start()
