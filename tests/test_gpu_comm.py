@@ -1,6 +1,6 @@
 """The generic cross-GPU entry points of the C-ABI (mirec_alltoallv_rows_f32,
-mirec_allreduce_sum_f32; csrc/comm.hip) with two ranks (spawned processes, a gloo group
-for the IPC handle exchange, both on cuda:0 — this covers the flag / barrier protocol,
+mirec_allreduce_sum_f32; csrc/comm.hip) with 2 and 3 ranks (spawned processes, a gloo group
+for the IPC handle exchange, all on cuda:0 — this covers the flag / barrier protocol,
 not xGMI itself):
   * ragged send_counts, the received blocks and recv_counts exact;
   * all-reduce bit-identical to the rank-order sum torch computes on the host;
@@ -20,10 +20,10 @@ from conftest import free_port
 
 pytestmark = pytest.mark.gpu
 
-WORLD, WCAP, D, ROUNDS = 2, 96, 64, 6
+WCAP, D, ROUNDS = 96, 64, 6
 
 
-def _data(rank, r):
+def _data(rank, r, WORLD):
     g = torch.Generator().manual_seed(1000 * r + rank)
     send = torch.randn(WORLD, WCAP, D, generator=g)
     counts = torch.randint(0, WCAP + 1, (WORLD,), generator=g)
@@ -32,7 +32,7 @@ def _data(rank, r):
     return send, counts, vec
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, WORLD):
     import ctypes
 
     import torch.distributed as tdist
@@ -50,7 +50,7 @@ def _worker(rank, port, q):
         outs = []
         keep = []
         for r in range(ROUNDS):                       # no host sync inside the loop
-            send, counts, vec = _data(rank, r)
+            send, counts, vec = _data(rank, r, WORLD)
             s_d, c_d = send.to(dev), counts.to(dev)
             recv = torch.full((WORLD, WCAP, D), -7.0, device=dev)
             rc = torch.full((WORLD,), -1, dtype=torch.int64, device=dev)
@@ -71,11 +71,12 @@ def _worker(rank, port, q):
         tdist.destroy_process_group()
 
 
-def test_alltoallv_and_allreduce_two_ranks():
+@pytest.mark.parametrize('WORLD', [2, 3])
+def test_alltoallv_and_allreduce_ranks(WORLD):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, WORLD)) for r in range(WORLD)]
     for p in procs:
         p.start()
     got = dict((r, (s, res)) for r, s, res in (q.get(timeout=300) for _ in range(WORLD)))
@@ -88,7 +89,7 @@ def test_alltoallv_and_allreduce_two_ranks():
         for r, (recv, rc, buf) in enumerate(res):
             exp_sum = None
             for src in range(WORLD):
-                send, counts, vec = _data(src, r)
+                send, counts, vec = _data(src, r, WORLD)
                 n = int(counts[me])
                 assert rc[src] == n, (me, r, src)
                 np.testing.assert_array_equal(recv[src, :n], send[me, :n].numpy())
