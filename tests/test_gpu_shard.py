@@ -240,12 +240,12 @@ def test_sharded_cap_overflow_replans(tmp_path, graph):
         assert torch.equal(a, b)
 
 
-def _worker(rank, port, root, q, cap=None, exchange='rccl', sel=None):
+def _worker(rank, port, root, q, cap=None, exchange='rccl', sel=None, world=2):
     import torch.distributed as tdist
     from recbole_amd.trainer.fused import ShardedBPRTrainStep
     from recbole_amd.trainer.optim import FusedAdam
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    tdist.init_process_group('gloo', rank=rank, world_size=2)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         config, train, valid, test, model = _pipeline(root, 256)
@@ -267,11 +267,13 @@ def _worker(rank, port, root, q, cap=None, exchange='rccl', sel=None):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize('cap,exchange,sel', [(None, 'rccl', None), (40, 'rccl', None),
-                                              (None, 'rccl', {'u': 4, 'i': 12}),
-                                              (None, 'ipc', None), (40, 'ipc', None)])
-def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange, sel):
-    """cap=40: both ranks detect the same overflow and grow cap identically.
+@pytest.mark.parametrize('cap,exchange,sel,world', [(None, 'rccl', None, 2), (40, 'rccl', None, 2),
+                                                    (None, 'rccl', {'u': 4, 'i': 12}, 2),
+                                                    (None, 'ipc', None, 2), (40, 'ipc', None, 2),
+                                                    (None, 'rccl', None, 3), (None, 'ipc', None, 3)])
+def test_sharded_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange, sel, world):
+    """world ranks (2, 3) bitwise equal to one process on the global batch.
+    cap=40: every rank detects the same overflow and grows cap identically.
     sel: an owner-filtered grouping too small for the batches' owned slots — every chunk
     is re-selected at full size before it runs (ShardedBPRTrainStep._grow_sel).
     exchange='ipc': the rows go through the peer windows (csrc/comm.hip: IPC-mapped, in-
@@ -284,21 +286,21 @@ def test_sharded_two_ranks_equal_one_gpu_global_batch(tmp_path, cap, exchange, s
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap, exchange, sel))
-             for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, root, q, cap, exchange, sel, world))
+             for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=600) for _ in range(2)]
+    got = [q.get(timeout=600) for _ in range(world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    config, train, valid, test, model = _pipeline(root, 512)
+    config, train, valid, test, model = _pipeline(root, 256 * world)
     opt = FusedAdam(model.parameters(), lr=config['learning_rate'])
     step = FusedBPRTrainStep(model, opt, train, chunk=CHUNK)
     assert train.dataset.inter_num % step.B != 0            # a ragged last batch
     ref_t, ref_l = _train(step)
     for rank, Bg, SU, tensors, losses in got:
-        assert Bg == step.B and SU == -(-step.nU // 2)
+        assert Bg == step.B and SU == -(-step.nU // world)
         assert losses == ref_l, rank
         for a, b in zip(ref_t, tensors):
             assert np.array_equal(a.numpy(), b), (rank, np.abs(a.numpy() - b).max())
