@@ -260,7 +260,7 @@ def roofline(step, events, uniq, d, M, W=None, K=None):
     if fused:   # + the BPR arithmetic K35 also does: (1+T) dots of 2d and 8d per pair
         flops += M * B * ((1 + T) * 2 * d + T * 8 * d)
     tf = flops / t_adam / 1e12
-    flush_k = 'adam_flush_row_kernel' if d >= 64 else 'adam_flush_kernel'
+    flush_k = 'adam_flush_row_kernel' if d >= 64 else 'adam_flush_list_kernel'
     per_k = f'bpr_adam_step_kernel<{d}>' if fused else f'adam_deferred_kernel<{d},'
     nd, nf = len(per.get(step_key, [])) + len(per.get('ahead', [])), len(per.get('flush', []))
     if fused:

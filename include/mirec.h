@@ -524,6 +524,16 @@ int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n_tables,
                             const float* step_consts_dev, const int32_t* step_base_dev,
                             int32_t step_off, double beta1, double beta2, double eps,
                             double weight_decay, void* stream);
+/* The deferred schedule (same semantics, same results) for a PAIR of tables in one
+ * launch: tables[0] of width d (4..256) and tables[1] of width 1 — DeepFM's token
+ * embeddings and first-order weights, which share the rows, the grouping and the step
+ * (replaces FusedAdam's two mirec_adam_deferred_f32 launches, at the forward's catch-up
+ * and at the step; reference: the optim.Adam.step of trainer.py:173 over both tables of
+ * deepfm.py / layers.py FMEmbedding + FMFirstOrderLinear). n_max_uniq: HOST array of 2. */
+int mirec_adam_deferred_pair_f32(const mirec_adam_table* tables, const int64_t* n_max_uniq,
+                                 int32_t d, const float* step_consts_dev,
+                                 const int32_t* step_base_dev, int32_t step_off, double beta1,
+                                 double beta2, double eps, double weight_decay, void* stream);
 
 /* Flush of the deferred schedule: every row r of every table with
  * last[r] < t = step_base_dev[0] + step_off replays steps last[r]..t-1 with a

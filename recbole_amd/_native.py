@@ -187,6 +187,9 @@ SIGNATURES = {
     "mirec_adam_deferred_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, _P, c_int32, _P,
                                         _P, c_int32, c_double, c_double, c_double, c_double,
                                         _P]),
+    "mirec_adam_deferred_pair_f32": (c_int, [ctypes.POINTER(AdamTable), _P, c_int32, _P, _P,
+                                             c_int32, c_double, c_double, c_double, c_double,
+                                             _P]),
     "mirec_adam_flush_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,
                                      c_int32, c_double, c_double, c_double, c_double, _P]),
     "mirec_adam_flush_rows_f32": (c_int, [ctypes.POINTER(AdamTable), c_int32, c_int32, _P, _P,

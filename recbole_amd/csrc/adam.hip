@@ -3,7 +3,7 @@
 //
 //  * streamed (adam_multi_kernel): one pass over p, m, v of EVERY row each step
 //    (6 * n_rows * d * 4 bytes per step, the HBM roofline of the step);
-//  * deferred (adam_deferred_kernel + adam_flush_kernel): a row whose gradient is
+//  * deferred (adam_deferred_kernel + the flush kernels): a row whose gradient is
 //    zero at step s is advanced by exactly the same per-element operations as
 //    the streamed kernel would apply — but only when the row is next touched,
 //    or at a flush. `last[row]` counts the steps already applied to the row. A
@@ -113,14 +113,14 @@ __host__ __device__ constexpr int deferred_block(int vpr) {
   return vpr > MIREC_DEFERRED_MIN_BLOCK ? vpr : MIREC_DEFERRED_MIN_BLOCK;
 }
 
+// One block of segment si (table si >> 1; touched rows, or look-ahead rows when si is odd).
 template <int D, typename V>
-__global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
-    const AdamTables tabs, const float* __restrict__ consts,
-    const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
+__device__ __forceinline__ void deferred_block_rows(const AdamTables& tabs, int si,
+                                                    const float* __restrict__ consts, int st,
+                                                    const AdamConsts& k) {
   constexpr int VPR = D / Lanes<V>::n;              // V = float or float2 per thread
   constexpr int RPB = deferred_block(VPR) / VPR;    // rows per block
   static_assert(deferred_block(VPR) % VPR == 0, "row width");
-  const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si >> 1];
   const bool ahead = si & 1;
   const int u = (int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) + threadIdx.x / VPR;
@@ -129,43 +129,111 @@ __global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
   // the grid is sized for the host's bound on the lists: blocks past the actual
   // count leave at once (block-uniform: no thread reaches the barrier below)
   if ((int)(((int64_t)blockIdx.x - tabs.block_start[si]) * RPB) >= n) return;
-  deferred_row<D, V>(T, ahead, u, n, step_base[0] + step_off, consts, k, c,
-                     [](bool, bool, int64_t, const V&) {});
+  deferred_row<D, V>(T, ahead, u, n, st, consts, k, c, [](bool, bool, int64_t, const V&) {});
 }
 
-// Bring every row up to `n_steps` applied steps (zero-gradient replays).
+template <int D, typename V>
+__global__ __launch_bounds__(kAdamThreads) void adam_deferred_kernel(
+    const AdamTables tabs, const float* __restrict__ consts,
+    const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
+  deferred_block_rows<D, V>(tabs, segment_of(tabs, blockIdx.x), consts, step_base[0] + step_off,
+                            k);
+}
+
+// A [V, D] table and a [V, 1] table in one launch (DeepFM's token embeddings and their
+// first-order weights: the same rows, the same step; they ran as two launches of ~6 us
+// each, twice a step — catch-up and step — where each launch is a dependent-load chain
+// that leaves most of the chip idle). Segments 0, 1: table 0 (width D, V columns per
+// lane); 2, 3: table 1 (one float per lane). Both block shapes are 256 lanes.
+template <int D, typename V>
+__global__ __launch_bounds__(kAdamThreads) void adam_deferred_pair_kernel(
+    const AdamTables tabs, const float* __restrict__ consts,
+    const int32_t* __restrict__ step_base, int step_off, AdamConsts k) {
+  static_assert(deferred_block(D / Lanes<V>::n) == deferred_block(1), "one block shape");
+  const int si = segment_of(tabs, blockIdx.x);
+  const int st = step_base[0] + step_off;
+  if (si < 2)
+    deferred_block_rows<D, V>(tabs, si, consts, st, k);
+  else
+    deferred_block_rows<1, float>(tabs, si, consts, st, k);
+}
+
+// Flush of narrow rows (d < 64; d = 1 is DeepFM's first-order [V, 1] table): a block owns
+// kFlushRows consecutive rows. Its threads read the rows' `last` marks in one coalesced
+// pass (kFlushRows / 256 independent loads per thread), the rows that lag are listed in
+// LDS, and only those are loaded and replayed, VPR lanes per row (float4 columns; one
+// float per lane at d = 1). The list's order depends on the LDS atomics, the results do
+// not: every row's replay is its own (adam_replay's wave votes only skip p updates that
+// provably round away). The form this replaces walked its rows in 16 dependent passes,
+// loaded or not: 371 us for DeepFM's 33 M-row token table (+71 us for the [V, 1] one)
+// where the `last` reads alone are 132 MB (~17 us at HBM rate).
+template <int D> struct NarrowVec { using T = float4; static constexpr int vpr = D / 4; };
+template <> struct NarrowVec<1> { using T = float; static constexpr int vpr = 1; };
+
 template <int D>
-__global__ __launch_bounds__(kAdamThreads) void adam_flush_kernel(
+__global__ __launch_bounds__(kAdamThreads) void adam_flush_list_kernel(
     const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
     int step_off, AdamConsts k) {
-  constexpr int VPR = D / 4;
-  constexpr int RPP = kAdamThreads / VPR;
+  using V = typename NarrowVec<D>::T;
+  constexpr int VPR = NarrowVec<D>::vpr;
+  constexpr int RPP = kAdamThreads / VPR;           // rows per pass
+  constexpr int PER = kFlushRows / kAdamThreads;    // `last` loads per thread
+  static_assert(kFlushRows % kAdamThreads == 0 && kAdamThreads % VPR == 0, "block shape");
+  __shared__ int32_t s_row[kFlushRows];             // lagging rows (offset in the block)
+  __shared__ int32_t s_last[kFlushRows];            // and their marks
+  __shared__ int32_t s_n;
   const int si = segment_of(tabs, blockIdx.x);
   const mirec_adam_table& T = tabs.t[si];
   const int64_t lo = ((int64_t)blockIdx.x - tabs.block_start[si]) * kFlushRows;
-  const int64_t hi = min(T.n_rows, lo + kFlushRows);
   const int target = step_base[0] + step_off;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) s_n = 0;
+  int raw[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int64_t r = lo + j * kAdamThreads + threadIdx.x;
+    raw[j] = r < T.n_rows ? T.last[r] : target;
+  }
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const bool need = min(raw[j], target) < target;
+    const uint64_t b = __ballot(need);
+    int at = 0;
+    if (lane == 0 && b) at = atomicAdd(&s_n, __popcll(b));
+    at = __shfl(at, 0, 64);
+    if (need) {
+      const int pos = at + __popcll(b & below);
+      s_row[pos] = j * kAdamThreads + threadIdx.x;
+      s_last[pos] = raw[j];
+    }
+  }
+  __syncthreads();
+  const int n = s_n;
   const int rsub = threadIdx.x / VPR;
   const int c = threadIdx.x % VPR;
-  // wave-uniform trip count (adam_replay's step loop runs over the whole wave)
-  for (int64_t base = lo; base < hi; base += RPP) {
-    const int64_t r = base + rsub;
-    const bool valid = r < hi;
-    const int last = valid ? min(T.last[r], target) : target;
-    const bool work = last < target;
+  for (int base = 0; base < n; base += RPP) {       // block-uniform trip count
+    const int i = base + rsub;
+    const bool work = i < n;
+    const int64_t r = lo + (work ? s_row[i] : 0);
+    const int last = work ? min(s_last[i], target) : target;
     const int64_t off = r * VPR + c;
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
+    V p, m, v;
+    memset(&p, 0, sizeof(V));
+    m = p;
+    v = p;
     if (work) {
-      p = reinterpret_cast<const float4*>(T.p)[off];
-      m = reinterpret_cast<const float4*>(T.m)[off];
-      v = reinterpret_cast<const float4*>(T.v)[off];
+      p = reinterpret_cast<const V*>(T.p)[off];
+      m = reinterpret_cast<const V*>(T.m)[off];
+      v = reinterpret_cast<const V*>(T.v)[off];
     }
     adam_replay(p, m, v, last, target, consts, k);
     if (work) {
-      reinterpret_cast<float4*>(T.p)[off] = p;
-      reinterpret_cast<float4*>(T.m)[off] = m;
-      reinterpret_cast<float4*>(T.v)[off] = v;
-      if (c == 0) T.last[r] = target;  // a row lies in one wave here (VPR <= 64)
+      reinterpret_cast<V*>(T.p)[off] = p;
+      reinterpret_cast<V*>(T.m)[off] = m;
+      reinterpret_cast<V*>(T.v)[off] = v;
+      if (c == 0) T.last[r] = target;
     }
   }
 }
@@ -274,44 +342,13 @@ __global__ __launch_bounds__(kAdamThreads) void adam_flush_scan_kernel(
   }
 }
 
-// Flush of a width-1 table (DeepFM's first-order [V, 1] weights): one row per
-// lane; the rows of a wave lag by different step counts, so the general replay
-// (wave-uniform step loop from the wave's smallest count, lanes active from their
-// own) applies.
-__global__ __launch_bounds__(kAdamThreads) void adam_flush_scalar_kernel(
-    const AdamTables tabs, const float* __restrict__ consts, const int32_t* __restrict__ step_base,
-    int step_off, AdamConsts k) {
-  const int si = segment_of(tabs, blockIdx.x);
-  const mirec_adam_table& T = tabs.t[si];
-  const int target = step_base[0] + step_off;
-  const int64_t r0 = ((int64_t)blockIdx.x - tabs.block_start[si]) * kFlushScalarRows;
-  for (int64_t r = r0 + threadIdx.x; r < r0 + kFlushScalarRows; r += kAdamThreads) {
-    const bool valid = r < T.n_rows;
-    const int last = valid ? min(T.last[r], target) : target;
-    if (__all(last >= target)) continue;         // wave-uniform
-    float p = 0.f, m = 0.f, v = 0.f;
-    if (last < target) {
-      p = T.p[r];
-      m = T.m[r];
-      v = T.v[r];
-    }
-    adam_replay(p, m, v, last, target, consts, k);
-    if (last < target) {
-      T.p[r] = p;
-      T.m[r] = m;
-      T.v[r] = v;
-      T.last[r] = target;
-    }
-  }
-}
-
 }  // namespace mirec
 
 using namespace mirec;
 
 namespace {
 
-enum class Sched { kStreamed, kDeferred, kFlush };
+enum class Sched { kStreamed, kDeferred, kFlush, kDeferredPair };
 
 int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                 const int64_t* n_max_uniq, int32_t d, const float* consts,
@@ -332,6 +369,16 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     return -1;
   }
   const int VPR = d / 4;
+  // deferred pair (mirec_adam_deferred_pair_f32): tables[0] width d, tables[1] width 1
+  const bool pair = sched == Sched::kDeferredPair;
+  if (pair) {
+    if (n_tables != 2 || d == 1) {
+      set_error("%s: a pair is two tables, the first of width d > 1 (got %d tables, d=%d)",
+                what, n_tables, d);
+      return -1;
+    }
+    sched = Sched::kDeferred;
+  }
   // flush with R rows per wave (adam_flush_scan_kernel): d >= 64, R in [1, 64] per table
   FlushRows fr;
   bool scan = false;
@@ -358,7 +405,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
   int dvec = 1;
   if (deferred && n_max_uniq && d >= 4) {
     int64_t waves = 0;
-    for (int q = 0; q < n_tables; ++q)
+    for (int q = 0; q < (pair ? 1 : n_tables); ++q)
       if (n_max_uniq[q] > 0)
         waves += n_max_uniq[q] * (tables[q].ahead_uniq ? 2 : 1) * ((d + 63) / 64);
     if (waves > 16 * 1024) dvec = 2;
@@ -375,14 +422,14 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       set_error("%s: bad table %d", what, q);
       return -1;
     }
-    if (t.p_alt && (sched == Sched::kStreamed || d < 64)) {
+    if (t.p_alt && (sched == Sched::kStreamed || d < 64 || pair)) {
       set_error("%s: table %d: parity buffer (p_alt) needs the deferred schedule and d >= 64",
                 what, q);
       return -1;
     }
     tabs.t[q] = t;
     if (deferred) {
-      const int rpb = deferred_block(d / dvec) / (d / dvec);
+      const int rpb = (pair && q == 1) ? deferred_block(1) : deferred_block(d / dvec) / (d / dvec);
       const int64_t nb = (n_max_uniq[q] + rpb - 1) / rpb;
       tabs.block_start[2 * q] = blocks;
       blocks += nb;
@@ -391,8 +438,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     } else {
       tabs.block_start[q] = blocks;
       const int64_t rows_per_block =
-          d == 1 ? kFlushScalarRows                // adam_flush_scalar_kernel
-          : scan ? (int64_t)(kAdamThreads / 64) * fr.r[q]
+          scan ? (int64_t)(kAdamThreads / 64) * fr.r[q]
           : (sched == Sched::kFlush && d >= 64) ? kFlushRowThreads / 64
           : sched == Sched::kFlush ? kFlushRows
                                    : kAdamRows;
@@ -417,6 +463,11 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
     if (sched == Sched::kStreamed)                                                           \
       hipLaunchKernelGGL(adam_multi_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
                          step_off, k);                                                       \
+    else if (deferred && pair)                                                               \
+      hipLaunchKernelGGL((dvec == 2 ? adam_deferred_pair_kernel<DD, float2>                  \
+                                    : adam_deferred_pair_kernel<DD, float>),                 \
+                         grd, dim3(deferred_block(1)), 0, st, tabs, consts, step_base,       \
+                         step_off, k);                                                       \
     else if (deferred)                                                                       \
       hipLaunchKernelGGL((dvec == 2 ? adam_deferred_kernel<DD, float2>                       \
                                     : adam_deferred_kernel<DD, float>),                      \
@@ -430,8 +481,8 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                          dim3(kFlushRowThreads), 0, st, tabs,                                \
                          consts, step_base, step_off, k);                                    \
     else                                                                                     \
-      hipLaunchKernelGGL(adam_flush_kernel<DD>, grd, blk, 0, st, tabs, consts, step_base,    \
-                         step_off, k);                                                       \
+      hipLaunchKernelGGL(adam_flush_list_kernel<(DD < 64 ? DD : 16)>, grd, blk, 0, st, tabs, \
+                         consts, step_base, step_off, k);                                    \
     break;
   switch (d) {
     case 1:
@@ -439,7 +490,7 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
         hipLaunchKernelGGL((adam_deferred_kernel<1, float>), grd, dim3(deferred_block(1)), 0, st,
                            tabs, consts, step_base, step_off, k);
       else
-        hipLaunchKernelGGL(adam_flush_scalar_kernel, grd, blk, 0, st, tabs, consts, step_base,
+        hipLaunchKernelGGL(adam_flush_list_kernel<1>, grd, blk, 0, st, tabs, consts, step_base,
                            step_off, k);
       break;
     MIREC_ADAM_SCHED(4)
@@ -473,6 +524,17 @@ extern "C" int mirec_adam_deferred_f32(const mirec_adam_table* tables, int32_t n
   return launch_adam(Sched::kDeferred, tables, n_tables, n_max_uniq, d, step_consts_dev,
                      step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
                      "mirec_adam_deferred_f32");
+}
+
+extern "C" int mirec_adam_deferred_pair_f32(const mirec_adam_table* tables,
+                                            const int64_t* n_max_uniq, int32_t d,
+                                            const float* step_consts_dev,
+                                            const int32_t* step_base_dev, int32_t step_off,
+                                            double beta1, double beta2, double eps,
+                                            double weight_decay, void* stream) {
+  return launch_adam(Sched::kDeferredPair, tables, 2, n_max_uniq, d, step_consts_dev,
+                     step_base_dev, step_off, beta1, beta2, eps, weight_decay, stream,
+                     "mirec_adam_deferred_pair_f32");
 }
 
 extern "C" int mirec_adam_flush_f32(const mirec_adam_table* tables, int32_t n_tables, int32_t d,

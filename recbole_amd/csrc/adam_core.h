@@ -36,10 +36,9 @@ static __device__ unsigned long long g_work[16];
 
 constexpr int kAdamThreads = 256;
 constexpr int kAdamRows = 64;  // table rows per block (streamed)
-// Flush of narrow rows (d < 64): rows per block, looped in passes of 256 / (d / 4) rows —
-// a whole-table flush of DeepFM's 33 M token rows dispatched 516 K one-pass blocks
+// Flush of narrow rows (d < 64, d = 1; adam_flush_list_kernel): rows per block (their
+// `last` marks are read in one pass, the lagging ones listed in LDS)
 constexpr int kFlushRows = 1024;
-constexpr int kFlushScalarRows = 2048;   // d = 1: eight passes of 256 rows
 constexpr int kMaxTables = 4;
 // last[row] mark of the deferred schedule (MIREC_ADAM_ZERO_STATE in mirec.h): the
 // row's m and v are all +0 and weight_decay is 0, so every zero-gradient step is

@@ -158,6 +158,10 @@ class _CtxFMFn(torch.autograd.Function):
                   for k, v in tables.items()}
         keys = torch.empty(len(layout.token_names) * B, dtype=torch.int64, device=bias.device)
         h = getattr(T, '_mirec_deferred', None) if T is not None else None
+        h1 = getattr(T1, '_mirec_deferred', None) if T1 is not None else None
+        # the first-order [V, 1] table is read by the same keys: caught up with T (one
+        # launch, mirec_adam_deferred_pair_f32) when the same optimizer runs both
+        pair = T1 if (h1 is not None and h1 is h) else None
         if h is not None:                     # deferred Adam: complete the rows read
             # keys[f*B + i] = id + the field's table offset, every field in one launch
             cols = [_col(interaction, n, torch.int64) for n in layout.token_names]
@@ -169,7 +173,7 @@ class _CtxFMFn(torch.autograd.Function):
                 # one launch
                 keys, segs = ops.segment_sort_fields(cols, layout.token_offsets, B, T.shape[0],
                                                      status)
-                ctx.segs = h.catch_up(T, keys, segs=segs)
+                ctx.segs = h.catch_up(T, keys, segs=segs, pair=pair)
             else:
                 cptr = (ctypes.c_void_p * nt)(*[ptr(x) for x in cols])
                 offs = (ctypes.c_int64 * nt)(*layout.token_offsets)
@@ -178,9 +182,8 @@ class _CtxFMFn(torch.autograd.Function):
                 # one key block per field (ranges increase with the field offsets): K2
                 # sorts each field's B keys in LDS instead of a device-wide radix sort
                 blocks = B if (layout.blocks_ok and 0 < B <= 8192 and nt > 1) else None
-                ctx.segs = h.catch_up(T, keys, blocks=blocks)
-            h1 = getattr(T1, '_mirec_deferred', None)
-            if h1 is not None:                # the first-order [V, 1] table, same rows
+                ctx.segs = h.catch_up(T, keys, blocks=blocks, pair=pair)
+            if h1 is not None and pair is None:   # the first-order [V, 1] table, same rows
                 h1.catch_up(T1, keys, ctx.segs)
         else:
             ctx.segs = None

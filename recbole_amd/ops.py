@@ -898,7 +898,8 @@ def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
                schedule: str = "streamed", n_max_uniq=None, beta1=0.9, beta2=0.999, eps=1e-8,
                weight_decay=0.0, flush_rows=None):
     """K5 over several tables in one launch: schedule 'streamed' (every row),
-    'deferred' (touched rows, replaying skipped zero-gradient steps) or 'flush'
+    'deferred' (touched rows, replaying skipped zero-gradient steps), 'deferred_pair'
+    (two tables, widths d and 1, same semantics, one launch) or 'flush'
     (flush_rows: rows per wave per table, mirec_adam_flush_rows_f32; None = one wave
     per row)."""
     import ctypes
@@ -911,6 +912,9 @@ def adam_multi(tables, d: int, step_consts, step_base, step_off: int = 0,
     elif schedule == "deferred":
         nm = (ctypes.c_int64 * len(tables))(*n_max_uniq)
         rc = lib().mirec_adam_deferred_f32(tables, len(tables), nm, d, *args)
+    elif schedule == "deferred_pair":          # tables: ([V, d], [V, 1]), one launch
+        nm = (ctypes.c_int64 * 2)(*n_max_uniq)
+        rc = lib().mirec_adam_deferred_pair_f32(tables, nm, d, *args)
     elif schedule == "flush" and flush_rows is not None:
         rpw = (ctypes.c_int32 * len(tables))(*flush_rows)
         rc = lib().mirec_adam_flush_rows_f32(tables, len(tables), d, rpw, *args)

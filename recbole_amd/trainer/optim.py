@@ -118,9 +118,13 @@ class FusedAdam(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         deferred = getattr(self, '_deferred', {})
         params = [p for p in self._params() if p.grad is not None and p not in deferred]
-        self._pair_reduce(deferred)
+        done = set()
+        for p, q in self._pair_reduce(deferred):
+            if self._pair_step(p, q):
+                done.update((p, q))
         for p in deferred:
-            self._deferred_step(p)
+            if p not in done:
+                self._deferred_step(p)
         advanced = False
         if params:
             advanced = self._dense_step(params)
@@ -269,14 +273,29 @@ class FusedAdam(torch.optim.Optimizer):
                 ds['marked'] = True
         return ds
 
-    def _dtable(self, p, ds, **kw):
+    def _dspec(self, p, ds, **kw):
         st = self.state[p]
         pt = ds['shard']['p'] if 'shard' in ds else p.data
         spec = {'p': pt, 'm': st['exp_avg'], 'v': st['exp_avg_sq'], 'last': ds['last']}
         spec.update(kw)
-        return ops.adam_tables([spec])
+        return spec
 
-    def catch_up(self, p, keys, segs=None, blocks=None, drop_key=None):
+    def _dtable(self, p, ds, **kw):
+        return ops.adam_tables([self._dspec(p, ds, **kw)])
+
+    def _pair_state(self, p, q):
+        """The deferred state of q when p ([V, d], d > 1) and q ([V, 1]) can share one
+        launch (mirec_adam_deferred_pair_f32): neither sharded, windows opened at the
+        same step (the same step constants), else None."""
+        dq = self._deferred.get(q) if q is not None else None
+        ds = self._deferred[p]
+        if (dq is None or 'shard' in dq or 'shard' in ds or q.shape[1] != 1 or p.shape[1] < 4
+                or p.shape[0] != q.shape[0]):
+            return None
+        ds, dq = self._dstate(p), self._dstate(q)
+        return dq if (dq['t0'] == ds['t0'] and dq['window'] == ds['window']) else None
+
+    def catch_up(self, p, keys, segs=None, blocks=None, drop_key=None, pair=None):
         """Make the rows `keys` (int64, any order / duplicates) current before a
         forward pass reads them; returns their K2 grouping (`segs`: the grouping
         when the caller already has it, e.g. another table read by the same keys;
@@ -287,7 +306,9 @@ class FusedAdam(torch.optim.Optimizer):
         stays untouched, which the deferred schedule makes bit-identical to a step with a
         zero gradient, and the reduction skips what can be half of a padded sequence
         batch's positions. Only with weight_decay 0: the row then never moves (a zero-
-        gradient step keeps m = v = 0 and p), so the forward may read it un-caught-up."""
+        gradient step keeps m = v = 0 and p), so the forward may read it un-caught-up.
+        pair: a [V, 1] table of this optimizer read by the same keys (DeepFM's first-order
+        weights): caught up too, in the same launch when _pair_state allows."""
         if (segs is None and drop_key is not None and 'shard' not in self._deferred[p]
                 and self._group_args()['weight_decay'] == 0):
             n_rows = p.shape[0]
@@ -303,19 +324,24 @@ class FusedAdam(torch.optim.Optimizer):
             segs = ops.segment_sort(keys.contiguous(), p.shape[0])
         if 'shard' in self._deferred[p]:
             self._catch_up_sharded(p, keys)
+            if pair is not None:
+                self.catch_up(pair, keys, segs)
             return segs
+        dq = self._pair_state(p, pair)
         ds = self._dstate(p)
         r = self.n_steps - ds['t0']
         if r > 0 or self._g is not None:      # (graph mode at r = 0: a no-op launch)
             class _Z:
                 perm = uniq = seg = self._dummy_i32
                 n_uniq = self._zero_i32
-            tab = self._dtable(p, ds, rows=self._dummy_f32, segs=_Z,
-                               ahead=(segs.uniq, segs.n_uniq))
+            kw = dict(rows=self._dummy_f32, segs=_Z, ahead=(segs.uniq, segs.n_uniq))
+            specs = [self._dspec(p, ds, **kw)] + ([self._dspec(pair, dq, **kw)] if dq else [])
             base, off = self._sref(r, -1)
-            ops.adam_multi(tab, p.shape[1], ds['consts'], base, off,
-                           schedule='deferred', n_max_uniq=[keys.numel()],
-                           **self._group_args())
+            ops.adam_multi(ops.adam_tables(specs), p.shape[1], ds['consts'], base, off,
+                           schedule='deferred_pair' if dq else 'deferred',
+                           n_max_uniq=[keys.numel()] * len(specs), **self._group_args())
+        if pair is not None and dq is None:
+            self.catch_up(pair, keys, segs)
         return segs
 
     def stash(self, p, rows, keys, segs=None):
@@ -355,6 +381,7 @@ class FusedAdam(torch.optim.Optimizer):
                and p.grad is None]
         wide = [(p, ds) for p, ds in one if 2 <= p.shape[1] <= 16]
         narrow = [(p, ds) for p, ds in one if p.shape[1] == 1]
+        pairs = []
         for p, ds in wide:
             rows, keys, segs = ds['stash'][0]
             for q, dq in narrow:
@@ -364,7 +391,32 @@ class FusedAdam(torch.optim.Optimizer):
                                                            r1.contiguous().view(-1, 1), segs)
                     ds['pre'] = (out, ident, ident.n)
                     dq['pre'] = (out1, ident, ident.n)
+                    pairs.append((p, q))
                     break
+        return pairs
+
+    def _pair_step(self, p, q):
+        """The deferred steps of a pair reduced together (_pair_reduce) in one launch
+        (mirec_adam_deferred_pair_f32) when _pair_state allows; False: not taken (each
+        table then takes _deferred_step)."""
+        dq = self._pair_state(p, q)
+        if dq is None or p.grad is not None or q.grad is not None:
+            return False
+        ds = self._deferred[p]
+        ds['stash'], dq['stash'] = [], []
+        rows, segs, n_keys = ds.pop('pre')
+        rows1, segs1, n1 = dq.pop('pre')
+        r = self.n_steps - ds['t0']
+        tabs = ops.adam_tables([self._dspec(p, ds, rows=rows.contiguous(), segs=segs),
+                                self._dspec(q, dq, rows=rows1.contiguous(), segs=segs1)])
+        base, off = self._sref(r, 0)
+        ops.adam_multi(tabs, p.shape[1], ds['consts'], base, off, schedule='deferred_pair',
+                       n_max_uniq=[n_keys, n1], **self._group_args())
+        if self._g is None and r + 1 >= ds['window']:   # window full: complete every row
+            for t, dt in ((p, ds), (q, dq)):
+                self._flush_table(t, dt, r + 1)
+                dt['t0'] = None
+        return True
 
     def _combine_stash(self, p, stash):
         """One summed gradient row per touched table row. Each source (one autograd

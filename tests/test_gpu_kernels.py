@@ -361,7 +361,8 @@ def test_fused_adam_dense_step_matches_torch(dev):
         torch.testing.assert_close(m.detach().cpu(), r.detach(), rtol=RTOL, atol=1e-6)
 
 
-@pytest.mark.parametrize('d,beta1,wd', [(128, 0.9, 0.0), (32, 0.3, 0.01), (64, 0.9, 0.0)])
+@pytest.mark.parametrize('d,beta1,wd', [(128, 0.9, 0.0), (32, 0.3, 0.01), (64, 0.9, 0.0),
+                                         (16, 0.9, 0.0), (4, 0.9, 0.0)])
 @pytest.mark.parametrize('wide', [False, True])    # True: a row bound that selects float2 columns
 @pytest.mark.parametrize('marks', [False, True])   # True: zero-state marks (MIREC_ADAM_ZERO_STATE)
 def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide, marks):
@@ -369,11 +370,12 @@ def test_adam_deferred_bitwise_equals_streamed(dev, d, beta1, wd, wide, marks):
     p, m, v bit-identical to the streamed dense Adam over every row. With marks,
     half the rows start from a nonzero (m, v) and the rest from +0 marked as a
     zero-gradient fixed point (skipped by look-aheads and flushes until their
-    first gradient step)."""
+    first gradient step). d = 16 / 4: tables over several 1,024-row blocks of the
+    narrow flush (adam_flush_list_kernel), the last one partial."""
     from recbole_amd import ops
     from recbole_amd.trainer.optim import FusedAdam
     g = torch.Generator().manual_seed(d)
-    sizes, R, steps = (300, 517), (40, 200), 37
+    sizes, R, steps = ((2500, 1031), (300, 200), 37) if d < 32 else ((300, 517), (40, 200), 37)
     init = [torch.randn(n, d, generator=g) * 0.1 for n in sizes]
     # a hot set touched often plus a cold tail touched rarely, as in a Zipf stream
     batches = []
@@ -492,6 +494,96 @@ def test_adam_flush_rows_equals_flush(dev, d, rows, target):
     ref, got = run(None), run(rows)
     for a, b in zip(ref, got):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+
+
+@pytest.mark.parametrize('d,wide', [(16, False), (16, True), (4, False), (128, False)])
+def test_adam_deferred_pair_equals_two_launches(dev, d, wide):
+    """mirec_adam_deferred_pair_f32 ([V, d] + [V, 1] tables, one launch) leaves every
+    buffer bit-identical to two mirec_adam_deferred_f32 launches: touched rows with
+    grouped gradients, look-ahead rows, rows in the zero state and lagging rows."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(d + wide)
+    n, nk, st = 3001, 900, 9
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(1))], lr=1e-2)
+    consts = torch.from_numpy(opt.step_constants(1, 64).reshape(-1)).to(dev)
+    base = torch.full((1,), st, dtype=torch.int32, device=dev)
+    keys = torch.randint(0, n // 3, (nk,), generator=g)
+    segs = ops.segment_sort(keys.to(dev), n)
+    ah = np.setdiff1d(torch.randint(0, n, (400,), generator=g).numpy(), keys.numpy())
+    ahead = (torch.as_tensor(ah.astype(np.int32), device=dev),
+             torch.tensor([len(ah)], dtype=torch.int32, device=dev))
+    state = []
+    for w in (d, 1):
+        P = torch.randn(n, w, generator=g) * 0.1
+        M = torch.randn(n, w, generator=g) * 1e-3
+        V = torch.rand(n, w, generator=g) * 1e-6
+        last = torch.randint(0, st + 1, (n,), generator=g, dtype=torch.int32)
+        zs = torch.rand(n, generator=g) < 0.3
+        last[zs] = ops.ADAM_ZERO_STATE
+        M[zs] = 0
+        V[zs] = 0
+        rows = torch.randn(nk, w, generator=g) * 0.05
+        state.append((P, M, V, last, rows))
+    nmax = [max(nk, 40000 if wide else 0)] * 2
+
+    def specs(bufs):
+        return [dict(p=P, m=M, v=V, last=L, rows=R, segs=segs, ahead=ahead)
+                for P, M, V, L, R in bufs]
+
+    def run(paired):
+        bufs = [[x.clone().to(dev) for x in s] for s in state]
+        sp = specs(bufs)
+        if paired:
+            ops.adam_multi(ops.adam_tables(sp), d, consts, base, 0, 'deferred_pair',
+                           n_max_uniq=nmax)
+        else:
+            for s, w in zip(sp, (d, 1)):
+                ops.adam_multi(ops.adam_tables([s]), w, consts, base, 0, 'deferred',
+                               n_max_uniq=nmax[:1])
+        return [x.cpu() for b in bufs for x in b[:4]]
+
+    ref, got = run(False), run(True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max()
+    assert bool((ref[3] == st + 1).any()) and bool((ref[7] == st + 1).any())
+
+
+@pytest.mark.parametrize('target', [7, 40])
+def test_adam_flush_width1_equals_columns(dev, target):
+    """The d = 1 flush (DeepFM's first-order [V, 1] table) replays each row exactly as
+    the d = 4 flush replays each column: a [n, 1] table flushed alone equals column 0
+    of the same values repeated over four columns (d = 4 is pinned to the streamed
+    Adam above). Rows lag by 0..target steps, sit in the zero state, or are current;
+    n spans several 1,024-row blocks with a partial last one."""
+    from recbole_amd import ops
+    from recbole_amd.trainer.optim import FusedAdam
+    g = torch.Generator().manual_seed(target)
+    n = 3077
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(1))], lr=1e-2)
+    consts = torch.from_numpy(opt.step_constants(1, 64).reshape(-1)).to(dev)
+    base = torch.full((1,), target, dtype=torch.int32, device=dev)
+    P = torch.randn(n, 1, generator=g) * 0.1
+    M = torch.randn(n, 1, generator=g) * 1e-3
+    V = torch.rand(n, 1, generator=g) * 1e-6
+    last = torch.randint(0, target + 1, (n,), generator=g, dtype=torch.int32)
+    kind = torch.randint(0, 4, (n,), generator=g)
+    last[kind == 0] = ops.ADAM_ZERO_STATE
+    M[kind == 0] = 0
+    V[kind == 0] = 0
+    out = {}
+    for d in (1, 4):
+        bufs = [x.repeat(1, d).contiguous().to(dev) for x in (P, M, V)] + [last.clone().to(dev)]
+        tabs = ops.adam_tables([dict(p=bufs[0], m=bufs[1], v=bufs[2], last=bufs[3])])
+        ops.adam_multi(tabs, d, consts, base, 0, 'flush')
+        out[d] = [x.cpu() for x in bufs]
+    for a, b in zip(out[1][:3], out[4][:3]):
+        assert torch.equal(a[:, 0], b[:, 0]), (a[:, 0] - b[:, 0]).abs().max()
+        assert torch.equal(b, b[:, :1].repeat(1, 4))
+    assert torch.equal(out[1][3], out[4][3])
+    assert bool(((out[1][3] == target) | (out[1][3] == ops.ADAM_ZERO_STATE)).all())
+    lag = (kind != 0) & (last < target)
+    assert bool((out[1][0][lag] != P[lag]).any())          # lagging rows did move
 
 
 @pytest.mark.parametrize('lr', [1e-3, 3e-2])
