@@ -916,6 +916,25 @@ int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const f
 int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
                          const float* gamma, const float* beta, float eps, float* out,
                          float* mean, float* rstd, void* stream);
+/* K9e  The attention core of MultiHeadAttention (reference layers.py:338-407, the lines
+ * scores = q k^T / sqrt(dh); + attention_mask; softmax; attn_dropout; @ v), L <= 64 and
+ * dh = 64, one workgroup per (sequence, head), fp32 MFMA. q, k, v, out / dout, dq, dk, dv:
+ * [B, L, H*64] row-major (the Linear outputs before transpose_for_scores; the context is
+ * written back in the same layout, i.e. after the reference's permute + view); mask:
+ * [B, L, L] additive (SASRec's [B, 1, L, L] extended mask); lse: [B*H, 64] floats (the
+ * forward writes each query row's log-sum-exp, the backward reads it). Dropout p > 0:
+ * counter-based draws (csrc/attn.hip header: seed, the device int64 counter — advanced by
+ * the forward's last block through the int32 ticket `arrive`, zero between launches),
+ * the keep bits written to keep_words [B*H, 64] uint64 and read back by the backward.
+ * Replaces torch's fused scaled_dot_product_attention and the context permute copy. */
+int mirec_attn_fwd_f32(const float* q, const float* k, const float* v, const float* mask,
+                       int64_t B, int32_t L, int32_t H, float dropout_p, uint64_t seed,
+                       int64_t* counter, int32_t* arrive, float* out, float* lse,
+                       uint64_t* keep_words, void* stream);
+int mirec_attn_bwd_f32(const float* q, const float* k, const float* v, const float* mask,
+                       const float* dout, const float* lse, const uint64_t* keep_words,
+                       int64_t B, int32_t L, int32_t H, float dropout_p, float* dq, float* dk,
+                       float* dv, void* stream);
 /* GELU (erf form) of the feed-forward block, forward and backward, elementwise. */
 int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream);
 int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, float* dx, void* stream);

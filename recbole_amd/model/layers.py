@@ -279,7 +279,55 @@ class _GeluFn(torch.autograd.Function):
         return dx
 
 
-SDPA = True     # MultiHeadAttention through torch's fused scaled_dot_product_attention
+SDPA = True     # fallback for shapes K9e does not take: torch's fused scaled_dot_product_attention
+K9E = True      # MultiHeadAttention's core through K9e (csrc/attn.hip) where it applies
+_ATTN_MODULES = [0]
+
+
+class _AttnFn(torch.autograd.Function):
+    """K9e (csrc/attn.hip): softmax(q k^T / sqrt(dh) + mask) -> dropout(p) -> @ v for the
+    [B, L, H*64] Linear outputs q, k, v (L <= 64), the context returned as [B, L, H*64]
+    (the reference's permute(0, 2, 1, 3) + view, layers.py:391-397, without the copy).
+    rng = (seed, device counter, ticket) when p > 0."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, mask, H, p, rng):
+        B, L, _ = q.shape
+        out = torch.empty_like(q)
+        lse = torch.empty(B * H, 64, dtype=torch.float32, device=q.device)
+        keep = torch.empty(B * H, 64, dtype=torch.int64, device=q.device) if p > 0 else None
+        seed, counter, arrive = rng if p > 0 else (0, None, None)
+        check(lib().mirec_attn_fwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), B, L, H, float(p),
+                                       seed, ptr(counter) if p > 0 else None,
+                                       ptr(arrive) if p > 0 else None, ptr(out), ptr(lse),
+                                       ptr(keep) if p > 0 else None, stream_handle()),
+              'mirec_attn_fwd_f32')
+        ctx.save_for_backward(q, k, v, mask, lse, keep)
+        ctx.H, ctx.p = H, p
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, mask, lse, keep = ctx.saved_tensors
+        B, L, _ = q.shape
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        check(lib().mirec_attn_bwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), ptr(g.contiguous()),
+                                       ptr(lse), ptr(keep) if keep is not None else None, B, L,
+                                       ctx.H, float(ctx.p), ptr(dq), ptr(dk), ptr(dv),
+                                       stream_handle()), 'mirec_attn_bwd_f32')
+        return dq, dk, dv, None, None, None, None
+
+
+def attn_k9e_applies(q, mask, n_heads, head_size):
+    """K9e's shapes: fp32 CUDA [B, L, H*64] with L <= 64 and a float32 additive mask of
+    B*L*L elements ([B, 1, L, L], contiguous) that needs no gradient."""
+    if not (K9E and q.is_cuda and q.dtype == torch.float32 and q.dim() == 3 and head_size == 64
+            and 1 <= q.shape[1] <= 64 and q.shape[2] == n_heads * 64):
+        return False
+    B, L = q.shape[0], q.shape[1]
+    return (isinstance(mask, torch.Tensor) and mask.dtype == torch.float32 and mask.is_cuda
+            and mask.is_contiguous() and mask.numel() == B * L * L and not mask.requires_grad
+            and tuple(mask.shape[-2:]) == (L, L))
 
 
 class MultiHeadAttention(nn.Module):
@@ -301,15 +349,41 @@ class MultiHeadAttention(nn.Module):
         self.dense = nn.Linear(hidden_size, hidden_size)
         self.LayerNorm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
         self.out_dropout = nn.Dropout(hidden_dropout_prob)
+        self._attn_index = _ATTN_MODULES[0]    # K9e dropout stream of this module
+        _ATTN_MODULES[0] += 1
+        self._attn_rng = None
+
+    def _k9e_rng(self, dev):
+        """(seed, device draw counter, ticket) of this module's K9e dropout: the seed
+        from the device generator's initial seed (torch.manual_seed sets it; no CPU
+        generator draw, so the reference's CPU random streams are untouched) and the
+        module's construction index."""
+        if self._attn_rng is None or self._attn_rng[1].device != dev:
+            seed = (torch.cuda.default_generators[dev.index or 0].initial_seed()
+                    * 0x9E3779B1 + self._attn_index) & ((1 << 64) - 1)
+            self._attn_rng = (seed, torch.zeros(1, dtype=torch.int64, device=dev),
+                              torch.zeros(1, dtype=torch.int32, device=dev))
+        return self._attn_rng
 
     def transpose_for_scores(self, x):
         x = x.view(*(x.size()[:-1] + (self.num_attention_heads, self.attention_head_size)))
         return x.permute(0, 2, 1, 3)
 
     def forward(self, input_tensor, attention_mask):
-        q = self.transpose_for_scores(linear(self.query, input_tensor))
-        k = self.transpose_for_scores(linear(self.key, input_tensor))
-        v = self.transpose_for_scores(linear(self.value, input_tensor))
+        ql = linear(self.query, input_tensor)
+        kl = linear(self.key, input_tensor)
+        vl = linear(self.value, input_tensor)
+        if attn_k9e_applies(ql, attention_mask, self.num_attention_heads,
+                            self.attention_head_size):
+            p = self.attn_dropout.p if self.training else 0.0
+            ctx = _AttnFn.apply(ql.contiguous(), kl.contiguous(), vl.contiguous(),
+                                attention_mask, self.num_attention_heads, p,
+                                self._k9e_rng(ql.device) if p > 0 else None)
+            hidden = self.out_dropout(linear(self.dense, ctx))
+            return add_layer_norm(hidden, input_tensor, self.LayerNorm)
+        q = self.transpose_for_scores(ql)
+        k = self.transpose_for_scores(kl)
+        v = self.transpose_for_scores(vl)
         if input_tensor.is_cuda and SDPA:
             # softmax(q k^T / sqrt(dh) + mask) with dropout on the weights, @ v: the same
             # computation in torch's fused attention (no copies of the permuted q, k, v)

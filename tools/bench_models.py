@@ -398,9 +398,21 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
     dh = d // H
     seq0 = b0['item_id_list']
     mask = model.get_attention_mask(seq0)
-    p_drop = model.trm_encoder.layer[0].multi_head_attention.attn_dropout.p
-    q, k, v = (torch.randn(B, H, L, dh, device=dev, requires_grad=True) for _ in range(3))
-    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p_drop)
+    mha = model.trm_encoder.layer[0].multi_head_attention
+    p_drop = mha.attn_dropout.p
+    from recbole_amd.model import layers as _layers
+    k9e = _layers.attn_k9e_applies(torch.empty(B, L, d, device=dev), mask, H, dh)
+    if k9e:   # K9e (csrc/attn.hip), the step's own attention: forward, then backward
+        q, k, v = (torch.randn(B, L, d, device=dev, requires_grad=True) for _ in range(3))
+        rng = mha._k9e_rng(q.device) if p_drop > 0 else None
+        o = _layers._AttnFn.apply(q, k, v, mask, H, p_drop, rng)
+        ta_fwd = _event_time(lambda: _layers._AttnFn.apply(q.detach(), k.detach(), v.detach(),
+                                                           mask, H, p_drop, rng))
+    else:
+        q, k, v = (torch.randn(B, H, L, dh, device=dev, requires_grad=True) for _ in range(3))
+        o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask,
+                                                             dropout_p=p_drop)
+        ta_fwd = None
     go = torch.randn_like(o)
     ta = _event_time(lambda: torch.autograd.grad(o, (q, k, v), go, retain_graph=True))
     attn_flops = 5 * 2 * B * H * L * L * dh
@@ -433,16 +445,23 @@ def bench_c3(dev, steps, warmup, scale=1.0, B=2048, L=50, d=128, n_neg=100, n_ba
         'dtype': 'fp32', 'data': 'synthetic (Zipf(1.1) items, Poisson(20)+4 lengths, seeded)',
         'transformer_tflops_at_step_rate': round(flops / t / 1e12, 2),
         'step_breakdown': _step_breakdown('C3'),
-        'roofline': {'kernel': 'attention backward of torch scaled_dot_product_attention '
-                               '(bwd_kernel_fuse, library; the timed step\'s dominant kernel)',
+        'roofline': {'kernel': ('K9e attn_bwd_kernel (csrc/attn.hip: the attention backward, '
+                                'one workgroup per sequence x head; P recomputed, dP, dS, dQ, '
+                                'dK, dV on fp32 MFMA)') if k9e else
+                               ('attention backward of torch scaled_dot_product_attention '
+                                '(bwd_kernel_fuse, library)'),
                      'bound': 'mfma', 'achieved': round(attn_flops / ta / 1e12, 2),
                      'peak': 157.3, 'unit': 'TFLOP/s',
                      'frac': round(attn_flops / ta / 1e12 / 157.3, 4),
                      'flops_per_launch': attn_flops, 'launch_us': round(ta * 1e6, 1),
-                     'timing': 'HIP events around torch.autograd.grad of one attention at the '
-                               'step shapes (median of 10)',
-                     'note': 'fp32 dense peak; our own largest kernel in the step is listed in '
-                             'step_breakdown'},
+                     'fwd_us': round(ta_fwd * 1e6, 1) if ta_fwd else None,
+                     'fwd_tflops': (round(2 * 2 * B * H * L * L * dh / ta_fwd / 1e12, 2)
+                                    if ta_fwd else None),
+                     'timing': 'HIP events around the backward (torch.autograd.grad) of one '
+                               'attention at the step shapes, and around one forward (median '
+                               'of 10, host-inclusive)',
+                     'note': 'fp32 dense MFMA peak; FLOPs of the five L x L x dh products of '
+                             'the backward (S recomputed, dV, dP, dQ, dK)'},
         'k9b': _k9b_line(d, n_neg, k9_bytes, tk),
     }
 
