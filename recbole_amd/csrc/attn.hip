@@ -16,8 +16,10 @@
 //             through the dropout), then all waves take 16-row strips of
 //             dQ = dS K / sqrt(dh), dK = dS^T Q / sqrt(dh), dV = P'^T dO.
 //
-// Dropout draws are counter-based: element (b, h, i, j) of a forward with counter value c
-// is kept iff splitmix64(splitmix64(seed + c) ^ (((b H + h) 64 + i) 64 + j)) >> 32 < thr;
+// Dropout draws are counter-based: key = splitmix64(seed + c), c the forward's counter
+// value; for a row i = 16w + 4lk + r with r even and a column j, one draw
+// x = splitmix64(key ^ (((b H + h) 64 + i) 64 + j)) decides element (i, j) by its low 32
+// bits and element (i + 1, j) by its high 32 bits (kept iff < thr);
 // the keep bits are saved as the forward's ballot words (64 per (b, h): wave w, column
 // tile c, row r -> word (w 4 + c) 4 + r, bit li + 16 lk for row 16w + 4lk + r, column
 // 16c + li) and read back by the backward. The last block of a forward with dropout
@@ -27,6 +29,21 @@
 namespace mirec {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// exp / log / the softmax's division in their hardware forms (v_exp_f32, v_log_f32, one
+// reciprocal per row: a few ulp, inside the path's 1e-4 tolerance; fwd 71 -> 66 us at C3's
+// shapes); MIREC_ATTN_EXACTMATH builds the libm forms
+#if !defined(MIREC_ATTN_EXACTMATH)
+#define AT_EXP(x) __expf(x)
+#define AT_LOG(x) __logf(x)
+#define AT_RCP(x) __frcp_rn(x)
+#define AT_DIV(x, y, ry) ((x) * (ry))
+#else
+#define AT_EXP(x) expf(x)
+#define AT_LOG(x) logf(x)
+#define AT_RCP(x) (x)
+#define AT_DIV(x, y, ry) ((x) / (y))
+#endif
 
 constexpr int kAtL = 64;         // padded sequence length (one 64-row tile)
 constexpr int kAtD = 64;         // head dimension
@@ -114,13 +131,17 @@ __device__ __forceinline__ void at_abt(floatx4 (&acc)[4], const float4 (&a)[4],
     float4 b[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) b[c] = *reinterpret_cast<const float4*>(&Bt[16 * c + li][16 * u + 4 * lk]);
+    // the four accumulators interleaved: consecutive MFMAs are independent (one chain
+    // would wait the 40-cycle dependent latency per MFMA); each still sums x, y, z, w in
+    // order
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      acc[c] = at_mfma(a[u].x, b[c].x, acc[c]);
-      acc[c] = at_mfma(a[u].y, b[c].y, acc[c]);
-      acc[c] = at_mfma(a[u].z, b[c].z, acc[c]);
-      acc[c] = at_mfma(a[u].w, b[c].w, acc[c]);
-    }
+    for (int c = 0; c < 4; ++c) acc[c] = at_mfma(a[u].x, b[c].x, acc[c]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = at_mfma(a[u].y, b[c].y, acc[c]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = at_mfma(a[u].z, b[c].z, acc[c]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = at_mfma(a[u].w, b[c].w, acc[c]);
   }
 }
 
@@ -219,7 +240,7 @@ __global__ __launch_bounds__(kAtThreads) void attn_fwd_kernel(AttnArgs a) {
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      p[c][r] = expf(p[c][r] - mx[r]);
+      p[c][r] = AT_EXP(p[c][r] - mx[r]);
       sum[r] += p[c][r];
     }
 #pragma unroll
@@ -227,25 +248,35 @@ __global__ __launch_bounds__(kAtThreads) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[r] += __shfl_xor(sum[r], o, 64);
   uint64_t word = 0ull;
+  float rsum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rsum[r] = AT_RCP(sum[r]);
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = p[c][r] / sum[r];
+    for (int r = 0; r < 4; r += 2) {
+      // one draw per two elements (rows r, r + 1 of column 16c + li): its halves
+      uint64_t d = 0ull;
       if (drop) {
         const int row = 16 * w + 4 * lk + r, col = 16 * c + li;
-        const uint64_t e = ((uint64_t)bh * kAtL + row) * kAtL + col;
-        const bool kept = (uint32_t)(at_mix(key ^ e) >> 32) < a.keep_thr;
-        const uint64_t bal = __ballot(kept);
-        if (lane == c * 4 + r) word = bal;
-        x = kept ? x * a.keep_scale : 0.f;
+        d = at_mix(key ^ (((uint64_t)bh * kAtL + row) * kAtL + col));
       }
-      p[c][r] = x;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        float x = AT_DIV(p[c][r + h2], sum[r + h2], rsum[r + h2]);
+        if (drop) {
+          const bool kept = (uint32_t)(h2 ? d >> 32 : d) < a.keep_thr;
+          const uint64_t bal = __ballot(kept);
+          if (lane == c * 4 + r + h2) word = bal;
+          x = kept ? x * a.keep_scale : 0.f;
+        }
+        p[c][r + h2] = x;
+      }
     }
   if (drop && lane < 16) a.keep[bh * kAtWords + w * 16 + lane] = word;
   if (li == 0)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) a.lse[bh * kAtL + 16 * w + 4 * lk + r] = mx[r] + logf(sum[r]);
+    for (int r = 0; r < 4; ++r) a.lse[bh * kAtL + 16 * w + 4 * lk + r] = mx[r] + AT_LOG(sum[r]);
   __syncthreads();                         // every wave's K reads are done: Ks takes P'
 #pragma unroll
   for (int c = 0; c < 4; ++c)
@@ -331,7 +362,7 @@ __global__ __launch_bounds__(kAtThreads) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 16 * w + 4 * lk + r, col = 16 * c + li;
-      const float pv = (row < L && col < L) ? expf(s[c][r] * a.scale + mk[c][r] - lse[r]) : 0.f;
+      const float pv = (row < L && col < L) ? AT_EXP(s[c][r] * a.scale + mk[c][r] - lse[r]) : 0.f;
       float g = dp[c][r];
       float pd = pv;
       if (drop) {
