@@ -165,7 +165,7 @@ class _SplitKLinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
-        return nn.functional.linear(x, W, b)
+        return linear_rows(x, W, b)
 
     @staticmethod
     def backward(ctx, gy):
@@ -177,7 +177,7 @@ class _SplitKLinearFn(torch.autograd.Function):
         C = 1
         while K % (2 * C) == 0 and K // (2 * C) >= 2048 and C < 64:
             C *= 2
-        dx = torch.matmul(gy, W)
+        dx = linear_rows_grad(gy, W)
         if C > 1:
             P = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2), x2.view(C, K // C, n_in))
             dW = torch.empty_like(W)
@@ -204,10 +204,49 @@ class _SplitKLinearFn(torch.autograd.Function):
 
 
 def linear(module, x):
-    """module(x), with the split-K weight gradient for tall GPU inputs."""
-    if x.is_cuda and x.requires_grad and x.numel() // x.shape[-1] >= 16384:
-        return _SplitKLinearFn.apply(x, module.weight, module.bias)
+    """module(x): K11 for tall GPU inputs (with the split-K weight gradient when training)."""
+    if x.is_cuda and x.numel() // x.shape[-1] >= 16384:
+        if x.requires_grad or module.weight.requires_grad and torch.is_grad_enabled():
+            return _SplitKLinearFn.apply(x, module.weight, module.bias)
+        return linear_rows(x, module.weight, module.bias)
     return module(x)
+
+
+K11 = True      # the tall Linears through K11 (csrc/linear.hip) where the widths allow
+
+
+def _k11(x, n_in, n_out):
+    """K11 where its widths allow (C3 step trace: the four 128 x 128 products 68-80 -> 49 us
+    each; the 256-wide forward / data-gradient four 72-124 -> 82-88 us, 362 -> 340 us in
+    all)."""
+    return (K11 and x.is_cuda and x.dtype == torch.float32
+            and lib().mirec_linear_shape_ok(n_in, n_out) != 0)
+
+
+def linear_rows(x, W, b):
+    """x W^T + b over the rows of x (K11 where it applies, else the library)."""
+    n_out, n_in = W.shape
+    if not _k11(x, n_in, n_out):
+        return nn.functional.linear(x, W, b)
+    x2 = x.reshape(-1, n_in).contiguous()
+    y = torch.empty(x2.shape[0], n_out, dtype=torch.float32, device=x.device)
+    check(lib().mirec_linear_fwd_f32(ptr(x2), x2.shape[0], n_in, n_out, ptr(W.detach().contiguous()),
+                                     ptr(b.detach()) if b is not None else None, ptr(y),
+                                     stream_handle()), 'mirec_linear_fwd_f32')
+    return y.view(*x.shape[:-1], n_out)
+
+
+def linear_rows_grad(gy, W):
+    """dL/dx = gy W of linear_rows (K11 where it applies, else the library)."""
+    n_out, n_in = W.shape
+    if not _k11(gy, n_in, n_out):
+        return torch.matmul(gy, W)
+    g2 = gy.reshape(-1, n_out).contiguous()
+    gx = torch.empty(g2.shape[0], n_in, dtype=torch.float32, device=gy.device)
+    check(lib().mirec_linear_bwd_data_f32(ptr(g2), g2.shape[0], n_out, n_in,
+                                          ptr(W.detach().contiguous()), ptr(gx), stream_handle()),
+          'mirec_linear_bwd_data_f32')
+    return gx.view(*gy.shape[:-1], n_in)
 
 
 class _AddLNFn(torch.autograd.Function):
