@@ -918,14 +918,15 @@ int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
                          float* mean, float* rstd, void* stream);
 /* K11  nn.Linear over tall inputs on fp32 MFMA (SASRec's transformer Linears, reference
  * layers.py:338-461: B x L rows of width 64..256): y[M, N] = x[M, K] w[N, K]^T (+ bias[N])
- * and the data gradient gx[M, n_in] = gy[M, n_out] w[n_out, n_in]. Row-major, x / gy / w
+ * and the data gradient gx[M, n_in] = gy[M, n_out] w[n_out, n_in] (accumulate != 0: added
+ * to what gx holds — the sum of several Linears' input gradients). Row-major, x / gy / w
  * 16-byte aligned; widths with mirec_linear_shape_ok(K, N) != 0 ({64,128,256}^2 except
  * 256 x 256: the weight stays in one workgroup's LDS). */
 int mirec_linear_shape_ok(int32_t K, int32_t N);
 int mirec_linear_fwd_f32(const float* x, int64_t M, int32_t K, int32_t N, const float* w,
                          const float* bias, float* y, void* stream);
 int mirec_linear_bwd_data_f32(const float* gy, int64_t M, int32_t n_out, int32_t n_in,
-                              const float* w, float* gx, void* stream);
+                              const float* w, float* gx, int32_t accumulate, void* stream);
 /* K9e  The attention core of MultiHeadAttention (reference layers.py:338-407, the lines
  * scores = q k^T / sqrt(dh); + attention_mask; softmax; attn_dropout; @ v), L <= 64 and
  * dh = 64, one workgroup per (sequence, head), fp32 MFMA. q, k, v, out / dout, dq, dk, dv:

@@ -37,7 +37,7 @@ __device__ __forceinline__ floatx4 ln_mfma(float a, float b, floatx4 c) {
 // workgroup per CU stages the whole weight once; each of its waves then walks 16-row slabs
 // s = its global wave index + i * (waves in the grid), the next slab's A rows loaded while
 // the current slab's products run (no workgroup barrier after the staging).
-template <int K, int N, bool WT>
+template <int K, int N, bool WT, bool ACC>
 __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W,
     const float* __restrict__ bias, float* __restrict__ Y) {
@@ -129,7 +129,10 @@ __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
       const int64_t r = 16 * s + 4 * lk + i;
       if (r < M)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) Y[r * N + 16 * c + li] = acc[c][i] + bv[c];
+        for (int c = 0; c < NC; ++c) {
+          float* yp = Y + r * N + 16 * c + li;
+          *yp = ACC ? *yp + (acc[c][i] + bv[c]) : acc[c][i] + bv[c];
+        }
     }
     if (kPre) {
 #pragma unroll
@@ -140,13 +143,13 @@ __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
   }
 }
 
-template <int K, int N, bool WT>
+template <int K, int N, bool WT, bool ACC>
 int launch_linear(const float* X, int64_t M, const float* W, const float* bias, float* Y,
                   hipStream_t st, const char* what) {
   constexpr size_t lds = (size_t)N * (K + 4) * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    if (hip_status(hipFuncSetAttribute((const void*)linear_mfma_kernel<K, N, WT>,
+    if (hip_status(hipFuncSetAttribute((const void*)linear_mfma_kernel<K, N, WT, ACC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                    what))
       return -1;
@@ -162,16 +165,18 @@ int launch_linear(const float* X, int64_t M, const float* W, const float* bias, 
   }
   const int64_t slabs = (M + 15) / 16;
   const int64_t grid = std::min<int64_t>((slabs + kLnWaves - 1) / kLnWaves, (int64_t)cus * per_cu);
-  hipLaunchKernelGGL((linear_mfma_kernel<K, N, WT>), dim3((unsigned)grid), dim3(kLnThreads), lds,
-                     st, X, M, W, bias, Y);
+  hipLaunchKernelGGL((linear_mfma_kernel<K, N, WT, ACC>), dim3((unsigned)grid), dim3(kLnThreads),
+                     lds, st, X, M, W, bias, Y);
   return launch_status(what);
 }
 
 template <bool WT>
 int linear_dispatch(const float* X, int64_t M, int K, int N, const float* W, const float* bias,
-                    float* Y, hipStream_t st, const char* what) {
+                    float* Y, bool accumulate, hipStream_t st, const char* what) {
 #define MIREC_LN(KK, NN) \
-  if (K == KK && N == NN) return launch_linear<KK, NN, WT>(X, M, W, bias, Y, st, what);
+  if (K == KK && N == NN)                                                                    \
+    return accumulate ? launch_linear<KK, NN, WT, WT>(X, M, W, bias, Y, st, what)            \
+                      : launch_linear<KK, NN, WT, false>(X, M, W, bias, Y, st, what);
   MIREC_LN(64, 64)
   MIREC_LN(64, 128)
   MIREC_LN(64, 256)
@@ -202,18 +207,19 @@ extern "C" int mirec_linear_fwd_f32(const float* x, int64_t M, int32_t K, int32_
     return -1;
   }
   if (M == 0) return 0;
-  return linear_dispatch<false>(x, M, K, N, w, bias, y, (hipStream_t)stream,
+  return linear_dispatch<false>(x, M, K, N, w, bias, y, false, (hipStream_t)stream,
                                 "mirec_linear_fwd_f32");
 }
 
 extern "C" int mirec_linear_bwd_data_f32(const float* gy, int64_t M, int32_t n_out,
-                                         int32_t n_in, const float* w, float* gx, void* stream) {
+                                         int32_t n_in, const float* w, float* gx,
+                                         int32_t accumulate, void* stream) {
   if (M < 0 || !gy || !w || !gx || (((uintptr_t)gy | (uintptr_t)w) & 15)) {
     set_error("mirec_linear_bwd_data_f32: bad arguments (16-byte aligned gy, w)");
     return -1;
   }
   if (M == 0) return 0;
   // dX[M, n_in] = dY[M, n_out] W[n_out, n_in]: reduction n_out, B[k][n] = W[k][n]
-  return linear_dispatch<true>(gy, M, n_out, n_in, w, nullptr, gx, (hipStream_t)stream,
-                               "mirec_linear_bwd_data_f32");
+  return linear_dispatch<true>(gy, M, n_out, n_in, w, nullptr, gx, accumulate != 0,
+                               (hipStream_t)stream, "mirec_linear_bwd_data_f32");
 }

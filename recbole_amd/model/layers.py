@@ -155,11 +155,47 @@ class FMFirstOrderLinear(nn.Module):
         self.bias = nn.Parameter(torch.zeros((output_dim,)), requires_grad=True)
 
 
+def _wgrad(x, gy, W, has_b):
+    """(dW, db) of y = x W^T + b over the rows of x: the weight gradient dW = dY^T X as a
+    batched GEMM over C row blocks, then summed — the library picks a 32x32-tile kernel for
+    the single [out, K] x [K, in] product, which leaves most CUs idle at K = 10^5 (SASRec
+    on C3); C blocks give C times the tiles — with the bias column sum in the same finish
+    launch."""
+    n_in, n_out = W.shape[1], W.shape[0]
+    x2 = x.reshape(-1, n_in)
+    g2 = gy.reshape(-1, n_out)
+    K = x2.shape[0]
+    C = 1
+    while K % (2 * C) == 0 and K // (2 * C) >= 2048 and C < 64:
+        C *= 2
+    if C > 1:
+        P = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2), x2.view(C, K // C, n_in))
+        dW = torch.empty_like(W)
+    else:
+        P = dW = g2.t().mm(x2)
+    db = None
+    if has_b and (n_out % 4 or n_in % 4):        # outside the finish kernel's shapes
+        if C > 1:
+            dW = P.sum(0)
+        return dW, g2.sum(0)
+    if has_b or C > 1:
+        # the C partials' sum and the bias column sum in one launch (two torch
+        # reductions before)
+        g2 = g2.contiguous()
+        if has_b:
+            db = torch.empty(n_out, dtype=torch.float32, device=gy.device)
+        scratch = torch.empty(max(lib().mirec_linear_grad_finish_scratch(K, n_out), 2),
+                              dtype=torch.float32, device=gy.device)
+        check(lib().mirec_linear_grad_finish_f32(
+            ptr(P), C, n_out * n_in, ptr(dW), ptr(g2), K, n_out, ptr(db) if db is not None
+            else None, ptr(scratch), ptr(ops.finish_ticket(gy.device, 'linear')),
+            stream_handle()), 'mirec_linear_grad_finish_f32')
+    return dW, db
+
+
 class _SplitKLinearFn(torch.autograd.Function):
-    """nn.Linear whose weight gradient dW = dY^T X over K = batch*positions rows is
-    formed as a batched GEMM over C row blocks, then summed: the library picks a
-    32x32-tile kernel for the single [out, K] x [K, in] product, which leaves most
-    CUs idle at K = 10^5 (SASRec on C3); C blocks give C times the tiles."""
+    """nn.Linear over tall inputs: forward and input gradient through K11
+    (linear_rows / linear_rows_grad), weight and bias gradients through _wgrad."""
 
     @staticmethod
     def forward(ctx, x, W, b):
@@ -170,37 +206,38 @@ class _SplitKLinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, W = ctx.saved_tensors
-        n_in, n_out = W.shape[1], W.shape[0]
-        x2 = x.reshape(-1, n_in)
-        g2 = gy.reshape(-1, n_out)
-        K = x2.shape[0]
-        C = 1
-        while K % (2 * C) == 0 and K // (2 * C) >= 2048 and C < 64:
-            C *= 2
         dx = linear_rows_grad(gy, W)
-        if C > 1:
-            P = torch.bmm(g2.view(C, K // C, n_out).transpose(1, 2), x2.view(C, K // C, n_in))
-            dW = torch.empty_like(W)
-        else:
-            P = dW = g2.t().mm(x2)
-        db = None
-        if ctx.has_b and (n_out % 4 or n_in % 4):        # outside the finish kernel's shapes
-            if C > 1:
-                dW = P.sum(0)
-            return dx, dW, g2.sum(0)
-        if ctx.has_b or C > 1:
-            # the C partials' sum and the bias column sum in one launch (two torch
-            # reductions before)
-            g2 = g2.contiguous()
-            if ctx.has_b:
-                db = torch.empty(n_out, dtype=torch.float32, device=gy.device)
-            scratch = torch.empty(max(lib().mirec_linear_grad_finish_scratch(K, n_out), 2),
-                                  dtype=torch.float32, device=gy.device)
-            check(lib().mirec_linear_grad_finish_f32(
-                ptr(P), C, n_out * n_in, ptr(dW), ptr(g2), K, n_out, ptr(db) if db is not None
-                else None, ptr(scratch), ptr(ops.finish_ticket(gy.device, 'linear')),
-                stream_handle()), 'mirec_linear_grad_finish_f32')
+        dW, db = _wgrad(x, gy, W, ctx.has_b)
         return dx, dW, db
+
+
+class _QKVFn(torch.autograd.Function):
+    """The query / key / value Linears of MultiHeadAttention over one input (layers.py
+    :338-407): three K11 products forward; backward, the input gradient of all three in
+    one buffer — dx = gq Wq, then += gk Wk, += gv Wv in K11's accumulating epilogue —
+    instead of three buffers and autograd's two adds."""
+
+    @staticmethod
+    def forward(ctx, x, Wq, bq, Wk, bk, Wv, bv):
+        ctx.save_for_backward(x, Wq, Wk, Wv)
+        ctx.has_b = (bq is not None, bk is not None, bv is not None)
+        return linear_rows(x, Wq, bq), linear_rows(x, Wk, bk), linear_rows(x, Wv, bv)
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv):
+        x, Wq, Wk, Wv = ctx.saved_tensors
+        dx = None
+        out = []
+        for g, W, hb in ((gq, Wq, ctx.has_b[0]), (gk, Wk, ctx.has_b[1]), (gv, Wv, ctx.has_b[2])):
+            if g is None:
+                out += [None, None]
+                continue
+            g = g.contiguous()
+            dx = linear_rows_grad(g, W, acc=dx)
+            out += list(_wgrad(x, g, W, hb))
+        if dx is None:
+            dx = torch.zeros_like(x)
+        return (dx, *out)
 
 
 def linear(module, x):
@@ -236,15 +273,22 @@ def linear_rows(x, W, b):
     return y.view(*x.shape[:-1], n_out)
 
 
-def linear_rows_grad(gy, W):
-    """dL/dx = gy W of linear_rows (K11 where it applies, else the library)."""
+def linear_rows_grad(gy, W, acc=None):
+    """dL/dx = gy W of linear_rows (K11 where it applies, else the library); acc: a
+    previous input gradient of the same shape, added to (in place with K11)."""
     n_out, n_in = W.shape
     if not _k11(gy, n_in, n_out):
-        return torch.matmul(gy, W)
+        gx = torch.matmul(gy, W)
+        return gx if acc is None else acc.add_(gx)
     g2 = gy.reshape(-1, n_out).contiguous()
-    gx = torch.empty(g2.shape[0], n_in, dtype=torch.float32, device=gy.device)
+    if acc is None:
+        gx = torch.empty(g2.shape[0], n_in, dtype=torch.float32, device=gy.device)
+    else:
+        gx = acc.view(-1, n_in)
+        assert gx.is_contiguous() and gx.shape[0] == g2.shape[0]
     check(lib().mirec_linear_bwd_data_f32(ptr(g2), g2.shape[0], n_out, n_in,
-                                          ptr(W.detach().contiguous()), ptr(gx), stream_handle()),
+                                          ptr(W.detach().contiguous()), ptr(gx),
+                                          int(acc is not None), stream_handle()),
           'mirec_linear_bwd_data_f32')
     return gx.view(*gy.shape[:-1], n_in)
 
@@ -409,9 +453,15 @@ class MultiHeadAttention(nn.Module):
         return x.permute(0, 2, 1, 3)
 
     def forward(self, input_tensor, attention_mask):
-        ql = linear(self.query, input_tensor)
-        kl = linear(self.key, input_tensor)
-        vl = linear(self.value, input_tensor)
+        if (input_tensor.is_cuda and input_tensor.numel() // input_tensor.shape[-1] >= 16384
+                and torch.is_grad_enabled() and input_tensor.requires_grad):
+            ql, kl, vl = _QKVFn.apply(input_tensor, self.query.weight, self.query.bias,
+                                      self.key.weight, self.key.bias, self.value.weight,
+                                      self.value.bias)
+        else:
+            ql = linear(self.query, input_tensor)
+            kl = linear(self.key, input_tensor)
+            vl = linear(self.value, input_tensor)
         if attn_k9e_applies(ql, attention_mask, self.num_attention_heads,
                             self.attention_head_size):
             p = self.attn_dropout.p if self.training else 0.0

@@ -65,3 +65,39 @@ def test_k11_linear_function_matches_autograd(dev):
     # dW and db sum 20,000 rows (entries ~ 1e2): fp32 accumulation, absolute slack scaled
     for a, e, atol in zip(got, [yr.detach(), xr.grad, Wr.grad, br.grad], (1e-5, 1e-5, 2e-3, 2e-3)):
         torch.testing.assert_close(a, e.float(), rtol=1e-4, atol=atol)
+
+
+def test_k11_data_grad_accumulates(dev):
+    """mirec_linear_bwd_data_f32 with accumulate: gx += gy W (in place)."""
+    from recbole_amd.model import layers
+    g = torch.Generator().manual_seed(9)
+    gy = torch.randn(3000, 128, generator=g)
+    W = torch.randn(128, 64, generator=g) / 8
+    prev = torch.randn(3000, 64, generator=g)
+    acc = prev.to(dev)
+    out = layers.linear_rows_grad(gy.to(dev), W.to(dev), acc=acc)
+    assert out.data_ptr() == acc.data_ptr()
+    torch.testing.assert_close(out.cpu(), (prev.double() + gy.double() @ W.double()).float(),
+                               rtol=1e-4, atol=1e-5)
+
+
+def test_qkv_fn_matches_three_linears(dev):
+    """_QKVFn (the three projections, one accumulated input gradient) equals three
+    separate nn.Linear calls: outputs and all seven gradients."""
+    from recbole_amd.model import layers
+    torch.manual_seed(1)
+    lins = [torch.nn.Linear(128, 128).to(dev) for _ in range(3)]
+    x = torch.randn(400, 50, 128, device=dev, requires_grad=True)
+    gs = [torch.randn(400, 50, 128, device=dev) for _ in range(3)]
+    outs = layers._QKVFn.apply(x, *[p for l in lins for p in (l.weight, l.bias)])
+    torch.autograd.backward(outs, gs)
+    got = [o.detach().cpu() for o in outs] + [x.grad.cpu()] + \
+        [p.grad.cpu() for l in lins for p in (l.weight, l.bias)]
+    xr = x.detach().cpu().double().requires_grad_()
+    ps = [p.detach().cpu().double().requires_grad_() for l in lins for p in (l.weight, l.bias)]
+    refs = [torch.nn.functional.linear(xr, ps[2 * i], ps[2 * i + 1]) for i in range(3)]
+    torch.autograd.backward(refs, [t.cpu().double() for t in gs])
+    want = [r.detach() for r in refs] + [xr.grad] + [p.grad for p in ps]
+    atols = [1e-5] * 4 + [2e-3] * 6          # weight / bias grads sum 20,000 rows
+    for a, e, atol in zip(got, want, atols):
+        torch.testing.assert_close(a, e.float(), rtol=1e-4, atol=atol)
