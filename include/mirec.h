@@ -934,18 +934,19 @@ int mirec_linear_bwd_data_f32(const float* gy, int64_t M, int32_t n_out, int32_t
  * written back in the same layout, i.e. after the reference's permute + view); mask:
  * [B, L, L] additive (SASRec's [B, 1, L, L] extended mask); lse: [B*H, 64] floats (the
  * forward writes each query row's log-sum-exp, the backward reads it). Dropout p > 0:
- * counter-based draws (csrc/attn.hip header: seed, the device int64 counter — advanced by
- * the forward's last block through the int32 ticket `arrive`, zero between launches),
- * the keep bits written to keep_words [B*H, 64] uint64 and read back by the backward.
+ * counter-based draws (csrc/attn.hip header: seed, the device int64 counter — read by the
+ * forward, advanced by one by the backward when it gets the counter; a forward without a
+ * backward leaves the advance to the caller), the keep bits written to keep_words [B*H, 64]
+ * uint64 and read back by the backward.
  * Replaces torch's fused scaled_dot_product_attention and the context permute copy. */
 int mirec_attn_fwd_f32(const float* q, const float* k, const float* v, const float* mask,
                        int64_t B, int32_t L, int32_t H, float dropout_p, uint64_t seed,
-                       int64_t* counter, int32_t* arrive, float* out, float* lse,
-                       uint64_t* keep_words, void* stream);
+                       int64_t* counter, float* out, float* lse, uint64_t* keep_words,
+                       void* stream);
 int mirec_attn_bwd_f32(const float* q, const float* k, const float* v, const float* mask,
                        const float* dout, const float* lse, const uint64_t* keep_words,
-                       int64_t B, int32_t L, int32_t H, float dropout_p, float* dq, float* dk,
-                       float* dv, void* stream);
+                       int64_t* counter, int64_t B, int32_t L, int32_t H, float dropout_p,
+                       float* dq, float* dk, float* dv, void* stream);
 /* GELU (erf form) of the feed-forward block, forward and backward, elementwise. */
 int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream);
 int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, float* dx, void* stream);
@@ -953,6 +954,22 @@ int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
                          const float* gamma, const float* mean, const float* rstd,
                          const float* grad_out, float* dx, float* part_gamma, float* part_beta,
                          void* stream);
+/* K9d with the hidden dropout folded in (layers.py:338-461: LayerNorm(dropout(hidden) +
+ * input_tensor), the MultiHeadAttention out_dropout / FeedForward dropout): y =
+ * LayerNorm(drop_p(a) + b). Counter-based draws (csrc/seq.hip K9d header): the forward reads
+ * the device int64 `counter` and writes the value it used to drawn[0]; the backward redraws
+ * the same keep flags from drawn[0], sets counter = drawn[0] + 1 (a forward without a
+ * backward leaves the advance to the caller) and writes dx_a = dLN * keep / (1 - p) (the
+ * gradient of `a`) and dx_b = dLN (of `b`). 0 < p < 1. */
+int mirec_add_ln_drop_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                              const float* gamma, const float* beta, float eps, float p,
+                              uint64_t seed, int64_t* counter, int64_t* drawn, float* out,
+                              float* mean, float* rstd, void* stream);
+int mirec_add_ln_drop_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                              const float* gamma, const float* mean, const float* rstd,
+                              const float* grad_out, float p, uint64_t seed, int64_t* drawn,
+                              int64_t* counter, float* dx_a, float* dx_b, float* part_gamma,
+                              float* part_beta, void* stream);
 
 /* K9c: sampled evaluation (uni-N) of a sequential model — rank[q] = number of the
  * m sampled items neg[q*m .. q*m+m) (row-major: the sampler's per-row walk order)

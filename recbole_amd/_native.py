@@ -157,9 +157,13 @@ SIGNATURES = {
     "mirec_linear_shape_ok": (c_int, [c_int32, c_int32]),
     "mirec_linear_fwd_f32": (c_int, [_P, c_int64, c_int32, c_int32, _P, _P, _P, _P]),
     "mirec_linear_bwd_data_f32": (c_int, [_P, c_int64, c_int32, c_int32, _P, _P, c_int32, _P]),
+    "mirec_add_ln_drop_fwd_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_float, c_float,
+                                          ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
+    "mirec_add_ln_drop_bwd_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, _P, _P, c_float,
+                                          ctypes.c_uint64, _P, _P, _P, _P, _P, _P, _P]),
     "mirec_attn_fwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int32, c_int32, c_float,
-                                   ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
-    "mirec_attn_bwd_f32": (c_int, [_P, _P, _P, _P, _P, _P, _P, c_int64, c_int32, c_int32,
+                                   ctypes.c_uint64, _P, _P, _P, _P, _P]),
+    "mirec_attn_bwd_f32": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int64, c_int32, c_int32,
                                    c_float, _P, _P, _P, _P]),
     "mirec_gelu_fwd_f32": (c_int, [_P, c_int64, _P, _P]),
     "mirec_gelu_bwd_f32": (c_int, [_P, _P, c_int64, _P, _P]),

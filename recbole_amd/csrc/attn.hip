@@ -22,8 +22,9 @@
 // bits and element (i + 1, j) by its high 32 bits (kept iff < thr);
 // the keep bits are saved as the forward's ballot words (64 per (b, h): wave w, column
 // tile c, row r -> word (w 4 + c) 4 + r, bit li + 16 lk for row 16w + 4lk + r, column
-// 16c + li) and read back by the backward. The last block of a forward with dropout
-// advances the device counter (captured steps draw new masks every replay).
+// 16c + li) and read back by the backward, which advances the device counter by one store
+// (captured steps draw new masks every replay; a last-block ticket in the forward serialised
+// 4,096 atomics on one word, ~11 us a launch).
 #include "common.h"
 
 namespace mirec {
@@ -69,8 +70,7 @@ struct AttnArgs {
   uint32_t keep_thr;    // keep iff draw < keep_thr
   float keep_scale;     // 1 / (1 - p)
   uint64_t seed;
-  const int64_t* counter;
-  int32_t* arrive;
+  int64_t* counter;     // forward: read; backward: advanced (one store)
 };
 
 __device__ __forceinline__ uint64_t at_mix(uint64_t z) {
@@ -295,13 +295,6 @@ __global__ __launch_bounds__(kAtThreads) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) a.out[base + (int64_t)row * ld + 16 * c + li] = o[c][r];
   }
-  if (drop && tid == 0) {                  // the last block advances the draw counter
-    const int prev = atomicAdd(a.arrive, 1);
-    if (prev == (int)gridDim.x - 1) {
-      atomicExch(a.arrive, 0);
-      atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<int64_t*>(a.counter)), 1ull);
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -344,6 +337,7 @@ __global__ __launch_bounds__(kAtThreads) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) lse[r] = a.lse[bh * kAtL + 16 * w + 4 * lk + r];
   const uint64_t word = (drop && lane < 16) ? a.keep[bh * kAtWords + w * 16 + lane] : 0ull;
+  if (drop && a.counter && bh == 0 && tid == 0) a.counter[0] += 1;   // the next draw
   __syncthreads();
 
   floatx4 s[4], dp[4];
@@ -449,9 +443,8 @@ using namespace mirec;
 
 extern "C" int mirec_attn_fwd_f32(const float* q, const float* k, const float* v,
                                   const float* mask, int64_t B, int32_t L, int32_t H,
-                                  float dropout_p, uint64_t seed, int64_t* counter,
-                                  int32_t* arrive, float* out, float* lse, uint64_t* keep_words,
-                                  void* stream) {
+                                  float dropout_p, uint64_t seed, int64_t* counter, float* out,
+                                  float* lse, uint64_t* keep_words, void* stream) {
   AttnArgs a;
   memset(&a, 0, sizeof(a));
   a.q = q; a.k = k; a.v = v; a.mask = mask; a.out = out; a.lse = lse;
@@ -462,8 +455,8 @@ extern "C" int mirec_attn_fwd_f32(const float* q, const float* k, const float* v
     return -1;
   }
   if (dropout_p > 0.f) {
-    if (dropout_p >= 1.f || !counter || !arrive || !keep_words) {
-      set_error("mirec_attn_fwd_f32: dropout %g needs p < 1, a counter, a ticket and keep words",
+    if (dropout_p >= 1.f || !counter || !keep_words) {
+      set_error("mirec_attn_fwd_f32: dropout %g needs p < 1, a counter and keep words",
                 (double)dropout_p);
       return -1;
     }
@@ -472,7 +465,6 @@ extern "C" int mirec_attn_fwd_f32(const float* q, const float* k, const float* v
     a.keep_scale = 1.0f / (1.0f - dropout_p);
     a.seed = seed;
     a.counter = counter;
-    a.arrive = arrive;
   }
   if (B == 0) return 0;
   hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(B * H)), dim3(kAtThreads), 0,
@@ -482,9 +474,9 @@ extern "C" int mirec_attn_fwd_f32(const float* q, const float* k, const float* v
 
 extern "C" int mirec_attn_bwd_f32(const float* q, const float* k, const float* v,
                                   const float* mask, const float* dout, const float* lse,
-                                  const uint64_t* keep_words, int64_t B, int32_t L, int32_t H,
-                                  float dropout_p, float* dq, float* dk, float* dv,
-                                  void* stream) {
+                                  const uint64_t* keep_words, int64_t* counter, int64_t B,
+                                  int32_t L, int32_t H, float dropout_p, float* dq, float* dk,
+                                  float* dv, void* stream) {
   AttnArgs a;
   memset(&a, 0, sizeof(a));
   a.q = q; a.k = k; a.v = v; a.mask = mask; a.dout = dout; a.lse = const_cast<float*>(lse);
@@ -504,6 +496,7 @@ extern "C" int mirec_attn_bwd_f32(const float* q, const float* k, const float* v
     }
     a.keep = const_cast<uint64_t*>(keep_words);
     a.keep_scale = 1.0f / (1.0f - dropout_p);
+    a.counter = counter;          // may be NULL: the caller advances it
   }
   if (B == 0) return 0;
   hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(B * H)), dim3(kAtThreads), 0,

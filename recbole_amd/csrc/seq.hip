@@ -142,48 +142,98 @@ __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
 }
 
 // K9d  residual + LayerNorm of the transformer blocks (layers.py MultiHeadAttention /
-//   FeedForward: LayerNorm(hidden + input_tensor), reference layers.py:338-552):
-//   y = LayerNorm(a + b) in one pass (the sum is never written), and its backward
-//   from the saved mean / rstd with x = a + b recomputed; same arithmetic as K9a.
-template <int D>
+//   FeedForward: LayerNorm(dropout(hidden) + input_tensor), reference layers.py:338-552):
+//   y = LayerNorm(drop(a) + b) in one pass (the sum is never written), and its backward
+//   from the saved mean / rstd with x = drop(a) + b recomputed; same arithmetic as K9a.
+//   DROP: the hidden dropout folded in (torch ran it as its own kernel each way). Draws are
+//   counter-based: key = splitmix64(seed + c), c the device counter's value at the forward
+//   (saved in drawn[0]); the backward redraws from drawn[0] and sets the counter to c + 1
+//   (one store: a last-block ticket over the forward's 12,800 workgroups serialised that
+//   many atomics on one word, 153 us against 28 for the kernel itself);
+//   element e = row * D + column is kept iff the 32-bit half e & 1 of
+//   splitmix64(key ^ (e >> 1)) is below thr; a kept element is scaled by 1 / (1 - p).
+struct LnDrop {
+  uint32_t thr;
+  float scale;
+  uint64_t seed;
+  int64_t* counter;     // forward: read; backward: set to drawn + 1
+  int64_t* drawn;       // forward writes the counter value used; backward reads it
+};
+
+__device__ __forceinline__ uint64_t ln_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// keep flags of the four elements e0 .. e0 + 3 (e0 a multiple of 4)
+__device__ __forceinline__ void ln_keep4(uint64_t key, uint64_t e0, uint32_t thr, bool (&k)[4]) {
+  const uint64_t h0 = ln_mix(key ^ (e0 >> 1)), h1 = ln_mix(key ^ ((e0 >> 1) + 1));
+  k[0] = (uint32_t)h0 < thr;
+  k[1] = (uint32_t)(h0 >> 32) < thr;
+  k[2] = (uint32_t)h1 < thr;
+  k[3] = (uint32_t)(h1 >> 32) < thr;
+}
+
+template <int D, bool DROP>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Bv, int64_t n_rows,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    float* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+    float* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    LnDrop dr) {
   constexpr int LPR = D / 4, GPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int g = lane / LPR, l = lane % LPR;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t r = wave * GPW + g;
-  if (r >= n_rows) return;
-  const float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
-  const float4 b = reinterpret_cast<const float4*>(Bv + r * D)[l];
-  float4 x = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-  const float mean = lane_group_sum<LPR>(sum4(x)) * (1.0f / D);
-  float4 c = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
-  const float var = lane_group_sum<LPR>(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) *
-                    (1.0f / D);
-  const float rstd = 1.0f / sqrtf(var + eps);
-  const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
-  const float4 bt = reinterpret_cast<const float4*>(beta)[l];
-  float4 y;
-  y.x = c.x * rstd * gm.x + bt.x;
-  y.y = c.y * rstd * gm.y + bt.y;
-  y.z = c.z * rstd * gm.z + bt.z;
-  y.w = c.w * rstd * gm.w + bt.w;
-  reinterpret_cast<float4*>(out + r * D)[l] = y;
-  if (l == 0) {
-    mean_out[r] = mean;
-    rstd_out[r] = rstd;
+  uint64_t key = 0;
+  if (DROP) {
+    const int64_t c = dr.counter[0];
+    key = ln_mix(dr.seed + (uint64_t)c);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dr.drawn[0] = c;
+  }
+  if (r < n_rows) {
+    float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
+    if (DROP) {
+      bool k[4];
+      ln_keep4(key, (uint64_t)r * D + 4 * l, dr.thr, k);
+      a.x = k[0] ? a.x * dr.scale : 0.f;
+      a.y = k[1] ? a.y * dr.scale : 0.f;
+      a.z = k[2] ? a.z * dr.scale : 0.f;
+      a.w = k[3] ? a.w * dr.scale : 0.f;
+    }
+    const float4 b = reinterpret_cast<const float4*>(Bv + r * D)[l];
+    float4 x = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    const float mean = lane_group_sum<LPR>(sum4(x)) * (1.0f / D);
+    float4 c = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+    const float var = lane_group_sum<LPR>(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) *
+                      (1.0f / D);
+    const float rstd = 1.0f / sqrtf(var + eps);
+    const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+    const float4 bt = reinterpret_cast<const float4*>(beta)[l];
+    float4 y;
+    y.x = c.x * rstd * gm.x + bt.x;
+    y.y = c.y * rstd * gm.y + bt.y;
+    y.z = c.z * rstd * gm.z + bt.z;
+    y.w = c.w * rstd * gm.w + bt.w;
+    reinterpret_cast<float4*>(out + r * D)[l] = y;
+    if (l == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
   }
 }
 
-template <int D>
+// DROP: dx_a = dLN * keep * scale (the gradient of the dropped input), dx_b = dLN; else the
+// one dx (both inputs' gradient) in dxb.
+template <int D, bool DROP>
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Bv, int64_t n_rows,
     const float* __restrict__ gamma, const float* __restrict__ mean_in,
-    const float* __restrict__ rstd_in, const float* __restrict__ gy, float* __restrict__ dx,
-    float* __restrict__ part_gamma, float* __restrict__ part_beta) {
+    const float* __restrict__ rstd_in, const float* __restrict__ gy, float* __restrict__ dxb,
+    float* __restrict__ dxa, float* __restrict__ part_gamma, float* __restrict__ part_beta,
+    LnDrop dr) {
   constexpr int LPR = D / 4, GPW = 64 / LPR;
   __shared__ float4 red_g[4 * GPW][LPR];
   __shared__ float4 red_b[4 * GPW][LPR];
@@ -191,12 +241,23 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(
   const int w = threadIdx.x >> 6;
   const int g = lane / LPR, l = lane % LPR;
   const float4 gm = reinterpret_cast<const float4*>(gamma)[l];
+  const int64_t c = DROP ? dr.drawn[0] : 0;
+  const uint64_t key = DROP ? ln_mix(dr.seed + (uint64_t)c) : 0ull;
+  if (DROP && blockIdx.x == 0 && threadIdx.x == 0) dr.counter[0] = c + 1;   // the next draw
   float4 ag = make_float4(0.f, 0.f, 0.f, 0.f), ab = ag;
   const int64_t base = (int64_t)blockIdx.x * kLnRowsPerBlock;
   for (int i = w * GPW + g; i < kLnRowsPerBlock; i += 4 * GPW) {
     const int64_t r = base + i;
     if (r >= n_rows) break;
-    const float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
+    float4 a = reinterpret_cast<const float4*>(A + r * D)[l];
+    bool k[4] = {true, true, true, true};
+    if (DROP) {
+      ln_keep4(key, (uint64_t)r * D + 4 * l, dr.thr, k);
+      a.x = k[0] ? a.x * dr.scale : 0.f;
+      a.y = k[1] ? a.y * dr.scale : 0.f;
+      a.z = k[2] ? a.z * dr.scale : 0.f;
+      a.w = k[3] ? a.w * dr.scale : 0.f;
+    }
     const float4 b = reinterpret_cast<const float4*>(Bv + r * D)[l];
     const float mean = mean_in[r], rstd = rstd_in[r];
     float4 xh;
@@ -215,7 +276,11 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(
     o.y = rstd * (gg.y - m1 - xh.y * m2);
     o.z = rstd * (gg.z - m1 - xh.z * m2);
     o.w = rstd * (gg.w - m1 - xh.w * m2);
-    reinterpret_cast<float4*>(dx + r * D)[l] = o;
+    reinterpret_cast<float4*>(dxb + r * D)[l] = o;
+    if (DROP)
+      reinterpret_cast<float4*>(dxa + r * D)[l] =
+          make_float4(k[0] ? o.x * dr.scale : 0.f, k[1] ? o.y * dr.scale : 0.f,
+                      k[2] ? o.z * dr.scale : 0.f, k[3] ? o.w * dr.scale : 0.f);
     ag.x += gv.x * xh.x;
     ag.y += gv.y * xh.y;
     ag.z += gv.z * xh.z;
@@ -432,21 +497,29 @@ extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_ite
   return launch_status("mirec_seq_embed_ln_bwd_f32");
 }
 
-extern "C" int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
-                                    const float* gamma, const float* beta, float eps, float* out,
-                                    float* mean, float* rstd, void* stream) {
+static int add_ln_fwd_impl(const float* a, const float* b, int64_t n, int32_t d,
+                           const float* gamma, const float* beta, float eps, float* out,
+                           float* mean, float* rstd, const LnDrop* dr, void* stream,
+                           const char* what) {
   if (n == 0) return 0;
   if (!a || !b || !gamma || !beta || !out || !mean || !rstd || n < 0) {
-    set_error("mirec_add_ln_fwd_f32: bad arguments");
+    set_error("%s: bad arguments", what);
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
+  LnDrop none;
+  memset(&none, 0, sizeof(none));
 #define MIREC_ALF(DD)                                                                        \
   case DD: {                                                                                 \
     constexpr int GPW = 64 / (DD / 4);                                                       \
     const int64_t waves = (n + GPW - 1) / GPW;                                               \
-    hipLaunchKernelGGL(add_ln_fwd_kernel<DD>, dim3((unsigned)((waves + 3) / 4)), dim3(256),  \
-                       0, st, a, b, n, gamma, beta, eps, out, mean, rstd);                   \
+    const dim3 grd((unsigned)((waves + 3) / 4));                                             \
+    if (dr)                                                                                  \
+      hipLaunchKernelGGL((add_ln_fwd_kernel<DD, true>), grd, dim3(256), 0, st, a, b, n,      \
+                         gamma, beta, eps, out, mean, rstd, *dr);                            \
+    else                                                                                     \
+      hipLaunchKernelGGL((add_ln_fwd_kernel<DD, false>), grd, dim3(256), 0, st, a, b, n,     \
+                         gamma, beta, eps, out, mean, rstd, none);                           \
   } break;
   switch (d) {
     MIREC_ALF(32)
@@ -454,29 +527,36 @@ extern "C" int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, i
     MIREC_ALF(128)
     MIREC_ALF(256)
     default:
-      set_error("mirec_add_ln_fwd_f32: hidden size %d not in {32,64,128,256}", d);
+      set_error("%s: hidden size %d not in {32,64,128,256}", what, d);
       return -1;
   }
 #undef MIREC_ALF
-  return launch_status("mirec_add_ln_fwd_f32");
+  return launch_status(what);
 }
 
-extern "C" int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
-                                    const float* gamma, const float* mean, const float* rstd,
-                                    const float* grad_out, float* dx, float* part_gamma,
-                                    float* part_beta, void* stream) {
+static int add_ln_bwd_impl(const float* a, const float* b, int64_t n, int32_t d,
+                           const float* gamma, const float* mean, const float* rstd,
+                           const float* grad_out, float* dxb, float* dxa, float* part_gamma,
+                           float* part_beta, const LnDrop* dr, void* stream, const char* what) {
   if (n == 0) return 0;
-  if (!a || !b || !gamma || !mean || !rstd || !grad_out || !dx || !part_gamma || !part_beta ||
-      n < 0) {
-    set_error("mirec_add_ln_bwd_f32: bad arguments");
+  if (!a || !b || !gamma || !mean || !rstd || !grad_out || !dxb || !part_gamma || !part_beta ||
+      n < 0 || (dr && !dxa)) {
+    set_error("%s: bad arguments", what);
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
   const dim3 grd((unsigned)mirec_seq_embed_ln_partials(n));
+  LnDrop none;
+  memset(&none, 0, sizeof(none));
 #define MIREC_ALB(DD)                                                                        \
   case DD:                                                                                   \
-    hipLaunchKernelGGL(add_ln_bwd_kernel<DD>, grd, dim3(256), 0, st, a, b, n, gamma, mean,   \
-                       rstd, grad_out, dx, part_gamma, part_beta);                           \
+    if (dr)                                                                                  \
+      hipLaunchKernelGGL((add_ln_bwd_kernel<DD, true>), grd, dim3(256), 0, st, a, b, n,      \
+                         gamma, mean, rstd, grad_out, dxb, dxa, part_gamma, part_beta, *dr); \
+    else                                                                                     \
+      hipLaunchKernelGGL((add_ln_bwd_kernel<DD, false>), grd, dim3(256), 0, st, a, b, n,     \
+                         gamma, mean, rstd, grad_out, dxb, nullptr, part_gamma, part_beta,   \
+                         none);                                                              \
     break;
   switch (d) {
     MIREC_ALB(32)
@@ -484,11 +564,63 @@ extern "C" int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, i
     MIREC_ALB(128)
     MIREC_ALB(256)
     default:
-      set_error("mirec_add_ln_bwd_f32: hidden size %d not in {32,64,128,256}", d);
+      set_error("%s: hidden size %d not in {32,64,128,256}", what, d);
       return -1;
   }
 #undef MIREC_ALB
-  return launch_status("mirec_add_ln_bwd_f32");
+  return launch_status(what);
+}
+
+static int ln_drop_args(float p, uint64_t seed, int64_t* counter, int64_t* drawn, LnDrop* dr,
+                        const char* what) {
+  if (!(p > 0.f && p < 1.f) || !drawn || !counter) {
+    set_error("%s: dropout %g needs 0 < p < 1, the counter and the drawn word", what, (double)p);
+    return -1;
+  }
+  dr->thr = (uint32_t)fmin(4294967295.0, ldexp(1.0 - (double)p, 32));
+  dr->scale = 1.0f / (1.0f - p);
+  dr->seed = seed;
+  dr->counter = counter;
+  dr->drawn = drawn;
+  return 0;
+}
+
+extern "C" int mirec_add_ln_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                    const float* gamma, const float* beta, float eps, float* out,
+                                    float* mean, float* rstd, void* stream) {
+  return add_ln_fwd_impl(a, b, n, d, gamma, beta, eps, out, mean, rstd, nullptr, stream,
+                         "mirec_add_ln_fwd_f32");
+}
+
+extern "C" int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                    const float* gamma, const float* mean, const float* rstd,
+                                    const float* grad_out, float* dx, float* part_gamma,
+                                    float* part_beta, void* stream) {
+  return add_ln_bwd_impl(a, b, n, d, gamma, mean, rstd, grad_out, dx, nullptr, part_gamma,
+                         part_beta, nullptr, stream, "mirec_add_ln_bwd_f32");
+}
+
+extern "C" int mirec_add_ln_drop_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                         const float* gamma, const float* beta, float eps,
+                                         float p, uint64_t seed, int64_t* counter,
+                                         int64_t* drawn, float* out, float* mean, float* rstd,
+                                         void* stream) {
+  LnDrop dr;
+  if (ln_drop_args(p, seed, counter, drawn, &dr, "mirec_add_ln_drop_fwd_f32")) return -1;
+  return add_ln_fwd_impl(a, b, n, d, gamma, beta, eps, out, mean, rstd, &dr, stream,
+                         "mirec_add_ln_drop_fwd_f32");
+}
+
+extern "C" int mirec_add_ln_drop_bwd_f32(const float* a, const float* b, int64_t n, int32_t d,
+                                         const float* gamma, const float* mean,
+                                         const float* rstd, const float* grad_out, float p,
+                                         uint64_t seed, int64_t* drawn, int64_t* counter,
+                                         float* dx_a, float* dx_b, float* part_gamma,
+                                         float* part_beta, void* stream) {
+  LnDrop dr;
+  if (ln_drop_args(p, seed, counter, drawn, &dr, "mirec_add_ln_drop_bwd_f32")) return -1;
+  return add_ln_bwd_impl(a, b, n, d, gamma, mean, rstd, grad_out, dx_b, dx_a, part_gamma,
+                         part_beta, &dr, stream, "mirec_add_ln_drop_bwd_f32");
 }
 
 static unsigned elem_grid(int64_t n) {

@@ -332,11 +332,93 @@ class _AddLNFn(torch.autograd.Function):
         return dx, dx, dgamma, dbeta, None
 
 
-def add_layer_norm(hidden, input_tensor, ln):
-    """ln(hidden + input_tensor) — the fused K9d kernel on the GPU (fp32, d in
-    {32, 64, 128, 256}), the module itself otherwise."""
-    if (hidden.is_cuda and hidden.dtype == torch.float32 and hidden.shape[-1] in (32, 64, 128, 256)
-            and ln.elementwise_affine and hidden.shape == input_tensor.shape):
+class _AddLNDropFn(torch.autograd.Function):
+    """LayerNorm(dropout(a) + b) (K9d with the dropout folded in, mirec_add_ln_drop_fwd/bwd_f32):
+    no dropped copy of a in HBM, no separate dropout kernels; rng = (seed, device counter,
+    unused) of the calling module; the backward advances the counter."""
+
+    @staticmethod
+    def forward(ctx, a, b, gamma, beta, eps, p, rng):
+        a, b = a.contiguous(), b.contiguous()
+        d = a.shape[-1]
+        n = a.numel() // d
+        out = torch.empty_like(a)
+        mean = torch.empty(n, dtype=torch.float32, device=a.device)
+        rstd = torch.empty(n, dtype=torch.float32, device=a.device)
+        drawn = torch.empty(1, dtype=torch.int64, device=a.device)
+        seed, counter, _ = rng
+        check(lib().mirec_add_ln_drop_fwd_f32(ptr(a), ptr(b), n, d, ptr(gamma.detach()),
+                                              ptr(beta.detach()), eps, float(p), seed,
+                                              ptr(counter), ptr(drawn), ptr(out), ptr(mean),
+                                              ptr(rstd), stream_handle()),
+              'mirec_add_ln_drop_fwd_f32')
+        ctx.save_for_backward(a, b, gamma, mean, rstd, drawn)
+        ctx.p, ctx.seed, ctx.counter = p, seed, counter
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, gamma, mean, rstd, drawn = ctx.saved_tensors
+        d = a.shape[-1]
+        n = a.numel() // d
+        parts = lib().mirec_seq_embed_ln_partials(n)
+        dxa, dxb = torch.empty_like(a), torch.empty_like(a)
+        pg = torch.empty(parts, d, dtype=torch.float32, device=a.device)
+        pb = torch.empty(parts, d, dtype=torch.float32, device=a.device)
+        check(lib().mirec_add_ln_drop_bwd_f32(ptr(a), ptr(b), n, d, ptr(gamma.detach()),
+                                              ptr(mean), ptr(rstd), ptr(g.contiguous()),
+                                              float(ctx.p), ctx.seed, ptr(drawn),
+                                              ptr(ctx.counter), ptr(dxa), ptr(dxb), ptr(pg),
+                                              ptr(pb), stream_handle()),
+              'mirec_add_ln_drop_bwd_f32')
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(gamma)
+        check(lib().mirec_colsum_f32(ptr(pg), parts, d, ptr(dgamma), stream_handle()),
+              'mirec_colsum_f32')
+        check(lib().mirec_colsum_f32(ptr(pb), parts, d, ptr(dbeta), stream_handle()),
+              'mirec_colsum_f32')
+        return dxa, dxb, dgamma, dbeta, None, None, None
+
+
+_DROP_SITES = [0]
+
+
+def _drop_rng(owner, dev):
+    """(seed, device draw counter, ticket) of a module's folded dropout: the seed from the
+    device generator's initial seed (no CPU generator draw) and the module's index."""
+    st = getattr(owner, '_ln_drop_rng', None)
+    if st is None or st[1].device != dev:
+        if not hasattr(owner, '_ln_drop_index'):
+            owner._ln_drop_index = _DROP_SITES[0]
+            _DROP_SITES[0] += 1
+        seed = (torch.cuda.default_generators[dev.index or 0].initial_seed() * 0x85EBCA6B
+                + 0x1000 + owner._ln_drop_index) & ((1 << 64) - 1)
+        st = (seed, torch.zeros(1, dtype=torch.int64, device=dev),
+              torch.zeros(1, dtype=torch.int32, device=dev))
+        owner._ln_drop_rng = st
+    return st
+
+
+K9D_DROP = True     # the hidden dropout before add_layer_norm folded into K9d
+
+
+def add_layer_norm(hidden, input_tensor, ln, drop=None, owner=None):
+    """ln(drop(hidden) + input_tensor) — the fused K9d kernel on the GPU (fp32, d in
+    {32, 64, 128, 256}; drop: the nn.Dropout on hidden, folded in while training with
+    p > 0), the modules themselves otherwise."""
+    fused = (hidden.is_cuda and hidden.dtype == torch.float32
+             and hidden.shape[-1] in (32, 64, 128, 256) and ln.elementwise_affine
+             and hidden.shape == input_tensor.shape)
+    p = drop.p if (drop is not None and drop.training) else 0.0
+    if fused and p > 0 and K9D_DROP and p < 1:
+        rng = _drop_rng(owner if owner is not None else drop, hidden.device)
+        out = _AddLNDropFn.apply(hidden, input_tensor, ln.weight, ln.bias, float(ln.eps), p, rng)
+        if not out.requires_grad:             # no backward will advance the draw counter
+            rng[1].add_(1)
+        return out
+    if drop is not None:
+        hidden = drop(hidden)
+    if fused:
         return _AddLNFn.apply(hidden, input_tensor, ln.weight, ln.bias, float(ln.eps))
     return ln(hidden + input_tensor)
 
@@ -371,7 +453,7 @@ class _AttnFn(torch.autograd.Function):
     """K9e (csrc/attn.hip): softmax(q k^T / sqrt(dh) + mask) -> dropout(p) -> @ v for the
     [B, L, H*64] Linear outputs q, k, v (L <= 64), the context returned as [B, L, H*64]
     (the reference's permute(0, 2, 1, 3) + view, layers.py:391-397, without the copy).
-    rng = (seed, device counter, ticket) when p > 0."""
+    rng = (seed, device counter, unused) when p > 0; the backward advances the counter."""
 
     @staticmethod
     def forward(ctx, q, k, v, mask, H, p, rng):
@@ -379,14 +461,13 @@ class _AttnFn(torch.autograd.Function):
         out = torch.empty_like(q)
         lse = torch.empty(B * H, 64, dtype=torch.float32, device=q.device)
         keep = torch.empty(B * H, 64, dtype=torch.int64, device=q.device) if p > 0 else None
-        seed, counter, arrive = rng if p > 0 else (0, None, None)
+        seed, counter, _ = rng if p > 0 else (0, None, None)
         check(lib().mirec_attn_fwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), B, L, H, float(p),
-                                       seed, ptr(counter) if p > 0 else None,
-                                       ptr(arrive) if p > 0 else None, ptr(out), ptr(lse),
+                                       seed, ptr(counter) if p > 0 else None, ptr(out), ptr(lse),
                                        ptr(keep) if p > 0 else None, stream_handle()),
               'mirec_attn_fwd_f32')
         ctx.save_for_backward(q, k, v, mask, lse, keep)
-        ctx.H, ctx.p = H, p
+        ctx.H, ctx.p, ctx.counter = H, p, counter
         return out
 
     @staticmethod
@@ -395,7 +476,8 @@ class _AttnFn(torch.autograd.Function):
         B, L, _ = q.shape
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         check(lib().mirec_attn_bwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), ptr(g.contiguous()),
-                                       ptr(lse), ptr(keep) if keep is not None else None, B, L,
+                                       ptr(lse), ptr(keep) if keep is not None else None,
+                                       ptr(ctx.counter) if keep is not None else None, B, L,
                                        ctx.H, float(ctx.p), ptr(dq), ptr(dk), ptr(dv),
                                        stream_handle()), 'mirec_attn_bwd_f32')
         return dq, dk, dv, None, None, None, None
@@ -465,11 +547,13 @@ class MultiHeadAttention(nn.Module):
         if attn_k9e_applies(ql, attention_mask, self.num_attention_heads,
                             self.attention_head_size):
             p = self.attn_dropout.p if self.training else 0.0
+            rng = self._k9e_rng(ql.device) if p > 0 else None
             ctx = _AttnFn.apply(ql.contiguous(), kl.contiguous(), vl.contiguous(),
-                                attention_mask, self.num_attention_heads, p,
-                                self._k9e_rng(ql.device) if p > 0 else None)
-            hidden = self.out_dropout(linear(self.dense, ctx))
-            return add_layer_norm(hidden, input_tensor, self.LayerNorm)
+                                attention_mask, self.num_attention_heads, p, rng)
+            if rng is not None and not ctx.requires_grad:   # no backward to advance it
+                rng[1].add_(1)
+            return add_layer_norm(linear(self.dense, ctx), input_tensor, self.LayerNorm,
+                                  drop=self.out_dropout)
         q = self.transpose_for_scores(ql)
         k = self.transpose_for_scores(kl)
         v = self.transpose_for_scores(vl)
@@ -488,8 +572,8 @@ class MultiHeadAttention(nn.Module):
             probs = self.attn_dropout(probs)
             ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
         ctx = ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
-        hidden = self.out_dropout(linear(self.dense, ctx))
-        return add_layer_norm(hidden, input_tensor, self.LayerNorm)
+        return add_layer_norm(linear(self.dense, ctx), input_tensor, self.LayerNorm,
+                              drop=self.out_dropout)
 
 
 class FeedForward(nn.Module):
@@ -517,8 +601,7 @@ class FeedForward(nn.Module):
 
     def forward(self, input_tensor):
         hidden = linear(self.dense_2, self.intermediate_act_fn(linear(self.dense_1, input_tensor)))
-        hidden = self.dropout(hidden)
-        return add_layer_norm(hidden, input_tensor, self.LayerNorm)
+        return add_layer_norm(hidden, input_tensor, self.LayerNorm, drop=self.dropout)
 
 
 class TransformerLayer(nn.Module):

@@ -35,20 +35,19 @@ def main():
     lse = torch.empty(B * H, 64, device=dev)
     keep = torch.empty(B * H, 64, dtype=torch.int64, device=dev)
     counter = torch.zeros(1, dtype=torch.int64, device=dev)
-    arrive = torch.zeros(1, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     L_ = lib()
     res = {}
     for p in (0.0, 0.5):
         def fwd():
             check(L_.mirec_attn_fwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), B, L, H, p, 7,
-                                        ptr(counter) if p else None, ptr(arrive) if p else None,
-                                        ptr(out), ptr(lse), ptr(keep) if p else None, st), 'fwd')
+                                        ptr(counter) if p else None, ptr(out), ptr(lse),
+                                        ptr(keep) if p else None, st), 'fwd')
 
         def bwd():
             check(L_.mirec_attn_bwd_f32(ptr(q), ptr(k), ptr(v), ptr(mask), ptr(go), ptr(lse),
-                                        ptr(keep) if p else None, B, L, H, p, ptr(dq), ptr(dk),
-                                        ptr(dv), st), 'bwd')
+                                        ptr(keep) if p else None, ptr(counter) if p else None,
+                                        B, L, H, p, ptr(dq), ptr(dk), ptr(dv), st), 'bwd')
         for name, fn in (('fwd', fwd), ('bwd', bwd)):
             ts = []
             for _ in range(22):
