@@ -947,6 +947,11 @@ int mirec_attn_bwd_f32(const float* q, const float* k, const float* v, const flo
                        const float* dout, const float* lse, const uint64_t* keep_words,
                        int64_t* counter, int64_t B, int32_t L, int32_t H, float dropout_p,
                        float* dq, float* dk, float* dv, void* stream);
+/* SASRec.get_attention_mask (sasrec.py:91-105) in one launch: mask [B, 1, L, L] float =
+ * (1 - [item_seq[b][j] > 0] * [j <= i]) * -10000, the reference's values bit for bit (-0.0
+ * where attention is allowed). item_seq: [B, L] int64. */
+int mirec_seq_attn_mask_f32(const int64_t* item_seq, int64_t B, int32_t L, float* mask,
+                            void* stream);
 /* GELU (erf form) of the feed-forward block, forward and backward, elementwise. */
 int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream);
 int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, float* dx, void* stream);

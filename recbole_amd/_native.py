@@ -165,6 +165,7 @@ SIGNATURES = {
                                    ctypes.c_uint64, _P, _P, _P, _P, _P]),
     "mirec_attn_bwd_f32": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int64, c_int32, c_int32,
                                    c_float, _P, _P, _P, _P]),
+    "mirec_seq_attn_mask_f32": (c_int, [_P, c_int64, c_int32, _P, _P]),
     "mirec_gelu_fwd_f32": (c_int, [_P, c_int64, _P, _P]),
     "mirec_gelu_bwd_f32": (c_int, [_P, _P, c_int64, _P, _P]),
     "mirec_add_ln_fwd_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_float, _P, _P, _P, _P]),

@@ -623,9 +623,37 @@ extern "C" int mirec_add_ln_drop_bwd_f32(const float* a, const float* b, int64_t
                          part_beta, &dr, stream, "mirec_add_ln_drop_bwd_f32");
 }
 
+// SASRec.get_attention_mask (reference sasrec.py:91-105) in one launch: mask[b][i][j] =
+// (1 - [item_seq[b][j] > 0] * [j <= i]) * -10000 as the reference's float ops round it —
+// -0.0 where attention is allowed ((1 - 1) * -10000), -10000 elsewhere.
+__global__ __launch_bounds__(256) void seq_attn_mask_kernel(const int64_t* __restrict__ seq,
+                                                            int64_t B, int L,
+                                                            float* __restrict__ mask) {
+  const int64_t n = B * (int64_t)L * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / ((int64_t)L * L);
+    const int i = (int)((e / L) % L), j = (int)(e % L);
+    const float keep = (seq[b * L + j] > 0 && j <= i) ? 1.0f : 0.0f;
+    mask[e] = (1.0f - keep) * -10000.0f;
+  }
+}
+
 static unsigned elem_grid(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 256 * 32 ? 256 * 32 : g));
+}
+
+extern "C" int mirec_seq_attn_mask_f32(const int64_t* item_seq, int64_t B, int32_t L,
+                                       float* mask, void* stream) {
+  if (B == 0 || L == 0) return 0;
+  if (!item_seq || !mask || B < 0 || L < 0) {
+    set_error("mirec_seq_attn_mask_f32: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(seq_attn_mask_kernel, dim3(elem_grid(B * (int64_t)L * L)), dim3(256), 0,
+                     (hipStream_t)stream, item_seq, B, L, mask);
+  return launch_status("mirec_seq_attn_mask_f32");
 }
 
 extern "C" int mirec_gelu_fwd_f32(const float* x, int64_t n, float* y, void* stream) {

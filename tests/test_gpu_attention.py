@@ -146,3 +146,22 @@ def test_multihead_attention_module_k9e(dev):
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=2e-5)
     for a, b in zip(outs[0][1], outs[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
+def test_sasrec_attention_mask_kernel_bitwise(dev):
+    """SASRec.get_attention_mask on the GPU (one launch) equals the reference's seven-op
+    construction (sasrec.py:91-105) bit for bit, -0.0 entries included."""
+    g = torch.Generator().manual_seed(8)
+    B, L = 33, 50
+    lens = torch.randint(0, L + 1, (B,), generator=g)
+    seq = torch.randint(1, 1000, (B, L), generator=g) * (torch.arange(L)[None, :] < lens[:, None])
+    seq[3, 7] = 0                                   # a gap inside a sequence
+    ext = (seq > 0).long()[:, None, None, :] * \
+        (torch.triu(torch.ones((1, L, L)), diagonal=1) == 0).unsqueeze(1).long()
+    want = (1.0 - ext.to(torch.float32)) * -10000.0
+    from recbole_amd._native import check, lib, ptr
+    got = torch.empty(B, 1, L, L, device=dev)
+    sd = seq.to(dev)
+    check(lib().mirec_seq_attn_mask_f32(ptr(sd), B, L, ptr(got),
+                                        torch.cuda.current_stream(dev).cuda_stream), 'mask')
+    assert torch.equal(got.cpu().view(torch.int32), want.view(torch.int32))
