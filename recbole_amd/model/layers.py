@@ -256,7 +256,7 @@ def _k11(x, n_in, n_out):
     """K11 where its widths allow (C3 step trace: the four 128 x 128 products 68-80 -> 49 us
     each; the 256-wide forward / data-gradient four 72-124 -> 82-88 us, 362 -> 340 us in
     all)."""
-    return (K11 and x.is_cuda and x.dtype == torch.float32
+    return (K11 and x.is_cuda and x.dtype == torch.float32 and x.data_ptr() % 16 == 0
             and lib().mirec_linear_shape_ok(n_in, n_out) != 0)
 
 
