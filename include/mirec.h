@@ -909,6 +909,23 @@ int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items, const f
                                const float* gamma, const float* mean, const float* rstd,
                                const float* grad_out, float* dx, float* ditem,
                                float* part_gamma, float* part_beta, void* stream);
+/* K9a with SASRec's embedding dropout after the LayerNorm (sasrec.py:107-114) folded in:
+ * out = drop_p(LayerNorm(...)); the backward masks grad_out with the same flags. Draws as
+ * mirec_add_ln_drop_fwd_f32 (the forward records the counter value in drawn[0], the backward
+ * redraws from it and sets counter = drawn[0] + 1). */
+int mirec_seq_embed_ln_drop_fwd_f32(const float* item_table, int64_t n_items,
+                                    const float* pos_table, const int64_t* item_seq, int64_t B,
+                                    int32_t L, int32_t d, const float* gamma, const float* beta,
+                                    float eps, float p, uint64_t seed, int64_t* counter,
+                                    int64_t* drawn, float* out, float* mean, float* rstd,
+                                    void* stream);
+int mirec_seq_embed_ln_drop_bwd_f32(const float* item_table, int64_t n_items,
+                                    const float* pos_table, const int64_t* item_seq, int64_t B,
+                                    int32_t L, int32_t d, const float* gamma, const float* mean,
+                                    const float* rstd, const float* grad_out, float p,
+                                    uint64_t seed, int64_t* drawn, int64_t* counter, float* dx,
+                                    float* ditem, float* part_gamma, float* part_beta,
+                                    void* stream);
 /* K9d  LayerNorm(a + b) of the transformer blocks' residual connections (layers.py
  * MultiHeadAttention / FeedForward, reference layers.py:338-552) in one pass, and its
  * backward (dx = d(a + b), per-block dgamma / dbeta partials as K9a, summed with

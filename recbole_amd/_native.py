@@ -268,6 +268,12 @@ SIGNATURES = {
     "mirec_seq_embed_ln_partials": (c_int64, [c_int64]),
     "mirec_seq_embed_ln_bwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32, _P,
                                            _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mirec_seq_embed_ln_drop_fwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32,
+                                                _P, _P, c_float, c_float, ctypes.c_uint64, _P,
+                                                _P, _P, _P, _P, _P]),
+    "mirec_seq_embed_ln_drop_bwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32,
+                                                _P, _P, _P, _P, c_float, ctypes.c_uint64, _P,
+                                                _P, _P, _P, _P, _P, _P]),
     "mirec_sampled_softmax_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32,
                                           c_float, _P, _P, _P, _P]),
     "mirec_rank_of_pos_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32, _P,

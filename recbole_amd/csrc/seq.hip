@@ -33,17 +33,51 @@ __device__ __forceinline__ float sum4(float4 a) { return (a.x + a.y) + (a.z + a.
 
 constexpr int kLnRowsPerBlock = 64;   // K9a backward partial-sum chunk (fixed)
 
-template <int D>
+// Dropout folded into K9a / K9d (counter-based draws; the K9d header below spells them out)
+struct LnDrop {
+  uint32_t thr;
+  float scale;
+  uint64_t seed;
+  int64_t* counter;     // forward: read; backward: set to drawn + 1
+  int64_t* drawn;       // forward writes the counter value used; backward reads it
+};
+
+__device__ __forceinline__ uint64_t ln_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// keep flags of the four elements e0 .. e0 + 3 (e0 a multiple of 4)
+__device__ __forceinline__ void ln_keep4(uint64_t key, uint64_t e0, uint32_t thr, bool (&k)[4]) {
+  const uint64_t h0 = ln_mix(key ^ (e0 >> 1)), h1 = ln_mix(key ^ ((e0 >> 1) + 1));
+  k[0] = (uint32_t)h0 < thr;
+  k[1] = (uint32_t)(h0 >> 32) < thr;
+  k[2] = (uint32_t)h1 < thr;
+  k[3] = (uint32_t)(h1 >> 32) < thr;
+}
+
+
+// DROP: SASRec's embedding dropout (sasrec.py:107-114, after the LayerNorm) folded in: the
+// output is drop(LayerNorm(...)), the backward masks the incoming gradient the same way.
+template <int D, bool DROP = false>
 __global__ __launch_bounds__(256) void seq_embed_ln_fwd_kernel(
     const float* __restrict__ E, int64_t n_items, const float* __restrict__ P,
     const int64_t* __restrict__ seq, int64_t n_rows, int L, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out,
-    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, LnDrop dr) {
   constexpr int LPR = D / 4, GPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int g = lane / LPR, l = lane % LPR;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t r = wave * GPW + g;
+  uint64_t key = 0;
+  if (DROP) {
+    const int64_t cv = dr.counter[0];
+    key = ln_mix(dr.seed + (uint64_t)cv);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dr.drawn[0] = cv;
+  }
   if (r >= n_rows) return;
   int64_t id = seq[r];
   id = id < 0 ? 0 : (id >= n_items ? n_items - 1 : id);
@@ -63,6 +97,14 @@ __global__ __launch_bounds__(256) void seq_embed_ln_fwd_kernel(
   y.y = c.y * rstd * gm.y + bt.y;
   y.z = c.z * rstd * gm.z + bt.z;
   y.w = c.w * rstd * gm.w + bt.w;
+  if (DROP) {
+    bool k[4];
+    ln_keep4(key, (uint64_t)r * D + 4 * l, dr.thr, k);
+    y.x = k[0] ? y.x * dr.scale : 0.f;
+    y.y = k[1] ? y.y * dr.scale : 0.f;
+    y.z = k[2] ? y.z * dr.scale : 0.f;
+    y.w = k[3] ? y.w * dr.scale : 0.f;
+  }
   reinterpret_cast<float4*>(out + r * D)[l] = y;
   if (l == 0) {
     mean_out[r] = mean;
@@ -72,14 +114,17 @@ __global__ __launch_bounds__(256) void seq_embed_ln_fwd_kernel(
 
 // Block = 4 waves over kLnRowsPerBlock consecutive rows; writes dx rows, the
 // item-row gradient (0 for padding id 0) and the block's partial dgamma / dbeta.
-template <int D>
+template <int D, bool DROP = false>
 __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
     const float* __restrict__ E, int64_t n_items, const float* __restrict__ P,
     const int64_t* __restrict__ seq, int64_t n_rows, int L, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const float* __restrict__ gy, float* __restrict__ dx, float* __restrict__ ditem,
-    float* __restrict__ part_gamma, float* __restrict__ part_beta) {
+    float* __restrict__ part_gamma, float* __restrict__ part_beta, LnDrop dr) {
   constexpr int LPR = D / 4, GPW = 64 / LPR;
+  const int64_t cv = DROP ? dr.drawn[0] : 0;
+  const uint64_t key = DROP ? ln_mix(dr.seed + (uint64_t)cv) : 0ull;
+  if (DROP && blockIdx.x == 0 && threadIdx.x == 0) dr.counter[0] = cv + 1;   // the next draw
   __shared__ float4 red_g[4 * GPW][LPR];
   __shared__ float4 red_b[4 * GPW][LPR];
   const int lane = threadIdx.x & 63;
@@ -103,7 +148,15 @@ __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
     xh.y = (e.y + p.y - mean) * rstd;
     xh.z = (e.z + p.z - mean) * rstd;
     xh.w = (e.w + p.w - mean) * rstd;
-    const float4 gv = reinterpret_cast<const float4*>(gy + r * D)[l];
+    float4 gv = reinterpret_cast<const float4*>(gy + r * D)[l];
+    if (DROP) {
+      bool k[4];
+      ln_keep4(key, (uint64_t)r * D + 4 * l, dr.thr, k);
+      gv.x = k[0] ? gv.x * dr.scale : 0.f;
+      gv.y = k[1] ? gv.y * dr.scale : 0.f;
+      gv.z = k[2] ? gv.z * dr.scale : 0.f;
+      gv.w = k[3] ? gv.w * dr.scale : 0.f;
+    }
     const float4 gg = make_float4(gv.x * gm.x, gv.y * gm.y, gv.z * gm.z, gv.w * gm.w);
     const float m1 = lane_group_sum<LPR>(sum4(gg)) * (1.0f / D);
     const float m2 =
@@ -152,30 +205,6 @@ __global__ __launch_bounds__(256) void seq_embed_ln_bwd_kernel(
 //   many atomics on one word, 153 us against 28 for the kernel itself);
 //   element e = row * D + column is kept iff the 32-bit half e & 1 of
 //   splitmix64(key ^ (e >> 1)) is below thr; a kept element is scaled by 1 / (1 - p).
-struct LnDrop {
-  uint32_t thr;
-  float scale;
-  uint64_t seed;
-  int64_t* counter;     // forward: read; backward: set to drawn + 1
-  int64_t* drawn;       // forward writes the counter value used; backward reads it
-};
-
-__device__ __forceinline__ uint64_t ln_mix(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// keep flags of the four elements e0 .. e0 + 3 (e0 a multiple of 4)
-__device__ __forceinline__ void ln_keep4(uint64_t key, uint64_t e0, uint32_t thr, bool (&k)[4]) {
-  const uint64_t h0 = ln_mix(key ^ (e0 >> 1)), h1 = ln_mix(key ^ ((e0 >> 1) + 1));
-  k[0] = (uint32_t)h0 < thr;
-  k[1] = (uint32_t)(h0 >> 32) < thr;
-  k[2] = (uint32_t)h1 < thr;
-  k[3] = (uint32_t)(h1 >> 32) < thr;
-}
-
 template <int D, bool DROP>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(
     const float* __restrict__ A, const float* __restrict__ Bv, int64_t n_rows,
@@ -425,26 +454,34 @@ __global__ __launch_bounds__(256) void sampled_softmax_kernel(
 
 using namespace mirec;
 
-extern "C" int mirec_seq_embed_ln_fwd_f32(const float* item_table, int64_t n_items,
-                                          const float* pos_table, const int64_t* item_seq,
-                                          int64_t B, int32_t L, int32_t d, const float* gamma,
-                                          const float* beta, float eps, float* out, float* mean,
-                                          float* rstd, void* stream) {
+static int seq_embed_ln_fwd_impl(const float* item_table, int64_t n_items,
+                                 const float* pos_table, const int64_t* item_seq, int64_t B,
+                                 int32_t L, int32_t d, const float* gamma, const float* beta,
+                                 float eps, float* out, float* mean, float* rstd,
+                                 const LnDrop* dr, void* stream, const char* what) {
   const int64_t n = B * L;
   if (n == 0) return 0;
   if (!item_table || !pos_table || !item_seq || !gamma || !beta || !out || !mean || !rstd ||
       B < 0 || L <= 0 || n_items <= 0) {
-    set_error("mirec_seq_embed_ln_fwd_f32: bad arguments");
+    set_error("%s: bad arguments", what);
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
+  LnDrop none;
+  memset(&none, 0, sizeof(none));
 #define MIREC_LNF(DD)                                                                        \
   case DD: {                                                                                 \
     constexpr int GPW = 64 / (DD / 4);                                                       \
     const int64_t waves = (n + GPW - 1) / GPW;                                               \
-    hipLaunchKernelGGL(seq_embed_ln_fwd_kernel<DD>, dim3((unsigned)((waves + 3) / 4)),       \
-                       dim3(256), 0, st, item_table, n_items, pos_table, item_seq, n, L,     \
-                       gamma, beta, eps, out, mean, rstd);                                   \
+    const dim3 grd((unsigned)((waves + 3) / 4));                                             \
+    if (dr)                                                                                  \
+      hipLaunchKernelGGL((seq_embed_ln_fwd_kernel<DD, true>), grd, dim3(256), 0, st,         \
+                         item_table, n_items, pos_table, item_seq, n, L, gamma, beta, eps,   \
+                         out, mean, rstd, *dr);                                              \
+    else                                                                                     \
+      hipLaunchKernelGGL((seq_embed_ln_fwd_kernel<DD, false>), grd, dim3(256), 0, st,        \
+                         item_table, n_items, pos_table, item_seq, n, L, gamma, beta, eps,   \
+                         out, mean, rstd, none);                                             \
   } break;
   switch (d) {
     MIREC_LNF(32)
@@ -452,37 +489,44 @@ extern "C" int mirec_seq_embed_ln_fwd_f32(const float* item_table, int64_t n_ite
     MIREC_LNF(128)
     MIREC_LNF(256)
     default:
-      set_error("mirec_seq_embed_ln_fwd_f32: hidden size %d not in {32,64,128,256}", d);
+      set_error("%s: hidden size %d not in {32,64,128,256}", what, d);
       return -1;
   }
 #undef MIREC_LNF
-  return launch_status("mirec_seq_embed_ln_fwd_f32");
+  return launch_status(what);
 }
 
 extern "C" int64_t mirec_seq_embed_ln_partials(int64_t n_rows) {
   return (n_rows + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
 }
 
-extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items,
-                                          const float* pos_table, const int64_t* item_seq,
-                                          int64_t B, int32_t L, int32_t d, const float* gamma,
-                                          const float* mean, const float* rstd,
-                                          const float* grad_out, float* dx, float* ditem,
-                                          float* part_gamma, float* part_beta, void* stream) {
+static int seq_embed_ln_bwd_impl(const float* item_table, int64_t n_items,
+                                 const float* pos_table, const int64_t* item_seq, int64_t B,
+                                 int32_t L, int32_t d, const float* gamma, const float* mean,
+                                 const float* rstd, const float* grad_out, float* dx,
+                                 float* ditem, float* part_gamma, float* part_beta,
+                                 const LnDrop* dr, void* stream, const char* what) {
   const int64_t n = B * L;
   if (n == 0) return 0;
   if (!item_table || !pos_table || !item_seq || !gamma || !mean || !rstd || !grad_out ||
       !part_gamma || !part_beta || B < 0 || L <= 0 || n_items <= 0) {
-    set_error("mirec_seq_embed_ln_bwd_f32: bad arguments");
+    set_error("%s: bad arguments", what);
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
   const dim3 grd((unsigned)mirec_seq_embed_ln_partials(n));
+  LnDrop none;
+  memset(&none, 0, sizeof(none));
 #define MIREC_LNB(DD)                                                                        \
   case DD:                                                                                   \
-    hipLaunchKernelGGL(seq_embed_ln_bwd_kernel<DD>, grd, dim3(256), 0, st, item_table,       \
-                       n_items, pos_table, item_seq, n, L, gamma, mean, rstd, grad_out, dx,  \
-                       ditem, part_gamma, part_beta);                                        \
+    if (dr)                                                                                  \
+      hipLaunchKernelGGL((seq_embed_ln_bwd_kernel<DD, true>), grd, dim3(256), 0, st,         \
+                         item_table, n_items, pos_table, item_seq, n, L, gamma, mean, rstd,  \
+                         grad_out, dx, ditem, part_gamma, part_beta, *dr);                   \
+    else                                                                                     \
+      hipLaunchKernelGGL((seq_embed_ln_bwd_kernel<DD, false>), grd, dim3(256), 0, st,        \
+                         item_table, n_items, pos_table, item_seq, n, L, gamma, mean, rstd,  \
+                         grad_out, dx, ditem, part_gamma, part_beta, none);                  \
     break;
   switch (d) {
     MIREC_LNB(32)
@@ -490,11 +534,11 @@ extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_ite
     MIREC_LNB(128)
     MIREC_LNB(256)
     default:
-      set_error("mirec_seq_embed_ln_bwd_f32: hidden size %d not in {32,64,128,256}", d);
+      set_error("%s: hidden size %d not in {32,64,128,256}", what, d);
       return -1;
   }
 #undef MIREC_LNB
-  return launch_status("mirec_seq_embed_ln_bwd_f32");
+  return launch_status(what);
 }
 
 static int add_ln_fwd_impl(const float* a, const float* b, int64_t n, int32_t d,
@@ -598,6 +642,57 @@ extern "C" int mirec_add_ln_bwd_f32(const float* a, const float* b, int64_t n, i
                                     float* part_beta, void* stream) {
   return add_ln_bwd_impl(a, b, n, d, gamma, mean, rstd, grad_out, dx, nullptr, part_gamma,
                          part_beta, nullptr, stream, "mirec_add_ln_bwd_f32");
+}
+
+extern "C" int mirec_seq_embed_ln_fwd_f32(const float* item_table, int64_t n_items,
+                                          const float* pos_table, const int64_t* item_seq,
+                                          int64_t B, int32_t L, int32_t d, const float* gamma,
+                                          const float* beta, float eps, float* out, float* mean,
+                                          float* rstd, void* stream) {
+  return seq_embed_ln_fwd_impl(item_table, n_items, pos_table, item_seq, B, L, d, gamma, beta,
+                               eps, out, mean, rstd, nullptr, stream,
+                               "mirec_seq_embed_ln_fwd_f32");
+}
+
+extern "C" int mirec_seq_embed_ln_bwd_f32(const float* item_table, int64_t n_items,
+                                          const float* pos_table, const int64_t* item_seq,
+                                          int64_t B, int32_t L, int32_t d, const float* gamma,
+                                          const float* mean, const float* rstd,
+                                          const float* grad_out, float* dx, float* ditem,
+                                          float* part_gamma, float* part_beta, void* stream) {
+  return seq_embed_ln_bwd_impl(item_table, n_items, pos_table, item_seq, B, L, d, gamma, mean,
+                               rstd, grad_out, dx, ditem, part_gamma, part_beta, nullptr, stream,
+                               "mirec_seq_embed_ln_bwd_f32");
+}
+
+extern "C" int mirec_seq_embed_ln_drop_fwd_f32(const float* item_table, int64_t n_items,
+                                               const float* pos_table, const int64_t* item_seq,
+                                               int64_t B, int32_t L, int32_t d,
+                                               const float* gamma, const float* beta, float eps,
+                                               float p, uint64_t seed, int64_t* counter,
+                                               int64_t* drawn, float* out, float* mean,
+                                               float* rstd, void* stream) {
+  LnDrop dr;
+  if (ln_drop_args(p, seed, counter, drawn, &dr, "mirec_seq_embed_ln_drop_fwd_f32")) return -1;
+  return seq_embed_ln_fwd_impl(item_table, n_items, pos_table, item_seq, B, L, d, gamma, beta,
+                               eps, out, mean, rstd, &dr, stream,
+                               "mirec_seq_embed_ln_drop_fwd_f32");
+}
+
+extern "C" int mirec_seq_embed_ln_drop_bwd_f32(const float* item_table, int64_t n_items,
+                                               const float* pos_table, const int64_t* item_seq,
+                                               int64_t B, int32_t L, int32_t d,
+                                               const float* gamma, const float* mean,
+                                               const float* rstd, const float* grad_out,
+                                               float p, uint64_t seed, int64_t* drawn,
+                                               int64_t* counter, float* dx, float* ditem,
+                                               float* part_gamma, float* part_beta,
+                                               void* stream) {
+  LnDrop dr;
+  if (ln_drop_args(p, seed, counter, drawn, &dr, "mirec_seq_embed_ln_drop_bwd_f32")) return -1;
+  return seq_embed_ln_bwd_impl(item_table, n_items, pos_table, item_seq, B, L, d, gamma, mean,
+                               rstd, grad_out, dx, ditem, part_gamma, part_beta, &dr, stream,
+                               "mirec_seq_embed_ln_drop_bwd_f32");
 }
 
 extern "C" int mirec_add_ln_drop_fwd_f32(const float* a, const float* b, int64_t n, int32_t d,

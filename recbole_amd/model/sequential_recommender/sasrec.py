@@ -22,7 +22,7 @@ import torch.nn as nn
 from recbole_amd import ops
 from recbole_amd._native import check, lib, ptr, stream_handle
 from recbole_amd.model.abstract_recommender import SequentialRecommender
-from recbole_amd.model.layers import TransformerEncoder
+from recbole_amd.model.layers import TransformerEncoder, _drop_rng
 from recbole_amd.model.loss import BPRLoss
 
 
@@ -30,7 +30,7 @@ class _SeqEmbedLNFn(torch.autograd.Function):
     """LayerNorm(item_embedding[item_seq] + position_embedding[t]) (K9a)."""
 
     @staticmethod
-    def forward(ctx, E, P, gamma, beta, item_seq, eps):
+    def forward(ctx, E, P, gamma, beta, item_seq, eps, p=0.0, rng=None):
         B, L = item_seq.shape
         d = E.shape[1]
         dev = E.device
@@ -43,17 +43,27 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         out = torch.empty(B, L, d, dtype=torch.float32, device=dev)
         mean = torch.empty(B * L, dtype=torch.float32, device=dev)
         rstd = torch.empty(B * L, dtype=torch.float32, device=dev)
-        rc = lib().mirec_seq_embed_ln_fwd_f32(ptr(E.detach()), E.shape[0], ptr(P.detach()),
-                                              ptr(seq), B, L, d, ptr(gamma.detach()),
-                                              ptr(beta.detach()), eps, ptr(out), ptr(mean),
-                                              ptr(rstd), stream_handle())
-        check(rc, "mirec_seq_embed_ln_fwd_f32")
-        ctx.save_for_backward(E, P, gamma, seq, mean, rstd)
+        drawn = None
+        if p > 0:                             # the embedding dropout folded in
+            drawn = torch.empty(1, dtype=torch.int64, device=dev)
+            rc = lib().mirec_seq_embed_ln_drop_fwd_f32(
+                ptr(E.detach()), E.shape[0], ptr(P.detach()), ptr(seq), B, L, d,
+                ptr(gamma.detach()), ptr(beta.detach()), eps, float(p), rng[0], ptr(rng[1]),
+                ptr(drawn), ptr(out), ptr(mean), ptr(rstd), stream_handle())
+            check(rc, "mirec_seq_embed_ln_drop_fwd_f32")
+        else:
+            rc = lib().mirec_seq_embed_ln_fwd_f32(ptr(E.detach()), E.shape[0], ptr(P.detach()),
+                                                  ptr(seq), B, L, d, ptr(gamma.detach()),
+                                                  ptr(beta.detach()), eps, ptr(out), ptr(mean),
+                                                  ptr(rstd), stream_handle())
+            check(rc, "mirec_seq_embed_ln_fwd_f32")
+        ctx.save_for_backward(E, P, gamma, seq, mean, rstd, drawn)
+        ctx.p, ctx.rng = p, rng
         return out
 
     @staticmethod
     def backward(ctx, g):
-        E, P, gamma, seq, mean, rstd = ctx.saved_tensors
+        E, P, gamma, seq, mean, rstd, drawn = ctx.saved_tensors
         B, L = seq.shape
         d = E.shape[1]
         dev = E.device
@@ -63,11 +73,20 @@ class _SeqEmbedLNFn(torch.autograd.Function):
         ditem = torch.empty(n, d, dtype=torch.float32, device=dev)
         pg = torch.empty(nparts, d, dtype=torch.float32, device=dev)
         pb = torch.empty(nparts, d, dtype=torch.float32, device=dev)
-        rc = lib().mirec_seq_embed_ln_bwd_f32(ptr(E.detach()), E.shape[0], ptr(P.detach()),
-                                              ptr(seq), B, L, d, ptr(gamma.detach()), ptr(mean),
-                                              ptr(rstd), ptr(g.contiguous()), ptr(dx),
-                                              ptr(ditem), ptr(pg), ptr(pb), stream_handle())
-        check(rc, "mirec_seq_embed_ln_bwd_f32")
+        if ctx.p > 0:
+            rc = lib().mirec_seq_embed_ln_drop_bwd_f32(
+                ptr(E.detach()), E.shape[0], ptr(P.detach()), ptr(seq), B, L, d,
+                ptr(gamma.detach()), ptr(mean), ptr(rstd), ptr(g.contiguous()), float(ctx.p),
+                ctx.rng[0], ptr(drawn), ptr(ctx.rng[1]), ptr(dx), ptr(ditem), ptr(pg), ptr(pb),
+                stream_handle())
+            check(rc, "mirec_seq_embed_ln_drop_bwd_f32")
+        else:
+            rc = lib().mirec_seq_embed_ln_bwd_f32(ptr(E.detach()), E.shape[0], ptr(P.detach()),
+                                                  ptr(seq), B, L, d, ptr(gamma.detach()),
+                                                  ptr(mean), ptr(rstd), ptr(g.contiguous()),
+                                                  ptr(dx), ptr(ditem), ptr(pg), ptr(pb),
+                                                  stream_handle())
+            check(rc, "mirec_seq_embed_ln_bwd_f32")
         if ctx.deferred:
             E._mirec_deferred.stash(E, ditem, seq.view(-1), ctx.segs)
             dE = None
@@ -83,7 +102,7 @@ class _SeqEmbedLNFn(torch.autograd.Function):
               "mirec_colsum_f32")
         check(lib().mirec_colsum_f32(ptr(pb), nparts, d, ptr(dbeta), stream_handle()),
               "mirec_colsum_f32")
-        return dE, dP, dgamma, dbeta, None, None
+        return dE, dP, dgamma, dbeta, None, None, None, None
 
 
 def _catch_up(ctx, E, items):
@@ -220,10 +239,17 @@ class SASRec(SequentialRecommender):
         return (1.0 - extended) * -10000.0
 
     def forward(self, item_seq, item_seq_len):
+        # the embedding dropout folds into K9a while training (p > 0); the module otherwise
+        p = self.dropout.p if (self.dropout.training and 0 < self.dropout.p < 1) else 0.0
+        rng = _drop_rng(self.dropout, item_seq.device) if p > 0 else None
         input_emb = _SeqEmbedLNFn.apply(self.item_embedding.weight,
                                         self.position_embedding.weight, self.LayerNorm.weight,
-                                        self.LayerNorm.bias, item_seq, self.layer_norm_eps)
-        input_emb = self.dropout(input_emb)
+                                        self.LayerNorm.bias, item_seq, self.layer_norm_eps, p,
+                                        rng)
+        if p == 0:
+            input_emb = self.dropout(input_emb)
+        elif not input_emb.requires_grad:     # no backward to advance the draw counter
+            rng[1].add_(1)
         mask = self.get_attention_mask(item_seq)
         out = self.trm_encoder(input_emb, mask, output_all_encoded_layers=True)[-1]
         return self.gather_indexes(out, item_seq_len - 1)

@@ -98,3 +98,39 @@ def test_ffn_block_folded_dropout_trains(dev):
         finally:
             layers.K9D_DROP = True
     torch.testing.assert_close(a, b)
+
+
+@pytest.mark.parametrize('p', [0.2, 0.5])
+def test_seq_embed_ln_drop_matches_restatement(dev, p):
+    """K9a with SASRec's embedding dropout folded in (mirec_seq_embed_ln_drop_fwd/bwd_f32,
+    through _SeqEmbedLNFn): dropout(LayerNorm(E[seq] + P[t])) of the reference
+    sasrec.py:107-114 against float64 torch applying the same keep flags (element index
+    (b L + t) d + j); forward and the gradients of E (rows 1..), P, gamma and beta; the
+    counter is read by the forward and advanced by the backward."""
+    from recbole_amd.model.sequential_recommender.sasrec import _SeqEmbedLNFn
+    B, L, d, n_items, eps, seed = 97, 50, 64, 500, 1e-12, 4242
+    g = torch.Generator().manual_seed(int(p * 10))
+    E, P = torch.randn(n_items, d, generator=g), torch.randn(L, d, generator=g)
+    gamma, beta = torch.rand(d, generator=g) + 0.5, torch.randn(d, generator=g)
+    seq = torch.randint(0, n_items, (B, L), generator=g)
+    gy = torch.randn(B, L, d, generator=g)
+    rng = (seed, torch.full((1,), 7, dtype=torch.int64, device=dev))
+    Ed, Pd, Gd, Bd = (t.to(dev).requires_grad_() for t in (E, P, gamma, beta))
+    y = _SeqEmbedLNFn.apply(Ed, Pd, Gd, Bd, seq.to(dev), eps, p, rng)
+    torch.cuda.synchronize(dev)
+    assert int(rng[1].item()) == 7
+    y.backward(gy.to(dev))
+    torch.cuda.synchronize(dev)
+    assert int(rng[1].item()) == 8
+    keep = torch.as_tensor(_keep(seed, 7, B * L * d, p).reshape(B, L, d))
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    E64, P64, G64, B64 = (t.double().requires_grad_() for t in (E, P, gamma, beta))
+    x = E64[seq] + P64[None]
+    want = torch.nn.functional.layer_norm(x, (d,), G64, B64, eps) * keep / (1 - p)
+    want.backward(gy.double())
+    tol = dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.detach().cpu(), want.detach().float(), **tol)
+    torch.testing.assert_close(Ed.grad.cpu()[1:], E64.grad[1:].float(), **tol)
+    torch.testing.assert_close(Pd.grad.cpu(), P64.grad.float(), rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(Gd.grad.cpu(), G64.grad.float(), rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(Bd.grad.cpu(), B64.grad.float(), rtol=1e-4, atol=2e-3)
