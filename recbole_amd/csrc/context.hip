@@ -300,8 +300,12 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(const ColsumJobs J) 
 // chunk (agent-scope ticket; write-through partial stores drained before it, an agent
 // acquire after, then plain loads) adds them.
 constexpr int kLgThreads = 256;
-constexpr int kLgRows = 1024;         // bias rows per chunk (2048: 50 blocks for K = 10^5 rows,
-                                      // too few waves to stream g)
+#ifndef MIREC_LG_ROWS
+#define MIREC_LG_ROWS 512
+#endif
+constexpr int kLgRows = MIREC_LG_ROWS;  // bias rows per chunk (C3: 512 -> 15.6 us, 1024 -> 20.1,
+                                        // 256 no better; 2048: 50 blocks for K = 10^5
+                                        // rows, too few waves to stream g)
 constexpr int kLgSumThreads = 64;     // lanes per block of the partial sum (256: 16 blocks for
                                       // a 128 x 128 dW, each lane walking C partials)
 struct LinearGradFinish {
@@ -400,20 +404,47 @@ __global__ __launch_bounds__(kLgThreads) void linear_grad_finish_kernel(const Li
   }
   __syncthreads();
   if (!s_last) return;
-  // after the acquire: plain loads (the guide's consumer form), 16 chunks' loads in flight
-  for (int j = tid; j < F.n_out; j += kLgThreads) {
-    const float* src = F.scratch + j;
-    float t = src[0];
-    int c = 1;
-    for (; c + 16 <= F.nB; c += 16) {
-      float v[16];
+  // after the acquire: plain loads (the guide's consumer form). Thread = (float4 column
+  // group, chunk slice): each slice sums its consecutive chunks in chunk order (8 loads in
+  // flight), then the slices are added in slice order — a fixed order, and a few dependent
+  // load rounds where one lane per column walking all nB chunks took nB / 16
+  const int ns = ng >= kLgThreads ? 1 : kLgThreads / ng;     // slices
+  const int cpp = kLgThreads / ns;                            // column groups per pass
+  const int per = (F.nB + ns - 1) / ns;
+  float4* tp = &part[0][0];                                   // 264 >= kLgThreads float4
+  const int sl = tid / cpp, cgt = tid % cpp;
+  for (int cg0 = 0; cg0 < ng; cg0 += cpp) {
+    const int cg = cg0 + cgt;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cg < ng) {
+      const float4* src = reinterpret_cast<const float4*>(F.scratch) + cg;
+      const int c1 = min(F.nB, (sl + 1) * per);
+      int c = sl * per;
+      for (; c + 8 <= c1; c += 8) {
+        float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)(c + u) * F.n_out];
+        for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(c + u) * ng];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t += v[u];
+        for (int u = 0; u < 8; ++u) {
+          t.x += v[u].x; t.y += v[u].y; t.z += v[u].z; t.w += v[u].w;
+        }
+      }
+      for (; c < c1; ++c) {
+        const float4 v = src[(int64_t)c * ng];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
     }
-    for (; c < F.nB; ++c) t += src[(int64_t)c * F.n_out];
-    F.db[j] = t;
+    tp[tid] = t;
+    __syncthreads();
+    if (sl == 0 && cg < ng) {
+      float4 u = tp[cgt];
+      for (int q = 1; q < ns; ++q) {
+        const float4 w = tp[q * cpp + cgt];
+        u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
+      }
+      reinterpret_cast<float4*>(F.db)[cg] = u;
+    }
+    __syncthreads();
   }
 }
 
@@ -632,7 +663,7 @@ extern "C" int mirec_linear_grad_finish_f32(const float* P, int32_t C, int64_t n
   if (C < 1 || n_w < 0 || (n_w % 4) != 0 || (sum && !dW) ||
       ((uintptr_t)P % 16) != 0 || ((uintptr_t)dW % 16) != 0 ||
       (bias && (!g || n_out <= 0 || (n_out % 4) != 0 || ((uintptr_t)g % 16) != 0 || !scratch ||
-                !ticket || ((uintptr_t)scratch % 8) != 0))) {
+                !ticket || ((uintptr_t)scratch % 16) != 0 || ((uintptr_t)db % 16) != 0))) {
     set_error("%s: bad arguments", what);
     return -1;
   }
