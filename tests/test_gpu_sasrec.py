@@ -249,3 +249,14 @@ def test_add_layernorm_and_gelu_match_torch(dev, d):
     (rx,) = torch.autograd.grad(yr, x2, gy)
     torch.testing.assert_close(yg, yr, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(gx, rx, rtol=1e-4, atol=1e-5)
+    # the float4 kernels (n % 4 == 0, aligned) and the one-element kernels (an odd
+    # count) compute the same bits per element
+    from recbole_amd._native import check, lib, ptr
+    xs, gs = x.detach().reshape(-1), gy.reshape(-1).contiguous()
+    m = xs.numel() - 1
+    y1, d1 = torch.empty(m, device=dev), torch.empty(m, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    check(lib().mirec_gelu_fwd_f32(ptr(xs), m, ptr(y1), st), 'gelu_fwd')
+    check(lib().mirec_gelu_bwd_f32(ptr(xs), ptr(gs), m, ptr(d1), st), 'gelu_bwd')
+    assert torch.equal(y1, yg.detach().reshape(-1)[:m])
+    assert torch.equal(d1, gx.reshape(-1)[:m])
