@@ -944,6 +944,11 @@ int mirec_linear_fwd_f32(const float* x, int64_t M, int32_t K, int32_t N, const 
                          const float* bias, float* y, void* stream);
 int mirec_linear_bwd_data_f32(const float* gy, int64_t M, int32_t n_out, int32_t n_in,
                               const float* w, float* gx, int32_t accumulate, void* stream);
+/* gx = acc + gy W (the residual gradient of a block's input plus the Linear's data
+ * gradient, one pass; acc may equal gx). Replaces autograd's add of the two input
+ * gradients where x feeds both a Linear and a residual (reference layers.py:338-461). */
+int mirec_linear_bwd_data_acc_f32(const float* gy, int64_t M, int32_t n_out, int32_t n_in,
+                                  const float* w, const float* acc, float* gx, void* stream);
 /* K9e  The attention core of MultiHeadAttention (reference layers.py:338-407, the lines
  * scores = q k^T / sqrt(dh); + attention_mask; softmax; attn_dropout; @ v), L <= 64 and
  * dh = 64, one workgroup per (sequence, head), fp32 MFMA. q, k, v, out / dout, dq, dk, dv:

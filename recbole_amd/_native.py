@@ -156,6 +156,7 @@ SIGNATURES = {
     "mirec_write_bytes": (c_int, [_P, _P, c_size_t, _P]),
     "mirec_linear_shape_ok": (c_int, [c_int32, c_int32]),
     "mirec_linear_fwd_f32": (c_int, [_P, c_int64, c_int32, c_int32, _P, _P, _P, _P]),
+    "mirec_linear_bwd_data_acc_f32": (c_int, [_P, c_int64, c_int32, c_int32, _P, _P, _P, _P]),
     "mirec_linear_bwd_data_f32": (c_int, [_P, c_int64, c_int32, c_int32, _P, _P, c_int32, _P]),
     "mirec_add_ln_drop_fwd_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_float, c_float,
                                           ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),

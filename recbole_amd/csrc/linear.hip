@@ -40,7 +40,10 @@ __device__ __forceinline__ floatx4 ln_mfma(float a, float b, floatx4 c) {
 template <int K, int N, bool WT, bool ACC>
 __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
     const float* __restrict__ X, int64_t M, const float* __restrict__ W,
-    const float* __restrict__ bias, float* __restrict__ Y) {
+    const float* __restrict__ bias, const float* __restrict__ R, float* __restrict__ Y) {
+  // ACC: Y = R + X B. R may be Y (in place): each element is read once and then written
+  // once by the same lane, so no other access depends on their order (the restrict
+  // qualifiers keep the epilogue's loads batched: without them 48.6 -> 78 us)
   constexpr int KP = K + 4;               // LDS row stride (floats)
   constexpr int NU = K / 16;              // 16-wide k slices
   constexpr int NC = N / 16;              // 16-wide column tiles
@@ -130,8 +133,8 @@ __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
       if (r < M)
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          float* yp = Y + r * N + 16 * c + li;
-          *yp = ACC ? *yp + (acc[c][i] + bv[c]) : acc[c][i] + bv[c];
+          const int64_t o = r * N + 16 * c + li;
+          Y[o] = ACC ? R[o] + (acc[c][i] + bv[c]) : acc[c][i] + bv[c];
         }
     }
     if (kPre) {
@@ -144,8 +147,8 @@ __global__ __launch_bounds__(kLnThreads) void linear_mfma_kernel(
 }
 
 template <int K, int N, bool WT, bool ACC>
-int launch_linear(const float* X, int64_t M, const float* W, const float* bias, float* Y,
-                  hipStream_t st, const char* what) {
+int launch_linear(const float* X, int64_t M, const float* W, const float* bias, const float* R,
+                  float* Y, hipStream_t st, const char* what) {
   constexpr size_t lds = (size_t)N * (K + 4) * sizeof(float);
   static bool attr = false;
   if (!attr) {
@@ -166,17 +169,17 @@ int launch_linear(const float* X, int64_t M, const float* W, const float* bias, 
   const int64_t slabs = (M + 15) / 16;
   const int64_t grid = std::min<int64_t>((slabs + kLnWaves - 1) / kLnWaves, (int64_t)cus * per_cu);
   hipLaunchKernelGGL((linear_mfma_kernel<K, N, WT, ACC>), dim3((unsigned)grid), dim3(kLnThreads),
-                     lds, st, X, M, W, bias, Y);
+                     lds, st, X, M, W, bias, R, Y);
   return launch_status(what);
 }
 
 template <bool WT>
 int linear_dispatch(const float* X, int64_t M, int K, int N, const float* W, const float* bias,
-                    float* Y, bool accumulate, hipStream_t st, const char* what) {
+                    const float* R, float* Y, hipStream_t st, const char* what) {
 #define MIREC_LN(KK, NN) \
   if (K == KK && N == NN)                                                                    \
-    return accumulate ? launch_linear<KK, NN, WT, WT>(X, M, W, bias, Y, st, what)            \
-                      : launch_linear<KK, NN, WT, false>(X, M, W, bias, Y, st, what);
+    return R ? launch_linear<KK, NN, WT, WT>(X, M, W, bias, R, Y, st, what)                  \
+             : launch_linear<KK, NN, WT, false>(X, M, W, bias, nullptr, Y, st, what);
   MIREC_LN(64, 64)
   MIREC_LN(64, 128)
   MIREC_LN(64, 256)
@@ -207,7 +210,7 @@ extern "C" int mirec_linear_fwd_f32(const float* x, int64_t M, int32_t K, int32_
     return -1;
   }
   if (M == 0) return 0;
-  return linear_dispatch<false>(x, M, K, N, w, bias, y, false, (hipStream_t)stream,
+  return linear_dispatch<false>(x, M, K, N, w, bias, nullptr, y, (hipStream_t)stream,
                                 "mirec_linear_fwd_f32");
 }
 
@@ -220,6 +223,19 @@ extern "C" int mirec_linear_bwd_data_f32(const float* gy, int64_t M, int32_t n_o
   }
   if (M == 0) return 0;
   // dX[M, n_in] = dY[M, n_out] W[n_out, n_in]: reduction n_out, B[k][n] = W[k][n]
-  return linear_dispatch<true>(gy, M, n_out, n_in, w, nullptr, gx, accumulate != 0,
+  return linear_dispatch<true>(gy, M, n_out, n_in, w, nullptr, accumulate ? gx : nullptr, gx,
                                (hipStream_t)stream, "mirec_linear_bwd_data_f32");
+}
+
+extern "C" int mirec_linear_bwd_data_acc_f32(const float* gy, int64_t M, int32_t n_out,
+                                             int32_t n_in, const float* w, const float* acc,
+                                             float* gx, void* stream) {
+  if (M < 0 || !gy || !w || !gx || !acc || (((uintptr_t)gy | (uintptr_t)w) & 15)) {
+    set_error("mirec_linear_bwd_data_acc_f32: bad arguments (16-byte aligned gy, w; acc)");
+    return -1;
+  }
+  if (M == 0) return 0;
+  // dX = acc + dY W, into gx (acc == gx: in place, as mirec_linear_bwd_data_f32 accumulating)
+  return linear_dispatch<true>(gy, M, n_out, n_in, w, nullptr, acc, gx, (hipStream_t)stream,
+                               "mirec_linear_bwd_data_acc_f32");
 }

@@ -374,8 +374,15 @@ __device__ __forceinline__ float gelu_d(float v, float g, float rs2, float k) {
 __global__ __launch_bounds__(256) void gelu_fwd4_kernel(const float4* __restrict__ x, int64_t n4,
                                                         float4* __restrict__ y) {
   const float rs2 = (float)(1.0 / 1.4142135623730951);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + st < n4; i += 2 * st) {               // two float4 loads in flight per lane
+    const float4 v = x[i], w = x[i + st];
+    y[i] = make_float4(gelu_f(v.x, rs2), gelu_f(v.y, rs2), gelu_f(v.z, rs2), gelu_f(v.w, rs2));
+    y[i + st] =
+        make_float4(gelu_f(w.x, rs2), gelu_f(w.y, rs2), gelu_f(w.z, rs2), gelu_f(w.w, rs2));
+  }
+  if (i < n4) {
     const float4 v = x[i];
     y[i] = make_float4(gelu_f(v.x, rs2), gelu_f(v.y, rs2), gelu_f(v.z, rs2), gelu_f(v.w, rs2));
   }
@@ -386,8 +393,16 @@ __global__ __launch_bounds__(256) void gelu_bwd4_kernel(const float4* __restrict
                                                         float4* __restrict__ dx) {
   const float rs2 = (float)(1.0 / 1.4142135623730951);
   const float k = (float)(0.3989422804014327);      // 1 / sqrt(2 pi)
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + st < n4; i += 2 * st) {               // four float4 loads in flight per lane
+    const float4 v = x[i], gv = g[i], w = x[i + st], gw = g[i + st];
+    dx[i] = make_float4(gelu_d(v.x, gv.x, rs2, k), gelu_d(v.y, gv.y, rs2, k),
+                        gelu_d(v.z, gv.z, rs2, k), gelu_d(v.w, gv.w, rs2, k));
+    dx[i + st] = make_float4(gelu_d(w.x, gw.x, rs2, k), gelu_d(w.y, gw.y, rs2, k),
+                             gelu_d(w.z, gw.z, rs2, k), gelu_d(w.w, gw.w, rs2, k));
+  }
+  if (i < n4) {
     const float4 v = x[i], gv = g[i];
     dx[i] = make_float4(gelu_d(v.x, gv.x, rs2, k), gelu_d(v.y, gv.y, rs2, k),
                         gelu_d(v.z, gv.z, rs2, k), gelu_d(v.w, gv.w, rs2, k));

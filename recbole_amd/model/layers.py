@@ -211,29 +211,54 @@ class _SplitKLinearFn(torch.autograd.Function):
         return dx, dW, db
 
 
+class _LinearResFn(torch.autograd.Function):
+    """_SplitKLinearFn whose input also feeds a residual (FeedForward: dense_1(x) and the
+    LayerNorm(... + x)): the second output is x itself (a view), and the backward adds
+    gy W to that output's gradient in K11's epilogue (mirec_linear_bwd_data_acc_f32, into
+    a new buffer: the handed-over gradient is not written) — autograd's add of the two
+    input gradients (a [B L, d] torch add per block) goes."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return linear_rows(x, W, b), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gres):
+        x, W = ctx.saved_tensors
+        dx = linear_rows_grad(gy.contiguous(), W, acc=gres, in_place=False)
+        dW, db = _wgrad(x, gy, W, ctx.has_b)
+        return dx, dW, db
+
+
 class _QKVFn(torch.autograd.Function):
     """The query / key / value Linears of MultiHeadAttention over one input (layers.py
     :338-407): three K11 products forward; backward, the input gradient of all three in
     one buffer — dx = gq Wq, then += gk Wk, += gv Wv in K11's accumulating epilogue —
-    instead of three buffers and autograd's two adds."""
+    instead of three buffers and autograd's two adds. The fourth output is x itself (a
+    view) for the block's residual LayerNorm; the first product starts from its gradient
+    (read by K11's epilogue into a new buffer, as _LinearResFn), so that add goes too."""
 
     @staticmethod
     def forward(ctx, x, Wq, bq, Wk, bk, Wv, bv):
         ctx.save_for_backward(x, Wq, Wk, Wv)
         ctx.has_b = (bq is not None, bk is not None, bv is not None)
-        return linear_rows(x, Wq, bq), linear_rows(x, Wk, bk), linear_rows(x, Wv, bv)
+        return (linear_rows(x, Wq, bq), linear_rows(x, Wk, bk), linear_rows(x, Wv, bv),
+                x.view_as(x))
 
     @staticmethod
-    def backward(ctx, gq, gk, gv):
+    def backward(ctx, gq, gk, gv, gres):
         x, Wq, Wk, Wv = ctx.saved_tensors
-        dx = None
+        dx, own = gres, False                 # own: dx is this backward's buffer
         out = []
         for g, W, hb in ((gq, Wq, ctx.has_b[0]), (gk, Wk, ctx.has_b[1]), (gv, Wv, ctx.has_b[2])):
             if g is None:
                 out += [None, None]
                 continue
             g = g.contiguous()
-            dx = linear_rows_grad(g, W, acc=dx)
+            dx = linear_rows_grad(g, W, acc=dx, in_place=own)
+            own = True
             out += list(_wgrad(x, g, W, hb))
         if dx is None:
             dx = torch.zeros_like(x)
@@ -273,21 +298,33 @@ def linear_rows(x, W, b):
     return y.view(*x.shape[:-1], n_out)
 
 
-def linear_rows_grad(gy, W, acc=None):
+def linear_rows_grad(gy, W, acc=None, in_place=True):
     """dL/dx = gy W of linear_rows (K11 where it applies, else the library); acc: a
-    previous input gradient of the same shape, added to (in place with K11)."""
+    previous input gradient of the same shape, added to — in place (in_place: a buffer
+    of the caller's own), or into a new buffer (a gradient autograd handed over, which
+    must not be written: mirec_linear_bwd_data_acc_f32 reads it in the epilogue)."""
     n_out, n_in = W.shape
     if not _k11(gy, n_in, n_out):
         gx = torch.matmul(gy, W)
-        return gx if acc is None else acc.add_(gx)
+        if acc is None:
+            return gx
+        return acc.add_(gx) if in_place else acc + gx
     g2 = gy.reshape(-1, n_out).contiguous()
+    Wc = W.detach().contiguous()
+    if acc is not None and not in_place:
+        a2 = acc.reshape(-1, n_in).contiguous()
+        assert a2.shape[0] == g2.shape[0]
+        gx = torch.empty(g2.shape[0], n_in, dtype=torch.float32, device=gy.device)
+        check(lib().mirec_linear_bwd_data_acc_f32(ptr(g2), g2.shape[0], n_out, n_in, ptr(Wc),
+                                                  ptr(a2), ptr(gx), stream_handle()),
+              'mirec_linear_bwd_data_acc_f32')
+        return gx.view(*gy.shape[:-1], n_in)
     if acc is None:
         gx = torch.empty(g2.shape[0], n_in, dtype=torch.float32, device=gy.device)
     else:
         gx = acc.view(-1, n_in)
         assert gx.is_contiguous() and gx.shape[0] == g2.shape[0]
-    check(lib().mirec_linear_bwd_data_f32(ptr(g2), g2.shape[0], n_out, n_in,
-                                          ptr(W.detach().contiguous()), ptr(gx),
+    check(lib().mirec_linear_bwd_data_f32(ptr(g2), g2.shape[0], n_out, n_in, ptr(Wc), ptr(gx),
                                           int(acc is not None), stream_handle()),
           'mirec_linear_bwd_data_f32')
     return gx.view(*gy.shape[:-1], n_in)
@@ -537,10 +574,11 @@ class MultiHeadAttention(nn.Module):
     def forward(self, input_tensor, attention_mask):
         if (input_tensor.is_cuda and input_tensor.numel() // input_tensor.shape[-1] >= 16384
                 and torch.is_grad_enabled() and input_tensor.requires_grad):
-            ql, kl, vl = _QKVFn.apply(input_tensor, self.query.weight, self.query.bias,
-                                      self.key.weight, self.key.bias, self.value.weight,
-                                      self.value.bias)
+            ql, kl, vl, res = _QKVFn.apply(input_tensor, self.query.weight, self.query.bias,
+                                           self.key.weight, self.key.bias, self.value.weight,
+                                           self.value.bias)
         else:
+            res = input_tensor
             ql = linear(self.query, input_tensor)
             kl = linear(self.key, input_tensor)
             vl = linear(self.value, input_tensor)
@@ -552,7 +590,7 @@ class MultiHeadAttention(nn.Module):
                                 attention_mask, self.num_attention_heads, p, rng)
             if rng is not None and not ctx.requires_grad:   # no backward to advance it
                 rng[1].add_(1)
-            return add_layer_norm(linear(self.dense, ctx), input_tensor, self.LayerNorm,
+            return add_layer_norm(linear(self.dense, ctx), res, self.LayerNorm,
                                   drop=self.out_dropout)
         q = self.transpose_for_scores(ql)
         k = self.transpose_for_scores(kl)
@@ -572,7 +610,7 @@ class MultiHeadAttention(nn.Module):
             probs = self.attn_dropout(probs)
             ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
         ctx = ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
-        return add_layer_norm(linear(self.dense, ctx), input_tensor, self.LayerNorm,
+        return add_layer_norm(linear(self.dense, ctx), res, self.LayerNorm,
                               drop=self.out_dropout)
 
 
@@ -600,8 +638,14 @@ class FeedForward(nn.Module):
         return x * torch.sigmoid(x)
 
     def forward(self, input_tensor):
-        hidden = linear(self.dense_2, self.intermediate_act_fn(linear(self.dense_1, input_tensor)))
-        return add_layer_norm(hidden, input_tensor, self.LayerNorm, drop=self.dropout)
+        x = input_tensor
+        if (x.is_cuda and x.numel() // x.shape[-1] >= 16384 and torch.is_grad_enabled()
+                and x.requires_grad):
+            h, res = _LinearResFn.apply(x, self.dense_1.weight, self.dense_1.bias)
+        else:
+            h, res = linear(self.dense_1, x), x
+        hidden = linear(self.dense_2, self.intermediate_act_fn(h))
+        return add_layer_norm(hidden, res, self.LayerNorm, drop=self.dropout)
 
 
 class TransformerLayer(nn.Module):

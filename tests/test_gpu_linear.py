@@ -81,23 +81,51 @@ def test_k11_data_grad_accumulates(dev):
                                rtol=1e-4, atol=1e-5)
 
 
-def test_qkv_fn_matches_three_linears(dev):
+@pytest.mark.parametrize('with_res', [True, False])
+def test_qkv_fn_matches_three_linears(dev, with_res):
     """_QKVFn (the three projections, one accumulated input gradient) equals three
-    separate nn.Linear calls: outputs and all seven gradients."""
+    separate nn.Linear calls: outputs and all seven gradients; its fourth output (x, the
+    block's residual input) brings its gradient into the same buffer (with_res), or is
+    left unused."""
     from recbole_amd.model import layers
     torch.manual_seed(1)
     lins = [torch.nn.Linear(128, 128).to(dev) for _ in range(3)]
     x = torch.randn(400, 50, 128, device=dev, requires_grad=True)
-    gs = [torch.randn(400, 50, 128, device=dev) for _ in range(3)]
+    gs = [torch.randn(400, 50, 128, device=dev) for _ in range(4)]
     outs = layers._QKVFn.apply(x, *[p for l in lins for p in (l.weight, l.bias)])
-    torch.autograd.backward(outs, gs)
-    got = [o.detach().cpu() for o in outs] + [x.grad.cpu()] + \
+    n = 4 if with_res else 3
+    torch.autograd.backward(outs[:n], gs[:n])
+    got = [o.detach().cpu() for o in outs[:3]] + [x.grad.cpu()] + \
         [p.grad.cpu() for l in lins for p in (l.weight, l.bias)]
     xr = x.detach().cpu().double().requires_grad_()
     ps = [p.detach().cpu().double().requires_grad_() for l in lins for p in (l.weight, l.bias)]
     refs = [torch.nn.functional.linear(xr, ps[2 * i], ps[2 * i + 1]) for i in range(3)]
-    torch.autograd.backward(refs, [t.cpu().double() for t in gs])
+    torch.autograd.backward(refs + [xr] * (n - 3), [t.cpu().double() for t in gs[:n]])
     want = [r.detach() for r in refs] + [xr.grad] + [p.grad for p in ps]
     atols = [1e-5] * 4 + [2e-3] * 6          # weight / bias grads sum 20,000 rows
     for a, e, atol in zip(got, want, atols):
         torch.testing.assert_close(a, e.float(), rtol=1e-4, atol=atol)
+
+
+@pytest.mark.parametrize('n_in,n_out', [(128, 256), (128, 128)])
+def test_linear_res_fn_matches_linear_plus_residual(dev, n_in, n_out):
+    """_LinearResFn (FeedForward's dense_1 with its input passed through for the residual):
+    x's gradient = gy W + the residual's gradient, accumulated in K11's epilogue."""
+    from recbole_amd.model import layers
+    torch.manual_seed(2)
+    lin = torch.nn.Linear(n_in, n_out).to(dev)
+    x = torch.randn(400, 50, n_in, device=dev, requires_grad=True)
+    gy, gr = torch.randn(400, 50, n_out, device=dev), torch.randn(400, 50, n_in, device=dev)
+    y, res = layers._LinearResFn.apply(x, lin.weight, lin.bias)
+    assert torch.equal(res, x)
+    gr0 = gr.clone()
+    torch.autograd.backward([y, res], [gy, gr])
+    assert torch.equal(gr, gr0)               # the handed-over gradient is not written
+    xr = x.detach().cpu().double().requires_grad_()
+    W, b = (t.detach().cpu().double().requires_grad_() for t in (lin.weight, lin.bias))
+    yr = torch.nn.functional.linear(xr, W, b)
+    torch.autograd.backward([yr, xr], [gy.cpu().double(), gr.cpu().double()])
+    torch.testing.assert_close(y.detach().cpu(), yr.detach().float(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(x.grad.cpu(), xr.grad.float(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(lin.weight.grad.cpu(), W.grad.float(), rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(lin.bias.grad.cpu(), b.grad.float(), rtol=1e-4, atol=2e-3)
