@@ -330,6 +330,20 @@ def linear_rows_grad(gy, W, acc=None, in_place=True):
     return gx.view(*gy.shape[:-1], n_in)
 
 
+def colsums(jobs):
+    """Column sums of up to four [n, m] row-major buffers in ONE launch
+    (mirec_colsum_multi_f32: each job with mirec_colsum_f32's tile, the same bits);
+    jobs = [(x, n, m, out)]. The LayerNorm backwards' dgamma / dbeta (and K9a's dP) went
+    as one launch each (11 colsum launches of ~7.6 us a C3 step)."""
+    import ctypes
+    nj = len(jobs)
+    check(lib().mirec_colsum_multi_f32((ctypes.c_void_p * nj)(*[ptr(j[0]) for j in jobs]),
+                                       (ctypes.c_int64 * nj)(*[j[1] for j in jobs]),
+                                       (ctypes.c_int64 * nj)(*[j[2] for j in jobs]),
+                                       (ctypes.c_void_p * nj)(*[ptr(j[3]) for j in jobs]),
+                                       nj, stream_handle()), 'mirec_colsum_multi_f32')
+
+
 class _AddLNFn(torch.autograd.Function):
     """LayerNorm(a + b) (K9d, mirec_add_ln_fwd/bwd_f32): the residual sum is never
     materialised; the backward returns the same dx for both inputs."""
@@ -362,10 +376,7 @@ class _AddLNFn(torch.autograd.Function):
                                          ptr(pb), stream_handle()), 'mirec_add_ln_bwd_f32')
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(gamma)
-        check(lib().mirec_colsum_f32(ptr(pg), parts, d, ptr(dgamma), stream_handle()),
-              'mirec_colsum_f32')
-        check(lib().mirec_colsum_f32(ptr(pb), parts, d, ptr(dbeta), stream_handle()),
-              'mirec_colsum_f32')
+        colsums([(pg, parts, d, dgamma), (pb, parts, d, dbeta)])
         return dx, dx, dgamma, dbeta, None
 
 
@@ -410,10 +421,7 @@ class _AddLNDropFn(torch.autograd.Function):
               'mirec_add_ln_drop_bwd_f32')
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(gamma)
-        check(lib().mirec_colsum_f32(ptr(pg), parts, d, ptr(dgamma), stream_handle()),
-              'mirec_colsum_f32')
-        check(lib().mirec_colsum_f32(ptr(pb), parts, d, ptr(dbeta), stream_handle()),
-              'mirec_colsum_f32')
+        colsums([(pg, parts, d, dgamma), (pb, parts, d, dbeta)])
         return dxa, dxb, dgamma, dbeta, None, None, None
 
 

@@ -22,7 +22,7 @@ import torch.nn as nn
 from recbole_amd import ops
 from recbole_amd._native import check, lib, ptr, stream_handle
 from recbole_amd.model.abstract_recommender import SequentialRecommender
-from recbole_amd.model.layers import TransformerEncoder, _drop_rng
+from recbole_amd.model.layers import TransformerEncoder, _drop_rng, colsums
 from recbole_amd.model.loss import BPRLoss
 
 
@@ -94,14 +94,9 @@ class _SeqEmbedLNFn(torch.autograd.Function):
             dE = ops.segment_scatter_add(ditem, ops.segment_sort(seq.view(-1), E.shape[0]),
                                          torch.zeros_like(E))
         dP = torch.zeros_like(P)
-        check(lib().mirec_colsum_f32(ptr(dx), B, L * d, ptr(dP), stream_handle()),
-              "mirec_colsum_f32")
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(gamma)
-        check(lib().mirec_colsum_f32(ptr(pg), nparts, d, ptr(dgamma), stream_handle()),
-              "mirec_colsum_f32")
-        check(lib().mirec_colsum_f32(ptr(pb), nparts, d, ptr(dbeta), stream_handle()),
-              "mirec_colsum_f32")
+        colsums([(dx, B, L * d, dP), (pg, nparts, d, dgamma), (pb, nparts, d, dbeta)])
         return dE, dP, dgamma, dbeta, None, None, None, None
 
 
