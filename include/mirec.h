@@ -1008,6 +1008,10 @@ int mirec_add_ln_drop_bwd_f32(const float* a, const float* b, int64_t n, int32_t
 int mirec_rank_of_pos_f32(const float* seq_out, const float* item_table, int64_t n_items,
                           int32_t d, const int64_t* pos, const int64_t* neg, int64_t n, int32_t m,
                           int32_t* rank, void* stream);
+/* x *= g[0] in place (n % 4 == 0, 16-byte aligned x; a device scalar g), a no-op when
+ * g[0] == 1: a loss Function's backward scaling its saved gradient rows by the incoming
+ * gradient (reference: autograd's grad_output * saved). */
+int mirec_scale_by_f32(float* x, int64_t n, const float* g, void* stream);
 int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table, int64_t n_items,
                               int32_t d, const int64_t* pos, const int64_t* neg, int64_t B,
                               int32_t n_neg, float grad_scale, float* loss, float* g_seq,

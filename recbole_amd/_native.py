@@ -275,6 +275,7 @@ SIGNATURES = {
     "mirec_seq_embed_ln_drop_bwd_f32": (c_int, [_P, c_int64, _P, _P, c_int64, c_int32, c_int32,
                                                 _P, _P, _P, _P, c_float, ctypes.c_uint64, _P,
                                                 _P, _P, _P, _P, _P, _P]),
+    "mirec_scale_by_f32": (c_int, [_P, c_int64, _P, _P]),
     "mirec_sampled_softmax_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32,
                                           c_float, _P, _P, _P, _P]),
     "mirec_rank_of_pos_f32": (c_int, [_P, _P, c_int64, c_int32, _P, _P, c_int64, c_int32, _P,

@@ -409,6 +409,22 @@ __global__ __launch_bounds__(256) void gelu_bwd4_kernel(const float4* __restrict
   }
 }
 
+// x *= g[0] in place, skipped when g[0] == 1 (x * 1 == x for every non-NaN x, zeros and
+// infinities included): a loss Function's backward scales its saved per-row gradients by
+// the incoming gradient, which a plain loss.backward() makes 1 — the read of g is the whole
+// launch then (K9b's item rows: 26.5 M floats, a 34.5 us torch multiply at C3's shape).
+__global__ __launch_bounds__(256) void scale_by_kernel(float4* __restrict__ x, int64_t n4,
+                                                       const float* __restrict__ g) {
+  const float s = g[0];
+  if (s == 1.0f) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 v = x[i];
+    v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+    x[i] = v;
+  }
+}
+
 // K9b. items: pos [B] and negs [N*B] (layout j*B + b, the sampler's).
 template <int D>
 __global__ __launch_bounds__(256) void sampled_softmax_kernel(
@@ -830,6 +846,19 @@ extern "C" int mirec_gelu_bwd_f32(const float* x, const float* g, int64_t n, flo
     hipLaunchKernelGGL(gelu_bwd_kernel, dim3(elem_grid(n)), dim3(256), 0, (hipStream_t)stream,
                        x, g, n, dx);
   return launch_status("mirec_gelu_bwd_f32");
+}
+
+extern "C" int mirec_scale_by_f32(float* x, int64_t n, const float* g, void* stream) {
+  if (n == 0) return 0;
+  if (!x || !g || n < 0 || n % 4 || ((uintptr_t)x & 15)) {
+    set_error("mirec_scale_by_f32: bad arguments (n %% 4 == 0, 16-byte aligned x)");
+    return -1;
+  }
+  const int64_t n4 = n / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(scale_by_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<float4*>(x), n4, g);
+  return launch_status("mirec_scale_by_f32");
 }
 
 extern "C" int mirec_sampled_softmax_f32(const float* seq_out, const float* item_table,

@@ -163,6 +163,16 @@ class _SampledSoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         items, gS, gI = ctx.saved_tensors
+        if (g.is_cuda and g.dtype == torch.float32 and g.numel() == 1 and gI.is_contiguous()
+                and gI.numel() % 4 == 0 and gI.data_ptr() % 16 == 0):
+            # gI * g in place, a no-op launch when g == 1 (mirec_scale_by_f32): the saved
+            # rows are this Function's own and serve one backward
+            if getattr(ctx, 'scaled', False):
+                raise RuntimeError('_SampledSoftmaxFn: one backward per forward')
+            ctx.scaled = True
+            check(lib().mirec_scale_by_f32(ptr(gI), gI.numel(), ptr(g.contiguous()),
+                                           stream_handle()), 'mirec_scale_by_f32')
+            return gS * g, _item_grad(ctx, gI, items), None, None
         return gS * g, _item_grad(ctx, gI * g, items), None, None
 
 

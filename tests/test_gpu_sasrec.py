@@ -260,3 +260,19 @@ def test_add_layernorm_and_gelu_match_torch(dev, d):
     check(lib().mirec_gelu_bwd_f32(ptr(xs), ptr(gs), m, ptr(d1), st), 'gelu_bwd')
     assert torch.equal(y1, yg.detach().reshape(-1)[:m])
     assert torch.equal(d1, gx.reshape(-1)[:m])
+
+
+def test_scale_by_in_place(dev):
+    """mirec_scale_by_f32 (the SSM backward's gI * g in place): bit for bit torch's
+    multiply, and an untouched buffer when g == 1."""
+    from recbole_amd._native import check, lib, ptr
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3001, 128, generator=g).to(dev)
+    x[0, :4] = torch.tensor([0.0, -0.0, float('inf'), -float('inf')])
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for s in (1.0, 0.37, -2.0):
+        y = x.clone()
+        sv = torch.tensor([s], device=dev)
+        check(lib().mirec_scale_by_f32(ptr(y), y.numel(), ptr(sv), st), 'scale_by')
+        torch.cuda.synchronize(dev)
+        assert torch.equal(y.view(torch.int32), (x * sv).view(torch.int32))
