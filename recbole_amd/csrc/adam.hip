@@ -409,6 +409,13 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
       if (n_max_uniq[q] > 0)
         waves += n_max_uniq[q] * (tables[q].ahead_uniq ? 2 : 1) * ((d + 63) / 64);
     if (waves > 16 * 1024) dvec = 2;
+    // a touched-rows-only launch (no look-ahead lists: the step after the forward's
+    // catch-ups, whose rows need no replay) streams p, m, v and the gradient rows: four
+    // columns per lane (C3's step launch 180 -> 149 us; rows that do lag still replay
+    // exactly, through the general replay)
+    bool ahead = false;
+    for (int q = 0; q < n_tables; ++q) ahead = ahead || tables[q].ahead_uniq != nullptr;
+    if (dvec == 2 && d >= 128 && !ahead && !pair) dvec = 4;
   }
   int64_t blocks = 0;
   for (int q = 0; q < n_tables; ++q) {
@@ -469,8 +476,9 @@ int launch_adam(Sched sched, const mirec_adam_table* tables, int32_t n_tables,
                          grd, dim3(deferred_block(1)), 0, st, tabs, consts, step_base,       \
                          step_off, k);                                                       \
     else if (deferred)                                                                       \
-      hipLaunchKernelGGL((dvec == 2 ? adam_deferred_kernel<DD, float2>                       \
-                                    : adam_deferred_kernel<DD, float>),                      \
+      hipLaunchKernelGGL((dvec == 4 ? adam_deferred_kernel<DD, float4>                       \
+                          : dvec == 2 ? adam_deferred_kernel<DD, float2>                     \
+                                      : adam_deferred_kernel<DD, float>),                    \
                          grd, dim3(deferred_block(DD / dvec)), 0, st, tabs, consts,          \
                          step_base, step_off, k);                                            \
     else if (DD >= 64 && scan)                                                               \
